@@ -1,0 +1,155 @@
+#!/usr/bin/env python
+"""Headline benchmark: pix2pix training throughput (train images/sec, whole job).
+
+Config (BASELINE.json): 256x256 paired images, U-Net-256 generator (ngf 64, instance
+norm, dropout) + 70x70 PatchGAN (basic, n_layers 3), GAN (BCE-with-logits) + 100*L1,
+Adam(2e-4, 0.5/0.999), bf16 compute, synthetic data, random-init weights.  Weak
+scaling: ``--batch`` images per GPU, one process per GPU (torchrun env), gradients
+all-reduced over RCCL by ``p2p_pytorch_amd.parallel.GradReducer``.
+
+    python bench.py --gpus N --steps K --warmup W [--batch B] [--impl native|torch]
+
+``--impl torch`` runs the same model on stock PyTorch-ROCm eager kernels (MIOpen /
+hipBLASLt, bf16 autocast, channels_last) -- the measured baseline of BASELINE.md.
+Rank 0 prints one JSON line; ``value`` = total images/sec over all ranks, from the MAX
+per-rank time of exactly K timed steps bracketed by barrier + device synchronize.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+# Measured stock PyTorch-ROCm eager baseline (images/sec per GPU) for this exact config,
+# recorded in BASELINE.md; None until measured.
+EAGER_BASELINE_IMG_S_PER_GPU = None
+
+
+def parse():
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=32, help="images per GPU")
+    p.add_argument("--size", type=int, default=256)
+    p.add_argument("--netG", default="unet_256")
+    p.add_argument("--netD", default="basic")
+    p.add_argument("--impl", default=os.environ.get("P2P_BACKEND", "native"), choices=["native", "torch"])
+    p.add_argument("--lamb", type=float, default=100.0)
+    p.add_argument("--gan_mode", default="vanilla")
+    p.add_argument("--bucket_mb", type=float, default=64.0)
+    p.add_argument("--no_graph", action="store_true", help="(native) disable hipGraph capture")
+    p.add_argument("--json_out", default=None)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    os.environ["P2P_BACKEND"] = args.impl
+    import p2p_pytorch_amd as p2p
+    from p2p_pytorch_amd.models import define_D, define_G
+    from p2p_pytorch_amd.engine.pix2pix import Pix2PixStep
+    from p2p_pytorch_amd.parallel import dist as pdist
+    p2p.set_backend(args.impl)
+
+    world, rank, local_rank = pdist.init_from_env()
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch with torchrun for N>1")
+    dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+        torch.backends.cudnn.benchmark = True
+    torch.manual_seed(123 + rank)
+
+    netG = define_G(netG=args.netG, gpu_id=dev, verbose=False)
+    netD = define_D(6, 64, norm="instance", netD=args.netD, gpu_id=dev, verbose=False)
+    pdist.broadcast_module(netG)
+    pdist.broadcast_module(netD)
+
+    reducer_g = reducer_d = None
+    if world > 1:
+        from p2p_pytorch_amd.parallel import GradReducer
+        reducer_g = GradReducer(netG, bucket_mb=args.bucket_mb)
+        reducer_d = GradReducer(netD, bucket_mb=args.bucket_mb)
+
+    if args.impl == "torch":
+        act_dtype = torch.float32
+        mf = torch.channels_last
+        autocast = torch.bfloat16 if dev.type == "cuda" else None
+        netG.to(memory_format=mf)
+        netD.to(memory_format=mf)
+    else:
+        act_dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+        mf = torch.channels_last
+        autocast = None
+    trainer = Pix2PixStep(netG, netD, lr=2e-4, beta1=0.5, gan_mode=args.gan_mode,
+                          lambda_L1=args.lamb, reducer_g=reducer_g, reducer_d=reducer_d,
+                          autocast_dtype=autocast)
+
+    B, S = args.batch, args.size
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    real_A = (torch.rand(B, 3, S, S, device=dev, generator=gen) * 2 - 1).to(act_dtype)
+    real_B = (torch.rand(B, 3, S, S, device=dev, generator=gen) * 2 - 1).to(act_dtype)
+    real_A = real_A.contiguous(memory_format=mf)
+    real_B = real_B.contiguous(memory_format=mf)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        losses = trainer.step(real_A, real_B)
+    sync()
+    pdist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        losses = trainer.step(real_A, real_B)
+    sync()
+    pdist.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    dt_max = pdist.max_scalar(dt, dev)
+    loss_vals = {k: float(v) for k, v in losses.items()}
+    finite = all(v == v and abs(v) != float("inf") for v in loss_vals.values())
+
+    img_s = world * B * args.steps / dt_max
+    base = EAGER_BASELINE_IMG_S_PER_GPU
+    out = {
+        "metric": "train images/sec (whole node), 256x256 pix2pix U-Net+PatchGAN",
+        "value": round(img_s, 2),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * dt_max / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(img_s / (base * world), 3) if base else None,
+        "dtype": "bf16",
+        "data": "synthetic (random paired images, random-init weights)",
+        "config": {"model": f"pix2pix {args.netG} + PatchGAN {args.netD} (70x70)",
+                   "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
+                   "image_size": S, "parallelism": f"dp{world}", "impl": args.impl,
+                   "gan_mode": args.gan_mode, "lambda_L1": args.lamb},
+        "losses_finite": finite,
+        "losses": loss_vals,
+    }
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    pdist.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,85 @@
+// Shared device helpers for the p2p_pytorch_amd HIP/CDNA4 (gfx950) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace p2p {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// activation codes shared with bindings.cpp / ops/hip.py
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_TANH = 3, ACT_SIGMOID = 4 };
+constexpr float LRELU_SLOPE = 0.2f;
+
+__device__ __forceinline__ float act_fwd(float v, int act) {
+  switch (act) {
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_LRELU: return v > 0.f ? v : LRELU_SLOPE * v;
+    case ACT_TANH: return tanhf(v);
+    case ACT_SIGMOID: return 1.f / (1.f + __expf(-v));
+    default: return v;
+  }
+}
+
+// derivative of act expressed through the activation's INPUT x (relu / lrelu)
+__device__ __forceinline__ float act_grad_from_input(float x, int act) {
+  switch (act) {
+    case ACT_RELU: return x > 0.f ? 1.f : 0.f;
+    case ACT_LRELU: return x > 0.f ? 1.f : LRELU_SLOPE;
+    default: return 1.f;
+  }
+}
+
+// derivative of act expressed through the activation's OUTPUT y (tanh / sigmoid / relu)
+__device__ __forceinline__ float act_grad_from_output(float y, int act) {
+  switch (act) {
+    case ACT_RELU: return y > 0.f ? 1.f : 0.f;
+    case ACT_LRELU: return y > 0.f ? 1.f : LRELU_SLOPE;
+    case ACT_TANH: return 1.f - y * y;
+    case ACT_SIGMOID: return y * (1.f - y);
+    default: return 1.f;
+  }
+}
+
+__device__ __forceinline__ u32x4 zero_u32x4() { return u32x4{0u, 0u, 0u, 0u}; }
+
+// apply relu / lrelu to 8 packed bf16 held in a 16-byte vector
+__device__ __forceinline__ u32x4 act8(u32x4 v, int act) {
+  if (act == ACT_NONE) return v;
+  bf16x8 b = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float f = (float)b[j];
+    b[j] = (bf16)act_fwd(f, act);
+  }
+  return __builtin_bit_cast(u32x4, b);
+}
+
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+  // PyTorch ReflectionPad semantics (pad < n)
+  i = i < 0 ? -i : i;
+  return i >= n ? 2 * (n - 1) - i : i;
+}
+
+// Bijective XCD-aware remap of a linear workgroup id: blocks b and b+8 share an XCD
+// (MI355X dispatches round-robin over 8 XCDs); give each XCD a contiguous range of
+// logical tiles so tiles that share operand panels hit the same L2.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  if (nwg < 16) return b;
+  int q = nwg / 8, r = nwg % 8;
+  int xcd = b % 8, loc = b / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace p2p

@@ -1,0 +1,65 @@
+// Argument blocks shared between the conv kernels and the host bindings.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace p2p {
+
+// Implicit-GEMM convolution forward.  MODE 0 (CONV): gathered im2col over a NHWC input
+// with stride / zero-or-reflect pad / nearest upsample / virtual concat / input act.
+// MODE 1 (CONVT): transposed conv by sub-pixel decomposition -- one GEMM per output
+// parity class, each with only the taps that hit that class (no zero-stuffing).
+// Also used for conv dgrad (CONVT on dY with the transposed weight) and ConvT dgrad
+// (CONV on dY).
+struct ConvFwdArgs {
+  const void* x1;  // NHWC bf16 [N][H][W][C1]
+  const void* x2;  // NHWC bf16 [N][H][W][C2] (virtual concat), may be null
+  int C1, C2, C;   // C = C1 + C2, all % 8 == 0
+  int N, H, W;     // input spatial size (before upsample)
+  int up;          // nearest upsample factor (1 or 2), CONV only
+  int KH, KW, stride, pad, reflect;
+  int act_in;      // activation applied to the input in the loader
+  int OH, OW, Cout;
+  const void* w;   // bf16 [Cout][KH][KW][C]
+  const float* bias;  // [Cout] or null
+  int act_out;
+  void* y1;        // bf16 output, channels [0, Csplit): NHWC with ld = Csplit
+  void* y2;        // bf16 output, channels [Csplit, Cout): ld = Cout - Csplit (may be null)
+  int Csplit;
+  const void* xb1; // dgrad epilogue: multiply by act'(xb) (same channel split as y)
+  const void* xb2;
+  int act_bwd;
+  float* ws;       // split-K fp32 accumulator [N*OH*OW][Cout] (pre-zeroed) when splits > 1
+  int splits;
+};
+
+// Weight gradient: C[R][Kq] = sum_m P[m][R] * im2col(Q)[m][Kq], written to per-split
+// fp32 slabs ws[split][R][Kq] and reduced (deterministically) by wgrad_reduce.
+struct ConvWgradArgs {
+  // P: plain NHWC rows (optionally virtual concat + activation); rows m enumerate the
+  // OUTPUT pixels of the CONV geometry below (N*OH*OW).
+  const void* p1;
+  const void* p2;
+  int R1, R2, R;   // R = R1 + R2 (% 8 == 0)
+  int p_act;
+  // Q: gathered with the CONV geometry (like ConvFwdArgs MODE 0)
+  const void* q1;
+  const void* q2;
+  int C1, C2, C;
+  int N, H, W, up, KH, KW, stride, pad, reflect;
+  int q_act;
+  int OH, OW;
+  float* ws;       // [splits][R][KH*KW*C]
+  int splits;
+  int M;           // N*OH*OW
+  int Kq;          // KH*KW*C
+};
+
+}  // namespace p2p
+
+extern "C" {
+int p2p_conv_fwd(const p2p::ConvFwdArgs* a, int mode, int bm, int bn, hipStream_t stream);
+int p2p_conv_finalize(const p2p::ConvFwdArgs* a, hipStream_t stream);
+int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t stream);
+int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int KW, int C, float* dw,
+                     int layout, float scale, int accumulate, hipStream_t stream);
+}

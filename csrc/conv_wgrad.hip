@@ -1,0 +1,246 @@
+// Weight gradient of conv / transposed conv on CDNA4 bf16 MFMA (gfx950).
+//
+//   dW[R][Kq] = sum_m P[m][R] * im2col(Q)[m][Kq]
+//
+//   conv  wgrad: P = dY (rows = output pixels, R = Cout),  Q = X  (conv geometry)
+//   convT wgrad: P = X  (rows = input pixels,  R = Cin),   Q = dY (conv geometry of the
+//                transposed conv's *adjoint*: stride s, pad p over the convT output)
+//
+// The reduction dimension m is the OUTER (strided) dimension of both NHWC operands, so
+// both MFMA operands are read k-transposed out of LDS with ds_read_b64_tr_b16 (gfx950's
+// transposing LDS read: 16 lanes fetch a 4x16 block and each lane receives one column).
+// LDS tiles are [64 m][128] bf16 (256-B rows); the 16-B chunk index is XOR-swizzled by
+// ((row&3) | ((row>>3)&1)<<2) << 1 so the 8 rows x 32 B one half-wave reads per
+// transposed load cover all 64 banks exactly once.
+//
+// The m range is split over gridDim.y workgroups (tens of thousands of pixels per image
+// batch); each writes its fp32 partial [R][Kq] slab with plain stores and
+// wgrad_reduce_kernel sums the slabs in a fixed order (bitwise deterministic, no
+// atomics) while permuting into PyTorch's [R][C][KH][KW] weight layout.
+#include "common.h"
+#include "conv.h"
+
+namespace p2p {
+
+constexpr int WBR = 128;   // tile rows (R)
+constexpr int WBQ = 128;   // tile cols (Kq)
+constexpr int WBM = 64;    // reduction rows per stage
+constexpr int WROW = 128;  // elements per LDS row
+
+__device__ __forceinline__ int swz_t(int row, int chunk) {
+  const int x = ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
+  return row * WROW + ((chunk ^ x) << 3);
+}
+
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* tile, int kbase, int cbase, int lane) {
+  // A/B operand of mfma_f32_16x16x32_bf16 with k along tile rows, the 16 operand
+  // rows/cols along tile columns [cbase, cbase+16).
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int chunk = (cbase >> 3) + (p >> 1);
+  s16x4 lo, hi;
+  {
+    const int row = kbase + 8 * g + q;
+    const bf16* ptr = tile + swz_t(row, chunk) + (p & 1) * 4;
+    lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(ptr));
+  }
+  {
+    const int row = kbase + 8 * g + 4 + q;
+    const bf16* ptr = tile + swz_t(row, chunk) + (p & 1) * 4;
+    hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(ptr));
+  }
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
+  constexpr int TM = 4, TN = 4;  // 2x2 waves, 64x64 per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* Ps = reinterpret_cast<bf16*>(smem);      // [2][WBM][128]
+  bf16* Qs = Ps + 2 * WBM * WROW;                // [2][WBM][128]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int qtiles = (a.Kq + WBQ - 1) / WBQ;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int rt = bid / qtiles, qt = bid % qtiles;
+  const int r0 = rt * WBR, q0 = qt * WBQ;
+
+  const int stages = (a.M + WBM - 1) / WBM;
+  const int sps = (stages + a.splits - 1) / a.splits;
+  const int s0 = blockIdx.y * sps;
+  const int s1 = min(stages, s0 + sps);
+
+  const bf16* __restrict__ p1 = static_cast<const bf16*>(a.p1);
+  const bf16* __restrict__ p2 = static_cast<const bf16*>(a.p2);
+  const bf16* __restrict__ q1 = static_cast<const bf16*>(a.q1);
+  const bf16* __restrict__ q2 = static_cast<const bf16*>(a.q2);
+
+  const int ck = tid & 15;          // this thread's 16-B chunk (of 16 per 256-B row)
+  const int rrow = tid >> 4;        // base row; rows rrow + 16*i
+  // P chunk decode (fixed): channel range r0 + 8*ck
+  const int pr = r0 + ck * 8;
+  const bool p_ok = pr < a.R;
+  const bool p_first = pr < a.R1;
+  const bf16* psrc = p_first ? p1 : p2;
+  const int pld = p_first ? a.R1 : a.R2;
+  const int pro = p_first ? pr : pr - a.R1;
+  // Q chunk decode (fixed): kq = q0 + 8*ck -> tap, ci
+  const int kq = q0 + ck * 8;
+  const bool q_ok = kq < a.Kq;
+  int tap = 0, ci = 0;
+  if (q_ok) {
+    tap = kq / a.C;
+    ci = kq - tap * a.C;
+  }
+  const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
+  const bool q_first = ci < a.C1;
+  const bf16* qsrc = q_first ? q1 : q2;
+  const int qld = q_first ? a.C1 : a.C2;
+  const int qco = q_first ? ci : ci - a.C1;
+  const int ush = a.up == 2 ? 1 : 0;
+  const int Hu = a.H << ush, Wu = a.W << ush;
+  const int OHW = a.OH * a.OW;
+
+  u32x4 rp[4], rq[4];
+  auto load_stage = [&](int st) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = st * WBM + rrow + 16 * i;
+      u32x4 vp = zero_u32x4(), vq = zero_u32x4();
+      if (m < a.M) {
+        if (p_ok) {
+          vp = *reinterpret_cast<const u32x4*>(psrc + (long)m * pld + pro);
+          vp = act8(vp, a.p_act);
+        }
+        if (q_ok) {
+          const int n = m / OHW;
+          const int rem = m - n * OHW;
+          const int oh = rem / a.OW;
+          const int ow = rem - oh * a.OW;
+          int uy = oh * a.stride - a.pad + kh;
+          int ux = ow * a.stride - a.pad + kw;
+          bool inb;
+          if (a.reflect) {
+            uy = reflect_idx(uy, Hu);
+            ux = reflect_idx(ux, Wu);
+            inb = true;
+          } else {
+            inb = (unsigned)uy < (unsigned)Hu && (unsigned)ux < (unsigned)Wu;
+          }
+          if (inb) {
+            const long pix = ((long)n * a.H + (uy >> ush)) * a.W + (ux >> ush);
+            vq = *reinterpret_cast<const u32x4*>(qsrc + pix * qld + qco);
+            vq = act8(vq, a.q_act);
+          }
+        }
+      }
+      rp[i] = vp;
+      rq[i] = vq;
+    }
+  };
+  auto store_stage = [&](int buf) {
+    bf16* P = Ps + buf * WBM * WROW;
+    bf16* Q = Qs + buf * WBM * WROW;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = rrow + 16 * i;
+      *reinterpret_cast<u32x4*>(P + swz_t(row, ck)) = rp[i];
+      *reinterpret_cast<u32x4*>(Q + swz_t(row, ck)) = rq[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (s0 < s1) {
+    load_stage(s0);
+    store_stage(0);
+    __syncthreads();
+  }
+  int buf = 0;
+  for (int st = s0; st < s1; ++st) {
+    const bool more = st + 1 < s1;
+    if (more) load_stage(st + 1);
+    const bf16* P = Ps + buf * WBM * WROW;
+    const bf16* Q = Qs + buf * WBM * WROW;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = tr_frag(P, kk * 32, wm * 64 + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = tr_frag(Q, kk * 32, wn * 64 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store_stage(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  // partial slab: ws[split][R][Kq]
+  float* slab = a.ws + (long)blockIdx.y * a.R * a.Kq;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = q0 + wn * 64 + j * 16 + (lane & 15);
+      const int rowb = r0 + wm * 64 + i * 16 + (lane >> 4) * 4;
+      if (col < a.Kq) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (rowb + r < a.R) slab[(long)(rowb + r) * a.Kq + col] = acc[i][j][r];
+      }
+    }
+}
+
+// dw[r][ci][kh][kw] (+)= scale * sum_s ws[s][r][(kh*KW+kw)*C + ci]
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, int splits,
+                                                           int R, int KH, int KW, int C,
+                                                           float* __restrict__ dw, float scale,
+                                                           int accumulate) {
+  const int Kq = KH * KW * C;
+  const long total = (long)R * Kq;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += ws[(long)k * total + e];
+    s *= scale;
+    const int r = (int)(e / Kq);
+    const int kq = (int)(e - (long)r * Kq);
+    const int tap = kq / C;
+    const int ci = kq - tap * C;
+    const long o = ((long)r * C + ci) * KH * KW + tap;
+    dw[o] = accumulate ? dw[o] + s : s;
+  }
+}
+
+}  // namespace p2p
+
+extern "C" int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t st) {
+  constexpr int smem = 2 * 2 * p2p::WBM * p2p::WROW * 2;  // 64 KB
+  const int rtiles = (a->R + p2p::WBR - 1) / p2p::WBR;
+  const int qtiles = (a->Kq + p2p::WBQ - 1) / p2p::WBQ;
+  dim3 grid(rtiles * qtiles, a->splits, 1);
+  hipLaunchKernelGGL(p2p::conv_wgrad_kernel, grid, dim3(256), smem, st, *a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int KW, int C, float* dw,
+                                int layout, float scale, int accumulate, hipStream_t st) {
+  (void)layout;
+  const long total = (long)R * KH * KW * C;
+  long blocks = (total + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(p2p::wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, ws, splits,
+                     R, KH, KW, C, dw, scale, accumulate);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,94 @@
+"""Family-P training step: conditional GAN (U-Net G, PatchGAN D) with GAN + lambda*L1.
+
+Phase order per step (explicit, so the DP reducer can sync each network at its own
+backward -- SURVEY.md section 5.8):
+
+  1. ``fake_B = G(real_A)``
+  2. D phase: ``D(cat(A, fake_B.detach()))`` vs fake label, ``D(cat(A, B))`` vs real label,
+     ``loss_D = 0.5 * (fake + real)`` -> backward -> all-reduce D grads -> Adam(D)
+  3. G phase (D params frozen, so D only back-propagates to its input):
+     ``D(cat(A, fake_B))`` vs real label + ``lambda_L1 * |fake_B - B|`` -> backward ->
+     all-reduce G grads -> Adam(G)
+
+The concat of (A, fake_B) is a *virtual* concat on the native path: D's first conv reads
+the two images through two base pointers (``ops.conv2d`` accepts a tuple input).
+Loss values stay on the device; nothing syncs the host inside ``step``.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+
+from .. import _native
+from ..models.losses import GANLoss
+from ..ops import l1
+from .optim import make_adam
+
+
+def set_requires_grad(nets, flag: bool):
+    for net in nets if isinstance(nets, (list, tuple)) else [nets]:
+        for p in net.parameters():
+            p.requires_grad_(flag)
+
+
+class Pix2PixStep:
+    def __init__(self, netG, netD, lr=2e-4, beta1=0.5, gan_mode="vanilla", lambda_L1=100.0,
+                 reducer_g=None, reducer_d=None, autocast_dtype=None):
+        self.netG, self.netD = netG, netD
+        self.criterionGAN = GANLoss(gan_mode=gan_mode)
+        self.lambda_L1 = float(lambda_L1)
+        self.opt_G = make_adam(netG.parameters(), lr=lr, betas=(beta1, 0.999))
+        self.opt_D = make_adam(netD.parameters(), lr=lr, betas=(beta1, 0.999))
+        self.reducer_g, self.reducer_d = reducer_g, reducer_d
+        self.autocast_dtype = autocast_dtype
+
+    def _ctx(self, device):
+        if self.autocast_dtype is not None:
+            return torch.autocast(device_type=device.type, dtype=self.autocast_dtype)
+        return contextlib.nullcontext()
+
+    @staticmethod
+    def _zero(opt, reducer):
+        # with a reducer, grads are views into its flat buckets: zero in place
+        if reducer is not None:
+            reducer.zero_grad()
+        else:
+            opt.zero_grad(set_to_none=True)
+
+    def _d_input(self, a, b):
+        # the eager baseline materialises the concat; the native conv reads a tuple
+        if a.is_cuda and _native.get_backend() == "native":
+            return (a, b)
+        return torch.cat((a, b), 1)
+
+    def step(self, real_A, real_B):
+        netG, netD = self.netG, self.netD
+        with self._ctx(real_A.device):
+            fake_B = netG(real_A)
+            # ---- D
+            set_requires_grad(netD, True)
+            pred_fake = netD(self._d_input(real_A, fake_B.detach()))
+            loss_D_fake = self.criterionGAN(pred_fake, False)
+            pred_real = netD(self._d_input(real_A, real_B))
+            loss_D_real = self.criterionGAN(pred_real, True)
+            loss_D = (loss_D_fake + loss_D_real) * 0.5
+        self._zero(self.opt_D, self.reducer_d)
+        loss_D.backward()
+        if self.reducer_d is not None:
+            self.reducer_d.finish()
+        self.opt_D.step()
+        # ---- G
+        set_requires_grad(netD, False)
+        with self._ctx(real_A.device):
+            pred_fake = netD(self._d_input(real_A, fake_B))
+            loss_G_GAN = self.criterionGAN(pred_fake, True)
+            loss_G_L1 = l1(fake_B, real_B) * self.lambda_L1
+            loss_G = loss_G_GAN + loss_G_L1
+        self._zero(self.opt_G, self.reducer_g)
+        loss_G.backward()
+        if self.reducer_g is not None:
+            self.reducer_g.finish()
+        self.opt_G.step()
+        return {"D": loss_D.detach(), "G_GAN": loss_G_GAN.detach(), "G_L1": loss_G_L1.detach(),
+                "G": loss_G.detach()}

@@ -1,0 +1,278 @@
+"""Model family R: the reference's learned-compression / bit-depth-expansion GAN.
+
+Parameter / buffer names match the reference exactly so generator checkpoints stay
+interchangeable:
+
+  * ``ExpandNetwork``        /root/reference/networks.py:447-523  (169 state-dict keys)
+  * ``CompressionNetwork``   networks.py:201-236
+  * ``ConvLayer`` / ``UpsampleConvLayer`` / ``ResidualBlock``  networks.py:395-444
+  * ``SpectralNorm``         networks.py:525-582 (``weight_u``/``weight_v``/``weight_bar``)
+  * ``NLayerDiscriminatorSN`` / ``MultiscaleDiscriminator``  networks.py:716-806
+
+The forward passes are re-expressed on the fused op layer: reflection pad and nearest
+upsample are folded into the conv's address generation (no padded / 4x tensor is ever
+materialised), LeakyReLU is a conv epilogue, and the spectral-norm 1/sigma is applied to
+the bf16 weight copy rather than materialised per call as a new parameter.
+Reference quirks that are *observable* are reproduced (single shared PReLU, SN convs
+keep PyTorch's default init, full-res input -> ``scale{num_D-1}_*``).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from .layers import BatchNorm2d, Conv2d
+
+
+class PReLU(nn.PReLU):
+    def forward(self, x):
+        return ops.prelu(x, self.weight)
+
+
+class PixelUnshuffle(nn.Module):
+    """Space-to-depth.  Output channel order ``c*r*r + dy*r + dx`` -- identical to the
+    reference's one-hot grouped conv (networks.py:173-187) and to F.pixel_unshuffle."""
+
+    def __init__(self, downscale_factor):
+        super().__init__()
+        self.downscale_factor = downscale_factor
+
+    def forward(self, x):
+        return ops.pixel_unshuffle(x, self.downscale_factor)
+
+
+def pixel_unshuffle(x, downscale_factor):
+    return ops.pixel_unshuffle(x, downscale_factor)
+
+
+class ConvLayer(nn.Module):
+    """ReflectionPad2d(k//2) + Conv2d(k, stride) -- pad folded into the conv."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride, act_out=None):
+        super().__init__()
+        self.conv2d = Conv2d(in_channels, out_channels, kernel_size, stride=stride,
+                             padding=kernel_size // 2, pad_mode="reflect", act_out=act_out)
+
+    def forward(self, x):
+        return self.conv2d(x)
+
+
+class UpsampleConvLayer(nn.Module):
+    """[nearest Upsample(x s)] + ReflectionPad2d(k//2) + Conv2d -- all one conv."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride, upsample=None):
+        super().__init__()
+        self.upsample = upsample
+        self.conv2d = Conv2d(in_channels, out_channels, kernel_size, stride=stride,
+                             padding=kernel_size // 2, pad_mode="reflect",
+                             upsample=int(upsample) if upsample else 1)
+
+    def forward(self, x):
+        return self.conv2d(x)
+
+
+class ResidualBlock(nn.Module):
+    """relu(BN(conv(relu(BN(conv(x))))) + x); BN attributes keep the reference's
+    misleading ``in1``/``in2`` names (networks.py:429-444)."""
+
+    def __init__(self, channels):
+        super().__init__()
+        self.conv1 = ConvLayer(channels, channels, kernel_size=3, stride=1)
+        self.in1 = BatchNorm2d(channels, affine=True, act="relu")
+        self.relu = nn.ReLU()
+        self.conv2 = ConvLayer(channels, channels, kernel_size=3, stride=1)
+        self.in2 = BatchNorm2d(channels, affine=True)
+
+    def forward(self, x):
+        out = self.in2(self.conv2(self.in1(self.conv1(x))))
+        return ops.act(out + x, "relu")
+
+
+class ExpandNetwork(nn.Module):
+    """Generator "G": bit-depth expansion ResNet (networks.py:447-523)."""
+
+    def __init__(self):
+        super().__init__()
+        self.relu = PReLU()              # ONE scalar shared by all 5 PReLU sites (quirk A9)
+        self.leakyRelu = nn.LeakyReLU(0.2)
+        self.tanh = nn.Tanh()
+        self.inversePixel = PixelUnshuffle(2)
+        self.upsclaing = nn.Upsample(scale_factor=2, mode="nearest")
+        self.conv1 = ConvLayer(12, 32, kernel_size=9, stride=1)
+        self.in1_e = BatchNorm2d(32, affine=True)
+        self.conv2 = ConvLayer(32, 64, kernel_size=3, stride=2)
+        self.in2_e = BatchNorm2d(64, affine=True)
+        self.conv3 = ConvLayer(64, 128, kernel_size=3, stride=2)
+        self.in3_e = BatchNorm2d(128, affine=True)
+        for k in range(1, 10):
+            setattr(self, f"res{k}", ResidualBlock(128))
+        self.deconv3 = UpsampleConvLayer(128, 64, kernel_size=3, stride=1, upsample=2)
+        self.in3_d = BatchNorm2d(64, affine=True)
+        self.deconv2 = UpsampleConvLayer(64, 32, kernel_size=3, stride=1, upsample=2)
+        self.in2_d = BatchNorm2d(32, affine=True)
+        self.deconv1 = UpsampleConvLayer(32, 3, kernel_size=9, stride=1)
+        self.in1_d = BatchNorm2d(3, affine=True, act="tanh")
+
+    def forward(self, x):
+        if x.shape[-1] % 4 or x.shape[-2] % 4:
+            raise ValueError(f"ExpandNetwork needs H, W divisible by 4, got {tuple(x.shape[-2:])}"
+                             " (quirk A16: the reference silently returns a wrong-size image)")
+        # pixel-unshuffle(2) followed by nearest x2: the conv sees 12 channels at full res.
+        y = self.inversePixel(x)
+        y = ops.conv2d(y, self.conv1.conv2d.weight, self.conv1.conv2d.bias, 1, 4, "reflect", 2)
+        y = self.relu(self.in1_e(y))
+        y = self.relu(self.in2_e(self.conv2(y)))
+        y = self.relu(self.in3_e(self.conv3(y)))
+        res = y
+        for k in range(1, 10):
+            res = getattr(self, f"res{k}")(res)
+        y = ops.act(res + y, "lrelu")
+        y = self.relu(self.in3_d(self.deconv3(y)))
+        y = self.relu(self.in2_d(self.deconv2(y)))
+        return self.in1_d(self.deconv1(y))
+
+
+class CompressionNetwork(nn.Module):
+    """Compressor "C": x + l2normalize_c(PixelShuffle2(conv s2(...))) (networks.py:201-236)."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv_input = nn.Sequential(ConvLayer(3, 64, kernel_size=5, stride=1), PReLU())
+        self.conv_block1 = nn.Sequential(ConvLayer(64, 64, kernel_size=3, stride=1),
+                                         BatchNorm2d(64), PReLU())
+        self.conv_block2 = nn.Sequential(ConvLayer(64, 12, kernel_size=3, stride=2),
+                                         nn.PixelShuffle(2))
+
+    def forward(self, x):
+        res = self.conv_block2(self.conv_block1(self.conv_input(x)))
+        return x + ops.l2_normalize_channels(res)
+
+
+# ----------------------------------------------------------------- spectral norm
+def l2normalize(v, eps=1e-12):
+    return v / (v.norm() + eps)
+
+
+class SpectralNorm(nn.Module):
+    """Spectral-norm wrapper with the reference's parameter layout.
+
+    ``weight`` is removed from the wrapped conv and replaced by ``weight_bar``
+    (trainable) plus ``weight_u``/``weight_v`` (Parameters, requires_grad=False).  Each
+    forward runs ``power_iterations`` steps of the power method (u, v updated in place,
+    no gradient) and convolves with ``weight_bar / sigma`` where
+    ``sigma = u . (W v)`` carries the gradient into ``weight_bar``.
+    """
+
+    def __init__(self, module, name="weight", power_iterations=1):
+        super().__init__()
+        self.module = module
+        self.name = name
+        self.power_iterations = power_iterations
+        if not all(hasattr(module, name + s) for s in ("_u", "_v", "_bar")):
+            w = getattr(module, name)
+            h = w.shape[0]
+            wd = w.detach().reshape(h, -1).shape[1]
+            u = nn.Parameter(l2normalize(w.detach().new_empty(h).normal_(0, 1)), requires_grad=False)
+            v = nn.Parameter(l2normalize(w.detach().new_empty(wd).normal_(0, 1)), requires_grad=False)
+            w_bar = nn.Parameter(w.detach().clone())
+            del module._parameters[name]
+            module.register_parameter(name + "_u", u)
+            module.register_parameter(name + "_v", v)
+            module.register_parameter(name + "_bar", w_bar)
+
+    def normalized_weight(self):
+        m = self.module
+        u = getattr(m, self.name + "_u")
+        v = getattr(m, self.name + "_v")
+        w = getattr(m, self.name + "_bar")
+        h = w.shape[0]
+        w2 = w.reshape(h, -1)
+        with torch.no_grad():
+            for _ in range(self.power_iterations):
+                v.copy_(l2normalize(torch.mv(w2.detach().t(), u)))
+                u.copy_(l2normalize(torch.mv(w2.detach(), v)))
+        sigma = torch.dot(u, torch.mv(w2, v))
+        return w / sigma
+
+    def forward(self, x):
+        m = self.module
+        w = self.normalized_weight()
+        return ops.conv2d(x, w, m.bias, m.stride, m.padding, getattr(m, "pad_mode", "zeros"), 1,
+                          getattr(m, "act_in", None), getattr(m, "act_out", None))
+
+
+class NLayerDiscriminatorSN(nn.Module):
+    """70x70 PatchGAN with spectral norm on the middle convs, padding 2, no norm layers,
+    LeakyReLU(0.2) fused into each conv (networks.py:758-806)."""
+
+    def __init__(self, input_nc, ndf=64, n_layers=3, norm_layer=None, use_sigmoid=False,
+                 getIntermFeat=False):
+        super().__init__()
+        self.getIntermFeat = getIntermFeat
+        self.n_layers = n_layers
+        kw, padw = 4, 2
+        seq = [[Conv2d(input_nc, ndf, kw, stride=2, padding=padw, act_out="lrelu")]]
+        nf = ndf
+        for _ in range(1, n_layers):
+            nf_prev, nf = nf, min(nf * 2, 512)
+            seq.append([SpectralNorm(Conv2d(nf_prev, nf, kw, stride=2, padding=padw,
+                                            act_out="lrelu"))])
+        nf_prev, nf = nf, min(nf * 2, 512)
+        seq.append([SpectralNorm(Conv2d(nf_prev, nf, kw, stride=1, padding=padw, act_out="lrelu"))])
+        seq.append([Conv2d(nf, 1, kw, stride=1, padding=padw,
+                           act_out="sigmoid" if use_sigmoid else None)])
+        if getIntermFeat:
+            for k, s in enumerate(seq):
+                setattr(self, f"model{k}", nn.Sequential(*s))
+        else:
+            self.model = nn.Sequential(*[m for s in seq for m in s])
+
+    def forward(self, x):
+        if self.getIntermFeat:
+            out = []
+            for k in range(self.n_layers + 2):
+                x = getattr(self, f"model{k}")(x)
+                out.append(x)
+            return out
+        return self.model(x)
+
+
+class MultiscaleDiscriminator(nn.Module):
+    """num_D PatchGANs on an AvgPool pyramid.  Modules registered flat as
+    ``scale{i}_layer{j}``; the full-resolution input goes to ``scale{num_D-1}`` (A10)."""
+
+    def __init__(self, input_nc, ndf=64, n_layers=3, norm_layer=None, use_sigmoid=False, num_D=3,
+                 getIntermFeat=False):
+        super().__init__()
+        self.num_D = num_D
+        self.n_layers = n_layers
+        self.getIntermFeat = getIntermFeat
+        for i in range(num_D):
+            d = NLayerDiscriminatorSN(input_nc, ndf, n_layers, norm_layer, use_sigmoid, getIntermFeat)
+            if getIntermFeat:
+                for j in range(n_layers + 2):
+                    setattr(self, f"scale{i}_layer{j}", getattr(d, f"model{j}"))
+            else:
+                setattr(self, f"layer{i}", d.model)
+
+    def downsample(self, x):
+        return ops.avg_pool3_s2(x)
+
+    def _single(self, i, x):
+        if self.getIntermFeat:
+            out = []
+            for j in range(self.n_layers + 2):
+                x = getattr(self, f"scale{i}_layer{j}")(x)
+                out.append(x)
+            return out
+        return [getattr(self, f"layer{i}")(x)]
+
+    def forward(self, x):
+        result = []
+        for i in range(self.num_D):
+            result.append(self._single(self.num_D - 1 - i, x))
+            if i != self.num_D - 1:
+                x = self.downsample(x)
+        return result

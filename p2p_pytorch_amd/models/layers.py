@@ -1,0 +1,109 @@
+"""Building-block modules.  They subclass the stock ``torch.nn`` classes so parameter
+names / shapes / ``state_dict`` keys are identical to what the reference saves, but
+their ``forward`` goes through ``p2p_pytorch_amd.ops`` (HIP kernels on the GPU) and can
+fuse the neighbouring pad / upsample / concat / activation into the conv itself.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+
+
+class Conv2d(nn.Conv2d):
+    """nn.Conv2d with fused prologue (pad mode, nearest upsample, input activation,
+    virtual concat of a tuple input) and fused output activation."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, bias=True,
+                 pad_mode="zeros", upsample=1, act_in=None, act_out=None):
+        super().__init__(in_channels, out_channels, kernel_size, stride=stride, padding=padding,
+                         bias=bias)
+        self.pad_mode = pad_mode
+        self.upsample = upsample
+        self.act_in = act_in
+        self.act_out = act_out
+
+    def forward(self, x):  # noqa: D401
+        return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.pad_mode,
+                          self.upsample, self.act_in, self.act_out)
+
+
+class ConvTranspose2d(nn.ConvTranspose2d):
+    """nn.ConvTranspose2d (weight [Cin, Cout, kh, kw]) with fused input activation and
+    virtual concat -- the pix2pix decoder ``ReLU -> ConvT`` on ``cat(skip, up)``."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=4, stride=2, padding=1, bias=True,
+                 act_in=None, act_out=None):
+        super().__init__(in_channels, out_channels, kernel_size, stride=stride, padding=padding,
+                         bias=bias)
+        self.act_in = act_in
+        self.act_out = act_out
+
+    def forward(self, x):
+        return ops.conv_transpose2d(x, self.weight, self.bias, self.stride[0], self.padding[0],
+                                    self.act_in, self.act_out)
+
+
+class InstanceNorm2d(nn.Module):
+    """InstanceNorm2d(affine=False, track_running_stats=False) + fused activation
+    (pix2pix 'instance' norm)."""
+
+    def __init__(self, num_features, eps=1e-5, act=None, affine=False):
+        super().__init__()
+        self.num_features = num_features
+        self.eps = eps
+        self.act = act
+        if affine:
+            self.weight = nn.Parameter(torch.ones(num_features))
+            self.bias = nn.Parameter(torch.zeros(num_features))
+        else:
+            self.register_parameter("weight", None)
+            self.register_parameter("bias", None)
+
+    def forward(self, x):
+        return ops.instance_norm(x, self.eps, self.act, self.weight, self.bias)
+
+
+class BatchNorm2d(nn.BatchNorm2d):
+    """nn.BatchNorm2d (same buffers/keys) with a fused output activation."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True, act=None):
+        super().__init__(num_features, eps=eps, momentum=momentum, affine=affine)
+        self.act = act
+
+    def forward(self, x):
+        training = self.training or not self.track_running_stats
+        if self.training and self.track_running_stats:
+            self.num_batches_tracked.add_(1)
+        return ops.batch_norm(x, self.running_mean if self.track_running_stats else None,
+                              self.running_var if self.track_running_stats else None,
+                              self.weight, self.bias, training, self.momentum, self.eps, self.act)
+
+
+class Act(nn.Module):
+    def __init__(self, name):
+        super().__init__()
+        self.name = name
+
+    def forward(self, x):
+        return ops.act(x, self.name)
+
+
+class Dropout(nn.Module):
+    def __init__(self, p=0.5):
+        super().__init__()
+        self.p = p
+
+    def forward(self, x):
+        return ops.dropout(x, self.p, self.training)
+
+
+def norm_layer(kind: str, channels: int, act=None):
+    if kind == "instance":
+        return InstanceNorm2d(channels, act=act)
+    if kind == "batch":
+        return BatchNorm2d(channels, act=act)
+    if kind in ("none", None):
+        return Act(act) if act else nn.Identity()
+    raise NotImplementedError(f"normalization layer [{kind}] is not found")

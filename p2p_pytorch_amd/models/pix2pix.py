@@ -1,0 +1,119 @@
+"""Model family P: the classic pix2pix U-Net generator and PatchGAN / pixel discriminators.
+
+The reference repository has no U-Net; BASELINE.json's benchmark
+configs name "U-Net-256 + 70x70 PatchGAN" and "4-layer U-Net + 1x1 PatchGAN".  The
+reference carries the knobs for this family (``--ngf`` /root/reference/train.py:148,
+``--lamb`` "weight on L1 term" train.py:156 and the commented L1 term train.py:341) and
+its D is built from the same 70x70 PatchGAN recipe (networks.py:758-806).
+
+Design (MI355X-first): the U-Net is kept *flat* -- explicit encoder/decoder lists --
+instead of the recursive skip-block nesting of the pix2pix template, so that
+  * every ``LeakyReLU -> Conv`` is one fused conv (``act_in='lrelu'``),
+  * every ``ReLU -> ConvT(cat(skip, up))`` is one fused transposed conv reading the two
+    halves of the concat through two base pointers (no ``torch.cat`` materialised),
+  * the final ``Tanh`` is the epilogue of the last ConvT.
+Numerically this is the standard U-Net: level ``i`` has ``ngf*min(2^i, 8)`` channels,
+no norm on the outermost/innermost down convs, dropout on the ``num_downs-5`` decoder
+levels right outside the innermost one.
+"""
+from __future__ import annotations
+
+import torch.nn as nn
+
+from .layers import Conv2d, ConvTranspose2d, Dropout, norm_layer
+
+
+class UnetGenerator(nn.Module):
+    def __init__(self, input_nc=3, output_nc=3, num_downs=8, ngf=64, norm="instance",
+                 use_dropout=True):
+        super().__init__()
+        if num_downs < 2:
+            raise ValueError("num_downs must be >= 2")
+        self.num_downs = num_downs
+        use_bias = norm != "batch"
+        ch = [ngf * min(2 ** i, 8) for i in range(num_downs)]
+        self.channels = ch
+        n = num_downs
+        self.downs = nn.ModuleList()
+        self.down_norms = nn.ModuleList()
+        for i in range(n):
+            cin = input_nc if i == 0 else ch[i - 1]
+            self.downs.append(Conv2d(cin, ch[i], 4, stride=2, padding=1, bias=use_bias,
+                                     act_in=None if i == 0 else "lrelu"))
+            has_norm = 0 < i < n - 1
+            self.down_norms.append(norm_layer(norm, ch[i]) if has_norm else nn.Identity())
+        self.ups = nn.ModuleList()
+        self.up_norms = nn.ModuleList()
+        self.drop_levels = set(range(max(1, n - 1 - max(0, n - 5)), n - 1)) if use_dropout else set()
+        for i in range(n):
+            cin = ch[i] if i == n - 1 else 2 * ch[i]
+            cout = output_nc if i == 0 else ch[i - 1]
+            self.ups.append(ConvTranspose2d(cin, cout, 4, stride=2, padding=1,
+                                            bias=True if i == 0 else use_bias, act_in="relu",
+                                            act_out="tanh" if i == 0 else None))
+            self.up_norms.append(norm_layer(norm, cout) if i > 0 else nn.Identity())
+        self.dropouts = nn.ModuleList(
+            [Dropout(0.5) if i in self.drop_levels else nn.Identity() for i in range(n)])
+
+    def forward(self, x):
+        n = self.num_downs
+        skips = []
+        h = x
+        for i in range(n):
+            h = self.down_norms[i](self.downs[i](h))
+            skips.append(h)
+        u = self.dropouts[n - 1](self.up_norms[n - 1](self.ups[n - 1](skips[n - 1])))
+        for i in range(n - 2, -1, -1):
+            u = self.ups[i]((skips[i], u))
+            u = self.dropouts[i](self.up_norms[i](u))
+        return u
+
+
+class NLayerDiscriminator(nn.Module):
+    """PatchGAN.  With n_layers=3 and 4x4 kernels the receptive field is 70x70
+    (reference networks.py:758-787 builds the same ladder with padding 2; pix2pix uses 1)."""
+
+    def __init__(self, input_nc, ndf=64, n_layers=3, norm="instance", use_sigmoid=False, padw=1):
+        super().__init__()
+        use_bias = norm != "batch"
+        layers = [Conv2d(input_nc, ndf, 4, stride=2, padding=padw)]
+        norms = [nn.Identity()]
+        nf = ndf
+        for k in range(1, n_layers):
+            nf_prev, nf = nf, ndf * min(2 ** k, 8)
+            layers.append(Conv2d(nf_prev, nf, 4, stride=2, padding=padw, bias=use_bias,
+                                 act_in="lrelu"))
+            norms.append(norm_layer(norm, nf))
+        nf_prev, nf = nf, ndf * min(2 ** n_layers, 8)
+        layers.append(Conv2d(nf_prev, nf, 4, stride=1, padding=padw, bias=use_bias, act_in="lrelu"))
+        norms.append(norm_layer(norm, nf))
+        layers.append(Conv2d(nf, 1, 4, stride=1, padding=padw, act_in="lrelu",
+                             act_out="sigmoid" if use_sigmoid else None))
+        norms.append(nn.Identity())
+        self.convs = nn.ModuleList(layers)
+        self.norms = nn.ModuleList(norms)
+
+    def forward(self, x):
+        for conv, norm in zip(self.convs, self.norms):
+            x = norm(conv(x))
+        return x
+
+
+class PixelDiscriminator(nn.Module):
+    """1x1 PatchGAN ('pixel' D): BASELINE config 1's discriminator."""
+
+    def __init__(self, input_nc, ndf=64, norm="instance", use_sigmoid=False):
+        super().__init__()
+        use_bias = norm != "batch"
+        self.convs = nn.ModuleList([
+            Conv2d(input_nc, ndf, 1),
+            Conv2d(ndf, ndf * 2, 1, bias=use_bias, act_in="lrelu"),
+            Conv2d(ndf * 2, 1, 1, bias=use_bias, act_in="lrelu",
+                   act_out="sigmoid" if use_sigmoid else None),
+        ])
+        self.norms = nn.ModuleList([nn.Identity(), norm_layer(norm, ndf * 2), nn.Identity()])
+
+    def forward(self, x):
+        for conv, norm in zip(self.convs, self.norms):
+            x = norm(conv(x))
+        return x

@@ -1,0 +1,120 @@
+"""Frozen VGG19 feature extractor + perceptual loss (reference ``Vgg19`` / ``VGGLoss``,
+/root/reference/networks.py:18-62).
+
+torchvision is not available, so the VGG19 'E' configuration is built in-repo with the
+same module indices (``slice{k}.{idx}``) as ``torchvision.models.vgg19().features``
+sliced at relu1_1 / relu2_1 / relu3_1 / relu4_1 / relu5_1.  ImageNet weights are read
+from a local file when ``P2P_VGG19_WEIGHTS`` points at one (a safetensors file or a
+``torch.save``d state dict, loaded with ``weights_only=True``); otherwise the network
+is random-initialised (there is no network access) -- the loss is then a random-feature
+perceptual loss with identical cost.  Inputs are fed in [-1, 1] with no ImageNet
+normalisation, exactly like the reference (quirk A15).
+
+Every ReLU is fused into its conv's epilogue and each max-pool is a separate kernel.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .layers import Conv2d
+
+# torchvision vgg19 'E' features: (index, kind, cin, cout)
+_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512, 512, "M",
+        512, 512, 512, 512, "M"]
+_SLICES = [(0, 2), (2, 7), (7, 12), (12, 21), (21, 30)]
+
+
+class _ReLU(nn.Module):
+    def forward(self, x):
+        return x  # fused into the preceding conv's epilogue
+
+
+class _MaxPool(nn.Module):
+    def forward(self, x):
+        return torch.nn.functional.max_pool2d(x, 2, 2)
+
+
+def _vgg19_features():
+    layers = []
+    cin = 3
+    for v in _CFG:
+        if v == "M":
+            layers.append(_MaxPool())
+        else:
+            layers.append(Conv2d(cin, v, 3, padding=1, act_out="relu"))
+            layers.append(_ReLU())
+            cin = v
+    return layers
+
+
+class Vgg19(nn.Module):
+    def __init__(self, requires_grad=False, weights_path=None):
+        super().__init__()
+        feats = _vgg19_features()
+        for k, (a, b) in enumerate(_SLICES, 1):
+            seq = nn.Sequential()
+            for idx in range(a, b):
+                seq.add_module(str(idx), feats[idx])
+            setattr(self, f"slice{k}", seq)
+        self._init(weights_path or os.environ.get("P2P_VGG19_WEIGHTS"))
+        if not requires_grad:
+            for p in self.parameters():
+                p.requires_grad = False
+
+    def _init(self, path):
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+                nn.init.zeros_(m.bias)
+        self.pretrained = False
+        if path and os.path.exists(path):
+            if path.endswith(".safetensors"):
+                from safetensors.torch import load_file
+                sd = load_file(path)
+            else:
+                sd = torch.load(path, map_location="cpu", weights_only=True)
+            mapped = {}
+            for k, v in sd.items():  # accept torchvision 'features.N.weight' keys
+                key = k[len("features."):] if k.startswith("features.") else k
+                idx, _, leaf = key.partition(".")
+                if not idx.isdigit():
+                    continue
+                i = int(idx)
+                for s, (a, b) in enumerate(_SLICES, 1):
+                    if a <= i < b:
+                        mapped[f"slice{s}.{i}.{leaf}"] = v
+            self.load_state_dict(mapped, strict=False)
+            self.pretrained = True
+
+    def forward(self, x):
+        h1 = self.slice1(x)
+        h2 = self.slice2(h1)
+        h3 = self.slice3(h2)
+        h4 = self.slice4(h3)
+        h5 = self.slice5(h4)
+        return [h1, h2, h3, h4, h5]
+
+
+class VGGLoss(nn.Module):
+    """sum_i w_i * L1(phi_i(x), phi_i(y).detach()), w = [1/32, 1/16, 1/8, 1/4, 1]."""
+
+    weights = [1.0 / 32, 1.0 / 16, 1.0 / 8, 1.0 / 4, 1.0]
+
+    def __init__(self, device=None):
+        super().__init__()
+        self.vgg = Vgg19()
+        if device is not None:
+            self.vgg = self.vgg.to(device)
+
+    def forward(self, x, y):
+        fx = self.vgg(x)
+        with torch.no_grad():
+            fy = self.vgg(y)
+        loss = 0
+        for w, a, b in zip(self.weights, fx, fy):
+            loss = loss + w * ops.l1(a, b.detach())
+        return loss

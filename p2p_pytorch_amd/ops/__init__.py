@@ -1,0 +1,133 @@
+"""Functional op layer used by every model in ``p2p_pytorch_amd.models``.
+
+Each op routes GPU tensors to the HIP/CDNA4 kernels (``ops/hip.py`` -> ``torch.ops.p2p``)
+and CPU tensors to the PyTorch oracle (``ops/reference.py``).  See ``_native.use_native``
+for the no-silent-fallback policy.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+from . import reference as ref
+
+LRELU_SLOPE = ref.LRELU_SLOPE
+apply_act = ref.apply_act
+
+
+def _first(x):
+    return x[0] if isinstance(x, (tuple, list)) else x
+
+
+def _hip():
+    from . import hip  # imported lazily: it touches torch.ops.p2p
+    return hip
+
+
+def conv2d(x, weight, bias=None, stride=1, padding=0, pad_mode="zeros", upsample=1,
+           act_in=None, act_out=None):
+    if _native.use_native(_first(x)):
+        return _hip().conv2d(x, weight, bias, stride, padding, pad_mode, upsample, act_in, act_out)
+    return ref.conv2d(x, weight, bias, stride, padding, pad_mode, upsample, act_in, act_out)
+
+
+def conv_transpose2d(x, weight, bias=None, stride=2, padding=1, act_in=None, act_out=None):
+    if _native.use_native(_first(x)):
+        return _hip().conv_transpose2d(x, weight, bias, stride, padding, act_in, act_out)
+    return ref.conv_transpose2d(x, weight, bias, stride, padding, act_in, act_out)
+
+
+def instance_norm(x, eps=1e-5, act=None, weight=None, bias=None):
+    if _native.use_native(x):
+        return _hip().instance_norm(x, eps, act, weight, bias)
+    return ref.instance_norm(x, eps, act, weight, bias)
+
+
+def batch_norm(x, running_mean, running_var, weight, bias, training, momentum=0.1, eps=1e-5,
+               act=None):
+    if _native.use_native(x):
+        return _hip().batch_norm(x, running_mean, running_var, weight, bias, training, momentum,
+                                 eps, act)
+    return ref.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps, act)
+
+
+def prelu(x, weight):
+    if _native.use_native(x):
+        return _hip().prelu(x, weight)
+    return ref.prelu(x, weight)
+
+
+def act(x, name):
+    if name is None:
+        return x
+    if _native.use_native(x):
+        return _hip().act(x, name)
+    return ref.apply_act(x, name)
+
+
+def dropout(x, p, training):
+    if not training or p == 0.0:
+        return x
+    if _native.use_native(x):
+        return _hip().dropout(x, p)
+    return ref.dropout(x, p, training)
+
+
+def mse_const(pred, target):
+    if _native.use_native(pred):
+        return _hip().mse_const(pred, target)
+    return ref.mse_const(pred, target)
+
+
+def bce_logits_const(pred, target):
+    if _native.use_native(pred):
+        return _hip().bce_logits_const(pred, target)
+    return ref.bce_logits_const(pred, target)
+
+
+def bce_const(prob, target):
+    return ref.bce_const(prob, target)
+
+
+def l1(a, b):
+    if _native.use_native(a):
+        return _hip().l1(a, b)
+    return ref.l1(a, b)
+
+
+def mse(a, b):
+    if _native.use_native(a):
+        return _hip().mse(a, b)
+    return ref.mse(a, b)
+
+
+def tv(x):
+    if _native.use_native(x):
+        return _hip().tv(x)
+    return ref.tv(x)
+
+
+def quantize(x, bits):
+    if _native.use_native(x):
+        return _hip().quantize(x, bits)
+    return ref.quantize(x, bits)
+
+
+def avg_pool3_s2(x):
+    if _native.use_native(x):
+        return _hip().avg_pool3_s2(x)
+    return ref.avg_pool3_s2(x)
+
+
+def l2_normalize_channels(x, eps=1e-12):
+    if _native.use_native(x):
+        return _hip().l2_normalize_channels(x, eps)
+    return ref.l2_normalize_channels(x, eps)
+
+
+def pixel_shuffle(x, r):
+    return torch.nn.functional.pixel_shuffle(x, r)
+
+
+def pixel_unshuffle(x, r):
+    return torch.nn.functional.pixel_unshuffle(x, r)

@@ -1,0 +1,102 @@
+"""Process-group plumbing: one process per GPU, RCCL ("nccl" backend on ROCm) over xGMI.
+
+The reference is single-device; everything here is new.  Gloo is
+used only when no GPU is present (CPU unit tests / the CPU plumbing config).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def init_from_env(timeout_s: float = 600.0):
+    """Initialise from torchrun's env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*).
+
+    Returns (world_size, rank, local_rank).  World size 1 without env -> no process group.
+    """
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        use_gpu = torch.cuda.is_available()
+        backend = "nccl" if use_gpu else "gloo"
+        kw = {}
+        if use_gpu:
+            torch.cuda.set_device(local_rank)
+            kw["device_id"] = torch.device("cuda", local_rank)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return world, rank, local_rank
+
+
+def is_dist() -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def world_size() -> int:
+    return dist.get_world_size() if is_dist() else 1
+
+
+def rank() -> int:
+    return dist.get_rank() if is_dist() else 0
+
+
+def barrier():
+    if is_dist():
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+@torch.no_grad()
+def broadcast_module(module: torch.nn.Module, src: int = 0):
+    """Broadcast parameters and buffers (BN running stats, SN u/v) from ``src``."""
+    if not is_dist():
+        return
+    tensors = [p.data for p in module.parameters()] + [b for b in module.buffers()]
+    # coalesce by dtype to issue few large broadcasts
+    by_dtype = {}
+    for t in tensors:
+        by_dtype.setdefault(t.dtype, []).append(t)
+    for ts in by_dtype.values():
+        flat = torch.cat([t.reshape(-1) for t in ts])
+        dist.broadcast(flat, src)
+        off = 0
+        for t in ts:
+            n = t.numel()
+            t.copy_(flat[off:off + n].view_as(t))
+            off += n
+
+
+def max_scalar(x: float, device) -> float:
+    if not is_dist():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_reduce_mean_(tensors):
+    """In-place mean of a list of (device) scalars/tensors across ranks -- used for logged
+    loss scalars and eval metrics every N steps (not every step)."""
+    if not is_dist():
+        return tensors
+    flat = torch.cat([t.reshape(-1).float() for t in tensors])
+    dist.all_reduce(flat)
+    flat /= world_size()
+    off = 0
+    for t in tensors:
+        n = t.numel()
+        t.copy_(flat[off:off + n].view_as(t))
+        off += n
+    return tensors
+
+
+def destroy():
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
