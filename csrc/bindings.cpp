@@ -1,0 +1,546 @@
+// torch.ops.p2p.* registrations for the HIP/CDNA4 kernels (gfx950).
+//
+// Host-side responsibilities kept in C++: argument checking, output / workspace
+// allocation through PyTorch's caching allocator (so every op is hipGraph-capturable --
+// no hipMalloc, no sync), GEMM tile and split-K selection, and launching on the current
+// HIP stream.  Autograd, weight-layout caching and channel padding live in
+// p2p_pytorch_amd/ops/hip.py.
+//
+// Tensor convention: activations are bf16 NCHW-shaped tensors in channels_last memory
+// (i.e. NHWC bytes) with C % 8 == 0 (16-B channel chunks); weights are pre-laid-out bf16
+// GEMM operands produced by weight_prep; master weights / grads / optimizer state fp32.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "conv.h"
+
+extern "C" {
+long p2p_norm_ws_floats(int N, int HW, int C);
+int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* gamma,
+                 const float* beta, const float* prelu_w, int act, float* mean, float* rstd,
+                 float* run_mean, float* run_var, float momentum, float* ws, void* y,
+                 hipStream_t st);
+int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const float* rstd,
+                   const float* gamma, const float* beta, const float* prelu_w, int act, void* y,
+                   hipStream_t st);
+int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const float* mean,
+                 const float* rstd, const float* gamma, float* dgamma, float* dbeta, float* ws,
+                 void* dx, hipStream_t st);
+int p2p_act(const void* a, const void* b, long n, int act, int mode, void* out, hipStream_t st);
+int p2p_dropout(const void* x, long n, float p, const int64_t* seed, unsigned salt, void* y,
+                hipStream_t st);
+int p2p_pad_channels(const void* a, int Ca, const void* b, int Cb, long P, int Co, void* out,
+                     hipStream_t st);
+int p2p_slice_channels(const void* in, int Ci, int c0, long P, int C, void* out, hipStream_t st);
+int p2p_colsum_blocks(long M, int C);
+int p2p_colsum(const void* x, long M, int C, float scale, int accumulate, float* ws, float* out,
+               hipStream_t st);
+int p2p_loss_blocks(long n);
+int p2p_loss_fwd(const void* a, const void* b, int is_f32, long n, int kind, float t, float scale,
+                 float* ws, float* out, hipStream_t st);
+int p2p_loss_bwd(const void* a, const void* b, int is_f32, long n, int kind, float t, float scale,
+                 const float* gout, void* ga, void* gb, hipStream_t st);
+int p2p_adam_max_tensors();
+int p2p_adam(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
+             const long* n, const float* lr, const float* step, float b1, float b2, float eps,
+             float wd, hipStream_t st);
+}
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+hipStream_t cur_stream(const Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check_act(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, ": expected a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, ": expected bf16, got ", t.scalar_type());
+  TORCH_CHECK(t.dim() == 4, name, ": expected NCHW-shaped tensor");
+  TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), name,
+              ": expected channels_last (NHWC) memory");
+  TORCH_CHECK(t.size(1) % 8 == 0, name, ": channels must be a multiple of 8, got ", t.size(1));
+}
+
+void check_rc(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, what, ": HIP launch failed: ", hipGetErrorString((hipError_t)rc));
+}
+
+Tensor empty_nhwc(int64_t N, int64_t C, int64_t H, int64_t W, const Tensor& like) {
+  return at::empty({N, C, H, W}, like.options().memory_format(at::MemoryFormat::ChannelsLast));
+}
+
+// ------------------------------------------------------------------ conv fwd / dgrad
+std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const Tensor& w,
+                             const optional<Tensor>& bias, int64_t mode, int64_t KH, int64_t KW,
+                             int64_t stride, int64_t pad, int64_t reflect, int64_t up,
+                             int64_t act_in, int64_t OH, int64_t OW, int64_t Cout, int64_t act_out,
+                             int64_t Csplit, const optional<Tensor>& xb1,
+                             const optional<Tensor>& xb2, int64_t act_bwd) {
+  check_act(x1, "conv_fwd x1");
+  const int64_t N = x1.size(0), H = x1.size(2), W = x1.size(3);
+  int64_t C2 = 0;
+  if (x2) {
+    check_act(*x2, "conv_fwd x2");
+    TORCH_CHECK(x2->size(0) == N && x2->size(2) == H && x2->size(3) == W, "conv_fwd: concat shape");
+    C2 = x2->size(1);
+  }
+  const int64_t C1 = x1.size(1), C = C1 + C2;
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous(), "conv_fwd: weight");
+  TORCH_CHECK(w.numel() >= Cout * KH * KW * C, "conv_fwd: weight too small for the GEMM view");
+  TORCH_CHECK(Cout % 8 == 0 && Csplit % 8 == 0 && Csplit > 0 && Csplit <= Cout, "conv_fwd: Cout/Csplit");
+  TORCH_CHECK(mode == 0 || mode == 1, "conv_fwd: mode");
+  TORCH_CHECK(up == 1 || up == 2, "conv_fwd: upsample must be 1 or 2");
+  TORCH_CHECK(mode == 0 || (up == 1 && reflect == 0), "conv_fwd: CONVT mode has no pad/upsample folds");
+  if (reflect) TORCH_CHECK(pad < H * up && pad < W * up, "conv_fwd: reflect pad too large");
+  if (bias) TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= Cout, "conv_fwd: bias");
+  if (act_bwd) {
+    TORCH_CHECK(xb1.has_value(), "conv_fwd: act_bwd needs xb1");
+    check_act(*xb1, "xb1");
+    TORCH_CHECK(xb1->size(1) == Csplit && xb1->size(2) == OH && xb1->size(3) == OW, "xb1 shape");
+    if (Csplit < Cout) {
+      TORCH_CHECK(xb2.has_value(), "conv_fwd: act_bwd needs xb2");
+      check_act(*xb2, "xb2");
+      TORCH_CHECK(xb2->size(1) == Cout - Csplit, "xb2 shape");
+    }
+  }
+  Tensor y1 = empty_nhwc(N, Csplit, OH, OW, x1);
+  Tensor y2;
+  if (Csplit < Cout) y2 = empty_nhwc(N, Cout - Csplit, OH, OW, x1);
+
+  p2p::ConvFwdArgs a{};
+  a.x1 = x1.data_ptr();
+  a.x2 = x2 ? x2->data_ptr() : nullptr;
+  a.C1 = (int)C1;
+  a.C2 = (int)C2;
+  a.C = (int)C;
+  a.N = (int)N;
+  a.H = (int)H;
+  a.W = (int)W;
+  a.up = (int)up;
+  a.KH = (int)KH;
+  a.KW = (int)KW;
+  a.stride = (int)stride;
+  a.pad = (int)pad;
+  a.reflect = (int)reflect;
+  a.act_in = (int)act_in;
+  a.OH = (int)OH;
+  a.OW = (int)OW;
+  a.Cout = (int)Cout;
+  a.w = w.data_ptr();
+  a.bias = bias ? bias->data_ptr<float>() : nullptr;
+  a.act_out = (int)act_out;
+  a.y1 = y1.data_ptr();
+  a.y2 = y2.defined() ? y2.data_ptr() : nullptr;
+  a.Csplit = (int)Csplit;
+  a.xb1 = act_bwd ? xb1->data_ptr() : nullptr;
+  a.xb2 = (act_bwd && Csplit < Cout) ? xb2->data_ptr() : nullptr;
+  a.act_bwd = (int)act_bwd;
+  a.ws = nullptr;
+  a.splits = 1;
+
+  // ---- tile choice: N-tile from Cout, M-tile from the largest parity class
+  const int classes = mode == 0 ? 1 : (int)(stride * stride);
+  int64_t mmax = 0;
+  int64_t kmax = 0;
+  for (int c = 0; c < classes; ++c) {
+    int64_t hq = OH, wq = OW, taps = KH * KW;
+    if (mode == 1) {
+      const int ry = c / (int)stride, rx = c % (int)stride;
+      hq = OH > ry ? (OH - ry + stride - 1) / stride : 0;
+      wq = OW > rx ? (OW - rx + stride - 1) / stride : 0;
+      const int ky0 = (int)((ry + pad) % stride), kx0 = (int)((rx + pad) % stride);
+      const int64_t tj = ky0 < KH ? (KH - ky0 + stride - 1) / stride : 0;
+      const int64_t ti = kx0 < KW ? (KW - kx0 + stride - 1) / stride : 0;
+      taps = tj * ti;
+    }
+    mmax = std::max(mmax, N * hq * wq);
+    kmax = std::max(kmax, taps * C);
+  }
+  int bm, bn;
+  if (Cout <= 16) {
+    bn = 16;
+    bm = mmax >= 4096 ? 256 : 64;
+  } else if (Cout <= 32) {
+    bn = 32;
+    bm = 256;
+  } else if (Cout <= 64) {
+    bn = 64;
+    bm = mmax >= 8192 ? 128 : 64;
+  } else {
+    bn = 128;
+    bm = mmax >= 16384 ? 128 : 64;
+  }
+  const int64_t tiles = ((mmax + bm - 1) / bm) * ((Cout + bn - 1) / bn) * classes;
+  const int64_t ktiles = (kmax + 63) / 64;
+  int splits = 1;
+  if (tiles < 512 && ktiles >= 8) {
+    splits = (int)std::min<int64_t>((1024 + tiles - 1) / tiles, ktiles / 4);
+    splits = std::max(1, std::min(splits, 32));
+  }
+  Tensor ws;
+  hipStream_t st = cur_stream(x1);
+  if (splits > 1) {
+    ws = at::zeros({N * OH * OW, Cout}, x1.options().dtype(at::kFloat));
+    a.ws = ws.data_ptr<float>();
+    a.splits = splits;
+  }
+  check_rc(p2p_conv_fwd(&a, (int)mode, bm, bn, st), "conv_fwd");
+  if (splits > 1) check_rc(p2p_conv_finalize(&a, st), "conv_finalize");
+  std::vector<Tensor> out{y1};
+  if (y2.defined()) out.push_back(y2);
+  return out;
+}
+
+// ------------------------------------------------------------------ conv wgrad
+void conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, const Tensor& q1,
+                const optional<Tensor>& q2, int64_t q_act, int64_t KH, int64_t KW, int64_t stride,
+                int64_t pad, int64_t reflect, int64_t up, Tensor dw, double scale,
+                int64_t accumulate) {
+  check_act(p1, "conv_wgrad p1");
+  check_act(q1, "conv_wgrad q1");
+  const int64_t N = p1.size(0), OH = p1.size(2), OW = p1.size(3);
+  int64_t R2 = 0, C2 = 0;
+  if (p2) {
+    check_act(*p2, "conv_wgrad p2");
+    TORCH_CHECK(p2->size(0) == N && p2->size(2) == OH && p2->size(3) == OW, "wgrad p concat shape");
+    R2 = p2->size(1);
+  }
+  const int64_t H = q1.size(2), W = q1.size(3);
+  TORCH_CHECK(q1.size(0) == N, "conv_wgrad: batch mismatch");
+  if (q2) {
+    check_act(*q2, "conv_wgrad q2");
+    TORCH_CHECK(q2->size(0) == N && q2->size(2) == H && q2->size(3) == W, "wgrad q concat shape");
+    C2 = q2->size(1);
+  }
+  const int64_t R = p1.size(1) + R2, C = q1.size(1) + C2;
+  TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == at::kFloat && dw.is_contiguous() && dw.dim() == 4,
+              "conv_wgrad: dw must be contiguous fp32 [R][C][KH][KW]");
+  const int64_t Rr = dw.size(0), Cr = dw.size(1);
+  TORCH_CHECK(Rr <= R && Cr <= C && dw.size(2) == KH && dw.size(3) == KW, "conv_wgrad: dw shape");
+  // the conv geometry over q must produce the p grid
+  const int64_t Hu = H * up, Wu = W * up;
+  TORCH_CHECK((Hu + 2 * pad - KH) / stride + 1 == OH && (Wu + 2 * pad - KW) / stride + 1 == OW,
+              "conv_wgrad: geometry mismatch");
+  p2p::ConvWgradArgs a{};
+  a.p1 = p1.data_ptr();
+  a.p2 = p2 ? p2->data_ptr() : nullptr;
+  a.R1 = (int)p1.size(1);
+  a.R2 = (int)R2;
+  a.R = (int)R;
+  a.p_act = (int)p_act;
+  a.q1 = q1.data_ptr();
+  a.q2 = q2 ? q2->data_ptr() : nullptr;
+  a.C1 = (int)q1.size(1);
+  a.C2 = (int)C2;
+  a.C = (int)C;
+  a.N = (int)N;
+  a.H = (int)H;
+  a.W = (int)W;
+  a.up = (int)up;
+  a.KH = (int)KH;
+  a.KW = (int)KW;
+  a.stride = (int)stride;
+  a.pad = (int)pad;
+  a.reflect = (int)reflect;
+  a.q_act = (int)q_act;
+  a.OH = (int)OH;
+  a.OW = (int)OW;
+  a.M = (int)(N * OH * OW);
+  a.Kq = (int)(KH * KW * C);
+  const int wbr = p2p_conv_wgrad_tile_rows(a.R);
+  const int64_t tiles = ((R + wbr - 1) / wbr) * ((a.Kq + 127) / 128);
+  const int64_t stages = ((int64_t)a.M + 63) / 64;
+  int64_t splits = std::max<int64_t>(1, 1024 / std::max<int64_t>(tiles, 1));
+  splits = std::min<int64_t>(splits, std::max<int64_t>(1, stages / 8));
+  // bound the fp32 slab workspace to ~256 MB
+  const int64_t slab = R * (int64_t)a.Kq;
+  splits = std::max<int64_t>(1, std::min<int64_t>(splits, (64ll << 20) / std::max<int64_t>(slab, 1)));
+  a.splits = (int)splits;
+  Tensor ws = at::empty({splits * slab}, p1.options().dtype(at::kFloat));
+  a.ws = ws.data_ptr<float>();
+  hipStream_t st = cur_stream(p1);
+  check_rc(p2p_conv_wgrad(&a, st), "conv_wgrad");
+  check_rc(p2p_wgrad_reduce(a.ws, a.splits, a.R, a.KH, a.KW, a.C, (int)Rr, (int)Cr,
+                            dw.data_ptr<float>(), (float)scale, (int)accumulate, st),
+           "wgrad_reduce");
+}
+
+// ------------------------------------------------------------------ weight prep
+Tensor weight_prep(const Tensor& w, int64_t swap, int64_t Xp, int64_t Yp,
+                   const optional<Tensor>& scale) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.dim() == 4,
+              "weight_prep: fp32 contiguous 4-D weight");
+  const int64_t A = w.size(0), B = w.size(1), KH = w.size(2), KW = w.size(3);
+  TORCH_CHECK(Xp >= (swap ? B : A) && Yp >= (swap ? A : B), "weight_prep: padding too small");
+  Tensor out = at::empty({Xp, KH, KW, Yp}, w.options().dtype(at::kBFloat16));
+  check_rc(p2p_weight_prep(w.data_ptr<float>(), (int)A, (int)B, (int)KH, (int)KW, (int)swap, (int)Xp,
+                           (int)Yp, scale ? scale->data_ptr<float>() : nullptr, out.data_ptr(),
+                           cur_stream(w)),
+           "weight_prep");
+  return out;
+}
+
+// ------------------------------------------------------------------ norms
+// batch=false: instance norm (groups n x c); batch=true: batch norm (groups c)
+std::vector<Tensor> norm_fwd(const Tensor& x, double eps, const optional<Tensor>& gamma,
+                             const optional<Tensor>& beta, const optional<Tensor>& prelu_w,
+                             int64_t act, const optional<Tensor>& run_mean,
+                             const optional<Tensor>& run_var, double momentum, bool batch) {
+  check_act(x, "norm_fwd x");
+  const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  TORCH_CHECK(C <= 2048, "norm_fwd: C > 2048 unsupported");
+  const int gN = batch ? 1 : (int)N;
+  const int gHW = batch ? (int)(N * HW) : (int)HW;
+  Tensor mean = at::empty({gN, C}, x.options().dtype(at::kFloat));
+  Tensor rstd = at::empty({gN, C}, x.options().dtype(at::kFloat));
+  Tensor ws = at::empty({p2p_norm_ws_floats(gN, gHW, (int)C)}, x.options().dtype(at::kFloat));
+  Tensor y = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  check_rc(p2p_norm_fwd(x.data_ptr(), gN, gHW, (int)C, (float)eps,
+                        gamma ? gamma->data_ptr<float>() : nullptr,
+                        beta ? beta->data_ptr<float>() : nullptr,
+                        prelu_w ? prelu_w->data_ptr<float>() : nullptr, (int)act,
+                        mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                        run_mean ? run_mean->data_ptr<float>() : nullptr,
+                        run_var ? run_var->data_ptr<float>() : nullptr, (float)momentum,
+                        ws.data_ptr<float>(), y.data_ptr(), cur_stream(x)),
+           "norm_fwd");
+  return {y, mean, rstd};
+}
+
+Tensor norm_apply(const Tensor& x, const Tensor& mean, const Tensor& rstd,
+                  const optional<Tensor>& gamma, const optional<Tensor>& beta,
+                  const optional<Tensor>& prelu_w, int64_t act, bool batch) {
+  check_act(x, "norm_apply x");
+  const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  Tensor y = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  check_rc(p2p_norm_apply(x.data_ptr(), batch ? 1 : (int)N, batch ? (int)(N * HW) : (int)HW, (int)C,
+                          mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                          gamma ? gamma->data_ptr<float>() : nullptr,
+                          beta ? beta->data_ptr<float>() : nullptr,
+                          prelu_w ? prelu_w->data_ptr<float>() : nullptr, (int)act, y.data_ptr(),
+                          cur_stream(x)),
+           "norm_apply");
+  return y;
+}
+
+Tensor norm_bwd(const Tensor& x, const Tensor& dy, const Tensor& mean, const Tensor& rstd,
+                const optional<Tensor>& gamma, const optional<Tensor>& dgamma,
+                const optional<Tensor>& dbeta, bool need_dx, bool batch) {
+  check_act(x, "norm_bwd x");
+  check_act(dy, "norm_bwd dy");
+  const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  const int gN = batch ? 1 : (int)N;
+  const int gHW = batch ? (int)(N * HW) : (int)HW;
+  Tensor ws = at::empty({p2p_norm_ws_floats(gN, gHW, (int)C)}, x.options().dtype(at::kFloat));
+  Tensor dx;
+  if (need_dx) dx = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  check_rc(p2p_norm_bwd(x.data_ptr(), dy.data_ptr(), gN, gHW, (int)C, mean.data_ptr<float>(),
+                        rstd.data_ptr<float>(), gamma ? gamma->data_ptr<float>() : nullptr,
+                        dgamma ? dgamma->data_ptr<float>() : nullptr,
+                        dbeta ? dbeta->data_ptr<float>() : nullptr, ws.data_ptr<float>(),
+                        need_dx ? dx.data_ptr() : nullptr, cur_stream(x)),
+           "norm_bwd");
+  return dx;
+}
+
+// ------------------------------------------------------------------ elementwise
+Tensor act(const Tensor& a, const optional<Tensor>& b, int64_t act, int64_t mode) {
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16, "act: bf16 GPU tensor");
+  TORCH_CHECK(a.numel() % 8 == 0, "act: numel % 8");
+  const auto mf = a.is_contiguous(at::MemoryFormat::ChannelsLast) && a.dim() == 4
+                      ? at::MemoryFormat::ChannelsLast
+                      : at::MemoryFormat::Contiguous;
+  TORCH_CHECK(a.is_contiguous(mf), "act: dense input");
+  if (b) TORCH_CHECK(b->is_contiguous(mf) && b->sizes() == a.sizes(), "act: b layout");
+  Tensor out = at::empty_like(a, a.options().memory_format(mf));
+  check_rc(p2p_act(a.data_ptr(), b ? b->data_ptr() : nullptr, a.numel(), (int)act, (int)mode,
+                   out.data_ptr(), cur_stream(a)),
+           "act");
+  return out;
+}
+
+Tensor dropout(const Tensor& x, double p, const Tensor& seed, int64_t salt) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.numel() % 8 == 0, "dropout: x");
+  TORCH_CHECK(seed.scalar_type() == at::kLong && seed.is_cuda(), "dropout: seed must be a GPU int64");
+  const auto mf = x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast)
+                      ? at::MemoryFormat::ChannelsLast
+                      : at::MemoryFormat::Contiguous;
+  TORCH_CHECK(x.is_contiguous(mf), "dropout: dense input");
+  Tensor y = at::empty_like(x, x.options().memory_format(mf));
+  check_rc(p2p_dropout(x.data_ptr(), x.numel(), (float)p, seed.data_ptr<int64_t>(), (unsigned)salt,
+                       y.data_ptr(), cur_stream(x)),
+           "dropout");
+  return y;
+}
+
+// pad_channels: NHWC a (Ca) [+ b (Cb)] -> Co channels, zero filled
+Tensor pad_channels(const Tensor& a, const optional<Tensor>& b, int64_t Co) {
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && a.dim() == 4, "pad_channels: a");
+  Tensor ac = a.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor bc;
+  int64_t Cb = 0;
+  if (b) {
+    bc = b->contiguous(at::MemoryFormat::ChannelsLast);
+    Cb = bc.size(1);
+  }
+  TORCH_CHECK(ac.size(1) + Cb <= Co, "pad_channels: Co too small");
+  Tensor out = empty_nhwc(a.size(0), Co, a.size(2), a.size(3), a);
+  check_rc(p2p_pad_channels(ac.data_ptr(), (int)ac.size(1), bc.defined() ? bc.data_ptr() : nullptr,
+                            (int)Cb, a.size(0) * a.size(2) * a.size(3), (int)Co, out.data_ptr(),
+                            cur_stream(a)),
+           "pad_channels");
+  return out;
+}
+
+Tensor slice_channels(const Tensor& x, int64_t c0, int64_t C) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4, "slice_channels: x");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "slice_channels: NHWC input");
+  TORCH_CHECK(c0 + C <= x.size(1), "slice_channels: range");
+  Tensor out = empty_nhwc(x.size(0), C, x.size(2), x.size(3), x);
+  check_rc(p2p_slice_channels(x.data_ptr(), (int)x.size(1), (int)c0, x.size(0) * x.size(2) * x.size(3),
+                              (int)C, out.data_ptr(), cur_stream(x)),
+           "slice_channels");
+  return out;
+}
+
+// out[c] (+)= scale * sum over all pixels of x[..., c]   (bias gradient)
+void colsum(const Tensor& x, Tensor out, double scale, bool accumulate) {
+  check_act(x, "colsum x");
+  const int64_t C = x.size(1), M = x.numel() / C;
+  TORCH_CHECK(C <= 2048, "colsum: C > 2048");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.numel() <= C && out.is_contiguous(),
+              "colsum: out");
+  const int nb = p2p_colsum_blocks(M, (int)C);
+  Tensor ws = at::empty({(int64_t)nb * C}, x.options().dtype(at::kFloat));
+  if (out.numel() == C) {
+    check_rc(p2p_colsum(x.data_ptr(), M, (int)C, (float)scale, accumulate ? 1 : 0, ws.data_ptr<float>(),
+                        out.data_ptr<float>(), cur_stream(x)),
+             "colsum");
+  } else {  // padded channels: reduce all, keep the leading out.numel()
+    Tensor full = at::empty({C}, x.options().dtype(at::kFloat));
+    check_rc(p2p_colsum(x.data_ptr(), M, (int)C, (float)scale, 0, ws.data_ptr<float>(),
+                        full.data_ptr<float>(), cur_stream(x)),
+             "colsum");
+    if (accumulate) out.add_(full.narrow(0, 0, out.numel()));
+    else out.copy_(full.narrow(0, 0, out.numel()));
+  }
+}
+
+// ------------------------------------------------------------------ losses
+Tensor loss_fwd(const Tensor& a, const optional<Tensor>& b, int64_t kind, double t, double scale) {
+  TORCH_CHECK(a.is_cuda() && (a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kFloat),
+              "loss_fwd: a");
+  TORCH_CHECK(a.is_contiguous() || a.is_contiguous(at::MemoryFormat::ChannelsLast), "loss_fwd: dense a");
+  if (b) {
+    TORCH_CHECK(b->scalar_type() == a.scalar_type() && b->sizes() == a.sizes() &&
+                    b->strides() == a.strides(), "loss_fwd: b must match a");
+  }
+  const int nb = p2p_loss_blocks(a.numel());
+  Tensor ws = at::empty({nb}, a.options().dtype(at::kFloat));
+  Tensor out = at::empty({}, a.options().dtype(at::kFloat));
+  check_rc(p2p_loss_fwd(a.data_ptr(), b ? b->data_ptr() : nullptr, a.scalar_type() == at::kFloat,
+                        a.numel(), (int)kind, (float)t, (float)scale, ws.data_ptr<float>(),
+                        out.data_ptr<float>(), cur_stream(a)),
+           "loss_fwd");
+  return out;
+}
+
+std::vector<Tensor> loss_bwd(const Tensor& a, const optional<Tensor>& b, int64_t kind, double t,
+                             double scale, const Tensor& gout, bool need_a, bool need_b) {
+  TORCH_CHECK(gout.scalar_type() == at::kFloat && gout.numel() == 1, "loss_bwd: gout");
+  Tensor gout_c = gout.contiguous();
+  Tensor ga, gb;
+  if (need_a) ga = at::empty_like(a);
+  if (need_b) gb = at::empty_like(a);
+  check_rc(p2p_loss_bwd(a.data_ptr(), b ? b->data_ptr() : nullptr, a.scalar_type() == at::kFloat,
+                        a.numel(), (int)kind, (float)t, (float)scale, gout_c.data_ptr<float>(),
+                        need_a ? ga.data_ptr() : nullptr, need_b ? gb.data_ptr() : nullptr,
+                        cur_stream(a)),
+           "loss_bwd");
+  return {ga, gb};
+}
+
+// ------------------------------------------------------------------ optimizer
+void adam(at::TensorList p, at::TensorList g, at::TensorList m, at::TensorList v, const Tensor& lr,
+          const Tensor& step, double b1, double b2, double eps, double wd) {
+  const size_t n = p.size();
+  TORCH_CHECK(g.size() == n && m.size() == n && v.size() == n, "adam: list sizes");
+  TORCH_CHECK(lr.scalar_type() == at::kFloat && step.scalar_type() == at::kFloat, "adam: lr/step fp32");
+  const int maxT = p2p_adam_max_tensors();
+  std::vector<float*> P, M, V;
+  std::vector<const float*> G;
+  std::vector<long> Nn;
+  hipStream_t st = n ? cur_stream(p[0]) : nullptr;
+  auto flush = [&]() {
+    if (P.empty()) return;
+    check_rc(p2p_adam((int)P.size(), P.data(), G.data(), M.data(), V.data(), Nn.data(),
+                      lr.data_ptr<float>(), step.data_ptr<float>(), (float)b1, (float)b2, (float)eps,
+                      (float)wd, st),
+             "adam");
+    P.clear(); G.clear(); M.clear(); V.clear(); Nn.clear();
+  };
+  for (size_t i = 0; i < n; ++i) {
+    TORCH_CHECK(p[i].scalar_type() == at::kFloat && p[i].is_contiguous() && g[i].is_contiguous() &&
+                    m[i].is_contiguous() && v[i].is_contiguous() && g[i].scalar_type() == at::kFloat,
+                "adam: fp32 contiguous tensors");
+    TORCH_CHECK(p[i].numel() == g[i].numel() && p[i].numel() < (1ll << 31), "adam: sizes");
+    P.push_back(p[i].data_ptr<float>());
+    G.push_back(g[i].data_ptr<float>());
+    M.push_back(m[i].data_ptr<float>());
+    V.push_back(v[i].data_ptr<float>());
+    Nn.push_back((long)p[i].numel());
+    if ((int)P.size() == maxT) flush();
+  }
+  flush();
+}
+
+}  // namespace
+
+TORCH_LIBRARY(p2p, m) {
+  m.def("conv_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, int mode, int KH, int KW, int stride, "
+        "int pad, int reflect, int up, int act_in, int OH, int OW, int Cout, int act_out, int Csplit, "
+        "Tensor? xb1, Tensor? xb2, int act_bwd) -> Tensor[]");
+  m.def("conv_wgrad(Tensor p1, Tensor? p2, int p_act, Tensor q1, Tensor? q2, int q_act, int KH, int KW, "
+        "int stride, int pad, int reflect, int up, Tensor(a!) dw, float scale, int accumulate) -> ()");
+  m.def("weight_prep(Tensor w, int swap, int Xp, int Yp, Tensor? scale) -> Tensor");
+  m.def("norm_fwd(Tensor x, float eps, Tensor? gamma, Tensor? beta, Tensor? prelu_w, int act, "
+        "Tensor(a!)? run_mean, Tensor(b!)? run_var, float momentum, bool batch) -> Tensor[]");
+  m.def("norm_apply(Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? prelu_w, "
+        "int act, bool batch) -> Tensor");
+  m.def("norm_bwd(Tensor x, Tensor dy, Tensor mean, Tensor rstd, Tensor? gamma, Tensor(a!)? dgamma, "
+        "Tensor(b!)? dbeta, bool need_dx, bool batch) -> Tensor");
+  m.def("act(Tensor a, Tensor? b, int act, int mode) -> Tensor");
+  m.def("dropout(Tensor x, float p, Tensor seed, int salt) -> Tensor");
+  m.def("pad_channels(Tensor a, Tensor? b, int Co) -> Tensor");
+  m.def("slice_channels(Tensor x, int c0, int C) -> Tensor");
+  m.def("colsum(Tensor x, Tensor(a!) out, float scale, bool accumulate) -> ()");
+  m.def("loss_fwd(Tensor a, Tensor? b, int kind, float t, float scale) -> Tensor");
+  m.def("loss_bwd(Tensor a, Tensor? b, int kind, float t, float scale, Tensor gout, bool need_a, "
+        "bool need_b) -> Tensor[]");
+  m.def("adam(Tensor(a!)[] p, Tensor[] g, Tensor(b!)[] m, Tensor(c!)[] v, Tensor lr, Tensor step, "
+        "float b1, float b2, float eps, float wd) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
+  m.impl("conv_fwd", conv_fwd);
+  m.impl("conv_wgrad", conv_wgrad);
+  m.impl("weight_prep", weight_prep);
+  m.impl("norm_fwd", norm_fwd);
+  m.impl("norm_apply", norm_apply);
+  m.impl("norm_bwd", norm_bwd);
+  m.impl("act", act);
+  m.impl("dropout", dropout);
+  m.impl("pad_channels", pad_channels);
+  m.impl("slice_channels", slice_channels);
+  m.impl("colsum", colsum);
+  m.impl("loss_fwd", loss_fwd);
+  m.impl("loss_bwd", loss_bwd);
+  m.impl("adam", adam);
+}

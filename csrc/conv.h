@@ -60,6 +60,9 @@ extern "C" {
 int p2p_conv_fwd(const p2p::ConvFwdArgs* a, int mode, int bm, int bn, hipStream_t stream);
 int p2p_conv_finalize(const p2p::ConvFwdArgs* a, hipStream_t stream);
 int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t stream);
-int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int KW, int C, float* dw,
-                     int layout, float scale, int accumulate, hipStream_t stream);
+int p2p_conv_wgrad_tile_rows(int R);
+int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int KW, int C, int Rr, int Cr,
+                     float* dw, float scale, int accumulate, hipStream_t stream);
+int p2p_weight_prep(const float* w, int A, int B, int KH, int KW, int swap, int Xp, int Yp,
+                    const float* scale, void* out, hipStream_t stream);
 }

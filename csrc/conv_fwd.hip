@@ -364,7 +364,7 @@ static int launch_fwd(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = FwdSmem<BM, BN>::bytes;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_fwd_kernel<BM, BN, WM, WN, MODE>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_fwd_kernel<BM, BN, WM, WN, MODE>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
@@ -416,5 +416,43 @@ extern "C" int p2p_conv_finalize(const p2p::ConvFwdArgs* a, hipStream_t st) {
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(p2p::conv_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, st, *a, P);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Weight preparation: fp32 master weight [A][B][KH][KW] (PyTorch Conv2d: [Cout][Cin][..],
+// ConvTranspose2d: [Cin][Cout][..]) -> bf16 GEMM operand [X][KH][KW][Yp] with X = A, Y = B
+// (swap = 0) or X = B, Y = A (swap = 1), zero-padded to Xp rows / Yp channels, optionally
+// scaled by a device scalar (1/sigma of spectral norm).  The four operand images:
+//   conv fwd   swap 0    conv dgrad (CONVT mode on dY)   swap 1
+//   convT fwd  swap 1    convT dgrad (CONV mode on dY)   swap 0
+namespace p2p {
+__global__ void __launch_bounds__(256) weight_prep_kernel(const float* __restrict__ w, int A, int B,
+                                                          int KH, int KW, int swap, int Xp, int Yp,
+                                                          const float* __restrict__ scale,
+                                                          bf16* __restrict__ out) {
+  const int T = KH * KW;
+  const long total = (long)Xp * T * Yp;
+  const float s = scale ? scale[0] : 1.f;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int y = (int)(e % Yp);
+    const long r = e / Yp;
+    const int t = (int)(r % T);
+    const int x = (int)(r / T);
+    const int a = swap ? y : x, b = swap ? x : y;
+    float v = 0.f;
+    if (a < A && b < B) v = w[((long)a * B + b) * T + t] * s;
+    out[e] = (bf16)v;
+  }
+}
+}  // namespace p2p
+
+extern "C" int p2p_weight_prep(const float* w, int A, int B, int KH, int KW, int swap, int Xp, int Yp,
+                               const float* scale, void* out, hipStream_t st) {
+  const long total = (long)Xp * KH * KW * Yp;
+  long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(p2p::weight_prep_kernel, dim3((unsigned)blocks), dim3(256), 0, st, w, A, B, KH, KW,
+                     swap, Xp, Yp, scale, static_cast<p2p::bf16*>(out));
   return (int)hipGetLastError();
 }

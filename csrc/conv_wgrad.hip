@@ -22,7 +22,6 @@
 
 namespace p2p {
 
-constexpr int WBR = 128;   // tile rows (R)
 constexpr int WBQ = 128;   // tile cols (Kq)
 constexpr int WBM = 64;    // reduction rows per stage
 constexpr int WROW = 128;  // elements per LDS row
@@ -55,18 +54,23 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* tile, int kbase, int cbase
   return __builtin_bit_cast(bf16x8, v);
 }
 
+template <int TBR, int WM, int WN>
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
-  constexpr int TM = 4, TN = 4;  // 2x2 waves, 64x64 per wave
+  // TBR = tile rows over R (128 / 64 / 16); the Kq tile is always WBQ = 128 wide.
+  static_assert(WM * WN == 4, "4 waves");
+  constexpr int TM = TBR / WM / 16, TN = WBQ / WN / 16;
+  constexpr int CPR_P = TBR / 8;                       // 16-B chunks per P row
+  constexpr int PL = (WBM * CPR_P + 255) / 256;        // P chunks loaded per thread per stage
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* Ps = reinterpret_cast<bf16*>(smem);      // [2][WBM][128]
+  bf16* Ps = reinterpret_cast<bf16*>(smem);      // [2][WBM][128] (first TBR columns used)
   bf16* Qs = Ps + 2 * WBM * WROW;                // [2][WBM][128]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
   const int qtiles = (a.Kq + WBQ - 1) / WBQ;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int rt = bid / qtiles, qt = bid % qtiles;
-  const int r0 = rt * WBR, q0 = qt * WBQ;
+  const int r0 = rt * TBR, q0 = qt * WBQ;
 
   const int stages = (a.M + WBM - 1) / WBM;
   const int sps = (stages + a.splits - 1) / a.splits;
@@ -78,16 +82,19 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
   const bf16* __restrict__ q1 = static_cast<const bf16*>(a.q1);
   const bf16* __restrict__ q2 = static_cast<const bf16*>(a.q2);
 
-  const int ck = tid & 15;          // this thread's 16-B chunk (of 16 per 256-B row)
-  const int rrow = tid >> 4;        // base row; rows rrow + 16*i
-  // P chunk decode (fixed): channel range r0 + 8*ck
-  const int pr = r0 + ck * 8;
+  // P chunk decode: chunk id c = tid + 256*i -> (row c / CPR_P, chunk c % CPR_P)
+  const int pck = tid % CPR_P;
+  const int prow0 = tid / CPR_P;
+  constexpr int PROWS_PER_PASS = 256 / CPR_P;
+  const int pr = r0 + pck * 8;
   const bool p_ok = pr < a.R;
   const bool p_first = pr < a.R1;
   const bf16* psrc = p_first ? p1 : p2;
   const int pld = p_first ? a.R1 : a.R2;
   const int pro = p_first ? pr : pr - a.R1;
   // Q chunk decode (fixed): kq = q0 + 8*ck -> tap, ci
+  const int ck = tid & 15;          // this thread's 16-B chunk (of 16 per 256-B row)
+  const int rrow = tid >> 4;        // base row; rows rrow + 16*i
   const int kq = q0 + ck * 8;
   const bool q_ok = kq < a.Kq;
   int tap = 0, ci = 0;
@@ -104,40 +111,44 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
   const int Hu = a.H << ush, Wu = a.W << ush;
   const int OHW = a.OH * a.OW;
 
-  u32x4 rp[4], rq[4];
+  u32x4 rp[PL], rq[4];
   auto load_stage = [&](int st) {
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+      const int row = prow0 + PROWS_PER_PASS * i;
+      const int m = st * WBM + row;
+      u32x4 vp = zero_u32x4();
+      if (row < WBM && m < a.M && p_ok) {
+        vp = *reinterpret_cast<const u32x4*>(psrc + (long)m * pld + pro);
+        vp = act8(vp, a.p_act);
+      }
+      rp[i] = vp;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = st * WBM + rrow + 16 * i;
-      u32x4 vp = zero_u32x4(), vq = zero_u32x4();
-      if (m < a.M) {
-        if (p_ok) {
-          vp = *reinterpret_cast<const u32x4*>(psrc + (long)m * pld + pro);
-          vp = act8(vp, a.p_act);
+      u32x4 vq = zero_u32x4();
+      if (m < a.M && q_ok) {
+        const int n = m / OHW;
+        const int rem = m - n * OHW;
+        const int oh = rem / a.OW;
+        const int ow = rem - oh * a.OW;
+        int uy = oh * a.stride - a.pad + kh;
+        int ux = ow * a.stride - a.pad + kw;
+        bool inb;
+        if (a.reflect) {
+          uy = reflect_idx(uy, Hu);
+          ux = reflect_idx(ux, Wu);
+          inb = true;
+        } else {
+          inb = (unsigned)uy < (unsigned)Hu && (unsigned)ux < (unsigned)Wu;
         }
-        if (q_ok) {
-          const int n = m / OHW;
-          const int rem = m - n * OHW;
-          const int oh = rem / a.OW;
-          const int ow = rem - oh * a.OW;
-          int uy = oh * a.stride - a.pad + kh;
-          int ux = ow * a.stride - a.pad + kw;
-          bool inb;
-          if (a.reflect) {
-            uy = reflect_idx(uy, Hu);
-            ux = reflect_idx(ux, Wu);
-            inb = true;
-          } else {
-            inb = (unsigned)uy < (unsigned)Hu && (unsigned)ux < (unsigned)Wu;
-          }
-          if (inb) {
-            const long pix = ((long)n * a.H + (uy >> ush)) * a.W + (ux >> ush);
-            vq = *reinterpret_cast<const u32x4*>(qsrc + pix * qld + qco);
-            vq = act8(vq, a.q_act);
-          }
+        if (inb) {
+          const long pix = ((long)n * a.H + (uy >> ush)) * a.W + (ux >> ush);
+          vq = *reinterpret_cast<const u32x4*>(qsrc + pix * qld + qco);
+          vq = act8(vq, a.q_act);
         }
       }
-      rp[i] = vp;
       rq[i] = vq;
     }
   };
@@ -145,9 +156,13 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
     bf16* P = Ps + buf * WBM * WROW;
     bf16* Q = Qs + buf * WBM * WROW;
 #pragma unroll
+    for (int i = 0; i < PL; ++i) {
+      const int row = prow0 + PROWS_PER_PASS * i;
+      if (row < WBM) *reinterpret_cast<u32x4*>(P + swz_t(row, pck)) = rp[i];
+    }
+#pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = rrow + 16 * i;
-      *reinterpret_cast<u32x4*>(P + swz_t(row, ck)) = rp[i];
       *reinterpret_cast<u32x4*>(Q + swz_t(row, ck)) = rq[i];
     }
   };
@@ -173,9 +188,9 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = tr_frag(P, kk * 32, wm * 64 + i * 16, lane);
+      for (int i = 0; i < TM; ++i) af[i] = tr_frag(P, kk * 32, wm * (TBR / WM) + i * 16, lane);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = tr_frag(Q, kk * 32, wn * 64 + j * 16, lane);
+      for (int j = 0; j < TN; ++j) bfr[j] = tr_frag(Q, kk * 32, wn * (WBQ / WN) + j * 16, lane);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -193,8 +208,8 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int col = q0 + wn * 64 + j * 16 + (lane & 15);
-      const int rowb = r0 + wm * 64 + i * 16 + (lane >> 4) * 4;
+      const int col = q0 + wn * (WBQ / WN) + j * 16 + (lane & 15);
+      const int rowb = r0 + wm * (TBR / WM) + i * 16 + (lane >> 4) * 4;
       if (col < a.Kq) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -205,9 +220,9 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
 
 // dw[r][ci][kh][kw] (+)= scale * sum_s ws[s][r][(kh*KW+kw)*C + ci]
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, int splits,
-                                                           int R, int KH, int KW, int C,
-                                                           float* __restrict__ dw, float scale,
-                                                           int accumulate) {
+                                                           int R, int KH, int KW, int C, int Rr,
+                                                           int Cr, float* __restrict__ dw,
+                                                           float scale, int accumulate) {
   const int Kq = KH * KW * C;
   const long total = (long)R * Kq;
   for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
@@ -218,29 +233,38 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     const int kq = (int)(e - (long)r * Kq);
     const int tap = kq / C;
     const int ci = kq - tap * C;
-    const long o = ((long)r * C + ci) * KH * KW + tap;
+    if (r >= Rr || ci >= Cr) continue;  // padded rows / channels of the GEMM view
+    const long o = ((long)r * Cr + ci) * KH * KW + tap;
     dw[o] = accumulate ? dw[o] + s : s;
   }
 }
 
 }  // namespace p2p
 
+extern "C" int p2p_conv_wgrad_tile_rows(int R) { return R <= 16 ? 16 : (R <= 64 ? 64 : 128); }
+
 extern "C" int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t st) {
-  constexpr int smem = 2 * 2 * p2p::WBM * p2p::WROW * 2;  // 64 KB
-  const int rtiles = (a->R + p2p::WBR - 1) / p2p::WBR;
-  const int qtiles = (a->Kq + p2p::WBQ - 1) / p2p::WBQ;
+  using namespace p2p;
+  constexpr int smem = 2 * 2 * WBM * WROW * 2;  // 64 KB
+  const int tbr = p2p_conv_wgrad_tile_rows(a->R);
+  const int rtiles = (a->R + tbr - 1) / tbr;
+  const int qtiles = (a->Kq + WBQ - 1) / WBQ;
   dim3 grid(rtiles * qtiles, a->splits, 1);
-  hipLaunchKernelGGL(p2p::conv_wgrad_kernel, grid, dim3(256), smem, st, *a);
+  if (tbr == 128)
+    hipLaunchKernelGGL((conv_wgrad_kernel<128, 2, 2>), grid, dim3(256), smem, st, *a);
+  else if (tbr == 64)
+    hipLaunchKernelGGL((conv_wgrad_kernel<64, 2, 2>), grid, dim3(256), smem, st, *a);
+  else
+    hipLaunchKernelGGL((conv_wgrad_kernel<16, 1, 4>), grid, dim3(256), smem, st, *a);
   return (int)hipGetLastError();
 }
 
-extern "C" int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int KW, int C, float* dw,
-                                int layout, float scale, int accumulate, hipStream_t st) {
-  (void)layout;
+extern "C" int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int KW, int C, int Rr,
+                                int Cr, float* dw, float scale, int accumulate, hipStream_t st) {
   const long total = (long)R * KH * KW * C;
   long blocks = (total + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(p2p::wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, ws, splits,
-                     R, KH, KW, C, dw, scale, accumulate);
+                     R, KH, KW, C, Rr, Cr, dw, scale, accumulate);
   return (int)hipGetLastError();
 }

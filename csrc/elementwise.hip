@@ -1,0 +1,318 @@
+// Memory-bound helpers on bf16 NHWC tensors (gfx950): activations and their backward,
+// counter-hash dropout, channel pad / slice (for C % 8 != 0 image tensors at the network
+// fringe), per-channel column sums (bias gradients) and the fused GAN / reconstruction
+// losses (forward value and input gradient, no target tensor ever materialised).
+//
+// Every vector path moves 16 B per lane (bf16x8) -- hipcc does not vectorise bf16.
+// Reductions are two-stage (fixed-order block partials -> one finishing block), so every
+// loss and bias gradient is bitwise reproducible run to run.
+#include "common.h"
+
+namespace p2p {
+
+__device__ __forceinline__ void unpack8e(u32x4 v, float* f) {
+  bf16x8 b = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = (float)b[j];
+}
+
+__device__ __forceinline__ u32x4 pack8e(const float* f) {
+  bf16x8 b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b[j] = (bf16)f[j];
+  return __builtin_bit_cast(u32x4, b);
+}
+
+static inline unsigned egrid(long work) {
+  long b = (work + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+// y = act(x)                                           mode 0
+// dx = dy * act'(x)   (relu / lrelu, from the input)    mode 1
+// dx = dy * act'(y)   (tanh / sigmoid / relu, from the output)  mode 2
+__global__ void __launch_bounds__(256) act_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b,
+                                                  long n8, int act, int mode, bf16* __restrict__ out) {
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n8; e += (long)gridDim.x * 256) {
+    float fa[8], fb[8];
+    unpack8e(*reinterpret_cast<const u32x4*>(a + e * 8), fa);
+    if (mode != 0) unpack8e(*reinterpret_cast<const u32x4*>(b + e * 8), fb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (mode == 0) fa[j] = act_fwd(fa[j], act);
+      else if (mode == 1) fa[j] = fa[j] * act_grad_from_input(fb[j], act);
+      else fa[j] = fa[j] * act_grad_from_output(fb[j], act);
+    }
+    *reinterpret_cast<u32x4*>(out + e * 8) = pack8e(fa);
+  }
+}
+
+// counter-based hash (PCG output permutation over a 32-bit state)
+__device__ __forceinline__ uint32_t hash32(uint32_t v) {
+  uint32_t s = v * 747796405u + 2891336453u;
+  uint32_t w = ((s >> ((s >> 28u) + 4u)) ^ s) * 277803737u;
+  return (w >> 22u) ^ w;
+}
+
+// keep(i) = hash(seed, salt, i) >= p ; y = keep ? x / (1-p) : 0.  Same call with dy gives dx.
+// seed is read from device memory so a captured hipGraph draws a new mask every replay.
+__global__ void __launch_bounds__(256) dropout_kernel(const bf16* __restrict__ x, long n8, float p,
+                                                      const int64_t* __restrict__ seed, uint32_t salt,
+                                                      bf16* __restrict__ y) {
+  const uint32_t s0 = hash32((uint32_t)seed[0] ^ hash32(salt * 0x9E3779B9u + 0x7F4A7C15u));
+  const float scale = 1.f / (1.f - p);
+  const uint32_t thr = (uint32_t)(p * 4294967296.0);
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n8; e += (long)gridDim.x * 256) {
+    float f[8];
+    unpack8e(*reinterpret_cast<const u32x4*>(x + e * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t h = hash32(s0 ^ hash32((uint32_t)(e * 8 + j)));
+      f[j] = h >= thr ? f[j] * scale : 0.f;
+    }
+    *reinterpret_cast<u32x4*>(y + e * 8) = pack8e(f);
+  }
+}
+
+// out[p][0:Ca] = a[p][:], out[p][Ca:Ca+Cb] = b[p][:], out[p][Ca+Cb:Co] = 0   (NHWC, any C)
+__global__ void __launch_bounds__(256) pad_channels_kernel(const bf16* __restrict__ a, int Ca,
+                                                           const bf16* __restrict__ b, int Cb,
+                                                           long P, int Co, bf16* __restrict__ out) {
+  const long total = P * Co;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long p = e / Co;
+    const int c = (int)(e - p * Co);
+    bf16 v = (bf16)0.f;
+    if (c < Ca) v = a[p * Ca + c];
+    else if (c < Ca + Cb) v = b[p * Cb + (c - Ca)];
+    out[e] = v;
+  }
+}
+
+// out[p][0:C] = in[p][c0:c0+C]   (in has Ci channels)
+__global__ void __launch_bounds__(256) slice_channels_kernel(const bf16* __restrict__ in, int Ci, int c0,
+                                                             long P, int C, bf16* __restrict__ out) {
+  const long total = P * C;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long p = e / C;
+    const int c = (int)(e - p * C);
+    out[e] = in[p * Ci + c0 + c];
+  }
+}
+
+// partial column sums of a [M][C] bf16 matrix: ws[block][C]  (C % 8 == 0, C <= 2048)
+__global__ void __launch_bounds__(256) colsum_partial_kernel(const bf16* __restrict__ x, long M, int C,
+                                                             long rows_per_block, float* __restrict__ ws) {
+  const int CP = C >> 3;
+  const int RP = 256 / CP;
+  const int tid = threadIdx.x, cg = tid % CP, tr = tid / CP;
+  const long m0 = blockIdx.x * rows_per_block;
+  const long m1 = min(M, m0 + rows_per_block);
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  if (tr < RP) {
+    for (long m = m0 + tr; m < m1; m += RP) {
+      float f[8];
+      unpack8e(*reinterpret_cast<const u32x4*>(x + m * C + cg * 8), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += f[j];
+    }
+  }
+  __shared__ float red[2048];
+  const int rows_red = 2048 / C;
+  for (int base_r = 0; base_r < RP; base_r += rows_red) {
+    if (tr >= base_r && tr < base_r + rows_red && tr < RP) {
+      const int r = tr - base_r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (base_r == 0) red[r * C + cg * 8 + j] = s[j];
+        else red[r * C + cg * 8 + j] += s[j];
+      }
+    }
+    __syncthreads();
+  }
+  const int rr = min(RP, rows_red);
+  for (int c = tid; c < C; c += 256) {
+    float a = 0.f;
+    for (int r = 0; r < rr; ++r) a += red[r * C + c];
+    ws[(long)blockIdx.x * C + c] = a;
+  }
+}
+
+// out[c] (+)= scale * sum_b ws[b][c]
+__global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restrict__ ws, int nb, int C,
+                                                           float scale, int accumulate,
+                                                           float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f;
+  for (int b = 0; b < nb; ++b) a += ws[(long)b * C + c];
+  a *= scale;
+  out[c] = accumulate ? out[c] + a : a;
+}
+
+// ---------------------------------------------------------------- losses
+// kinds: 0 = mse vs const t, 1 = bce-with-logits vs const t, 2 = bce(prob) vs const t,
+//        3 = l1(a, b), 4 = mse(a, b), 5 = mean(a)
+__device__ __forceinline__ float loss_elem(int kind, float a, float b, float t) {
+  switch (kind) {
+    case 0: { const float d = a - t; return d * d; }
+    case 1: return fmaxf(a, 0.f) - a * t + log1pf(__expf(-fabsf(a)));
+    case 2: {
+      const float lp = fmaxf(logf(a), -100.f), lq = fmaxf(logf(1.f - a), -100.f);
+      return -(t * lp + (1.f - t) * lq);
+    }
+    case 3: return fabsf(a - b);
+    case 4: { const float d = a - b; return d * d; }
+    default: return a;
+  }
+}
+
+__device__ __forceinline__ float loss_grad(int kind, float a, float b, float t) {
+  switch (kind) {
+    case 0: return 2.f * (a - t);
+    case 1: return 1.f / (1.f + __expf(-a)) - t;
+    case 2: {
+      const float den = fmaxf(a * (1.f - a), 1e-12f);
+      return (a - t) / den;
+    }
+    case 3: { const float d = a - b; return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); }
+    case 4: return 2.f * (a - b);
+    default: return 1.f;
+  }
+}
+
+__device__ __forceinline__ float ldval(const void* p, long i, int is_f32) {
+  return is_f32 ? static_cast<const float*>(p)[i] : (float)static_cast<const bf16*>(p)[i];
+}
+
+// partial sums of loss_elem over [0, n): one float per block
+__global__ void __launch_bounds__(256) loss_partial_kernel(const void* __restrict__ a,
+                                                           const void* __restrict__ b, int is_f32,
+                                                           long n, int kind, float t,
+                                                           float* __restrict__ ws) {
+  float s = 0.f;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256)
+    s += loss_elem(kind, ldval(a, e, is_f32), b ? ldval(b, e, is_f32) : 0.f, t);
+  __shared__ float red[4];
+  s = warp_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) ws[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void __launch_bounds__(256) loss_final_kernel(const float* __restrict__ ws, int nb,
+                                                         float scale, float* __restrict__ out) {
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 256) s += ws[i];
+  __shared__ float red[4];
+  s = warp_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = (red[0] + red[1] + red[2] + red[3]) * scale;
+}
+
+// ga = gout * scale * dloss/da (bf16 or fp32 like a); gb = -ga (l1 / mse pairs) if requested
+__global__ void __launch_bounds__(256) loss_grad_kernel(const void* __restrict__ a,
+                                                        const void* __restrict__ b, int is_f32, long n,
+                                                        int kind, float t, float scale,
+                                                        const float* __restrict__ gout,
+                                                        void* __restrict__ ga, void* __restrict__ gb) {
+  const float g = gout[0] * scale;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const float v = g * loss_grad(kind, ldval(a, e, is_f32), b ? ldval(b, e, is_f32) : 0.f, t);
+    if (ga) {
+      if (is_f32) static_cast<float*>(ga)[e] = v;
+      else static_cast<bf16*>(ga)[e] = (bf16)v;
+    }
+    if (gb) {
+      if (is_f32) static_cast<float*>(gb)[e] = -v;
+      else static_cast<bf16*>(gb)[e] = (bf16)(-v);
+    }
+  }
+}
+
+}  // namespace p2p
+
+extern "C" {
+
+int p2p_act(const void* a, const void* b, long n, int act, int mode, void* out, hipStream_t st) {
+  using namespace p2p;
+  hipLaunchKernelGGL(act_kernel, dim3(egrid(n / 8)), dim3(256), 0, st, static_cast<const bf16*>(a),
+                     static_cast<const bf16*>(b), n / 8, act, mode, static_cast<bf16*>(out));
+  return (int)hipGetLastError();
+}
+
+int p2p_dropout(const void* x, long n, float p, const int64_t* seed, unsigned salt, void* y,
+                hipStream_t st) {
+  using namespace p2p;
+  hipLaunchKernelGGL(dropout_kernel, dim3(egrid(n / 8)), dim3(256), 0, st, static_cast<const bf16*>(x),
+                     n / 8, p, seed, (uint32_t)salt, static_cast<bf16*>(y));
+  return (int)hipGetLastError();
+}
+
+int p2p_pad_channels(const void* a, int Ca, const void* b, int Cb, long P, int Co, void* out,
+                     hipStream_t st) {
+  using namespace p2p;
+  hipLaunchKernelGGL(pad_channels_kernel, dim3(egrid(P * Co)), dim3(256), 0, st,
+                     static_cast<const bf16*>(a), Ca, static_cast<const bf16*>(b), Cb, P, Co,
+                     static_cast<bf16*>(out));
+  return (int)hipGetLastError();
+}
+
+int p2p_slice_channels(const void* in, int Ci, int c0, long P, int C, void* out, hipStream_t st) {
+  using namespace p2p;
+  hipLaunchKernelGGL(slice_channels_kernel, dim3(egrid(P * C)), dim3(256), 0, st,
+                     static_cast<const bf16*>(in), Ci, c0, P, C, static_cast<bf16*>(out));
+  return (int)hipGetLastError();
+}
+
+// workspace: colsum_blocks(M, C) * C floats
+int p2p_colsum_blocks(long M, int C) {
+  long b = (M + 511) / 512;
+  if (b > 1024) b = 1024;
+  if (b < 1) b = 1;
+  (void)C;
+  return (int)b;
+}
+
+int p2p_colsum(const void* x, long M, int C, float scale, int accumulate, float* ws, float* out,
+               hipStream_t st) {
+  using namespace p2p;
+  const int nb = p2p_colsum_blocks(M, C);
+  const long rpb = (M + nb - 1) / nb;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb), dim3(256), 0, st, static_cast<const bf16*>(x), M,
+                     C, rpb, ws);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, nb, C, scale,
+                     accumulate, out);
+  return (int)hipGetLastError();
+}
+
+int p2p_loss_blocks(long n) {
+  long b = (n + 2047) / 2048;
+  if (b > 1024) b = 1024;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+int p2p_loss_fwd(const void* a, const void* b, int is_f32, long n, int kind, float t, float scale,
+                 float* ws, float* out, hipStream_t st) {
+  using namespace p2p;
+  const int nb = p2p_loss_blocks(n);
+  hipLaunchKernelGGL(loss_partial_kernel, dim3(nb), dim3(256), 0, st, a, b, is_f32, n, kind, t, ws);
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, ws, nb, scale, out);
+  return (int)hipGetLastError();
+}
+
+int p2p_loss_bwd(const void* a, const void* b, int is_f32, long n, int kind, float t, float scale,
+                 const float* gout, void* ga, void* gb, hipStream_t st) {
+  using namespace p2p;
+  hipLaunchKernelGGL(loss_grad_kernel, dim3(egrid(n)), dim3(256), 0, st, a, b, is_f32, n, kind, t, scale,
+                     gout, ga, gb);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

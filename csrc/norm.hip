@@ -1,0 +1,406 @@
+// Instance / batch normalisation over NHWC bf16 activations (gfx950).
+//
+// Both norms are the same three-kernel pipeline with a different reduction domain:
+//   IN : one group per (sample n, channel c), reduced over the H*W pixels of n
+//   BN : one group per channel, reduced over all N*H*W pixels  (host passes N=1, HW=N*H*W)
+// Forward
+//   1. norm_partial   grid (chunks, N): every block reduces a contiguous run of pixels of
+//      one sample; each thread owns one 16-B channel chunk (8 channels, bf16x8 vector loads)
+//      and accumulates shifted sums around a per-block pivot (the block's first pixel), so
+//      E[x^2]-E[x]^2 cancellation never happens.  Block partials (mean_b, M2_b) -> workspace.
+//   2. norm_finalize  one thread per (n, c): Chan's parallel merge of the block partials in
+//      a fixed order (deterministic), biased variance, rstd; BN also updates running stats
+//      with the unbiased variance (PyTorch semantics).
+//   3. norm_apply     y = act((x - mean) * rstd * gamma + beta), 16-B loads/stores.
+// Backward (dx = rstd*g*(dy - mean(dy) - xhat*mean(dy*xhat)), dgamma/dbeta for affine)
+//   1. norm_bwd_partial : block partial sums of dy and dy*xhat (recomputed from x)
+//   2. norm_bwd_finalize: per (n,c) coefficients; per-channel dgamma/dbeta (summed over n)
+//   3. norm_bwd_apply   : dx = A*dy + B + Cc*xhat
+#include "common.h"
+
+namespace p2p {
+
+struct NormGeom {
+  int N, HW, C;   // groups: N x C; pixels per group: HW
+  int chunk;      // pixels per block
+  int nchunks;    // blocks per sample
+};
+
+__device__ __forceinline__ void unpack8(u32x4 v, float* f) {
+  bf16x8 b = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = (float)b[j];
+}
+
+__device__ __forceinline__ u32x4 pack8(const float* f) {
+  bf16x8 b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b[j] = (bf16)f[j];
+  return __builtin_bit_cast(u32x4, b);
+}
+
+// ---------------------------------------------------------------- forward
+// ws layout: [N][nchunks][C] mean_b, then [N][nchunks][C] M2_b
+__global__ void __launch_bounds__(256) norm_partial_kernel(const bf16* __restrict__ x, NormGeom g,
+                                                           float* __restrict__ ws) {
+  const int n = blockIdx.y, cb = blockIdx.x;
+  const int CP = g.C >> 3;
+  const int RP = 256 / CP;           // pixel rows processed per pass
+  const int tid = threadIdx.x;
+  const int cg = tid % CP, tr = tid / CP;
+  const int p0 = cb * g.chunk;
+  const int p1 = min(g.HW, p0 + g.chunk);
+  const bf16* base = x + (long)n * g.HW * g.C;
+  float piv[8], s1[8], s2[8];
+  int cnt = 0;
+  {
+    u32x4 v = *reinterpret_cast<const u32x4*>(base + (long)p0 * g.C + cg * 8);
+    unpack8(v, piv);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  if (tr < RP) {
+    for (int p = p0 + tr; p < p1; p += RP) {
+      float f[8];
+      unpack8(*reinterpret_cast<const u32x4*>(base + (long)p * g.C + cg * 8), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = f[j] - piv[j];
+        s1[j] += d;
+        s2[j] += d * d;
+      }
+      ++cnt;
+    }
+  }
+  // block reduce over rows sharing a channel chunk: LDS [RP][C] x 2
+  __shared__ float red1[2048], red2[2048];
+  const int rows_red = 2048 / g.C;   // rows that fit in the LDS buffer at once
+  // every thread with tr < RP contributes; fold rows tr >= rows_red in a loop
+  for (int base_r = 0; base_r < RP; base_r += rows_red) {
+    if (tr >= base_r && tr < base_r + rows_red && tr < RP) {
+      const int r = tr - base_r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (base_r == 0) {
+          red1[r * g.C + cg * 8 + j] = s1[j];
+          red2[r * g.C + cg * 8 + j] = s2[j];
+        } else {
+          red1[r * g.C + cg * 8 + j] += s1[j];
+          red2[r * g.C + cg * 8 + j] += s2[j];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const int rr = min(RP, rows_red);
+  const int npx = p1 - p0;
+  for (int c = tid; c < g.C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rr; ++r) {
+      a += red1[r * g.C + c];
+      b += red2[r * g.C + c];
+    }
+    const float pv = (float)base[(long)p0 * g.C + c];
+    const float inv = 1.f / (float)npx;
+    const float mb = pv + a * inv;
+    const float m2 = fmaxf(b - a * a * inv, 0.f);
+    const long o = ((long)n * g.nchunks + cb) * g.C + c;
+    ws[o] = mb;
+    ws[(long)g.N * g.nchunks * g.C + o] = m2;
+  }
+  (void)cnt;
+}
+
+// stats: [N][C] mean, [N][C] rstd (fp32).  bn: running stats update (N == 1).
+__global__ void __launch_bounds__(256) norm_finalize_kernel(const float* __restrict__ ws, NormGeom g,
+                                                            float eps, float* __restrict__ mean_out,
+                                                            float* __restrict__ rstd_out,
+                                                            float* __restrict__ run_mean,
+                                                            float* __restrict__ run_var,
+                                                            float momentum) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= g.N * g.C) return;
+  const int n = i / g.C, c = i % g.C;
+  const float* mb = ws + (long)n * g.nchunks * g.C + c;
+  const float* m2 = mb + (long)g.N * g.nchunks * g.C;
+  float cntA = 0.f, meanA = 0.f, M2A = 0.f;
+  for (int b = 0; b < g.nchunks; ++b) {
+    const float cntB = (float)min(g.chunk, g.HW - b * g.chunk);
+    const float meanB = mb[(long)b * g.C], M2B = m2[(long)b * g.C];
+    const float tot = cntA + cntB;
+    const float d = meanB - meanA;
+    meanA += d * (cntB / tot);
+    M2A += M2B + d * d * (cntA * cntB / tot);
+    cntA = tot;
+  }
+  const float var = M2A / cntA;
+  mean_out[i] = meanA;
+  rstd_out[i] = rsqrtf(var + eps);
+  if (run_mean) {
+    const float unb = cntA > 1.f ? M2A / (cntA - 1.f) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * meanA;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+  }
+}
+
+// y = act((x - mean) * rstd * gamma + beta); mean/rstd indexed [n][c] (BN: n == 0 always)
+__global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict__ x, NormGeom g,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta,
+                                                         const float* __restrict__ prelu_w,
+                                                         int act, bf16* __restrict__ y) {
+  const long CP = g.C >> 3;
+  const long total = (long)g.N * g.HW * CP;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long pix = e / CP;
+    const int cg = (int)(e - pix * CP);
+    const int n = (int)(pix / g.HW);
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + e * 8), f);
+    const float* mu = mean + (long)n * g.C + cg * 8;
+    const float* rs = rstd + (long)n * g.C + cg * 8;
+    const float pw = prelu_w ? prelu_w[0] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = (f[j] - mu[j]) * rs[j];
+      if (gamma) v = v * gamma[cg * 8 + j] + beta[cg * 8 + j];
+      if (prelu_w) v = v > 0.f ? v : pw * v;
+      else v = act_fwd(v, act);
+      f[j] = v;
+    }
+    *reinterpret_cast<u32x4*>(y + e * 8) = pack8(f);
+  }
+}
+
+// ---------------------------------------------------------------- backward
+// ws: [N][nchunks][C] sum(dy), [N][nchunks][C] sum(dy*xhat)
+__global__ void __launch_bounds__(256) norm_bwd_partial_kernel(const bf16* __restrict__ x,
+                                                               const bf16* __restrict__ dy,
+                                                               NormGeom g,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ rstd,
+                                                               const float* __restrict__ gamma,
+                                                               float* __restrict__ ws) {
+  const int n = blockIdx.y, cb = blockIdx.x;
+  const int CP = g.C >> 3;
+  const int RP = 256 / CP;
+  const int tid = threadIdx.x;
+  const int cg = tid % CP, tr = tid / CP;
+  const int p0 = cb * g.chunk;
+  const int p1 = min(g.HW, p0 + g.chunk);
+  const long off = (long)n * g.HW * g.C;
+  float mu[8], rs[8], ga[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mu[j] = mean[(long)n * g.C + cg * 8 + j];
+    rs[j] = rstd[(long)n * g.C + cg * 8 + j];
+    ga[j] = gamma ? gamma[cg * 8 + j] : 1.f;
+    s1[j] = s2[j] = 0.f;
+  }
+  if (tr < RP) {
+    for (int p = p0 + tr; p < p1; p += RP) {
+      float fx[8], fd[8];
+      unpack8(*reinterpret_cast<const u32x4*>(x + off + (long)p * g.C + cg * 8), fx);
+      unpack8(*reinterpret_cast<const u32x4*>(dy + off + (long)p * g.C + cg * 8), fd);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = fd[j] * ga[j];
+        s1[j] += d;
+        s2[j] += d * (fx[j] - mu[j]) * rs[j];
+      }
+    }
+  }
+  __shared__ float red1[2048], red2[2048];
+  const int rows_red = 2048 / g.C;
+  for (int base_r = 0; base_r < RP; base_r += rows_red) {
+    if (tr >= base_r && tr < base_r + rows_red && tr < RP) {
+      const int r = tr - base_r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (base_r == 0) {
+          red1[r * g.C + cg * 8 + j] = s1[j];
+          red2[r * g.C + cg * 8 + j] = s2[j];
+        } else {
+          red1[r * g.C + cg * 8 + j] += s1[j];
+          red2[r * g.C + cg * 8 + j] += s2[j];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const int rr = min(RP, rows_red);
+  for (int c = tid; c < g.C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rr; ++r) {
+      a += red1[r * g.C + c];
+      b += red2[r * g.C + c];
+    }
+    const long o = ((long)n * g.nchunks + cb) * g.C + c;
+    ws[o] = a;
+    ws[(long)g.N * g.nchunks * g.C + o] = b;
+  }
+}
+
+// coef: [N][C] A, [N][C] B, [N][C] Cc  with dx = A*dy + B + Cc*xhat
+// dgamma/dbeta (affine): summed over n in a fixed order by a per-channel thread.
+__global__ void __launch_bounds__(256) norm_bwd_finalize_kernel(const float* __restrict__ ws,
+                                                                NormGeom g,
+                                                                const float* __restrict__ rstd,
+                                                                const float* __restrict__ gamma,
+                                                                float* __restrict__ coef) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= g.N * g.C) return;
+  const int n = i / g.C, c = i % g.C;
+  const float* a = ws + (long)n * g.nchunks * g.C + c;
+  const float* b = a + (long)g.N * g.nchunks * g.C;
+  float sdy = 0.f, sdx = 0.f;
+  for (int k = 0; k < g.nchunks; ++k) {
+    sdy += a[(long)k * g.C];
+    sdx += b[(long)k * g.C];
+  }
+  const float r = rstd[i];
+  const float inv = 1.f / (float)g.HW;
+  const float ga = gamma ? gamma[c] : 1.f;
+  const long NC = (long)g.N * g.C;
+  coef[i] = r * ga;
+  coef[NC + i] = -r * sdy * inv;
+  coef[2 * NC + i] = -r * sdx * inv;
+}
+
+__global__ void __launch_bounds__(256) norm_param_grad_kernel(const float* __restrict__ ws, NormGeom g,
+                                                              float* __restrict__ dgamma,
+                                                              float* __restrict__ dbeta) {
+  // d(gamma) = sum(dy * xhat), d(beta) = sum(dy); ws holds gamma-scaled sums, so the host
+  // passes gamma == nullptr to the partial kernel for this pass (unscaled dy).
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= g.C) return;
+  float sdy = 0.f, sdx = 0.f;
+  for (int n = 0; n < g.N; ++n) {
+    const float* a = ws + (long)n * g.nchunks * g.C + c;
+    const float* b = a + (long)g.N * g.nchunks * g.C;
+    for (int k = 0; k < g.nchunks; ++k) {
+      sdy += a[(long)k * g.C];
+      sdx += b[(long)k * g.C];
+    }
+  }
+  dgamma[c] += sdx;
+  dbeta[c] += sdy;
+}
+
+__global__ void __launch_bounds__(256) norm_bwd_apply_kernel(const bf16* __restrict__ x,
+                                                             const bf16* __restrict__ dy, NormGeom g,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ rstd,
+                                                             const float* __restrict__ coef,
+                                                             bf16* __restrict__ dx) {
+  const long CP = g.C >> 3;
+  const long NC = (long)g.N * g.C;
+  const long total = (long)g.N * g.HW * CP;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long pix = e / CP;
+    const int cg = (int)(e - pix * CP);
+    const int n = (int)(pix / g.HW);
+    float fx[8], fd[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + e * 8), fx);
+    unpack8(*reinterpret_cast<const u32x4*>(dy + e * 8), fd);
+    const long ci = (long)n * g.C + cg * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xh = (fx[j] - mean[ci + j]) * rstd[ci + j];
+      fd[j] = coef[ci + j] * fd[j] + coef[NC + ci + j] + coef[2 * NC + ci + j] * xh;
+    }
+    *reinterpret_cast<u32x4*>(dx + e * 8) = pack8(fd);
+  }
+}
+
+static inline unsigned grid_for(long work) {
+  long b = (work + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+static inline NormGeom make_geom(int N, int HW, int C) {
+  NormGeom g;
+  g.N = N;
+  g.HW = HW;
+  g.C = C;
+  // ~ 256 blocks per wave of work; at least 64 pixels per block
+  long total_px = (long)N * HW;
+  int chunk = (int)((total_px + 2047) / 2048);
+  chunk = chunk < 64 ? 64 : chunk;
+  chunk = ((chunk + 31) / 32) * 32;
+  if (chunk > HW) chunk = HW;
+  g.chunk = chunk;
+  g.nchunks = (HW + chunk - 1) / chunk;
+  return g;
+}
+
+}  // namespace p2p
+
+extern "C" {
+
+// workspace floats needed by p2p_norm_fwd / p2p_norm_bwd
+long p2p_norm_ws_floats(int N, int HW, int C) {
+  p2p::NormGeom g = p2p::make_geom(N, HW, C);
+  return 2L * N * g.nchunks * C + 3L * N * C;
+}
+
+int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* gamma,
+                 const float* beta, const float* prelu_w, int act, float* mean, float* rstd,
+                 float* run_mean, float* run_var, float momentum, float* ws, void* y,
+                 hipStream_t st) {
+  using namespace p2p;
+  NormGeom g = make_geom(N, HW, C);
+  hipLaunchKernelGGL(norm_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
+                     static_cast<const bf16*>(x), g, ws);
+  hipLaunchKernelGGL(norm_finalize_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, ws, g, eps,
+                     mean, rstd, run_mean, run_var, momentum);
+  if (y)
+    hipLaunchKernelGGL(norm_apply_kernel, dim3(grid_for((long)N * HW * C / 8)), dim3(256), 0, st,
+                       static_cast<const bf16*>(x), g, mean, rstd, gamma, beta, prelu_w, act,
+                       static_cast<bf16*>(y));
+  return (int)hipGetLastError();
+}
+
+// apply only (eval-mode BN with running stats: host passes mean/rstd computed from them)
+int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const float* rstd,
+                   const float* gamma, const float* beta, const float* prelu_w, int act, void* y,
+                   hipStream_t st) {
+  using namespace p2p;
+  NormGeom g = make_geom(N, HW, C);
+  hipLaunchKernelGGL(norm_apply_kernel, dim3(grid_for((long)N * HW * C / 8)), dim3(256), 0, st,
+                     static_cast<const bf16*>(x), g, mean, rstd, gamma, beta, prelu_w, act,
+                     static_cast<bf16*>(y));
+  return (int)hipGetLastError();
+}
+
+int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const float* mean,
+                 const float* rstd, const float* gamma, float* dgamma, float* dbeta, float* ws,
+                 void* dx, hipStream_t st) {
+  using namespace p2p;
+  NormGeom g = make_geom(N, HW, C);
+  float* coef = ws + 2L * N * g.nchunks * C;
+  if (dgamma) {
+    hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
+                       static_cast<const bf16*>(x), static_cast<const bf16*>(dy), g, mean, rstd,
+                       (const float*)nullptr, ws);
+    hipLaunchKernelGGL(norm_param_grad_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, g,
+                       dgamma, dbeta);
+  }
+  if (dx) {
+    hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
+                       static_cast<const bf16*>(x), static_cast<const bf16*>(dy), g, mean, rstd,
+                       gamma, ws);
+    hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, ws, g,
+                       rstd, gamma, coef);
+    hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for((long)N * HW * C / 8)), dim3(256), 0,
+                       st, static_cast<const bf16*>(x), static_cast<const bf16*>(dy), g, mean,
+                       rstd, coef, static_cast<bf16*>(dx));
+  }
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

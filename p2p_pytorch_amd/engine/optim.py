@@ -14,10 +14,23 @@ from .. import _native
 
 
 class FusedAdam(torch.optim.Optimizer):
+    """Adam whose update is the multi-tensor HIP kernel (``csrc/optim.hip``).
+
+    ``lr`` and the step count live in device tensors, so a step captured into a hipGraph
+    keeps following LR schedulers (``param_groups[i]['lr']`` is mirrored into the device
+    tensor on every eager ``step`` and by ``sync_lr()``) and bias correction.
+    """
+
     def __init__(self, params, lr=2e-4, betas=(0.5, 0.999), eps=1e-8, weight_decay=0.0):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
-        self._meta_cache = {}
+        dev = self.param_groups[0]["params"][0].device
+        self._lr_t = [torch.tensor([float(g["lr"])], device=dev) for g in self.param_groups]
+        self._step_t = [torch.zeros(1, device=dev) for _ in self.param_groups]
+
+    def sync_lr(self):
+        for g, t in zip(self.param_groups, self._lr_t):
+            t.fill_(float(g["lr"]))
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -25,7 +38,8 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        p2p = _native.ops()
+        from ..ops import hip
+        capturing = torch.cuda.is_current_stream_capturing()
         for gi, group in enumerate(self.param_groups):
             params, grads, m1, m2 = [], [], [], []
             for p in group["params"]:
@@ -34,26 +48,41 @@ class FusedAdam(torch.optim.Optimizer):
                 st = self.state[p]
                 if not st:
                     st["step"] = 0
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 st["step"] += 1
                 params.append(p)
-                grads.append(p.grad)
+                grads.append(p.grad.contiguous())
                 m1.append(st["exp_avg"])
                 m2.append(st["exp_avg_sq"])
             if not params:
                 continue
-            step = self.state[params[0]]["step"]
+            if not capturing:
+                self._lr_t[gi].fill_(float(group["lr"]))
+            self._step_t[gi].add_(1.0)
             b1, b2 = group["betas"]
-            p2p.adam_multi(params, grads, m1, m2, float(group["lr"]), float(b1), float(b2),
-                           float(group["eps"]), float(group["weight_decay"]), int(step))
+            hip.adam_(params, grads, m1, m2, self._lr_t[gi], self._step_t[gi], b1, b2,
+                      group["eps"], group["weight_decay"])
         return loss
+
+    def state_dict(self):
+        sd = super().state_dict()
+        sd["device_step"] = [float(t.item()) for t in self._step_t]
+        return sd
+
+    def load_state_dict(self, sd):
+        steps = sd.get("device_step")
+        sd = {k: v for k, v in sd.items() if k != "device_step"}
+        super().load_state_dict(sd)
+        if steps:
+            for t, v in zip(self._step_t, steps):
+                t.fill_(v)
 
 
 def make_adam(params, lr=2e-4, betas=(0.5, 0.999), eps=1e-8):
     params = [p for p in params]
     on_gpu = bool(params) and params[0].is_cuda
-    if on_gpu and _native.get_backend() == "native" and _native.available() and \
-            hasattr(_native.ops(), "adam_multi"):
+    if on_gpu and _native.get_backend() == "native":
+        _native.ops()  # fail loudly if the extension is missing
         return FusedAdam(params, lr=lr, betas=betas, eps=eps)
     return torch.optim.Adam(params, lr=lr, betas=betas, eps=eps)

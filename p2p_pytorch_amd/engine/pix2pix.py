@@ -64,6 +64,10 @@ class Pix2PixStep:
 
     def step(self, real_A, real_B):
         netG, netD = self.netG, self.netD
+        if real_A.is_cuda and _native.get_backend() == "native":
+            from ..ops import hip
+            hip.begin_step()      # weight images re-cast once per step (graph-safe)
+            hip.advance_rng()     # new dropout masks
         with self._ctx(real_A.device):
             fake_B = netG(real_A)
             # ---- D

@@ -1,0 +1,312 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+The HIP side runs bf16 activations (fp32 accumulate, fp32 master weights); the oracle runs
+the identical math in fp32 on the *same bf16-rounded inputs*, so the tolerance only has
+to absorb bf16 output rounding and accumulation order.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from p2p_pytorch_amd import _native
+from p2p_pytorch_amd import ops
+from p2p_pytorch_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _native_backend():
+    _native.set_backend("native")
+    assert _native.load(), _native.load_error()
+    yield
+
+
+def rel_err(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def bf(x):
+    return x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+
+def rand_img(n, c, h, w, scale=1.0, seed=0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return bf(torch.randn(n, c, h, w, device=DEV, generator=g) * scale)
+
+
+def _leaf(x):
+    return x.detach().clone().requires_grad_(True)
+
+
+CONV_CASES = [
+    # (name, N, C1, C2, H, Cout, k, s, p, act_in, act_out, bias)
+    ("enc_s2", 2, 64, 0, 32, 128, 4, 2, 1, "lrelu", None, True),
+    ("first_c3", 2, 3, 0, 32, 64, 4, 2, 1, None, None, True),
+    ("d_input_concat3+3", 2, 3, 3, 32, 64, 4, 2, 1, None, None, True),
+    ("patch_s1", 2, 256, 0, 10, 512, 4, 1, 1, "lrelu", None, True),
+    ("patch_out_c1", 2, 512, 0, 9, 1, 4, 1, 1, "lrelu", None, True),
+    ("bottleneck_splitk", 2, 512, 0, 4, 512, 4, 2, 1, "lrelu", None, True),
+    ("one_by_one", 2, 64, 0, 16, 128, 1, 1, 0, "lrelu", None, True),
+    ("concat_64+64", 2, 64, 64, 16, 64, 3, 1, 1, "relu", None, False),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=[c[0] for c in CONV_CASES])
+def test_conv2d_fwd_bwd(case):
+    name, N, C1, C2, H, Cout, k, s, p, act_in, act_out, use_bias = case
+    torch.manual_seed(0)
+    x1 = rand_img(N, C1, H, H, seed=1)
+    x2 = rand_img(N, C2, H, H, seed=2) if C2 else None
+    Cin = C1 + C2
+    w = (torch.randn(Cout, Cin, k, k, device=DEV) * (1.0 / (Cin * k * k) ** 0.5))
+    b = torch.randn(Cout, device=DEV) * 0.1 if use_bias else None
+    # HIP
+    hx1, hw = _leaf(x1), _leaf(w)
+    hx2 = _leaf(x2) if x2 is not None else None
+    hb = _leaf(b) if b is not None else None
+    xin = (hx1, hx2) if hx2 is not None else hx1
+    y = ops.conv2d(xin, hw, hb, s, p, act_in=act_in, act_out=act_out)
+    gy = rand_img(*y.shape, seed=3)
+    y.backward(gy)
+    # fp32 oracle on the same bf16 inputs
+    rx1, rw = _leaf(x1.float()), _leaf(w)
+    rx2 = _leaf(x2.float()) if x2 is not None else None
+    rb = _leaf(b) if b is not None else None
+    rin = (rx1, rx2) if rx2 is not None else rx1
+    # the HIP path computes with bf16 weights: round the oracle's weight the same way
+    ry = ref.conv2d(rin, rw.to(torch.bfloat16).float(), rb, s, p, act_in=act_in, act_out=act_out)
+    ry.backward(gy.float())
+    assert y.shape == ry.shape
+    assert rel_err(y, ry) < 2e-2, name
+    assert rel_err(hx1.grad, rx1.grad) < 3e-2, name
+    if x2 is not None:
+        assert rel_err(hx2.grad, rx2.grad) < 3e-2, name
+    assert rel_err(hw.grad, rw.grad) < 3e-2, name
+    if b is not None:
+        assert rel_err(hb.grad, rb.grad) < 3e-2, name
+
+
+CONVT_CASES = [
+    # (name, N, C1, C2, H, Cout, act_in, act_out, bias)
+    ("dec_concat", 2, 64, 64, 16, 32, "relu", None, True),
+    ("innermost_1x1", 4, 512, 0, 1, 512, "relu", None, True),
+    ("dec_2x2_concat", 2, 512, 512, 2, 512, "relu", None, True),
+    ("head_tanh_c3", 2, 64, 64, 32, 3, "relu", "tanh", True),
+]
+
+
+@pytest.mark.parametrize("case", CONVT_CASES, ids=[c[0] for c in CONVT_CASES])
+def test_conv_transpose2d_fwd_bwd(case):
+    name, N, C1, C2, H, Cout, act_in, act_out, use_bias = case
+    x1 = rand_img(N, C1, H, H, seed=4)
+    x2 = rand_img(N, C2, H, H, seed=5) if C2 else None
+    Cin = C1 + C2
+    w = torch.randn(Cin, Cout, 4, 4, device=DEV) * (1.0 / (Cin * 4) ** 0.5)
+    b = torch.randn(Cout, device=DEV) * 0.1 if use_bias else None
+    hx1, hw = _leaf(x1), _leaf(w)
+    hx2 = _leaf(x2) if x2 is not None else None
+    hb = _leaf(b) if b is not None else None
+    y = ops.conv_transpose2d((hx1, hx2) if hx2 is not None else hx1, hw, hb, 2, 1, act_in, act_out)
+    gy = rand_img(*y.shape, seed=6)
+    y.backward(gy)
+    rx1, rw = _leaf(x1.float()), _leaf(w)
+    rx2 = _leaf(x2.float()) if x2 is not None else None
+    rb = _leaf(b) if b is not None else None
+    ry = ref.conv_transpose2d((rx1, rx2) if rx2 is not None else rx1,
+                              rw.to(torch.bfloat16).float(), rb, 2, 1, act_in, act_out)
+    ry.backward(gy.float())
+    assert y.shape == ry.shape == (N, Cout, 2 * H, 2 * H)
+    assert rel_err(y, ry) < 2e-2, name
+    assert rel_err(hx1.grad, rx1.grad) < 3e-2, name
+    if x2 is not None:
+        assert rel_err(hx2.grad, rx2.grad) < 3e-2, name
+    assert rel_err(hw.grad, rw.grad) < 3e-2, name
+    if b is not None:
+        assert rel_err(hb.grad, rb.grad) < 3e-2, name
+
+
+@pytest.mark.parametrize("pad_mode,up", [("reflect", 1), ("zeros", 2), ("reflect", 2)])
+def test_conv_reflect_upsample_fwd(pad_mode, up):
+    x = rand_img(2, 32, 12, 12, seed=7)
+    w = torch.randn(64, 32, 3, 3, device=DEV) * 0.05
+    b = torch.randn(64, device=DEV) * 0.1
+    y = ops.conv2d(x, w, b, 1, 1, pad_mode=pad_mode, upsample=up)
+    ry = ref.conv2d(x.float(), w.to(torch.bfloat16).float(), b, 1, 1, pad_mode=pad_mode,
+                    upsample=up)
+    assert rel_err(y, ry) < 2e-2
+
+
+def test_conv_wgrad_large_m():
+    # many pixels per weight -> many split-K slabs; checks the deterministic slab reduce
+    x = rand_img(8, 64, 64, 64, seed=8)
+    w = torch.randn(128, 64, 4, 4, device=DEV) * 0.02
+    hw = _leaf(w)
+    y = ops.conv2d(x, hw, None, 2, 1, act_in="lrelu")
+    gy = rand_img(*y.shape, seed=9)
+    y.backward(gy)
+    g1 = hw.grad.clone()
+    hw.grad = None
+    y = ops.conv2d(x, hw, None, 2, 1, act_in="lrelu")
+    y.backward(gy)
+    assert torch.equal(g1, hw.grad), "wgrad must be bitwise reproducible"
+    rw = _leaf(w)
+    ry = ref.conv2d(x.float(), rw.to(torch.bfloat16).float(), None, 2, 1, act_in="lrelu")
+    ry.backward(gy.float())
+    assert rel_err(hw.grad, rw.grad) < 2e-2
+
+
+@pytest.mark.parametrize("N,C,H", [(2, 64, 32), (4, 512, 2), (2, 128, 64), (3, 256, 5)])
+def test_instance_norm(N, C, H):
+    x = rand_img(N, C, H, H, scale=3.0, seed=10)
+    x = bf(x.float() + 2.0)  # non-zero mean
+    hx = _leaf(x)
+    y = ops.instance_norm(hx)
+    gy = rand_img(N, C, H, H, seed=11)
+    y.backward(gy)
+    rx = _leaf(x.float())
+    ry = F.instance_norm(rx, eps=1e-5)
+    ry.backward(gy.float())
+    assert rel_err(y, ry) < 2e-2
+    if H * H > 1:
+        assert rel_err(hx.grad, rx.grad) < 3e-2
+
+
+def test_batch_norm_train_and_eval():
+    N, C, H = 4, 64, 16
+    x = bf(torch.randn(N, C, H, H, device=DEV) * 2 + 1)
+    g = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV) * 0.1
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    rm2, rv2 = rm.clone(), rv.clone()
+    hx, hg, hb = _leaf(x), _leaf(g), _leaf(b)
+    y = ops.batch_norm(hx, rm, rv, hg, hb, True, 0.1, 1e-5)
+    gy = rand_img(N, C, H, H, seed=12)
+    y.backward(gy)
+    rx, rg, rb = _leaf(x.float()), _leaf(g), _leaf(b)
+    ry = F.batch_norm(rx, rm2, rv2, rg, rb, True, 0.1, 1e-5)
+    ry.backward(gy.float())
+    assert rel_err(y, ry) < 2e-2
+    assert rel_err(hx.grad, rx.grad) < 3e-2
+    assert rel_err(hg.grad, rg.grad) < 2e-2
+    assert rel_err(hb.grad, rb.grad) < 2e-2
+    assert rel_err(rm, rm2) < 1e-3 and rel_err(rv, rv2) < 1e-3
+    ye = ops.batch_norm(x, rm, rv, g, b, False, 0.1, 1e-5)
+    rye = F.batch_norm(x.float(), rm2, rv2, g, b, False, 0.1, 1e-5)
+    assert rel_err(ye, rye) < 2e-2
+
+
+@pytest.mark.parametrize("name", ["relu", "lrelu", "tanh", "sigmoid"])
+def test_act(name):
+    x = rand_img(2, 16, 8, 8, seed=13)
+    hx = _leaf(x)
+    y = ops.act(hx, name)
+    gy = rand_img(2, 16, 8, 8, seed=14)
+    y.backward(gy)
+    rx = _leaf(x.float())
+    ry = ref.apply_act(rx, name)
+    ry.backward(gy.float())
+    assert rel_err(y, ry) < 1e-2
+    assert rel_err(hx.grad, rx.grad) < 2e-2
+
+
+def test_dropout_mask_and_grad():
+    from p2p_pytorch_amd.ops import hip
+    x = bf(torch.ones(4, 64, 16, 16, device=DEV))
+    hx = _leaf(x)
+    y = hip.dropout(hx, 0.5, salt=7)
+    frac = (y.float() == 0).float().mean().item()
+    assert 0.45 < frac < 0.55
+    assert torch.all((y.float() == 0) | (y.float() == 2.0))
+    y.backward(torch.ones_like(y))
+    assert torch.equal(hx.grad.float(), y.float()), "backward must reuse the forward mask"
+    y2 = hip.dropout(x, 0.5, salt=7)
+    assert torch.equal(y, y2)
+    hip.advance_rng()
+    y3 = hip.dropout(x, 0.5, salt=7)
+    assert not torch.equal(y, y3), "advance_rng must draw a new mask"
+
+
+@pytest.mark.parametrize("kind", ["bce_logits", "mse", "l1", "mse_pair", "bce"])
+def test_losses(kind):
+    a = rand_img(4, 1, 30, 30, seed=15)
+    b = rand_img(4, 1, 30, 30, seed=16)
+    ha = _leaf(a)
+    ra = _leaf(a.float())
+    if kind == "bce_logits":
+        v, r = ops.bce_logits_const(ha, 1.0), ref.bce_logits_const(ra, 1.0)
+    elif kind == "mse":
+        v, r = ops.mse_const(ha, 0.0), ref.mse_const(ra, 0.0)
+    elif kind == "l1":
+        v, r = ops.l1(ha, b), ref.l1(ra, b.float())
+    elif kind == "mse_pair":
+        v, r = ops.mse(ha, b), ref.mse(ra, b.float())
+    else:
+        ha2 = _leaf(bf(torch.sigmoid(a.float())))
+        ra2 = _leaf(ha2.detach().float())
+        v, r = ops.bce_const(ha2, 0.0), ref.bce_const(ra2, 0.0)
+        ha, ra = ha2, ra2
+    assert v.dtype == torch.float32 and v.dim() == 0
+    assert abs(v.item() - r.item()) <= 1e-3 * max(1.0, abs(r.item()))
+    (v * 3.0).backward()
+    (r * 3.0).backward()
+    assert rel_err(ha.grad, ra.grad) < 2e-2
+
+
+def test_fused_adam_matches_torch():
+    from p2p_pytorch_amd.engine.optim import FusedAdam
+    torch.manual_seed(0)
+    ps = [torch.randn(n, device=DEV) for n in (7, 4096, 10000, 64 * 3 * 4 * 4)]
+    qs = [p.clone() for p in ps]
+    ps = [torch.nn.Parameter(p) for p in ps]
+    qs = [torch.nn.Parameter(q) for q in qs]
+    o1 = FusedAdam(ps, lr=2e-4, betas=(0.5, 0.999))
+    o2 = torch.optim.Adam(qs, lr=2e-4, betas=(0.5, 0.999))
+    for it in range(5):
+        for p, q in zip(ps, qs):
+            g = torch.randn_like(p)
+            p.grad = g.clone()
+            q.grad = g.clone()
+        o1.step()
+        o2.step()
+    for p, q in zip(ps, qs):
+        assert torch.allclose(p, q, rtol=1e-5, atol=1e-6)
+
+
+def test_unet_patchgan_step_matches_oracle():
+    """A small U-Net + PatchGAN forward/backward: HIP path vs the fp32 CPU oracle."""
+    from p2p_pytorch_amd.models import define_D, define_G
+    torch.manual_seed(0)
+    G = define_G(netG="unet_64", gpu_id="cpu", verbose=False, use_dropout=False)
+    D = define_D(6, 64, norm="instance", netD="basic", gpu_id="cpu", verbose=False)
+    A = torch.rand(2, 3, 64, 64) * 2 - 1
+    B = torch.rand(2, 3, 64, 64) * 2 - 1
+    A = A.to(torch.bfloat16).float()
+    B = B.to(torch.bfloat16).float()
+
+    def run(G, D, A, B):
+        fake = G(A)
+        pred = D((A, fake))
+        loss = ops.bce_logits_const(pred, 1.0) + 100 * ops.l1(fake, B)
+        loss.backward()
+        return loss.detach().float().cpu(), fake.detach().float().cpu()
+
+    lc, fc = run(G, D, A, B)
+    gc = {n: p.grad.clone() for n, p in G.named_parameters()}
+    G.zero_grad()
+    D.zero_grad()
+    G.to(DEV)
+    D.to(DEV)
+    lg, fg = run(G, D, bf(A.to(DEV)), bf(B.to(DEV)))
+    assert rel_err(fg, fc) < 5e-2
+    assert abs(lg.item() - lc.item()) < 5e-2 * abs(lc.item())
+    for n, p in G.named_parameters():
+        assert torch.isfinite(p.grad).all(), n
+    # weight grads of the big middle layers agree to bf16 accuracy
+    for n in ("downs.2.weight", "ups.2.weight"):
+        p = dict(G.named_parameters())[n]
+        assert rel_err(p.grad.cpu(), gc[n]) < 1e-1, n
