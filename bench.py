@@ -28,8 +28,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 # Measured stock PyTorch-ROCm eager baseline (images/sec per GPU) for this exact config,
-# recorded in BASELINE.md; None until measured.
-EAGER_BASELINE_IMG_S_PER_GPU = None
+# recorded in BASELINE.md (stock PyTorch-ROCm eager, bf16 autocast, channels_last, per-GPU
+# batch 128, cudnn.benchmark; profiles/eager_baseline_r1.jsonl).
+EAGER_BASELINE_IMG_S_PER_GPU = 1790.23
 
 
 def parse():
@@ -37,7 +38,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=32, help="images per GPU")
+    p.add_argument("--batch", type=int, default=64, help="images per GPU")
     p.add_argument("--size", type=int, default=256)
     p.add_argument("--netG", default="unet_256")
     p.add_argument("--netD", default="basic")
@@ -46,6 +47,8 @@ def parse():
     p.add_argument("--gan_mode", default="vanilla")
     p.add_argument("--bucket_mb", type=float, default=64.0)
     p.add_argument("--no_graph", action="store_true", help="(native) disable hipGraph capture")
+    p.add_argument("--graph", action="store_true",
+                   help="(native) force hipGraph capture also for N>1 (default: N == 1 only)")
     p.add_argument("--json_out", default=None)
     return p.parse_args()
 
@@ -104,14 +107,21 @@ def main():
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
+    step = trainer.step
+    use_graph = (args.impl == "native" and dev.type == "cuda" and not args.no_graph
+                 and (world == 1 or args.graph))
+    if use_graph:
+        from p2p_pytorch_amd.engine.graph import CapturedStep
+        # capture runs its own warmup steps on a side stream, then records one step
+        step = CapturedStep(trainer.step, real_A, real_B, warmup=2)
     for _ in range(args.warmup):
-        losses = trainer.step(real_A, real_B)
+        losses = step(real_A, real_B)
     sync()
     pdist.barrier()
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        losses = trainer.step(real_A, real_B)
+        losses = step(real_A, real_B)
     sync()
     pdist.barrier()
     sync()
@@ -138,7 +148,8 @@ def main():
         "config": {"model": f"pix2pix {args.netG} + PatchGAN {args.netD} (70x70)",
                    "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
                    "image_size": S, "parallelism": f"dp{world}", "impl": args.impl,
-                   "gan_mode": args.gan_mode, "lambda_L1": args.lamb},
+                   "gan_mode": args.gan_mode, "lambda_L1": args.lamb,
+                   "hipgraph": bool(use_graph)},
         "losses_finite": finite,
         "losses": loss_vals,
     }

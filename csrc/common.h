@@ -76,6 +76,52 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
+// ReLU on 8 packed bf16: a bf16 is negative iff its int16 bit pattern is, so a packed
+// signed int16 max with 0 is an exact ReLU (-0.0 -> +0.0): 4 v_pk_max_i16 per 16 bytes.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t relu2(uint32_t w) {
+  s16x2 s = __builtin_bit_cast(s16x2, w);
+  s = __builtin_elementwise_max(s, (s16x2){0, 0});
+  return __builtin_bit_cast(uint32_t, s);
+}
+// NB: spelled out per component.  hipcc (ROCm 7.2) miscompiles __builtin_bit_cast applied
+// to a subscripted ext_vector element inside a loop (v[j]): it reads element 0 for every j.
+__device__ __forceinline__ u32x4 relu8(u32x4 v) {
+  u32x4 o;
+  o.x = relu2(v.x);
+  o.y = relu2(v.y);
+  o.z = relu2(v.z);
+  o.w = relu2(v.w);
+  return o;
+}
+
+// activation of a loaded 16-B chunk: ReLU on the integer pipe, anything else through fp32
+__device__ __forceinline__ u32x4 act_chunk(u32x4 v, int act) {
+  if (act == ACT_NONE) return v;
+  if (act == ACT_RELU) return relu8(v);
+  return act8(v, act);
+}
+
+// Division by a loop-invariant divisor: q = (umulhi(n, mul) + n) >> shift, exact for
+// n < 2^31 (Granlund-Montgomery).  Built from uniform values -> scalar registers.
+struct FastDiv {
+  uint32_t d, mul, shift;
+};
+
+__host__ __device__ __forceinline__ FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1u << s) < d) ++s;
+  f.shift = s;
+  f.mul = (uint32_t)((((1ull << 32) * ((1ull << s) - d)) / d) + 1ull);
+  return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.mul) + n) >> f.shift;
+}
+
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -2,31 +2,39 @@
 //
 // GEMM view: C[M][N] = A[M][K] * B[K][N] with M = output pixels (NHWC rows), N = output
 // channels, K = taps x input channels.  A is gathered on the fly (im2col never exists in
-// memory); B is the bf16 weight stored [Cout][KH][KW][Cin] so each output channel's K
-// run is contiguous.
+// memory); B is the bf16 weight image [Cout][KH][KW][Cin] so each output channel's K run
+// is contiguous (see weight_prep at the end of this file).
 //
 //  * 256 threads = 4 wave64s arranged WM x WN; each wave owns a (BM/WM) x (BN/WN) block
 //    of 16x16 accumulators fed by v_mfma_f32_16x16x32_bf16.
 //  * BK = 64: each K-tile is two 32-deep MFMA steps.  Double-buffered LDS with register
-//    staging: the next tile's global loads are issued before the current tile's MFMAs,
+//    staging: the next tile's global loads are issued before the current tile's MFMAs and
 //    written to the other LDS buffer after them, one barrier per K-tile.
 //  * LDS tiles are [rows][64] bf16 (128-B rows) with the 16-B chunk index XOR-swizzled
 //    by (row>>1)&7 so the 16 rows a ds_read_b128 lane-group touches land on 16 distinct
-//    16-B slots (conflict-free fragment reads, conflict-free 8-lane row writes).
-//  * The loader folds: zero / reflection padding, nearest upsample (src = dst / up),
-//    a virtual channel concat of two tensors (U-Net skip) and the input activation
-//    (LeakyReLU for encoders, ReLU for decoders) -- none of those tensors is materialised.
+//    16-B slots (conflict-free fragment reads and row writes).
+//  * Loader cost is what bounds an implicit GEMM on CDNA4 (one wave64 VALU op = 2 cycles
+//    of a SIMD that also issues the MFMAs), so it is kept to ~10 VALU ops per 16-B chunk:
+//      - FAST path (every channel group a multiple of 64, i.e. all U-Net / PatchGAN
+//        layers but the first): a 64-deep K tile never straddles a tap, so (tap, ci, src)
+//        are wave-uniform scalars per tile; each thread keeps its rows' (image base, y0,
+//        x0) and only adds the tap offset + one bounds test.
+//      - general path (C = 8 / 16 / 24 ...: packed image inputs): per-thread tap split by
+//        magic-number division, no hardware divide anywhere.
+//      - the input activation is folded in as a packed int16 max for ReLU (4 ops / 16 B);
+//        LeakyReLU is stored pre-applied by its producer (norm / epilogue) instead.
+//  * Folded into the gather: zero / reflection padding, nearest upsample (src = dst >> 1)
+//    and a virtual channel concat of two tensors (the U-Net skip) -- none materialised.
 //  * CONVT (MODE 1) = sub-pixel decomposition: blockIdx.z selects the output parity class
 //    (ry, rx); only the ceil(K/s)^2 taps that hit the class are iterated, so a 4x4 s2
-//    transposed conv costs 4 taps per output pixel instead of 16 with 3/4 zeros.
-//  * Epilogue is staged through LDS as fp32 so every lane stores 16 contiguous bytes:
-//    bias + output activation (tanh for the U-Net head) + optional act'(x) multiply for
-//    dgrad (backward through the activation fused into the producing dgrad) + a channel
-//    split into two tensors (gradient of a virtual concat).  Split-K (small-M layers at
-//    the U-Net bottleneck) accumulates fp32 into a workspace, finished by
-//    conv_finalize_kernel.
-//  * Workgroup ids are remapped XCD-aware (blocks b, b+8 share an L2) so the n-tiles of
-//    one m-tile run on one XCD and re-read the same activation panel from L2.
+//    transposed conv costs 4 taps per output pixel instead of 16 with 3/4 zeros.  MODE 1
+//    also serves conv dgrad (dY * W^T) and MODE 0 serves convT dgrad.
+//  * Epilogue: bias + output activation in registers, the tile staged through LDS as
+//    bf16 (fits inside the 64 KB pipeline buffers: 2 workgroups / CU), then 16-B stores
+//    with the optional act'(x) multiply of dgrad and a channel split into two tensors
+//    (gradient of a virtual concat).  Split-K (tiny-M bottleneck layers) accumulates
+//    fp32 atomics straight from the accumulators, finished by conv_finalize_kernel.
+//  * Workgroup ids are remapped XCD-aware so the n-tiles of one m-tile share an L2.
 #include "common.h"
 #include "conv.h"
 
@@ -72,11 +80,11 @@ __device__ __forceinline__ ClassGeom class_geom(const ConvFwdArgs& a, int cls) {
 template <int BM, int BN>
 struct FwdSmem {
   static constexpr int pipe = 2 * (BM + BN) * BK * 2;
-  static constexpr int epi = BM * (BN + 4) * 4;
+  static constexpr int epi = BM * (BN + 8) * 2;
   static constexpr int bytes = pipe > epi ? pipe : epi;
 };
 
-template <int BM, int BN, int WM, int WN, int MODE>
+template <int BM, int BN, int WM, int WN, int MODE, bool FAST>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvFwdArgs a) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = BM / WM / 16;
@@ -110,96 +118,123 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvFwdArgs a) {
   const bf16* __restrict__ w = static_cast<const bf16*>(a.w);
   const int C = a.C, C1 = a.C1, C2 = a.C2;
   const int kc = tid & 7;  // this thread's 16-B chunk within a 64-wide K tile
-
-  // ---- per-thread A rows (fixed over the K loop)
-  int a_ybase[AROWS], a_xbase[AROWS], a_nbase[AROWS];
-  bool a_ok[AROWS];
-  const int HWq = g.Hq * g.Wq;
-#pragma unroll
-  for (int i = 0; i < AROWS; ++i) {
-    int m = m0 + (tid >> 3) + 32 * i;
-    a_ok[i] = m < g.Mc;
-    int mm = a_ok[i] ? m : 0;
-    int n = mm / HWq;
-    int r = mm - n * HWq;
-    int qy = r / g.Wq;
-    int qx = r - qy * g.Wq;
-    a_nbase[i] = n * a.H;
-    if (MODE == 0) {
-      a_ybase[i] = qy * a.stride - a.pad;
-      a_xbase[i] = qx * a.stride - a.pad;
-    } else {
-      a_ybase[i] = qy + g.dy;
-      a_xbase[i] = qx + g.dx;
-    }
-  }
   const int ush = a.up == 2 ? 1 : 0;
   const int Hu = a.H << ush, Wu = a.W << ush;
 
+  // ---- per-thread A rows (fixed over the K loop): image base pixel, y0, x0
+  int r_img[AROWS], r_y[AROWS], r_x[AROWS];
+  const int HWq = g.Hq * g.Wq;
+  const FastDiv fd_hwq = make_fastdiv((uint32_t)HWq), fd_wq = make_fastdiv((uint32_t)g.Wq);
+#pragma unroll
+  for (int i = 0; i < AROWS; ++i) {
+    const int m = m0 + (tid >> 3) + 32 * i;
+    const int mm = m < g.Mc ? m : 0;
+    const int n = (int)fdiv((uint32_t)mm, fd_hwq);
+    const int r = mm - n * HWq;
+    const int qy = (int)fdiv((uint32_t)r, fd_wq);
+    const int qx = r - qy * g.Wq;
+    r_img[i] = n * a.H * a.W;
+    if (MODE == 0) {
+      r_y[i] = qy * a.stride - a.pad;
+      r_x[i] = qx * a.stride - a.pad;
+    } else {
+      r_y[i] = qy + g.dy;
+      r_x[i] = qx + g.dx;
+    }
+    if (m >= g.Mc) r_y[i] = -(1 << 28);  // forces the bounds test to fail (zero row)
+  }
+  const FastDiv fd_c = make_fastdiv((uint32_t)C), fd_ti = make_fastdiv((uint32_t)g.Ti);
+  const long wrow = (MODE == 0) ? (long)g.Kc : (long)a.KH * a.KW * C;  // weight row stride
+
   u32x4 ra[AROWS], rb[BROWS];
 
-  auto load_tile = [&](int kt) {
-    const int k = kt * BK + kc * 8;
-    const bool kok = k < g.Kc;
-    int tap = 0, ci = 0, t_y = 0, t_x = 0;
-    if (kok) {
-      tap = k / C;
-      ci = k - tap * C;
-      t_y = tap / g.Ti;
-      t_x = tap - t_y * g.Ti;
-    }
-    const bool src1 = ci < C1;
-    const bf16* src = src1 ? x1 : x2;
-    const int cs = src1 ? C1 : C2;
-    const int cio = src1 ? ci : ci - C1;
-#pragma unroll
-    for (int i = 0; i < AROWS; ++i) {
-      u32x4 v = zero_u32x4();
-      if (kok && a_ok[i]) {
-        int iy, ix;
-        bool inb;
-        if (MODE == 0) {
-          int uy = a_ybase[i] + t_y, ux = a_xbase[i] + t_x;
-          if (a.reflect) {
-            uy = reflect_idx(uy, Hu);
-            ux = reflect_idx(ux, Wu);
-            inb = true;
-          } else {
-            inb = (unsigned)uy < (unsigned)Hu && (unsigned)ux < (unsigned)Wu;
-          }
-          iy = uy >> ush;
-          ix = ux >> ush;
-        } else {
-          iy = a_ybase[i] - t_y;
-          ix = a_xbase[i] - t_x;
-          inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-        }
-        if (inb) {
-          const long pix = (long)(a_nbase[i] + iy) * a.W + ix;
-          v = *reinterpret_cast<const u32x4*>(src + pix * cs + cio);
-          v = act8(v, a.act_in);
-        }
-      }
-      ra[i] = v;
-    }
-    // B (weights)
-    long woff = 0;
+  // gather one 16-B chunk of row i at tap (t_y, t_x) from src + channel offset cio
+  auto gather = [&](int i, int t_y, int t_x, const bf16* src, int cs, int cio) -> u32x4 {
+    u32x4 v = zero_u32x4();
+    int iy, ix;
+    bool inb;
     if (MODE == 0) {
-      woff = k;
-    } else {
-      const int ky = g.ky0 + a.stride * t_y, kx = g.kx0 + a.stride * t_x;
-      woff = (long)(ky * a.KW + kx) * C + ci;
-    }
-#pragma unroll
-    for (int i = 0; i < BROWS; ++i) {
-      const int row = (tid >> 3) + 32 * i;
-      const int co = n0 + row;
-      u32x4 v = zero_u32x4();
-      if (kok && row < BN && co < a.Cout) {
-        const long base = (MODE == 0) ? (long)co * g.Kc : (long)co * a.KH * a.KW * C;
-        v = *reinterpret_cast<const u32x4*>(w + base + woff);
+      int uy = r_y[i] + t_y, ux = r_x[i] + t_x;
+      if (a.reflect && r_y[i] > -(1 << 27)) {
+        uy = reflect_idx(uy, Hu);
+        ux = reflect_idx(ux, Wu);
       }
-      rb[i] = v;
+      inb = (unsigned)uy < (unsigned)Hu && (unsigned)ux < (unsigned)Wu;
+      iy = uy >> ush;
+      ix = ux >> ush;
+    } else {
+      iy = r_y[i] - t_y;
+      ix = r_x[i] - t_x;
+      inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+    }
+    if (inb) {
+      const int pix = r_img[i] + iy * a.W + ix;
+      v = *reinterpret_cast<const u32x4*>(src + (long)pix * cs + cio);
+      v = act_chunk(v, a.act_in);
+    }
+    return v;
+  };
+
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * BK;
+    if constexpr (FAST) {
+      // wave-uniform: the whole 64-deep tile is one tap and one source tensor
+      const int tap = (int)fdiv((uint32_t)k0, fd_c);
+      const int ci0 = k0 - tap * C;
+      const int t_y = (int)fdiv((uint32_t)tap, fd_ti);
+      const int t_x = tap - t_y * g.Ti;
+      const bool s1 = ci0 < C1;
+      const bf16* src = s1 ? x1 : x2;
+      const int cs = s1 ? C1 : C2;
+      const int cio = (s1 ? ci0 : ci0 - C1) + kc * 8;
+#pragma unroll
+      for (int i = 0; i < AROWS; ++i) ra[i] = gather(i, t_y, t_x, src, cs, cio);
+      long woff;
+      if (MODE == 0) {
+        woff = k0 + kc * 8;
+      } else {
+        const int ky = g.ky0 + a.stride * t_y, kx = g.kx0 + a.stride * t_x;
+        woff = (long)(ky * a.KW + kx) * C + ci0 + kc * 8;
+      }
+#pragma unroll
+      for (int i = 0; i < BROWS; ++i) {
+        const int row = (tid >> 3) + 32 * i;
+        const int co = n0 + row;
+        u32x4 v = zero_u32x4();
+        if (row < BN && co < a.Cout) v = *reinterpret_cast<const u32x4*>(w + co * wrow + woff);
+        rb[i] = v;
+      }
+    } else {
+      const int k = k0 + kc * 8;
+      const bool kok = k < g.Kc;
+      int tap = 0, ci = 0, t_y = 0, t_x = 0;
+      if (kok) {
+        tap = (int)fdiv((uint32_t)k, fd_c);
+        ci = k - tap * C;
+        t_y = (int)fdiv((uint32_t)tap, fd_ti);
+        t_x = tap - t_y * g.Ti;
+      }
+      const bool s1 = ci < C1;
+      const bf16* src = s1 ? x1 : x2;
+      const int cs = s1 ? C1 : C2;
+      const int cio = s1 ? ci : ci - C1;
+#pragma unroll
+      for (int i = 0; i < AROWS; ++i) ra[i] = kok ? gather(i, t_y, t_x, src, cs, cio) : zero_u32x4();
+      long woff;
+      if (MODE == 0) {
+        woff = k;
+      } else {
+        const int ky = g.ky0 + a.stride * t_y, kx = g.kx0 + a.stride * t_x;
+        woff = (long)(ky * a.KW + kx) * C + ci;
+      }
+#pragma unroll
+      for (int i = 0; i < BROWS; ++i) {
+        const int row = (tid >> 3) + 32 * i;
+        const int co = n0 + row;
+        u32x4 v = zero_u32x4();
+        if (kok && row < BN && co < a.Cout) v = *reinterpret_cast<const u32x4*>(w + co * wrow + woff);
+        rb[i] = v;
+      }
     }
   };
 
@@ -260,68 +295,87 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvFwdArgs a) {
     buf ^= 1;
   }
 
-  // ---- epilogue: stage fp32 tile in LDS, then 16-B stores
-  float* Cs = reinterpret_cast<float*>(smem);
-  constexpr int LDC = BN + 4;
+  const int s = a.stride;
+  auto out_pix = [&](int m) -> long {
+    if (MODE == 0) return m;
+    const int n = (int)fdiv((uint32_t)m, fd_hwq);
+    const int r = m - n * HWq;
+    const int qy = (int)fdiv((uint32_t)r, fd_wq);
+    const int qx = r - qy * g.Wq;
+    return ((long)n * a.OH + qy * s + g.ry) * a.OW + qx * s + g.rx;
+  };
+
+  // ---- split-K: fp32 atomics straight from the accumulators (tiny-M layers only)
+  if (a.splits > 1) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = wn * TN * 16 + j * 16 + (lane & 15);
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * TN * 16 + j * 16 + (lane & 15);
+        const int rowb = m0 + wm * TM * 16 + i * 16 + (lane >> 4) * 4;
+        if (col >= a.Cout) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = rowb + r;
+          if (m < g.Mc) atomicAdd(a.ws + out_pix(m) * a.Cout + col, acc[i][j][r]);
+        }
+      }
+    return;
+  }
+
+  // ---- epilogue: bias + act in registers, bf16 tile staged in LDS, 16-B stores
+  bf16* Cs = reinterpret_cast<bf16*>(smem);
+  constexpr int LDC = BN + 8;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int coll = wn * TN * 16 + j * 16 + (lane & 15);
+    const int col = n0 + coll;
+    const float bj = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
       const int rowb = wm * TM * 16 + i * 16 + (lane >> 4) * 4;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Cs[(rowb + r) * LDC + col] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r)
+        Cs[(rowb + r) * LDC + coll] = (bf16)act_fwd(acc[i][j][r] + bj, a.act_out);
     }
+  }
   __syncthreads();
 
-  const int s = a.stride;
   constexpr int CPR = BN / 8;  // 8-channel chunks per row
   for (int c = tid; c < BM * CPR; c += 256) {
     const int row = c / CPR, cc = c - row * CPR;
     const int m = m0 + row;
     const int co = n0 + cc * 8;
     if (m >= g.Mc || co >= a.Cout) continue;
-    long pix;
-    if (MODE == 0) {
-      pix = m;
-    } else {
-      int n = m / HWq;
-      int r = m - n * HWq;
-      int qy = r / g.Wq;
-      int qx = r - qy * g.Wq;
-      pix = ((long)n * a.OH + qy * s + g.ry) * a.OW + qx * s + g.rx;
-    }
-    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + cc * 8);
-    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + cc * 8 + 4);
-    float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-    if (a.splits > 1) {
-      float* dst = a.ws + pix * a.Cout + co;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) atomicAdd(dst + j, v[j]);
-      continue;
-    }
-    if (a.bias) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += a.bias[co + j];
-    }
-    if (a.act_out) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = act_fwd(v[j], a.act_out);
-    }
+    const long pix = out_pix(m);
+    u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * LDC + cc * 8);
     const bool first = co < a.Csplit;
     const int ld = first ? a.Csplit : a.Cout - a.Csplit;
     const int cof = first ? co : co - a.Csplit;
     if (a.act_bwd) {
       const bf16* xb = static_cast<const bf16*>(first ? a.xb1 : a.xb2);
-      bf16x8 xv = *reinterpret_cast<const bf16x8*>(xb + pix * ld + cof);
+      const u32x4 xv = *reinterpret_cast<const u32x4*>(xb + pix * ld + cof);
+      if (a.act_bwd == ACT_RELU) {
+        // zero the gradient where x <= 0 (bf16 sign / zero test on the int pipe)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] *= act_grad_from_input((float)xv[j], a.act_bwd);
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t xw = xv[q];
+          uint32_t keep = 0;
+          if ((int16_t)(xw & 0xffffu) > 0) keep |= 0xffffu;
+          if ((int16_t)(xw >> 16) > 0) keep |= 0xffff0000u;
+          v[q] &= keep;
+        }
+      } else {
+        bf16x8 vb = __builtin_bit_cast(bf16x8, v);
+        const bf16x8 xb8 = __builtin_bit_cast(bf16x8, xv);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          vb[q] = (bf16)((float)vb[q] * act_grad_from_input((float)xb8[q], a.act_bwd));
+        v = __builtin_bit_cast(u32x4, vb);
+      }
     }
-    bf16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
     bf16* y = static_cast<bf16*>(first ? a.y1 : a.y2);
-    *reinterpret_cast<bf16x8*>(y + pix * ld + cof) = o;
+    *reinterpret_cast<u32x4*>(y + pix * ld + cof) = v;
   }
 }
 
@@ -359,16 +413,15 @@ __global__ void __launch_bounds__(256) conv_finalize_kernel(ConvFwdArgs a, long 
   }
 }
 
-template <int BM, int BN, int WM, int WN, int MODE>
+template <int BM, int BN, int WM, int WN, int MODE, bool FAST>
 static int launch_fwd(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = FwdSmem<BM, BN>::bytes;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_fwd_kernel<BM, BN, WM, WN, MODE>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_fwd_kernel<BM, BN, WM, WN, MODE, FAST>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
-  // max rows over classes
   int classes = MODE == 0 ? 1 : a.stride * a.stride;
   long mmax = 0;
   for (int c = 0; c < classes; ++c) {
@@ -387,20 +440,26 @@ static int launch_fwd(const ConvFwdArgs& a, hipStream_t st) {
   const long mtiles = (mmax + BM - 1) / BM;
   const long ntiles = (a.Cout + BN - 1) / BN;
   dim3 grid((unsigned)(mtiles * ntiles), 1, (unsigned)(classes * a.splits));
-  hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN, MODE>), grid, dim3(256), smem, st, a);
+  hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN, MODE, FAST>), grid, dim3(256), smem, st, a);
   return (int)hipGetLastError();
+}
+
+template <int MODE, bool FAST>
+static int dispatch_fwd2(const ConvFwdArgs& a, int bm, int bn, hipStream_t st) {
+  if (bm == 128 && bn == 128) return launch_fwd<128, 128, 2, 2, MODE, FAST>(a, st);
+  if (bm == 128 && bn == 64) return launch_fwd<128, 64, 2, 2, MODE, FAST>(a, st);
+  if (bm == 64 && bn == 128) return launch_fwd<64, 128, 2, 2, MODE, FAST>(a, st);
+  if (bm == 64 && bn == 64) return launch_fwd<64, 64, 2, 2, MODE, FAST>(a, st);
+  if (bm == 256 && bn == 32) return launch_fwd<256, 32, 4, 1, MODE, FAST>(a, st);
+  if (bm == 256 && bn == 16) return launch_fwd<256, 16, 4, 1, MODE, FAST>(a, st);
+  if (bm == 64 && bn == 16) return launch_fwd<64, 16, 4, 1, MODE, FAST>(a, st);
+  return -1;
 }
 
 template <int MODE>
 static int dispatch_fwd(const ConvFwdArgs& a, int bm, int bn, hipStream_t st) {
-  if (bm == 128 && bn == 128) return launch_fwd<128, 128, 2, 2, MODE>(a, st);
-  if (bm == 128 && bn == 64) return launch_fwd<128, 64, 2, 2, MODE>(a, st);
-  if (bm == 64 && bn == 128) return launch_fwd<64, 128, 2, 2, MODE>(a, st);
-  if (bm == 64 && bn == 64) return launch_fwd<64, 64, 2, 2, MODE>(a, st);
-  if (bm == 256 && bn == 32) return launch_fwd<256, 32, 4, 1, MODE>(a, st);
-  if (bm == 256 && bn == 16) return launch_fwd<256, 16, 4, 1, MODE>(a, st);
-  if (bm == 64 && bn == 16) return launch_fwd<64, 16, 4, 1, MODE>(a, st);
-  return -1;
+  const bool fast = (a.C1 % BK == 0) && (a.C2 % BK == 0);
+  return fast ? dispatch_fwd2<MODE, true>(a, bm, bn, st) : dispatch_fwd2<MODE, false>(a, bm, bn, st);
 }
 
 }  // namespace p2p

@@ -110,6 +110,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
   const int ush = a.up == 2 ? 1 : 0;
   const int Hu = a.H << ush, Wu = a.W << ush;
   const int OHW = a.OH * a.OW;
+  const FastDiv fd_ohw = make_fastdiv((uint32_t)OHW), fd_ow = make_fastdiv((uint32_t)a.OW);
 
   u32x4 rp[PL], rq[4];
   auto load_stage = [&](int st) {
@@ -120,7 +121,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
       u32x4 vp = zero_u32x4();
       if (row < WBM && m < a.M && p_ok) {
         vp = *reinterpret_cast<const u32x4*>(psrc + (long)m * pld + pro);
-        vp = act8(vp, a.p_act);
+        vp = act_chunk(vp, a.p_act);
       }
       rp[i] = vp;
     }
@@ -129,9 +130,9 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
       const int m = st * WBM + rrow + 16 * i;
       u32x4 vq = zero_u32x4();
       if (m < a.M && q_ok) {
-        const int n = m / OHW;
+        const int n = (int)fdiv((uint32_t)m, fd_ohw);
         const int rem = m - n * OHW;
-        const int oh = rem / a.OW;
+        const int oh = (int)fdiv((uint32_t)rem, fd_ow);
         const int ow = rem - oh * a.OW;
         int uy = oh * a.stride - a.pad + kh;
         int ux = ow * a.stride - a.pad + kw;
@@ -146,7 +147,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
         if (inb) {
           const long pix = ((long)n * a.H + (uy >> ush)) * a.W + (ux >> ush);
           vq = *reinterpret_cast<const u32x4*>(qsrc + pix * qld + qco);
-          vq = act8(vq, a.q_act);
+          vq = act_chunk(vq, a.q_act);
         }
       }
       rq[i] = vq;
@@ -219,24 +220,35 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
 }
 
 // dw[r][ci][kh][kw] (+)= scale * sum_s ws[s][r][(kh*KW+kw)*C + ci]
+// Block = EPB elements x G split-groups; each thread sums a fixed, strided subset of the
+// splits, then the G partials are combined in LDS in a fixed order (deterministic).
+template <int G>
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, int splits,
                                                            int R, int KH, int KW, int C, int Rr,
                                                            int Cr, float* __restrict__ dw,
                                                            float scale, int accumulate) {
+  constexpr int EPB = 256 / G;
   const int Kq = KH * KW * C;
   const long total = (long)R * Kq;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += ws[(long)k * total + e];
-    s *= scale;
-    const int r = (int)(e / Kq);
-    const int kq = (int)(e - (long)r * Kq);
-    const int tap = kq / C;
-    const int ci = kq - tap * C;
-    if (r >= Rr || ci >= Cr) continue;  // padded rows / channels of the GEMM view
-    const long o = ((long)r * Cr + ci) * KH * KW + tap;
-    dw[o] = accumulate ? dw[o] + s : s;
+  const int le = threadIdx.x % EPB, sg = threadIdx.x / EPB;
+  const long e = (long)blockIdx.x * EPB + le;
+  float s = 0.f;
+  if (e < total) {
+    for (int k = sg; k < splits; k += G) s += ws[(long)k * total + e];
   }
+  __shared__ float red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (sg != 0 || e >= total) return;
+  for (int q = 1; q < G; ++q) s += red[q * EPB + le];
+  s *= scale;
+  const int r = (int)(e / Kq);
+  const int kq = (int)(e - (long)r * Kq);
+  const int tap = kq / C;
+  const int ci = kq - tap * C;
+  if (r >= Rr || ci >= Cr) return;  // padded rows / channels of the GEMM view
+  const long o = ((long)r * Cr + ci) * KH * KW + tap;
+  dw[o] = accumulate ? dw[o] + s : s;
 }
 
 }  // namespace p2p
@@ -262,9 +274,23 @@ extern "C" int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t st) {
 extern "C" int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int KW, int C, int Rr,
                                 int Cr, float* dw, float scale, int accumulate, hipStream_t st) {
   const long total = (long)R * KH * KW * C;
-  long blocks = (total + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(p2p::wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, ws, splits,
-                     R, KH, KW, C, Rr, Cr, dw, scale, accumulate);
+  int G = 1;
+  while (G < 32 && splits > 8 * G) G *= 2;   // <= ~8 slab reads per thread
+  const int EPB = 256 / G;
+  const unsigned blocks = (unsigned)((total + EPB - 1) / EPB);
+#define P2P_RED(g)                                                                              \
+  case g:                                                                                        \
+    hipLaunchKernelGGL(p2p::wgrad_reduce_kernel<g>, dim3(blocks), dim3(256), 0, st, ws, splits, R, \
+                       KH, KW, C, Rr, Cr, dw, scale, accumulate);                                \
+    break;
+  switch (G) {
+    P2P_RED(1)
+    P2P_RED(2)
+    P2P_RED(4)
+    P2P_RED(8)
+    P2P_RED(16)
+    P2P_RED(32)
+  }
+#undef P2P_RED
   return (int)hipGetLastError();
 }

@@ -77,28 +77,31 @@ __global__ void __launch_bounds__(256) dropout_kernel(const bf16* __restrict__ x
 }
 
 // out[p][0:Ca] = a[p][:], out[p][Ca:Ca+Cb] = b[p][:], out[p][Ca+Cb:Co] = 0   (NHWC, any C)
+// one thread per pixel, 16-B stores of 8-channel chunks
 __global__ void __launch_bounds__(256) pad_channels_kernel(const bf16* __restrict__ a, int Ca,
                                                            const bf16* __restrict__ b, int Cb,
                                                            long P, int Co, bf16* __restrict__ out) {
-  const long total = P * Co;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-    const long p = e / Co;
-    const int c = (int)(e - p * Co);
-    bf16 v = (bf16)0.f;
-    if (c < Ca) v = a[p * Ca + c];
-    else if (c < Ca + Cb) v = b[p * Cb + (c - Ca)];
-    out[e] = v;
+  for (long p = blockIdx.x * 256L + threadIdx.x; p < P; p += (long)gridDim.x * 256) {
+    for (int c0 = 0; c0 < Co; c0 += 8) {
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        bf16 e = (bf16)0.f;
+        if (c < Ca) e = a[p * Ca + c];
+        else if (c < Ca + Cb) e = b[p * Cb + (c - Ca)];
+        v[j] = e;
+      }
+      *reinterpret_cast<bf16x8*>(out + p * Co + c0) = v;
+    }
   }
 }
 
-// out[p][0:C] = in[p][c0:c0+C]   (in has Ci channels)
+// out[p][0:C] = in[p][c0:c0+C]   (in has Ci channels); one thread per pixel
 __global__ void __launch_bounds__(256) slice_channels_kernel(const bf16* __restrict__ in, int Ci, int c0,
                                                              long P, int C, bf16* __restrict__ out) {
-  const long total = P * C;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-    const long p = e / C;
-    const int c = (int)(e - p * C);
-    out[e] = in[p * Ci + c0 + c];
+  for (long p = blockIdx.x * 256L + threadIdx.x; p < P; p += (long)gridDim.x * 256) {
+    for (int c = 0; c < C; ++c) out[p * C + c] = in[p * Ci + c0 + c];
   }
 }
 
@@ -142,14 +145,22 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const bf16* __restr
   }
 }
 
-// out[c] (+)= scale * sum_b ws[b][c]
+// out[c] (+)= scale * sum_b ws[b][c]: G threads per channel, fixed-order LDS combine
+template <int G>
 __global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restrict__ ws, int nb, int C,
                                                            float scale, int accumulate,
                                                            float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  constexpr int EPB = 256 / G;
+  const int le = threadIdx.x % EPB, sg = threadIdx.x / EPB;
+  const int c = blockIdx.x * EPB + le;
   float a = 0.f;
-  for (int b = 0; b < nb; ++b) a += ws[(long)b * C + c];
+  if (c < C)
+    for (int b = sg; b < nb; b += G) a += ws[(long)b * C + c];
+  __shared__ float red[256];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  if (sg != 0 || c >= C) return;
+  for (int q = 1; q < G; ++q) a += red[q * EPB + le];
   a *= scale;
   out[c] = accumulate ? out[c] + a : a;
 }
@@ -257,7 +268,7 @@ int p2p_dropout(const void* x, long n, float p, const int64_t* seed, unsigned sa
 int p2p_pad_channels(const void* a, int Ca, const void* b, int Cb, long P, int Co, void* out,
                      hipStream_t st) {
   using namespace p2p;
-  hipLaunchKernelGGL(pad_channels_kernel, dim3(egrid(P * Co)), dim3(256), 0, st,
+  hipLaunchKernelGGL(pad_channels_kernel, dim3(egrid(P)), dim3(256), 0, st,
                      static_cast<const bf16*>(a), Ca, static_cast<const bf16*>(b), Cb, P, Co,
                      static_cast<bf16*>(out));
   return (int)hipGetLastError();
@@ -265,7 +276,7 @@ int p2p_pad_channels(const void* a, int Ca, const void* b, int Cb, long P, int C
 
 int p2p_slice_channels(const void* in, int Ci, int c0, long P, int C, void* out, hipStream_t st) {
   using namespace p2p;
-  hipLaunchKernelGGL(slice_channels_kernel, dim3(egrid(P * C)), dim3(256), 0, st,
+  hipLaunchKernelGGL(slice_channels_kernel, dim3(egrid(P)), dim3(256), 0, st,
                      static_cast<const bf16*>(in), Ci, c0, P, C, static_cast<bf16*>(out));
   return (int)hipGetLastError();
 }
@@ -286,7 +297,8 @@ int p2p_colsum(const void* x, long M, int C, float scale, int accumulate, float*
   const long rpb = (M + nb - 1) / nb;
   hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb), dim3(256), 0, st, static_cast<const bf16*>(x), M,
                      C, rpb, ws);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, nb, C, scale,
+  // nb <= 1024 partials per channel: 32 threads per channel, <= 32 reads each
+  hipLaunchKernelGGL(colsum_final_kernel<32>, dim3((C + 7) / 8), dim3(256), 0, st, ws, nb, C, scale,
                      accumulate, out);
   return (int)hipGetLastError();
 }

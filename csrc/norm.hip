@@ -143,7 +143,9 @@ __global__ void __launch_bounds__(256) norm_finalize_kernel(const float* __restr
   }
 }
 
-// y = act((x - mean) * rstd * gamma + beta); mean/rstd indexed [n][c] (BN: n == 0 always)
+// y = act((x - mean) * rstd * gamma + beta); mean/rstd indexed [n][c] (BN: n == 0 always).
+// grid (chunks, N): each thread owns one 8-channel chunk (its 8 scale/shift pairs live in
+// registers) and strides over the block's pixels.
 __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict__ x, NormGeom g,
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ rstd,
@@ -151,26 +153,36 @@ __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict_
                                                          const float* __restrict__ beta,
                                                          const float* __restrict__ prelu_w,
                                                          int act, bf16* __restrict__ y) {
-  const long CP = g.C >> 3;
-  const long total = (long)g.N * g.HW * CP;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-    const long pix = e / CP;
-    const int cg = (int)(e - pix * CP);
-    const int n = (int)(pix / g.HW);
+  const int n = blockIdx.y, cb = blockIdx.x;
+  const int CP = g.C >> 3;
+  const int RP = 256 / CP;
+  const int tid = threadIdx.x;
+  const int cg = tid % CP, tr = tid / CP;
+  if (tr >= RP) return;
+  const int p0 = cb * g.chunk;
+  const int p1 = min(g.HW, p0 + g.chunk);
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = cg * 8 + j;
+    const float r = rstd[(long)n * g.C + c];
+    const float gm = gamma ? gamma[c] : 1.f;
+    sc[j] = r * gm;
+    sh[j] = (gamma ? beta[c] : 0.f) - mean[(long)n * g.C + c] * r * gm;
+  }
+  const float pw = prelu_w ? prelu_w[0] : 0.f;
+  const long base = (long)n * g.HW * g.C + cg * 8;
+  for (int p = p0 + tr; p < p1; p += RP) {
     float f[8];
-    unpack8(*reinterpret_cast<const u32x4*>(x + e * 8), f);
-    const float* mu = mean + (long)n * g.C + cg * 8;
-    const float* rs = rstd + (long)n * g.C + cg * 8;
-    const float pw = prelu_w ? prelu_w[0] : 0.f;
+    unpack8(*reinterpret_cast<const u32x4*>(x + base + (long)p * g.C), f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float v = (f[j] - mu[j]) * rs[j];
-      if (gamma) v = v * gamma[cg * 8 + j] + beta[cg * 8 + j];
+      float v = f[j] * sc[j] + sh[j];
       if (prelu_w) v = v > 0.f ? v : pw * v;
       else v = act_fwd(v, act);
       f[j] = v;
     }
-    *reinterpret_cast<u32x4*>(y + e * 8) = pack8(f);
+    *reinterpret_cast<u32x4*>(y + base + (long)p * g.C) = pack8(f);
   }
 }
 
@@ -295,31 +307,34 @@ __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(const bf16* __restr
                                                              const float* __restrict__ rstd,
                                                              const float* __restrict__ coef,
                                                              bf16* __restrict__ dx) {
-  const long CP = g.C >> 3;
+  // dx = A*dy + B + Cc*xhat = A*dy + (Cc*rstd)*x + (B - Cc*rstd*mean)
+  const int n = blockIdx.y, cb = blockIdx.x;
+  const int CP = g.C >> 3;
+  const int RP = 256 / CP;
+  const int tid = threadIdx.x;
+  const int cg = tid % CP, tr = tid / CP;
+  if (tr >= RP) return;
+  const int p0 = cb * g.chunk;
+  const int p1 = min(g.HW, p0 + g.chunk);
   const long NC = (long)g.N * g.C;
-  const long total = (long)g.N * g.HW * CP;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-    const long pix = e / CP;
-    const int cg = (int)(e - pix * CP);
-    const int n = (int)(pix / g.HW);
-    float fx[8], fd[8];
-    unpack8(*reinterpret_cast<const u32x4*>(x + e * 8), fx);
-    unpack8(*reinterpret_cast<const u32x4*>(dy + e * 8), fd);
-    const long ci = (long)n * g.C + cg * 8;
+  float ca[8], cx[8], c0[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float xh = (fx[j] - mean[ci + j]) * rstd[ci + j];
-      fd[j] = coef[ci + j] * fd[j] + coef[NC + ci + j] + coef[2 * NC + ci + j] * xh;
-    }
-    *reinterpret_cast<u32x4*>(dx + e * 8) = pack8(fd);
+  for (int j = 0; j < 8; ++j) {
+    const long ci = (long)n * g.C + cg * 8 + j;
+    const float cc = coef[2 * NC + ci] * rstd[ci];
+    ca[j] = coef[ci];
+    cx[j] = cc;
+    c0[j] = coef[NC + ci] - cc * mean[ci];
   }
-}
-
-static inline unsigned grid_for(long work) {
-  long b = (work + 255) / 256;
-  if (b > 8192) b = 8192;
-  if (b < 1) b = 1;
-  return (unsigned)b;
+  const long base = (long)n * g.HW * g.C + cg * 8;
+  for (int p = p0 + tr; p < p1; p += RP) {
+    float fx[8], fd[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + base + (long)p * g.C), fx);
+    unpack8(*reinterpret_cast<const u32x4*>(dy + base + (long)p * g.C), fd);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fd[j] = ca[j] * fd[j] + cx[j] * fx[j] + c0[j];
+    *reinterpret_cast<u32x4*>(dx + base + (long)p * g.C) = pack8(fd);
+  }
 }
 
 static inline NormGeom make_geom(int N, int HW, int C) {
@@ -359,7 +374,7 @@ int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* ga
   hipLaunchKernelGGL(norm_finalize_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, ws, g, eps,
                      mean, rstd, run_mean, run_var, momentum);
   if (y)
-    hipLaunchKernelGGL(norm_apply_kernel, dim3(grid_for((long)N * HW * C / 8)), dim3(256), 0, st,
+    hipLaunchKernelGGL(norm_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
                        static_cast<const bf16*>(x), g, mean, rstd, gamma, beta, prelu_w, act,
                        static_cast<bf16*>(y));
   return (int)hipGetLastError();
@@ -371,7 +386,7 @@ int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const
                    hipStream_t st) {
   using namespace p2p;
   NormGeom g = make_geom(N, HW, C);
-  hipLaunchKernelGGL(norm_apply_kernel, dim3(grid_for((long)N * HW * C / 8)), dim3(256), 0, st,
+  hipLaunchKernelGGL(norm_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
                      static_cast<const bf16*>(x), g, mean, rstd, gamma, beta, prelu_w, act,
                      static_cast<bf16*>(y));
   return (int)hipGetLastError();
@@ -396,8 +411,7 @@ int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const floa
                        gamma, ws);
     hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, ws, g,
                        rstd, gamma, coef);
-    hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for((long)N * HW * C / 8)), dim3(256), 0,
-                       st, static_cast<const bf16*>(x), static_cast<const bf16*>(dy), g, mean,
+    hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st, static_cast<const bf16*>(x), static_cast<const bf16*>(dy), g, mean,
                        rstd, coef, static_cast<bf16*>(dx));
   }
   return (int)hipGetLastError();

@@ -7,14 +7,22 @@ reference carries the knobs for this family (``--ngf`` /root/reference/train.py:
 its D is built from the same 70x70 PatchGAN recipe (networks.py:758-806).
 
 Design (MI355X-first): the U-Net is kept *flat* -- explicit encoder/decoder lists --
-instead of the recursive skip-block nesting of the pix2pix template, so that
-  * every ``LeakyReLU -> Conv`` is one fused conv (``act_in='lrelu'``),
+instead of the recursive skip-block nesting of the pix2pix template, and every
+activation is stored *pre-applied by its producer* so the conv loaders stay cheap:
+  * encoder level i stores ``LeakyReLU(norm(conv(.)))`` (the outermost conv: LeakyReLU in
+    its epilogue) -- the next encoder conv reads it as is;
+  * the innermost conv stores ``ReLU(conv(.))`` (its only consumer is ReLU -> ConvT);
+  * decoder levels store ``ReLU(norm(convT(.)))`` (dropout after it: ReLU commutes with
+    the positive 2x/0 dropout scale);
   * every ``ReLU -> ConvT(cat(skip, up))`` is one fused transposed conv reading the two
-    halves of the concat through two base pointers (no ``torch.cat`` materialised),
+    halves of the concat through two base pointers (no ``torch.cat`` materialised) with
+    a packed-int16 ReLU in its loader: ``relu(lrelu(x)) == relu(x)`` exactly, and
+    ``relu(relu(u)) == relu(u)``;
   * the final ``Tanh`` is the epilogue of the last ConvT.
-Numerically this is the standard U-Net: level ``i`` has ``ngf*min(2^i, 8)`` channels,
-no norm on the outermost/innermost down convs, dropout on the ``num_downs-5`` decoder
-levels right outside the innermost one.
+Numerically this is the standard U-Net (every derivative is exact too: d relu(lrelu(x))
+= [x > 0]): level ``i`` has ``ngf*min(2^i, 8)`` channels, no norm on the outermost /
+innermost down convs, dropout on the ``num_downs-5`` decoder levels right outside the
+innermost one.
 """
 from __future__ import annotations
 
@@ -38,10 +46,12 @@ class UnetGenerator(nn.Module):
         self.down_norms = nn.ModuleList()
         for i in range(n):
             cin = input_nc if i == 0 else ch[i - 1]
-            self.downs.append(Conv2d(cin, ch[i], 4, stride=2, padding=1, bias=use_bias,
-                                     act_in=None if i == 0 else "lrelu"))
             has_norm = 0 < i < n - 1
-            self.down_norms.append(norm_layer(norm, ch[i]) if has_norm else nn.Identity())
+            act_out = None if has_norm else ("relu" if i == n - 1 else "lrelu")
+            self.downs.append(Conv2d(cin, ch[i], 4, stride=2, padding=1, bias=use_bias,
+                                     act_out=act_out))
+            self.down_norms.append(norm_layer(norm, ch[i], act="lrelu") if has_norm
+                                   else nn.Identity())
         self.ups = nn.ModuleList()
         self.up_norms = nn.ModuleList()
         self.drop_levels = set(range(max(1, n - 1 - max(0, n - 5)), n - 1)) if use_dropout else set()
@@ -49,9 +59,10 @@ class UnetGenerator(nn.Module):
             cin = ch[i] if i == n - 1 else 2 * ch[i]
             cout = output_nc if i == 0 else ch[i - 1]
             self.ups.append(ConvTranspose2d(cin, cout, 4, stride=2, padding=1,
-                                            bias=True if i == 0 else use_bias, act_in="relu",
+                                            bias=True if i == 0 else use_bias,
+                                            act_in=None if i == n - 1 else "relu",
                                             act_out="tanh" if i == 0 else None))
-            self.up_norms.append(norm_layer(norm, cout) if i > 0 else nn.Identity())
+            self.up_norms.append(norm_layer(norm, cout, act="relu") if i > 0 else nn.Identity())
         self.dropouts = nn.ModuleList(
             [Dropout(0.5) if i in self.drop_levels else nn.Identity() for i in range(n)])
 
@@ -76,18 +87,18 @@ class NLayerDiscriminator(nn.Module):
     def __init__(self, input_nc, ndf=64, n_layers=3, norm="instance", use_sigmoid=False, padw=1):
         super().__init__()
         use_bias = norm != "batch"
-        layers = [Conv2d(input_nc, ndf, 4, stride=2, padding=padw)]
+        # LeakyReLU stored pre-applied: first conv's epilogue, then fused into each norm
+        layers = [Conv2d(input_nc, ndf, 4, stride=2, padding=padw, act_out="lrelu")]
         norms = [nn.Identity()]
         nf = ndf
         for k in range(1, n_layers):
             nf_prev, nf = nf, ndf * min(2 ** k, 8)
-            layers.append(Conv2d(nf_prev, nf, 4, stride=2, padding=padw, bias=use_bias,
-                                 act_in="lrelu"))
-            norms.append(norm_layer(norm, nf))
+            layers.append(Conv2d(nf_prev, nf, 4, stride=2, padding=padw, bias=use_bias))
+            norms.append(norm_layer(norm, nf, act="lrelu"))
         nf_prev, nf = nf, ndf * min(2 ** n_layers, 8)
-        layers.append(Conv2d(nf_prev, nf, 4, stride=1, padding=padw, bias=use_bias, act_in="lrelu"))
-        norms.append(norm_layer(norm, nf))
-        layers.append(Conv2d(nf, 1, 4, stride=1, padding=padw, act_in="lrelu",
+        layers.append(Conv2d(nf_prev, nf, 4, stride=1, padding=padw, bias=use_bias))
+        norms.append(norm_layer(norm, nf, act="lrelu"))
+        layers.append(Conv2d(nf, 1, 4, stride=1, padding=padw,
                              act_out="sigmoid" if use_sigmoid else None))
         norms.append(nn.Identity())
         self.convs = nn.ModuleList(layers)
@@ -106,12 +117,12 @@ class PixelDiscriminator(nn.Module):
         super().__init__()
         use_bias = norm != "batch"
         self.convs = nn.ModuleList([
-            Conv2d(input_nc, ndf, 1),
-            Conv2d(ndf, ndf * 2, 1, bias=use_bias, act_in="lrelu"),
-            Conv2d(ndf * 2, 1, 1, bias=use_bias, act_in="lrelu",
-                   act_out="sigmoid" if use_sigmoid else None),
+            Conv2d(input_nc, ndf, 1, act_out="lrelu"),
+            Conv2d(ndf, ndf * 2, 1, bias=use_bias),
+            Conv2d(ndf * 2, 1, 1, bias=use_bias, act_out="sigmoid" if use_sigmoid else None),
         ])
-        self.norms = nn.ModuleList([nn.Identity(), norm_layer(norm, ndf * 2), nn.Identity()])
+        self.norms = nn.ModuleList([nn.Identity(), norm_layer(norm, ndf * 2, act="lrelu"),
+                                    nn.Identity()])
 
     def forward(self, x):
         for conv, norm in zip(self.convs, self.norms):

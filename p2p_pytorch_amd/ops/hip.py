@@ -163,7 +163,7 @@ class ConvFn(torch.autograd.Function):
         ctx.geo = (C1, C2, Cp, packed, Cout, Coutp, H, W)
         ctx.has_x2 = x2 is not None
         ctx.has_bias = bias is not None
-        keep_y = cfg.act_out in ("tanh", "sigmoid", "relu")
+        keep_y = cfg.act_out not in (None, "none")
         ctx.save_for_backward(q1, q2, weight, y if keep_y else None)
         return y
 

@@ -278,35 +278,45 @@ def test_fused_adam_matches_torch():
 
 
 def test_unet_patchgan_step_matches_oracle():
-    """A small U-Net + PatchGAN forward/backward: HIP path vs the fp32 CPU oracle."""
+    """Small U-Net + PatchGAN forward/backward: HIP bf16 path vs the fp32 PyTorch oracle.
+
+    bf16 error compounds through a deep U-Net (instance norms over 2x2 maps amplify it),
+    so the bound is relative to stock PyTorch bf16 autocast on the same inputs: the HIP
+    path must be no less accurate than the eager bf16 baseline, per parameter.
+    """
     from p2p_pytorch_amd.models import define_D, define_G
     torch.manual_seed(0)
-    G = define_G(netG="unet_64", gpu_id="cpu", verbose=False, use_dropout=False)
-    D = define_D(6, 64, norm="instance", netD="basic", gpu_id="cpu", verbose=False)
-    A = torch.rand(2, 3, 64, 64) * 2 - 1
-    B = torch.rand(2, 3, 64, 64) * 2 - 1
-    A = A.to(torch.bfloat16).float()
-    B = B.to(torch.bfloat16).float()
+    G = define_G(netG="unet_64", gpu_id=DEV, verbose=False, use_dropout=False)
+    D = define_D(6, 64, norm="instance", netD="basic", gpu_id=DEV, verbose=False)
+    A = bf(torch.rand(2, 3, 64, 64, device=DEV) * 2 - 1)
+    B = bf(torch.rand(2, 3, 64, 64, device=DEV) * 2 - 1)
 
-    def run(G, D, A, B):
-        fake = G(A)
-        pred = D((A, fake))
-        loss = ops.bce_logits_const(pred, 1.0) + 100 * ops.l1(fake, B)
-        loss.backward()
-        return loss.detach().float().cpu(), fake.detach().float().cpu()
+    def run(backend, dtype=None):
+        _native.set_backend(backend)
+        G.zero_grad(set_to_none=True)
+        D.zero_grad(set_to_none=True)
+        try:
+            ctx = torch.autocast("cuda", dtype) if dtype else torch.autocast("cuda", enabled=False)
+            a, b = (A, B) if backend == "native" else (A.float(), B.float())
+            with ctx:
+                fake = G(a)
+                pred = D((a, fake) if backend == "native" else torch.cat((a, fake.to(a.dtype)), 1))
+                loss = ops.bce_logits_const(pred, 1.0) + 100 * ops.l1(fake, b)
+            loss.backward()
+        finally:
+            _native.set_backend("native")
+        grads = {n: p.grad.detach().float().clone() for n, p in G.named_parameters()}
+        return loss.detach().float(), fake.detach().float(), grads
 
-    lc, fc = run(G, D, A, B)
-    gc = {n: p.grad.clone() for n, p in G.named_parameters()}
-    G.zero_grad()
-    D.zero_grad()
-    G.to(DEV)
-    D.to(DEV)
-    lg, fg = run(G, D, bf(A.to(DEV)), bf(B.to(DEV)))
-    assert rel_err(fg, fc) < 5e-2
-    assert abs(lg.item() - lc.item()) < 5e-2 * abs(lc.item())
-    for n, p in G.named_parameters():
-        assert torch.isfinite(p.grad).all(), n
-    # weight grads of the big middle layers agree to bf16 accuracy
-    for n in ("downs.2.weight", "ups.2.weight"):
-        p = dict(G.named_parameters())[n]
-        assert rel_err(p.grad.cpu(), gc[n]) < 1e-1, n
+    l32, f32, g32 = run("torch")
+    l16, f16, g16 = run("torch", torch.bfloat16)
+    lh, fh, gh = run("native")
+    assert rel_err(fh, f32) < 5e-2
+    assert abs(lh.item() - l32.item()) < 2e-2 * abs(l32.item())
+    worse = []
+    for n in g32:
+        assert torch.isfinite(gh[n]).all(), n
+        eh, ee = rel_err(gh[n], g32[n]), rel_err(g16[n], g32[n])
+        if eh > 1.5 * ee + 0.03:
+            worse.append((n, eh, ee))
+    assert not worse, worse
