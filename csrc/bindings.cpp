@@ -14,6 +14,7 @@
 #include <torch/library.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "conv.h"
@@ -28,8 +29,8 @@ int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const
                    const float* gamma, const float* beta, const float* prelu_w, int act, void* y,
                    hipStream_t st);
 int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const float* mean,
-                 const float* rstd, const float* gamma, float* dgamma, float* dbeta, float* ws,
-                 void* dx, hipStream_t st);
+                 const float* rstd, const float* gamma, const float* beta, int act, float* dgamma,
+                 float* dbeta, float* ws, void* dx, float* dsum, hipStream_t st);
 int p2p_act(const void* a, const void* b, long n, int act, int mode, void* out, hipStream_t st);
 int p2p_dropout(const void* x, long n, float p, const int64_t* seed, unsigned salt, void* y,
                 hipStream_t st);
@@ -72,6 +73,25 @@ void check_rc(int rc, const char* what) {
   TORCH_CHECK(rc == 0, what, ": HIP launch failed: ", hipGetErrorString((hipError_t)rc));
 }
 
+// 4 KB of zeros per device: the padding source of the global_load_lds conv variant
+const void* zero_page(const Tensor& like) {
+  static std::vector<Tensor> pages(64);
+  const int d = like.device().index();
+  if (!pages[d].defined()) pages[d] = at::zeros({4096}, like.options().dtype(at::kByte));
+  return pages[d].data_ptr();
+}
+
+// conv kernel variant: P2P_CONV_VARIANT = v1 (register-staged) | g2 | g3 | g4 (LDS-DMA
+// rings) | unset = auto: g4 (256x128 tile, 8 waves, 3-stage ring) for Cout > 64, g2
+// (128x64, 2-stage) below -- the per-layer winners of tools/conv_bench.py on MI355X
+// (profiles/conv_variants_r1.jsonl).
+int conv_variant(int64_t Cout) {
+  const char* v = std::getenv("P2P_CONV_VARIANT");
+  if (v && v[0] == 'v') return 1;
+  if (v && v[0] == 'g' && v[1] >= '2' && v[1] <= '4') return v[1] - '0';
+  return Cout > 64 ? 4 : 2;
+}
+
 Tensor empty_nhwc(int64_t N, int64_t C, int64_t H, int64_t W, const Tensor& like) {
   return at::empty({N, C, H, W}, like.options().memory_format(at::MemoryFormat::ChannelsLast));
 }
@@ -82,7 +102,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                              int64_t stride, int64_t pad, int64_t reflect, int64_t up,
                              int64_t act_in, int64_t OH, int64_t OW, int64_t Cout, int64_t act_out,
                              int64_t Csplit, const optional<Tensor>& xb1,
-                             const optional<Tensor>& xb2, int64_t act_bwd) {
+                             const optional<Tensor>& xb2, int64_t act_bwd, int64_t Cvalid) {
   check_act(x1, "conv_fwd x1");
   const int64_t N = x1.size(0), H = x1.size(2), W = x1.size(3);
   int64_t C2 = 0;
@@ -144,6 +164,44 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   a.act_bwd = (int)act_bwd;
   a.ws = nullptr;
   a.splits = 1;
+  a.zero = zero_page(x1);
+
+  hipStream_t st = cur_stream(x1);
+  // ---- tiny-Cout "col" path: dense GEMM over the input pixels (N = taps x Cvalid) + col2im
+  const int64_t Cv = Cvalid > 0 ? Cvalid : Cout;
+  if (Cout <= 16 && Csplit == Cout && !reflect && up == 1 && C1 % 64 == 0 && C2 % 64 == 0) {
+    const int64_t T = KH * KW;
+    const int64_t Ncol = ((T * Cv + 7) / 8) * 8;
+    Tensor wv = w.reshape({-1}).narrow(0, 0, Cout * T * C).view({Cout, T, C}).narrow(0, 0, Cv).transpose(0, 1)
+                    .reshape({T * Cv, C});
+    if (Ncol != T * Cv) wv = at::cat({wv, at::zeros({Ncol - T * Cv, C}, wv.options())});
+    wv = wv.contiguous();
+    Tensor col = empty_nhwc(N, Ncol, H, W, x1);
+    p2p::ConvFwdArgs g = a;
+    g.KH = g.KW = 1;
+    g.stride = 1;
+    g.pad = 0;
+    g.OH = (int)H;
+    g.OW = (int)W;
+    g.Cout = (int)Ncol;
+    g.Csplit = (int)Ncol;
+    g.w = wv.data_ptr();
+    g.bias = nullptr;
+    g.act_out = 0;
+    g.act_bwd = 0;
+    g.xb1 = g.xb2 = nullptr;
+    g.y1 = col.data_ptr();
+    g.y2 = nullptr;
+    const int gbn = Ncol <= 16 ? 16 : (Ncol <= 32 ? 32 : (Ncol <= 64 ? 64 : 128));
+    const int gbm = gbn <= 32 ? 256 : 128;
+    check_rc(p2p_conv_fwd(&g, 0, gbm, gbn, st), "conv_fwd(col gemm)");
+    check_rc(p2p_col2im((int)mode, col.data_ptr(), (int)Ncol, (int)N, (int)H, (int)W, (int)OH, (int)OW,
+                        (int)KH, (int)KW, (int)stride, (int)pad, (int)Cv, (int)Cout, a.bias,
+                        (int)act_out, act_bwd ? xb1->data_ptr() : nullptr, (int)act_bwd, y1.data_ptr(),
+                        st),
+             "col2im");
+    return {y1};
+  }
 
   // ---- tile choice: N-tile from Cout, M-tile from the largest parity class
   const int classes = mode == 0 ? 1 : (int)(stride * stride);
@@ -163,8 +221,14 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     mmax = std::max(mmax, N * hq * wq);
     kmax = std::max(kmax, taps * C);
   }
+  const int variant = conv_variant(Cout);
+  const bool glds_ok = variant > 1 && C1 % 64 == 0 && C2 % 64 == 0 && Cout > 32 &&
+                       (act_in == 0 || act_in == 1);
   int bm, bn;
-  if (Cout <= 16) {
+  if (glds_ok) {
+    bn = Cout > 64 ? 128 : 64;
+    bm = variant == 4 ? 256 : 128;
+  } else if (Cout <= 16) {
     bn = 16;
     bm = mmax >= 4096 ? 256 : 64;
   } else if (Cout <= 32) {
@@ -180,18 +244,28 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   const int64_t tiles = ((mmax + bm - 1) / bm) * ((Cout + bn - 1) / bn) * classes;
   const int64_t ktiles = (kmax + 63) / 64;
   int splits = 1;
-  if (tiles < 512 && ktiles >= 8) {
-    splits = (int)std::min<int64_t>((1024 + tiles - 1) / tiles, ktiles / 4);
+  if (tiles < 256 && ktiles >= 8) {
+    splits = (int)std::min<int64_t>((512 + tiles - 1) / tiles, ktiles / 4);
     splits = std::max(1, std::min(splits, 32));
   }
   Tensor ws;
-  hipStream_t st = cur_stream(x1);
   if (splits > 1) {
     ws = at::zeros({N * OH * OW, Cout}, x1.options().dtype(at::kFloat));
     a.ws = ws.data_ptr<float>();
     a.splits = splits;
   }
-  check_rc(p2p_conv_fwd(&a, (int)mode, bm, bn, st), "conv_fwd");
+  int rc = -2;
+  if (glds_ok) rc = p2p_conv_fwd_glds(&a, (int)mode, variant, st);
+  if (rc == -2) {
+    // register-staged kernel: its own tile table
+    int vbm = bm, vbn = bn;
+    if (glds_ok) {
+      vbn = Cout > 64 ? 128 : 64;
+      vbm = 128;
+    }
+    rc = p2p_conv_fwd(&a, (int)mode, vbm, vbn, st);
+  }
+  check_rc(rc, "conv_fwd");
   if (splits > 1) check_rc(p2p_conv_finalize(&a, st), "conv_finalize");
   std::vector<Tensor> out{y1};
   if (y2.defined()) out.push_back(y2);
@@ -254,10 +328,13 @@ void conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, con
   a.OW = (int)OW;
   a.M = (int)(N * OH * OW);
   a.Kq = (int)(KH * KW * C);
-  const int wbr = p2p_conv_wgrad_tile_rows(a.R);
-  const int64_t tiles = ((R + wbr - 1) / wbr) * ((a.Kq + 127) / 128);
+  a.zero = zero_page(p1);
+  int wbr = 128, wbq = 128;
+  p2p_conv_wgrad_tile(&a, &wbr, &wbq);
+  const int64_t tiles = ((R + wbr - 1) / wbr) * ((a.Kq + wbq - 1) / wbq);
   const int64_t stages = ((int64_t)a.M + 63) / 64;
-  int64_t splits = std::max<int64_t>(1, 1024 / std::max<int64_t>(tiles, 1));
+  // >= 2 waves of 256 CUs; every split keeps >= 8 reduction stages (pipeline depth 3)
+  int64_t splits = std::max<int64_t>(1, 512 / std::max<int64_t>(tiles, 1));
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, stages / 8));
   // bound the fp32 slab workspace to ~256 MB
   const int64_t slab = R * (int64_t)a.Kq;
@@ -330,22 +407,28 @@ Tensor norm_apply(const Tensor& x, const Tensor& mean, const Tensor& rstd,
   return y;
 }
 
+// act: the ReLU / LeakyReLU fused by the forward (recomputed from x, no extra pass);
+// dsum: optional [C] fp32 output = column sums of dx (bias grad of the producing conv).
 Tensor norm_bwd(const Tensor& x, const Tensor& dy, const Tensor& mean, const Tensor& rstd,
-                const optional<Tensor>& gamma, const optional<Tensor>& dgamma,
-                const optional<Tensor>& dbeta, bool need_dx, bool batch) {
+                const optional<Tensor>& gamma, const optional<Tensor>& beta, int64_t act,
+                const optional<Tensor>& dgamma, const optional<Tensor>& dbeta, bool need_dx,
+                bool batch, const optional<Tensor>& dsum) {
   check_act(x, "norm_bwd x");
   check_act(dy, "norm_bwd dy");
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
   const int gN = batch ? 1 : (int)N;
   const int gHW = batch ? (int)(N * HW) : (int)HW;
+  if (dsum) TORCH_CHECK(dsum->numel() == C && dsum->scalar_type() == at::kFloat, "norm_bwd: dsum");
   Tensor ws = at::empty({p2p_norm_ws_floats(gN, gHW, (int)C)}, x.options().dtype(at::kFloat));
   Tensor dx;
   if (need_dx) dx = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   check_rc(p2p_norm_bwd(x.data_ptr(), dy.data_ptr(), gN, gHW, (int)C, mean.data_ptr<float>(),
                         rstd.data_ptr<float>(), gamma ? gamma->data_ptr<float>() : nullptr,
+                        beta ? beta->data_ptr<float>() : nullptr, (int)act,
                         dgamma ? dgamma->data_ptr<float>() : nullptr,
                         dbeta ? dbeta->data_ptr<float>() : nullptr, ws.data_ptr<float>(),
-                        need_dx ? dx.data_ptr() : nullptr, cur_stream(x)),
+                        need_dx ? dx.data_ptr() : nullptr,
+                        (need_dx && dsum) ? dsum->data_ptr<float>() : nullptr, cur_stream(x)),
            "norm_bwd");
   return dx;
 }
@@ -506,7 +589,7 @@ void adam(at::TensorList p, at::TensorList g, at::TensorList m, at::TensorList v
 TORCH_LIBRARY(p2p, m) {
   m.def("conv_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, int mode, int KH, int KW, int stride, "
         "int pad, int reflect, int up, int act_in, int OH, int OW, int Cout, int act_out, int Csplit, "
-        "Tensor? xb1, Tensor? xb2, int act_bwd) -> Tensor[]");
+        "Tensor? xb1, Tensor? xb2, int act_bwd, int Cvalid=0) -> Tensor[]");
   m.def("conv_wgrad(Tensor p1, Tensor? p2, int p_act, Tensor q1, Tensor? q2, int q_act, int KH, int KW, "
         "int stride, int pad, int reflect, int up, Tensor(a!) dw, float scale, int accumulate) -> ()");
   m.def("weight_prep(Tensor w, int swap, int Xp, int Yp, Tensor? scale) -> Tensor");
@@ -514,8 +597,8 @@ TORCH_LIBRARY(p2p, m) {
         "Tensor(a!)? run_mean, Tensor(b!)? run_var, float momentum, bool batch) -> Tensor[]");
   m.def("norm_apply(Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? prelu_w, "
         "int act, bool batch) -> Tensor");
-  m.def("norm_bwd(Tensor x, Tensor dy, Tensor mean, Tensor rstd, Tensor? gamma, Tensor(a!)? dgamma, "
-        "Tensor(b!)? dbeta, bool need_dx, bool batch) -> Tensor");
+  m.def("norm_bwd(Tensor x, Tensor dy, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, int act, "
+        "Tensor(a!)? dgamma, Tensor(b!)? dbeta, bool need_dx, bool batch, Tensor(c!)? dsum) -> Tensor");
   m.def("act(Tensor a, Tensor? b, int act, int mode) -> Tensor");
   m.def("dropout(Tensor x, float p, Tensor seed, int salt) -> Tensor");
   m.def("pad_channels(Tensor a, Tensor? b, int Co) -> Tensor");

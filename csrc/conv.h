@@ -30,6 +30,7 @@ struct ConvFwdArgs {
   int act_bwd;
   float* ws;       // split-K fp32 accumulator [N*OH*OW][Cout] (pre-zeroed) when splits > 1
   int splits;
+  const void* zero;  // >= 16 zero bytes in global memory (global_load_lds padding source)
 };
 
 // Weight gradient: C[R][Kq] = sum_m P[m][R] * im2col(Q)[m][Kq], written to per-split
@@ -52,6 +53,7 @@ struct ConvWgradArgs {
   int splits;
   int M;           // N*OH*OW
   int Kq;          // KH*KW*C
+  const void* zero;  // zero page for the global_load_lds variant
 };
 
 }  // namespace p2p
@@ -59,10 +61,17 @@ struct ConvWgradArgs {
 extern "C" {
 int p2p_conv_fwd(const p2p::ConvFwdArgs* a, int mode, int bm, int bn, hipStream_t stream);
 int p2p_conv_finalize(const p2p::ConvFwdArgs* a, hipStream_t stream);
+// global_load_lds pipelined variant (FAST layers, BN in {64, 128}); returns -2 if the
+// configuration is not supported so the caller can fall back to p2p_conv_fwd.
+int p2p_conv_fwd_glds(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t stream);
 int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t stream);
 int p2p_conv_wgrad_tile_rows(int R);
+int p2p_conv_wgrad_tile(const p2p::ConvWgradArgs* a, int* tile_r, int* tile_q);
 int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int KW, int C, int Rr, int Cr,
                      float* dw, float scale, int accumulate, hipStream_t stream);
+int p2p_col2im(int mode, const void* col, int ldc, int N, int H, int W, int OH, int OW, int KH, int KW,
+               int s, int p, int Cv, int Coutp, const float* bias, int act_out, const void* xb,
+               int act_bwd, void* y, hipStream_t stream);
 int p2p_weight_prep(const float* w, int A, int B, int KH, int KW, int swap, int Xp, int Yp,
                     const float* scale, void* out, hipStream_t stream);
 }

@@ -1,0 +1,144 @@
+// Device-side pieces shared by the implicit-GEMM conv kernels (conv_fwd.hip: register-
+// staged; conv_fwd_glds.hip: global_load_lds multi-stage): tile geometry of the two GEMM
+// modes, the LDS swizzle of the [rows][64] bf16 operand tiles, and the fused epilogue.
+#pragma once
+#include "common.h"
+#include "conv.h"
+
+namespace p2p {
+
+constexpr int BK = 64;
+
+__device__ __forceinline__ int swz(int row, int chunk) {  // element offset in a [rows][64] tile
+  return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3);
+}
+
+struct ClassGeom {
+  int ry, rx, ky0, kx0, dy, dx, Tj, Ti, Hq, Wq, Mc, Kc;
+};
+
+template <int MODE>
+__device__ __forceinline__ ClassGeom class_geom(const ConvFwdArgs& a, int cls) {
+  ClassGeom g;
+  if (MODE == 0) {
+    g.ry = g.rx = g.ky0 = g.kx0 = g.dy = g.dx = 0;
+    g.Tj = a.KH;
+    g.Ti = a.KW;
+    g.Hq = a.OH;
+    g.Wq = a.OW;
+  } else {
+    const int s = a.stride, p = a.pad;
+    g.ry = cls / s;
+    g.rx = cls % s;
+    g.ky0 = (g.ry + p) % s;
+    g.kx0 = (g.rx + p) % s;
+    g.dy = (g.ry + p - g.ky0) / s;
+    g.dx = (g.rx + p - g.kx0) / s;
+    g.Tj = g.ky0 < a.KH ? (a.KH - g.ky0 + s - 1) / s : 0;
+    g.Ti = g.kx0 < a.KW ? (a.KW - g.kx0 + s - 1) / s : 0;
+    g.Hq = a.OH > g.ry ? (a.OH - g.ry + s - 1) / s : 0;
+    g.Wq = a.OW > g.rx ? (a.OW - g.rx + s - 1) / s : 0;
+  }
+  g.Mc = a.N * g.Hq * g.Wq;
+  g.Kc = g.Tj * g.Ti * a.C;
+  return g;
+}
+
+// bias + output activation in registers, the bf16 tile staged through LDS, 16-B stores
+// with the optional act'(x) multiply (dgrad) and the concat channel split; split-K tiles
+// accumulate fp32 atomics instead.
+template <int BM, int BN, int WM, int WN, int MODE, int NT>
+__device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassGeom& g,
+                                              f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
+                                              int n0, char* smem, const FastDiv& fd_hwq,
+                                              const FastDiv& fd_wq) {
+  constexpr int TM = BM / WM / 16;
+  constexpr int TN = BN / WN / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int HWq = g.Hq * g.Wq;
+  const int s = a.stride;
+  auto out_pix = [&](int m) -> long {
+    if (MODE == 0) return m;
+    const int n = (int)fdiv((uint32_t)m, fd_hwq);
+    const int r = m - n * HWq;
+    const int qy = (int)fdiv((uint32_t)r, fd_wq);
+    const int qx = r - qy * g.Wq;
+    return ((long)n * a.OH + qy * s + g.ry) * a.OW + qx * s + g.rx;
+  };
+
+  // ---- split-K: fp32 atomics straight from the accumulators (tiny-M layers only)
+  if (a.splits > 1) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * TN * 16 + j * 16 + (lane & 15);
+        const int rowb = m0 + wm * TM * 16 + i * 16 + (lane >> 4) * 4;
+        if (col >= a.Cout) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = rowb + r;
+          if (m < g.Mc) atomicAdd(a.ws + out_pix(m) * a.Cout + col, acc[i][j][r]);
+        }
+      }
+    return;
+  }
+
+  // ---- epilogue: bias + act in registers, bf16 tile staged in LDS, 16-B stores
+  bf16* Cs = reinterpret_cast<bf16*>(smem);
+  constexpr int LDC = BN + 8;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int coll = wn * TN * 16 + j * 16 + (lane & 15);
+    const int col = n0 + coll;
+    const float bj = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rowb = wm * TM * 16 + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(rowb + r) * LDC + coll] = (bf16)act_fwd(acc[i][j][r] + bj, a.act_out);
+    }
+  }
+  __syncthreads();
+
+  constexpr int CPR = BN / 8;  // 8-channel chunks per row
+  for (int c = tid; c < BM * CPR; c += NT) {
+    const int row = c / CPR, cc = c - row * CPR;
+    const int m = m0 + row;
+    const int co = n0 + cc * 8;
+    if (m >= g.Mc || co >= a.Cout) continue;
+    const long pix = out_pix(m);
+    u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * LDC + cc * 8);
+    const bool first = co < a.Csplit;
+    const int ld = first ? a.Csplit : a.Cout - a.Csplit;
+    const int cof = first ? co : co - a.Csplit;
+    if (a.act_bwd) {
+      const bf16* xb = static_cast<const bf16*>(first ? a.xb1 : a.xb2);
+      const u32x4 xv = *reinterpret_cast<const u32x4*>(xb + pix * ld + cof);
+      if (a.act_bwd == ACT_RELU) {
+        // zero the gradient where x <= 0 (bf16 sign / zero test on the int pipe)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t xw = xv[q];
+          uint32_t keep = 0;
+          if ((int16_t)(xw & 0xffffu) > 0) keep |= 0xffffu;
+          if ((int16_t)(xw >> 16) > 0) keep |= 0xffff0000u;
+          v[q] &= keep;
+        }
+      } else {
+        bf16x8 vb = __builtin_bit_cast(bf16x8, v);
+        const bf16x8 xb8 = __builtin_bit_cast(bf16x8, xv);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          vb[q] = (bf16)((float)vb[q] * act_grad_from_input((float)xb8[q], a.act_bwd));
+        v = __builtin_bit_cast(u32x4, vb);
+      }
+    }
+    bf16* y = static_cast<bf16*>(first ? a.y1 : a.y2);
+    *reinterpret_cast<u32x4*>(y + pix * ld + cof) = v;
+  }
+}
+
+}  // namespace p2p

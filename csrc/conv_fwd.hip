@@ -35,47 +35,9 @@
 //    (gradient of a virtual concat).  Split-K (tiny-M bottleneck layers) accumulates
 //    fp32 atomics straight from the accumulators, finished by conv_finalize_kernel.
 //  * Workgroup ids are remapped XCD-aware so the n-tiles of one m-tile share an L2.
-#include "common.h"
-#include "conv.h"
+#include "conv_dev.h"
 
 namespace p2p {
-
-constexpr int BK = 64;
-
-__device__ __forceinline__ int swz(int row, int chunk) {  // element offset in a [rows][64] tile
-  return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3);
-}
-
-struct ClassGeom {
-  int ry, rx, ky0, kx0, dy, dx, Tj, Ti, Hq, Wq, Mc, Kc;
-};
-
-template <int MODE>
-__device__ __forceinline__ ClassGeom class_geom(const ConvFwdArgs& a, int cls) {
-  ClassGeom g;
-  if (MODE == 0) {
-    g.ry = g.rx = g.ky0 = g.kx0 = g.dy = g.dx = 0;
-    g.Tj = a.KH;
-    g.Ti = a.KW;
-    g.Hq = a.OH;
-    g.Wq = a.OW;
-  } else {
-    const int s = a.stride, p = a.pad;
-    g.ry = cls / s;
-    g.rx = cls % s;
-    g.ky0 = (g.ry + p) % s;
-    g.kx0 = (g.rx + p) % s;
-    g.dy = (g.ry + p - g.ky0) / s;
-    g.dx = (g.rx + p - g.kx0) / s;
-    g.Tj = g.ky0 < a.KH ? (a.KH - g.ky0 + s - 1) / s : 0;
-    g.Ti = g.kx0 < a.KW ? (a.KW - g.kx0 + s - 1) / s : 0;
-    g.Hq = a.OH > g.ry ? (a.OH - g.ry + s - 1) / s : 0;
-    g.Wq = a.OW > g.rx ? (a.OW - g.rx + s - 1) / s : 0;
-  }
-  g.Mc = a.N * g.Hq * g.Wq;
-  g.Kc = g.Tj * g.Ti * a.C;
-  return g;
-}
 
 template <int BM, int BN>
 struct FwdSmem {
@@ -295,88 +257,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvFwdArgs a) {
     buf ^= 1;
   }
 
-  const int s = a.stride;
-  auto out_pix = [&](int m) -> long {
-    if (MODE == 0) return m;
-    const int n = (int)fdiv((uint32_t)m, fd_hwq);
-    const int r = m - n * HWq;
-    const int qy = (int)fdiv((uint32_t)r, fd_wq);
-    const int qx = r - qy * g.Wq;
-    return ((long)n * a.OH + qy * s + g.ry) * a.OW + qx * s + g.rx;
-  };
-
-  // ---- split-K: fp32 atomics straight from the accumulators (tiny-M layers only)
-  if (a.splits > 1) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wn * TN * 16 + j * 16 + (lane & 15);
-        const int rowb = m0 + wm * TM * 16 + i * 16 + (lane >> 4) * 4;
-        if (col >= a.Cout) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = rowb + r;
-          if (m < g.Mc) atomicAdd(a.ws + out_pix(m) * a.Cout + col, acc[i][j][r]);
-        }
-      }
-    return;
-  }
-
-  // ---- epilogue: bias + act in registers, bf16 tile staged in LDS, 16-B stores
-  bf16* Cs = reinterpret_cast<bf16*>(smem);
-  constexpr int LDC = BN + 8;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int coll = wn * TN * 16 + j * 16 + (lane & 15);
-    const int col = n0 + coll;
-    const float bj = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int rowb = wm * TM * 16 + i * 16 + (lane >> 4) * 4;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Cs[(rowb + r) * LDC + coll] = (bf16)act_fwd(acc[i][j][r] + bj, a.act_out);
-    }
-  }
-  __syncthreads();
-
-  constexpr int CPR = BN / 8;  // 8-channel chunks per row
-  for (int c = tid; c < BM * CPR; c += 256) {
-    const int row = c / CPR, cc = c - row * CPR;
-    const int m = m0 + row;
-    const int co = n0 + cc * 8;
-    if (m >= g.Mc || co >= a.Cout) continue;
-    const long pix = out_pix(m);
-    u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * LDC + cc * 8);
-    const bool first = co < a.Csplit;
-    const int ld = first ? a.Csplit : a.Cout - a.Csplit;
-    const int cof = first ? co : co - a.Csplit;
-    if (a.act_bwd) {
-      const bf16* xb = static_cast<const bf16*>(first ? a.xb1 : a.xb2);
-      const u32x4 xv = *reinterpret_cast<const u32x4*>(xb + pix * ld + cof);
-      if (a.act_bwd == ACT_RELU) {
-        // zero the gradient where x <= 0 (bf16 sign / zero test on the int pipe)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t xw = xv[q];
-          uint32_t keep = 0;
-          if ((int16_t)(xw & 0xffffu) > 0) keep |= 0xffffu;
-          if ((int16_t)(xw >> 16) > 0) keep |= 0xffff0000u;
-          v[q] &= keep;
-        }
-      } else {
-        bf16x8 vb = __builtin_bit_cast(bf16x8, v);
-        const bf16x8 xb8 = __builtin_bit_cast(bf16x8, xv);
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          vb[q] = (bf16)((float)vb[q] * act_grad_from_input((float)xb8[q], a.act_bwd));
-        v = __builtin_bit_cast(u32x4, vb);
-      }
-    }
-    bf16* y = static_cast<bf16*>(first ? a.y1 : a.y2);
-    *reinterpret_cast<u32x4*>(y + pix * ld + cof) = v;
-  }
+  conv_epilogue<BM, BN, WM, WN, MODE, 256>(a, g, acc, m0, n0, smem, fd_hwq, fd_wq);
 }
 
 // split-K finish: ws [P][Cout] fp32 -> bias / act / act' / channel split -> bf16
@@ -513,5 +394,97 @@ extern "C" int p2p_weight_prep(const float* w, int A, int B, int KH, int KW, int
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(p2p::weight_prep_kernel, dim3((unsigned)blocks), dim3(256), 0, st, w, A, B, KH, KW,
                      swap, Xp, Yp, scale, static_cast<p2p::bf16*>(out));
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// col2im for the tiny-Cout "col" path (U-Net head, PatchGAN logits, first-layer dgrad):
+// the dense GEMM col[i][t*Cv + co] = sum_ci x[i][ci] w[co][t][ci] ran over the INPUT
+// pixels (N = taps x Cv, no MFMA lanes wasted on padded output channels); here every
+// output pixel gathers its taps:
+//   MODE 0 (conv):  input i = o*s - p + t            (if inside the image)
+//   MODE 1 (convT): input i = (o + p - t) / s        (if divisible and inside)
+// then bias, output activation, optional act'(xb) (dgrad) and zero padded channels.
+namespace p2p {
+template <int MODE>
+__global__ void __launch_bounds__(256) col2im_kernel(const bf16* __restrict__ col, int ldc, int N, int H,
+                                                     int W, int OH, int OW, int KH, int KW, int s, int p,
+                                                     int Cv, int Coutp, const float* __restrict__ bias,
+                                                     int act_out, const bf16* __restrict__ xb, int act_bwd,
+                                                     bf16* __restrict__ y) {
+  const int groups = Coutp / 8;
+  const long total = (long)N * OH * OW * groups;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int gq = (int)(e % groups);
+    const long o = e / groups;
+    const int ox = (int)(o % OW);
+    const long t1 = o / OW;
+    const int oy = (int)(t1 % OH);
+    const int n = (int)(t1 / OH);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int ky = 0; ky < KH; ++ky) {
+      int iy;
+      if (MODE == 0) {
+        iy = oy * s - p + ky;
+      } else {
+        const int num = oy + p - ky;
+        if (num < 0 || num % s) continue;
+        iy = num / s;
+      }
+      if ((unsigned)iy >= (unsigned)H) continue;
+      for (int kx = 0; kx < KW; ++kx) {
+        int ix;
+        if (MODE == 0) {
+          ix = ox * s - p + kx;
+        } else {
+          const int num = ox + p - kx;
+          if (num < 0 || num % s) continue;
+          ix = num / s;
+        }
+        if ((unsigned)ix >= (unsigned)W) continue;
+        const bf16* src = col + ((long)(n * H + iy) * W + ix) * ldc + (ky * KW + kx) * Cv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int co = gq * 8 + j;
+          if (co < Cv) acc[j] += (float)src[co];
+        }
+      }
+    }
+    bf16x8 out;
+    bf16x8 xv;
+    if (act_bwd) xv = *reinterpret_cast<const bf16x8*>(xb + o * Coutp + gq * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int co = gq * 8 + j;
+      float v = 0.f;
+      if (co < Cv) {
+        v = act_fwd(acc[j] + (bias ? bias[co] : 0.f), act_out);
+        if (act_bwd) v *= act_grad_from_input((float)xv[j], act_bwd);
+      }
+      out[j] = (bf16)v;
+    }
+    *reinterpret_cast<bf16x8*>(y + o * Coutp + gq * 8) = out;
+  }
+}
+}  // namespace p2p
+
+extern "C" int p2p_col2im(int mode, const void* col, int ldc, int N, int H, int W, int OH, int OW, int KH,
+                          int KW, int s, int p, int Cv, int Coutp, const float* bias, int act_out,
+                          const void* xb, int act_bwd, void* y, hipStream_t st) {
+  const long total = (long)N * OH * OW * (Coutp / 8);
+  long blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  const p2p::bf16* c = static_cast<const p2p::bf16*>(col);
+  const p2p::bf16* x = static_cast<const p2p::bf16*>(xb);
+  p2p::bf16* o = static_cast<p2p::bf16*>(y);
+  if (mode == 0)
+    hipLaunchKernelGGL(p2p::col2im_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, st, c, ldc, N, H, W, OH,
+                       OW, KH, KW, s, p, Cv, Coutp, bias, act_out, x, act_bwd, o);
+  else
+    hipLaunchKernelGGL(p2p::col2im_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, st, c, ldc, N, H, W, OH,
+                       OW, KH, KW, s, p, Cv, Coutp, bias, act_out, x, act_bwd, o);
   return (int)hipGetLastError();
 }

@@ -17,6 +17,8 @@
 // batch); each writes its fp32 partial [R][Kq] slab with plain stores and
 // wgrad_reduce_kernel sums the slabs in a fixed order (bitwise deterministic, no
 // atomics) while permuting into PyTorch's [R][C][KH][KW] weight layout.
+#include <cstdlib>
+
 #include "common.h"
 #include "conv.h"
 
@@ -219,6 +221,195 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// LDS-DMA (global_load_lds) pipelined variant for the big layers: 8 waves, a 256x128 or
+// 128x256 (R x Kq) output tile, a STAGES-deep ring of 64-row reduction stages.  Both
+// operand tiles are stored as 128-column [64][128] sub-tiles with the swz_t image above;
+// glds writes them lane-linearly (4 rows x 256 B per wave instruction), so the XOR
+// swizzle is applied to the SOURCE chunk index (rule 21).  Out-of-range rows / taps read
+// a zero page; the input activations (ReLU) are applied to the fragments after the
+// transposing LDS reads.
+template <int N>
+__device__ __forceinline__ void wg_wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int TBR, int TBQ, int WM, int WN, int STAGES>
+__global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgradArgs a) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int TM = TBR / WM / 16, TN = TBQ / WN / 16;
+  constexpr int PSUB = TBR / 128, QSUB = TBQ / 128;
+  constexpr int PL = WBM * (TBR / 8) / NT;   // glds per thread per stage
+  constexpr int QL = WBM * (TBQ / 8) / NT;
+  constexpr int LOADS = PL + QL;
+  constexpr int SUBE = WBM * WROW;           // elements per [64][128] sub-tile
+  static_assert(PL >= 1 && QL >= 1 && (WBM * (TBR / 8)) % NT == 0 && (WBM * (TBQ / 8)) % NT == 0,
+                "every wave issues the same glds count");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* Ps = reinterpret_cast<bf16*>(smem);          // [STAGES][PSUB][64][128]
+  bf16* Qs = Ps + STAGES * PSUB * SUBE;              // [STAGES][QSUB][64][128]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int qtiles = (a.Kq + TBQ - 1) / TBQ;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int rt = bid / qtiles, qt = bid % qtiles;
+  const int r0 = rt * TBR, q0 = qt * TBQ;
+
+  const int stages = (a.M + WBM - 1) / WBM;
+  const int sps = (stages + a.splits - 1) / a.splits;
+  const int s0 = blockIdx.y * sps;
+  const int s1 = min(stages, s0 + sps);
+
+  const bf16* __restrict__ p1 = static_cast<const bf16*>(a.p1);
+  const bf16* __restrict__ p2 = static_cast<const bf16*>(a.p2);
+  const bf16* __restrict__ q1 = static_cast<const bf16*>(a.q1);
+  const bf16* __restrict__ q2 = static_cast<const bf16*>(a.q2);
+  const bf16* zero = static_cast<const bf16*>(a.zero);
+
+  // ---- per-load fixed decode (row within stage, source column)
+  int p_row[PL], p_lds[PL];
+  const bf16* p_base[PL];
+  int p_ld[PL];
+#pragma unroll
+  for (int i = 0; i < PL; ++i) {
+    const int q = tid + NT * i;
+    const int sub = q >> 10, rem = q & 1023;
+    const int row = rem >> 4, slot = rem & 15;
+    const int x = ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
+    const int col = r0 + sub * 128 + ((slot ^ x) << 3);
+    const bool first = col < a.R1;
+    p_row[i] = col < a.R ? row : -1;
+    p_base[i] = first ? p1 + col : p2 + (col - a.R1);
+    p_ld[i] = first ? a.R1 : a.R2;
+    p_lds[i] = sub * SUBE + ((q & ~63) & 1023) * 8;   // wave-uniform LDS element offset
+  }
+  int q_row[QL], q_lds[QL], q_kh[QL], q_kw[QL], q_ld[QL];
+  const bf16* q_base[QL];
+#pragma unroll
+  for (int i = 0; i < QL; ++i) {
+    const int q = tid + NT * i;
+    const int sub = q >> 10, rem = q & 1023;
+    const int row = rem >> 4, slot = rem & 15;
+    const int x = ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
+    const int kq = q0 + sub * 128 + ((slot ^ x) << 3);
+    int tap = 0, ci = 0;
+    const bool ok = kq < a.Kq;
+    if (ok) {
+      tap = kq / a.C;
+      ci = kq - tap * a.C;
+    }
+    q_kh[i] = tap / a.KW;
+    q_kw[i] = tap - q_kh[i] * a.KW;
+    const bool first = ci < a.C1;
+    q_base[i] = first ? q1 + ci : q2 + (ci - a.C1);
+    q_ld[i] = first ? a.C1 : a.C2;
+    q_row[i] = ok ? row : -1;
+    q_lds[i] = sub * SUBE + ((q & ~63) & 1023) * 8;
+  }
+  const int ush = a.up == 2 ? 1 : 0;
+  const int Hu = a.H << ush, Wu = a.W << ush;
+  const int OHW = a.OH * a.OW;
+  const FastDiv fd_ohw = make_fastdiv((uint32_t)OHW), fd_ow = make_fastdiv((uint32_t)a.OW);
+
+  auto issue = [&](int st, int stage) {
+    bf16* Pst = Ps + stage * PSUB * SUBE;
+    bf16* Qst = Qs + stage * QSUB * SUBE;
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+      const int m = st * WBM + p_row[i];
+      const bool ok = p_row[i] >= 0 && m < a.M;
+      const bf16* gp = ok ? p_base[i] + (long)m * p_ld[i] : zero;
+      __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)(Pst + p_lds[i]),
+                                       16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < QL; ++i) {
+      const int m = st * WBM + (q_row[i] >= 0 ? q_row[i] : 0);
+      const int n = (int)fdiv((uint32_t)m, fd_ohw);
+      const int rem = m - n * OHW;
+      const int oh = (int)fdiv((uint32_t)rem, fd_ow);
+      const int ow = rem - oh * a.OW;
+      int uy = oh * a.stride - a.pad + q_kh[i];
+      int ux = ow * a.stride - a.pad + q_kw[i];
+      if (a.reflect) {
+        uy = reflect_idx(uy, Hu);
+        ux = reflect_idx(ux, Wu);
+      }
+      const bool ok = q_row[i] >= 0 && m < a.M && (unsigned)uy < (unsigned)Hu &&
+                      (unsigned)ux < (unsigned)Wu;
+      const long pix = ((long)n * a.H + (uy >> ush)) * a.W + (ux >> ush);
+      const bf16* gp = ok ? q_base[i] + pix * q_ld[i] : zero;
+      __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)(Qst + q_lds[i]),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int sgi = 0; sgi < STAGES - 1; ++sgi)
+    if (s0 + sgi < s1) issue(s0 + sgi, sgi);
+
+  const bool p_relu = a.p_act == ACT_RELU, q_relu = a.q_act == ACT_RELU;
+  int stage = 0;
+  for (int st = s0; st < s1; ++st) {
+    if (st + STAGES - 2 < s1) wg_wait_vmcnt<LOADS * (STAGES - 2)>();
+    else wg_wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + STAGES - 1 < s1) {
+      int ns = stage + STAGES - 1;
+      if (ns >= STAGES) ns -= STAGES;
+      issue(st + STAGES - 1, ns);
+    }
+    const bf16* P = Ps + stage * PSUB * SUBE;
+    const bf16* Q = Qs + stage * QSUB * SUBE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int cb = wm * (TBR / WM) + i * 16;
+        bf16x8 v = tr_frag(P + (cb >> 7) * SUBE, kk * 32, cb & 127, lane);
+        if (p_relu) v = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, v)));
+        af[i] = v;
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int cb = wn * (TBQ / WN) + j * 16;
+        bf16x8 v = tr_frag(Q + (cb >> 7) * SUBE, kk * 32, cb & 127, lane);
+        if (q_relu) v = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, v)));
+        bfr[j] = v;
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    stage = stage + 1 == STAGES ? 0 : stage + 1;
+  }
+
+  float* slab = a.ws + (long)blockIdx.y * a.R * a.Kq;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = q0 + wn * (TBQ / WN) + j * 16 + (lane & 15);
+      const int rowb = r0 + wm * (TBR / WM) + i * 16 + (lane >> 4) * 4;
+      if (col < a.Kq) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (rowb + r < a.R) slab[(long)(rowb + r) * a.Kq + col] = acc[i][j][r];
+      }
+    }
+}
+
 // dw[r][ci][kh][kw] (+)= scale * sum_s ws[s][r][(kh*KW+kw)*C + ci]
 // Block = EPB elements x G split-groups; each thread sums a fixed, strided subset of the
 // splits, then the G partials are combined in LDS in a fixed order (deterministic).
@@ -253,10 +444,56 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 
 }  // namespace p2p
 
+// glds variant geometry: 0 = none (fall back), 1 = 256(R) x 128(Kq), 2 = 128(R) x 256(Kq)
+static int wgrad_glds_shape(const p2p::ConvWgradArgs* a) {
+  if (!a->zero || a->R % 128 || a->Kq % 128) return 0;
+  // fragments get ReLU only (LeakyReLU inputs are stored pre-activated by the models)
+  if ((a->p_act != p2p::ACT_NONE && a->p_act != p2p::ACT_RELU) ||
+      (a->q_act != p2p::ACT_NONE && a->q_act != p2p::ACT_RELU))
+    return 0;
+  const char* v = std::getenv("P2P_CONV_VARIANT");
+  if (v && v[0] == 'v') return 0;
+  if (a->R >= 256) return 1;
+  return a->Kq >= 256 ? 2 : 0;
+}
+
+extern "C" int p2p_conv_wgrad_tile(const p2p::ConvWgradArgs* a, int* tr, int* tq) {
+  const int shape = wgrad_glds_shape(a);
+  if (shape == 1) { *tr = 256; *tq = 128; return shape; }
+  if (shape == 2) { *tr = 128; *tq = 256; return shape; }
+  *tr = a->R <= 16 ? 16 : (a->R <= 64 ? 64 : 128);
+  *tq = 128;
+  return 0;
+}
+
 extern "C" int p2p_conv_wgrad_tile_rows(int R) { return R <= 16 ? 16 : (R <= 64 ? 64 : 128); }
 
 extern "C" int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t st) {
   using namespace p2p;
+  const int shape = wgrad_glds_shape(a);
+  if (shape) {
+    constexpr int STG = 3;
+    const int tr = shape == 1 ? 256 : 128, tq = shape == 1 ? 128 : 256;
+    const int smem = STG * (tr + tq) * WBM * 2;
+    dim3 grid(((a->R + tr - 1) / tr) * ((a->Kq + tq - 1) / tq), a->splits, 1);
+    static bool set1 = false, set2 = false;
+    if (shape == 1) {
+      if (!set1) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_glds_kernel<256, 128, 4, 2, STG>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+        set1 = true;
+      }
+      hipLaunchKernelGGL((conv_wgrad_glds_kernel<256, 128, 4, 2, STG>), grid, dim3(512), smem, st, *a);
+    } else {
+      if (!set2) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_glds_kernel<128, 256, 2, 4, STG>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+        set2 = true;
+      }
+      hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 256, 2, 4, STG>), grid, dim3(512), smem, st, *a);
+    }
+    return (int)hipGetLastError();
+  }
   constexpr int smem = 2 * 2 * WBM * WROW * 2;  // 64 KB
   const int tbr = p2p_conv_wgrad_tile_rows(a->R);
   const int rtiles = (a->R + tbr - 1) / tbr;

@@ -187,14 +187,56 @@ __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict_
 }
 
 // ---------------------------------------------------------------- backward
-// ws: [N][nchunks][C] sum(dy), [N][nchunks][C] sum(dy*xhat)
-__global__ void __launch_bounds__(256) norm_bwd_partial_kernel(const bf16* __restrict__ x,
-                                                               const bf16* __restrict__ dy,
-                                                               NormGeom g,
-                                                               const float* __restrict__ mean,
-                                                               const float* __restrict__ rstd,
-                                                               const float* __restrict__ gamma,
-                                                               float* __restrict__ ws) {
+// The forward may have fused an activation: y = act(z), z = xhat*gamma + beta.  For ReLU /
+// LeakyReLU the backward recomputes z from x and the saved statistics, so the act' gate
+// (dy_eff = dy * act'(z)) costs no extra pass over memory.  Tanh / sigmoid (family-R
+// output layer only) go through the separate act kernel before this one.
+__device__ __forceinline__ float act_gate(float z, int act) {
+  if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
+  if (act == ACT_LRELU) return z > 0.f ? 1.f : LRELU_SLOPE;
+  return 1.f;
+}
+
+// block reduction of per-thread [8]-channel partials over the RP pixel rows -> out[c]
+__device__ __forceinline__ void block_rows_reduce(const float* s1, const float* s2, int C, int cg,
+                                                  int tr, int RP, float* red1, float* red2,
+                                                  float* out1, float* out2) {
+  const int tid = threadIdx.x;
+  const int rows_red = 2048 / C;
+  for (int base_r = 0; base_r < RP; base_r += rows_red) {
+    if (tr >= base_r && tr < base_r + rows_red && tr < RP) {
+      const int r = tr - base_r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (base_r == 0) {
+          red1[r * C + cg * 8 + j] = s1[j];
+          if (s2) red2[r * C + cg * 8 + j] = s2[j];
+        } else {
+          red1[r * C + cg * 8 + j] += s1[j];
+          if (s2) red2[r * C + cg * 8 + j] += s2[j];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const int rr = min(RP, rows_red);
+  for (int c = tid; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rr; ++r) {
+      a += red1[r * C + c];
+      if (s2) b += red2[r * C + c];
+    }
+    out1[c] = a;
+    if (s2) out2[c] = b;
+  }
+}
+
+// ws: [N][nchunks][C] sum(dy_eff * gs), [N][nchunks][C] sum(dy_eff * gs * xhat);
+// gs = gamma (dx pass) or 1 (dgamma / dbeta pass: scale_gamma = 0)
+__global__ void __launch_bounds__(256) norm_bwd_partial_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ dy, NormGeom g,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta, int act, int scale_gamma, float* __restrict__ ws) {
   const int n = blockIdx.y, cb = blockIdx.x;
   const int CP = g.C >> 3;
   const int RP = 256 / CP;
@@ -202,61 +244,43 @@ __global__ void __launch_bounds__(256) norm_bwd_partial_kernel(const bf16* __res
   const int cg = tid % CP, tr = tid / CP;
   const int p0 = cb * g.chunk;
   const int p1 = min(g.HW, p0 + g.chunk);
-  const long off = (long)n * g.HW * g.C;
-  float mu[8], rs[8], ga[8], s1[8], s2[8];
+  const long off = (long)n * g.HW * g.C + cg * 8;
+  float mu[8], rs[8], ga[8], be[8], gs[8], s1[8], s2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     mu[j] = mean[(long)n * g.C + cg * 8 + j];
     rs[j] = rstd[(long)n * g.C + cg * 8 + j];
     ga[j] = gamma ? gamma[cg * 8 + j] : 1.f;
+    be[j] = gamma ? beta[cg * 8 + j] : 0.f;
+    gs[j] = scale_gamma ? ga[j] : 1.f;
     s1[j] = s2[j] = 0.f;
   }
   if (tr < RP) {
     for (int p = p0 + tr; p < p1; p += RP) {
       float fx[8], fd[8];
-      unpack8(*reinterpret_cast<const u32x4*>(x + off + (long)p * g.C + cg * 8), fx);
-      unpack8(*reinterpret_cast<const u32x4*>(dy + off + (long)p * g.C + cg * 8), fd);
+      unpack8(*reinterpret_cast<const u32x4*>(x + off + (long)p * g.C), fx);
+      unpack8(*reinterpret_cast<const u32x4*>(dy + off + (long)p * g.C), fd);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float d = fd[j] * ga[j];
+        const float xh = (fx[j] - mu[j]) * rs[j];
+        const float d = fd[j] * act_gate(xh * ga[j] + be[j], act) * gs[j];
         s1[j] += d;
-        s2[j] += d * (fx[j] - mu[j]) * rs[j];
+        s2[j] += d * xh;
       }
     }
   }
   __shared__ float red1[2048], red2[2048];
-  const int rows_red = 2048 / g.C;
-  for (int base_r = 0; base_r < RP; base_r += rows_red) {
-    if (tr >= base_r && tr < base_r + rows_red && tr < RP) {
-      const int r = tr - base_r;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (base_r == 0) {
-          red1[r * g.C + cg * 8 + j] = s1[j];
-          red2[r * g.C + cg * 8 + j] = s2[j];
-        } else {
-          red1[r * g.C + cg * 8 + j] += s1[j];
-          red2[r * g.C + cg * 8 + j] += s2[j];
-        }
-      }
-    }
-    __syncthreads();
-  }
-  const int rr = min(RP, rows_red);
+  __shared__ float o1[2048], o2[2048];
+  block_rows_reduce(s1, s2, g.C, cg, tr, RP, red1, red2, o1, o2);
+  __syncthreads();
   for (int c = tid; c < g.C; c += 256) {
-    float a = 0.f, b = 0.f;
-    for (int r = 0; r < rr; ++r) {
-      a += red1[r * g.C + c];
-      b += red2[r * g.C + c];
-    }
     const long o = ((long)n * g.nchunks + cb) * g.C + c;
-    ws[o] = a;
-    ws[(long)g.N * g.nchunks * g.C + o] = b;
+    ws[o] = o1[c];
+    ws[(long)g.N * g.nchunks * g.C + o] = o2[c];
   }
 }
 
-// coef: [N][C] A, [N][C] B, [N][C] Cc  with dx = A*dy + B + Cc*xhat
-// dgamma/dbeta (affine): summed over n in a fixed order by a per-channel thread.
+// coef: [N][C] A, [N][C] B, [N][C] Cc  with dx = A*dy_eff + B + Cc*xhat
 __global__ void __launch_bounds__(256) norm_bwd_finalize_kernel(const float* __restrict__ ws,
                                                                 NormGeom g,
                                                                 const float* __restrict__ rstd,
@@ -281,11 +305,10 @@ __global__ void __launch_bounds__(256) norm_bwd_finalize_kernel(const float* __r
   coef[2 * NC + i] = -r * sdx * inv;
 }
 
+// d(gamma) = sum(dy_eff * xhat), d(beta) = sum(dy_eff) over every group of the channel
 __global__ void __launch_bounds__(256) norm_param_grad_kernel(const float* __restrict__ ws, NormGeom g,
                                                               float* __restrict__ dgamma,
                                                               float* __restrict__ dbeta) {
-  // d(gamma) = sum(dy * xhat), d(beta) = sum(dy); ws holds gamma-scaled sums, so the host
-  // passes gamma == nullptr to the partial kernel for this pass (unscaled dy).
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= g.C) return;
   float sdy = 0.f, sdx = 0.f;
@@ -301,40 +324,81 @@ __global__ void __launch_bounds__(256) norm_param_grad_kernel(const float* __res
   dbeta[c] += sdy;
 }
 
-__global__ void __launch_bounds__(256) norm_bwd_apply_kernel(const bf16* __restrict__ x,
-                                                             const bf16* __restrict__ dy, NormGeom g,
-                                                             const float* __restrict__ mean,
-                                                             const float* __restrict__ rstd,
-                                                             const float* __restrict__ coef,
-                                                             bf16* __restrict__ dx) {
-  // dx = A*dy + B + Cc*xhat = A*dy + (Cc*rstd)*x + (B - Cc*rstd*mean)
+// dx = A*dy_eff + B + Cc*xhat; optionally also block partial column sums of the (bf16)
+// dx -- the bias gradient of the conv that produced x, fused here instead of a re-read.
+__global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ dy, NormGeom g,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta, int act, const float* __restrict__ coef, bf16* __restrict__ dx,
+    float* __restrict__ dsum_ws) {
   const int n = blockIdx.y, cb = blockIdx.x;
   const int CP = g.C >> 3;
   const int RP = 256 / CP;
   const int tid = threadIdx.x;
   const int cg = tid % CP, tr = tid / CP;
-  if (tr >= RP) return;
   const int p0 = cb * g.chunk;
   const int p1 = min(g.HW, p0 + g.chunk);
   const long NC = (long)g.N * g.C;
-  float ca[8], cx[8], c0[8];
+  float mu[8], rs[8], ga[8], be[8], ca[8], cx[8], c0[8], ds[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const long ci = (long)n * g.C + cg * 8 + j;
-    const float cc = coef[2 * NC + ci] * rstd[ci];
+    mu[j] = mean[ci];
+    rs[j] = rstd[ci];
+    ga[j] = gamma ? gamma[cg * 8 + j] : 1.f;
+    be[j] = gamma ? beta[cg * 8 + j] : 0.f;
     ca[j] = coef[ci];
-    cx[j] = cc;
-    c0[j] = coef[NC + ci] - cc * mean[ci];
+    cx[j] = coef[2 * NC + ci];
+    c0[j] = coef[NC + ci];
+    ds[j] = 0.f;
   }
   const long base = (long)n * g.HW * g.C + cg * 8;
-  for (int p = p0 + tr; p < p1; p += RP) {
-    float fx[8], fd[8];
-    unpack8(*reinterpret_cast<const u32x4*>(x + base + (long)p * g.C), fx);
-    unpack8(*reinterpret_cast<const u32x4*>(dy + base + (long)p * g.C), fd);
+  if (tr < RP) {
+    for (int p = p0 + tr; p < p1; p += RP) {
+      float fx[8], fd[8];
+      unpack8(*reinterpret_cast<const u32x4*>(x + base + (long)p * g.C), fx);
+      unpack8(*reinterpret_cast<const u32x4*>(dy + base + (long)p * g.C), fd);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) fd[j] = ca[j] * fd[j] + cx[j] * fx[j] + c0[j];
-    *reinterpret_cast<u32x4*>(dx + base + (long)p * g.C) = pack8(fd);
+      for (int j = 0; j < 8; ++j) {
+        const float xh = (fx[j] - mu[j]) * rs[j];
+        const float d = fd[j] * act_gate(xh * ga[j] + be[j], act);
+        fd[j] = ca[j] * d + c0[j] + cx[j] * xh;
+      }
+      const u32x4 o = pack8(fd);
+      *reinterpret_cast<u32x4*>(dx + base + (long)p * g.C) = o;
+      if (dsum_ws) {
+        float fo[8];
+        unpack8(o, fo);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ds[j] += fo[j];
+      }
+    }
   }
+  if (dsum_ws) {
+    __shared__ float red1[2048];
+    __shared__ float o1[2048];
+    block_rows_reduce(ds, nullptr, g.C, cg, tr, RP, red1, nullptr, o1, nullptr);
+    __syncthreads();
+    for (int c = tid; c < g.C; c += 256) dsum_ws[((long)n * g.nchunks + cb) * g.C + c] = o1[c];
+  }
+}
+
+// out[c] = sum over all blocks of dsum_ws[b][c] (fixed order), G threads per channel
+template <int G>
+__global__ void __launch_bounds__(256) dsum_final_kernel(const float* __restrict__ ws, int nb, int C,
+                                                         float* __restrict__ out) {
+  constexpr int EPB = 256 / G;
+  const int le = threadIdx.x % EPB, sg = threadIdx.x / EPB;
+  const int c = blockIdx.x * EPB + le;
+  float a = 0.f;
+  if (c < C)
+    for (int b = sg; b < nb; b += G) a += ws[(long)b * C + c];
+  __shared__ float red[256];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  if (sg != 0 || c >= C) return;
+  for (int q = 1; q < G; ++q) a += red[q * EPB + le];
+  out[c] = a;
 }
 
 static inline NormGeom make_geom(int N, int HW, int C) {
@@ -342,7 +406,7 @@ static inline NormGeom make_geom(int N, int HW, int C) {
   g.N = N;
   g.HW = HW;
   g.C = C;
-  // ~ 256 blocks per wave of work; at least 64 pixels per block
+  // ~ 2048 blocks of work; at least 64 pixels per block
   long total_px = (long)N * HW;
   int chunk = (int)((total_px + 2047) / 2048);
   chunk = chunk < 64 ? 64 : chunk;
@@ -357,10 +421,10 @@ static inline NormGeom make_geom(int N, int HW, int C) {
 
 extern "C" {
 
-// workspace floats needed by p2p_norm_fwd / p2p_norm_bwd
+// workspace floats needed by p2p_norm_fwd / p2p_norm_bwd (incl. the fused bias-grad partials)
 long p2p_norm_ws_floats(int N, int HW, int C) {
   p2p::NormGeom g = p2p::make_geom(N, HW, C);
-  return 2L * N * g.nchunks * C + 3L * N * C;
+  return 3L * N * g.nchunks * C + 3L * N * C;
 }
 
 int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* gamma,
@@ -392,27 +456,34 @@ int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const
   return (int)hipGetLastError();
 }
 
+// act: ReLU / LeakyReLU fused by the forward (0 = none); dsum (optional, [C] fp32): column
+// sums of dx -- the bias gradient of the producing conv.
 int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const float* mean,
-                 const float* rstd, const float* gamma, float* dgamma, float* dbeta, float* ws,
-                 void* dx, hipStream_t st) {
+                 const float* rstd, const float* gamma, const float* beta, int act, float* dgamma,
+                 float* dbeta, float* ws, void* dx, float* dsum, hipStream_t st) {
   using namespace p2p;
   NormGeom g = make_geom(N, HW, C);
   float* coef = ws + 2L * N * g.nchunks * C;
+  float* dsum_ws = coef + 3L * N * C;
+  const bf16* xb = static_cast<const bf16*>(x);
+  const bf16* db = static_cast<const bf16*>(dy);
   if (dgamma) {
-    hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
-                       static_cast<const bf16*>(x), static_cast<const bf16*>(dy), g, mean, rstd,
-                       (const float*)nullptr, ws);
+    hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st, xb, db, g, mean,
+                       rstd, gamma, beta, act, 0, ws);
     hipLaunchKernelGGL(norm_param_grad_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, g,
                        dgamma, dbeta);
   }
   if (dx) {
-    hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
-                       static_cast<const bf16*>(x), static_cast<const bf16*>(dy), g, mean, rstd,
-                       gamma, ws);
+    hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st, xb, db, g, mean,
+                       rstd, gamma, beta, act, 1, ws);
     hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, ws, g,
                        rstd, gamma, coef);
-    hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st, static_cast<const bf16*>(x), static_cast<const bf16*>(dy), g, mean,
-                       rstd, coef, static_cast<bf16*>(dx));
+    hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st, xb, db, g, mean,
+                       rstd, gamma, beta, act, coef, static_cast<bf16*>(dx),
+                       dsum ? dsum_ws : (float*)nullptr);
+    if (dsum)
+      hipLaunchKernelGGL(dsum_final_kernel<32>, dim3((C + 7) / 8), dim3(256), 0, st, dsum_ws,
+                         N * g.nchunks, C, dsum);
   }
   return (int)hipGetLastError();
 }

@@ -45,6 +45,23 @@ def P():
 def begin_step():
     """Start a new step generation: weight images are re-cast on first use (graph-safe)."""
     _gen[0] += 1
+    _colsum_stash.clear()
+
+
+# Bias gradients fused into the norm backward: NormFn.backward computes the column sums of
+# the dx it returns (the producing conv's dY) in the same pass and parks them here keyed by
+# that tensor; ConvFn.backward picks them up instead of re-reading dY.  Holding the tensor
+# keeps its storage alive, so a key can never alias a recycled allocation.
+_colsum_stash: dict = {}
+
+
+def _stash_colsum(dx, colsum):
+    _colsum_stash[(dx.data_ptr(), tuple(dx.shape))] = (dx, colsum)
+
+
+def _take_colsum(gy):
+    ent = _colsum_stash.pop((gy.data_ptr(), tuple(gy.shape)), None)
+    return None if ent is None else ent[1]
 
 
 def _pad8(c: int) -> int:
@@ -156,7 +173,7 @@ class ConvFn(torch.autograd.Function):
         wimg = _weight_image(weight, swap, Coutp, Cp)
         y = P().conv_fwd(q1, q2, wimg, _bias_padded(bias, Coutp), mode, KH, KW, s, p,
                          int(cfg.reflect), cfg.up, _act_code(cfg.act_in), OH, OW, Coutp,
-                         _act_code(cfg.act_out), Coutp, None, None, 0)[0]
+                         _act_code(cfg.act_out), Coutp, None, None, 0, Cout)[0]
         if Coutp != Cout:
             y = P().slice_channels(y, 0, Cout)
         ctx.cfg = cfg
@@ -192,12 +209,12 @@ class ConvFn(torch.autograd.Function):
                 wimg = _weight_image(weight, 0, Cp, Coutp)
                 outs = P().conv_fwd(gyp, None, wimg, None, 0, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
                                     split, q1 if act_in else None,
-                                    q2 if (act_in and q2 is not None) else None, act_in)
+                                    q2 if (act_in and q2 is not None) else None, act_in, C1 + C2)
             else:
                 wimg = _weight_image(weight, 1, Cp, Coutp)
                 outs = P().conv_fwd(gyp, None, wimg, None, 1, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
                                     split, q1 if act_in else None,
-                                    q2 if (act_in and q2 is not None) else None, act_in)
+                                    q2 if (act_in and q2 is not None) else None, act_in, C1 + C2)
             if q2 is not None:
                 gx1, gx2 = outs[0], outs[1]
             elif packed:
@@ -219,8 +236,10 @@ class ConvFn(torch.autograd.Function):
                 P().conv_wgrad(gyp, None, 0, q1, q2, act_in, KH, KW, s, p, int(cfg.reflect),
                                cfg.up, gw, 1.0, 0)
         if need_b:
-            gb = torch.empty(Cout, device=gy.device, dtype=torch.float32)
-            P().colsum(gyp, gb, 1.0, False)
+            gb = _take_colsum(gy) if cfg.act_out in (None, "none") else None
+            if gb is None:
+                gb = torch.empty(Cout, device=gy.device, dtype=torch.float32)
+                P().colsum(gyp, gb, 1.0, False)
         return gx1, gx2, gw, gb, None
 
 
@@ -273,8 +292,8 @@ class NormFn(torch.autograd.Function):
             rstd = torch.rsqrt(run_var.float() + eps).view(1, -1)
             y = P().norm_apply(x, mean, rstd, g, b, pw, _act_code(act), True)
         ctx.cfg = (eps, act, batch, training)
-        ctx.save_for_backward(x, mean, rstd, gamma, beta, prelu_w,
-                              y if (act or pw is not None) else None)
+        keep_y = act not in (None, "none") and (act not in ("relu", "lrelu") or not training)
+        ctx.save_for_backward(x, mean, rstd, gamma, beta, prelu_w, y if keep_y else None)
         return y
 
     @staticmethod
@@ -283,6 +302,7 @@ class NormFn(torch.autograd.Function):
         eps, act, batch, training = ctx.cfg
         gy = to_nhwc_bf16(gy)
         gpw = None
+        fused_act = 0
         if prelu_w is not None:
             # y = prelu(z); dz = dy * (z > 0 ? 1 : w); dw = sum(dy * z * [z <= 0])
             z = _norm_recompute(x, mean, rstd, gamma, beta, batch)
@@ -292,6 +312,8 @@ class NormFn(torch.autograd.Function):
                 gpw = (gy.float() * zf * neg).sum().reshape(1)
             gy = (gy.float() * torch.where(neg, prelu_w.float(), torch.ones_like(zf))).to(
                 torch.bfloat16).contiguous(memory_format=CL)
+        elif act in ("relu", "lrelu") and training:
+            fused_act = _act_code(act)  # gate recomputed inside the norm backward kernels
         elif act not in (None, "none"):
             gy = P().act(gy, y, _act_code(act), 2)
         need_x = ctx.needs_input_grad[0]
@@ -300,8 +322,11 @@ class NormFn(torch.autograd.Function):
             dg = torch.zeros_like(gamma, dtype=torch.float32)
             db = torch.zeros_like(gamma, dtype=torch.float32)
         g = gamma.detach().float().contiguous() if gamma is not None else None
+        b = beta.detach().float().contiguous() if beta is not None else None
         if not training:
             # eval-mode BN: affine map with frozen statistics
+            if act not in (None, "none") and prelu_w is None:
+                gy = P().act(gy, y, _act_code(act), 2)
             dx = None
             if need_x:
                 scale = rstd.view(-1) * (g if g is not None else 1.0)
@@ -312,7 +337,10 @@ class NormFn(torch.autograd.Function):
                 dg = (gy.float() * xh).sum((0, 2, 3))
                 db = gy.float().sum((0, 2, 3))
             return dx, dg, db, gpw, None, None, None, None, None, None, None
-        dx = P().norm_bwd(x, gy, mean, rstd, g, dg, db, need_x, batch)
+        dsum = torch.empty(x.shape[1], device=x.device, dtype=torch.float32) if need_x else None
+        dx = P().norm_bwd(x, gy, mean, rstd, g, b, fused_act, dg, db, need_x, batch, dsum)
+        if need_x:
+            _stash_colsum(dx, dsum)
         return (dx if need_x else None), dg, db, gpw, None, None, None, None, None, None, None
 
 

@@ -176,6 +176,34 @@ def test_instance_norm(N, C, H):
         assert rel_err(hx.grad, rx.grad) < 3e-2
 
 
+@pytest.mark.parametrize("act", ["lrelu", "relu"])
+def test_conv_instance_norm_act_chain(act):
+    """conv(+bias) -> IN with fused act: the act' gate and the conv bias gradient are fused
+    into the norm backward (bias grad handed to the conv through the colsum stash)."""
+    x = rand_img(2, 64, 16, 16, seed=20)
+    w = torch.randn(128, 64, 4, 4, device=DEV) * 0.03
+    b = torch.randn(128, device=DEV) * 0.1
+    hx, hw, hb = _leaf(x), _leaf(w), _leaf(b)
+    y = ops.instance_norm(ops.conv2d(hx, hw, hb, 2, 1), act=act)
+    gy = rand_img(*y.shape, seed=21)
+    y.backward(gy)
+    rx, rw, rb = _leaf(x.float()), _leaf(w), _leaf(b)
+    # the HIP path stores the conv output in bf16 before the norm: round the oracle's conv
+    # output the same way (straight-through), so both evaluate the ReLU gate on the same
+    # pre-activation instead of flipping gates within bf16 rounding of 0
+    rc = ref.conv2d(rx, rw.to(torch.bfloat16).float(), rb, 2, 1)
+    rc = rc + (rc.to(torch.bfloat16).float() - rc).detach()
+    ry = ref.apply_act(F.instance_norm(rc), act)
+    ry.backward(gy.float())
+    assert rel_err(y, ry) < 3e-2
+    assert rel_err(hx.grad, rx.grad) < 4e-2
+    assert rel_err(hw.grad, rw.grad) < 4e-2
+    # bias before an instance norm has an exactly-zero true gradient: the HIP value is the
+    # column sum of bf16 dY (rounding noise), small against the weight-gradient scale
+    assert hb.grad.abs().max() < 0.05 * hw.grad.abs().max() * 64
+    assert rb.grad.abs().max() < 1e-3
+
+
 def test_batch_norm_train_and_eval():
     N, C, H = 4, 64, 16
     x = bf(torch.randn(N, C, H, H, device=DEV) * 2 + 1)
