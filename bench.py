@@ -38,7 +38,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=64, help="images per GPU")
+    p.add_argument("--batch", type=int, default=128, help="images per GPU (the eager baseline was measured at 128)")
     p.add_argument("--size", type=int, default=256)
     p.add_argument("--netG", default="unet_256")
     p.add_argument("--netD", default="basic")

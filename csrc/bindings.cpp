@@ -169,7 +169,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   hipStream_t st = cur_stream(x1);
   // ---- tiny-Cout "col" path: dense GEMM over the input pixels (N = taps x Cvalid) + col2im
   const int64_t Cv = Cvalid > 0 ? Cvalid : Cout;
-  if (Cout <= 16 && Csplit == Cout && !reflect && up == 1 && C1 % 64 == 0 && C2 % 64 == 0) {
+  if (Cout <= 16 && Cv <= 16 && Csplit == Cout && !reflect && up == 1 && C1 % 64 == 0 &&
+      C2 % 64 == 0) {
     const int64_t T = KH * KW;
     const int64_t Ncol = ((T * Cv + 7) / 8) * 8;
     Tensor wv = w.reshape({-1}).narrow(0, 0, Cout * T * C).view({Cout, T, C}).narrow(0, 0, Cv).transpose(0, 1)
@@ -222,8 +223,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     kmax = std::max(kmax, taps * C);
   }
   const int variant = conv_variant(Cout);
-  const bool glds_ok = variant > 1 && C1 % 64 == 0 && C2 % 64 == 0 && Cout > 32 &&
-                       (act_in == 0 || act_in == 1);
+  const bool glds_ok = variant > 1 && Cout > 32 && (act_in == 0 || act_in == 1);
   int bm, bn;
   if (glds_ok) {
     bn = Cout > 64 ? 128 : 64;
@@ -362,6 +362,46 @@ Tensor weight_prep(const Tensor& w, int64_t swap, int64_t Xp, int64_t Yp,
                            cur_stream(w)),
            "weight_prep");
   return out;
+}
+
+// all weight images of a network in one launch per WP_MAX tensors
+std::vector<Tensor> weight_prep_multi(at::TensorList ws, at::IntArrayRef swap, at::IntArrayRef xp,
+                                      at::IntArrayRef yp) {
+  const size_t n = ws.size();
+  TORCH_CHECK(swap.size() == n && xp.size() == n && yp.size() == n, "weight_prep_multi: list sizes");
+  std::vector<Tensor> outs;
+  outs.reserve(n);
+  const int maxT = p2p_weight_prep_max();
+  std::vector<const float*> W;
+  std::vector<void*> O;
+  std::vector<int> A, B, T, S, X, Y;
+  auto flush = [&]() {
+    if (W.empty()) return;
+    check_rc(p2p_weight_prep_multi((int)W.size(), W.data(), O.data(), A.data(), B.data(), T.data(),
+                                   S.data(), X.data(), Y.data(), cur_stream(ws[0])),
+             "weight_prep_multi");
+    W.clear(); O.clear(); A.clear(); B.clear(); T.clear(); S.clear(); X.clear(); Y.clear();
+  };
+  for (size_t i = 0; i < n; ++i) {
+    const Tensor& w = ws[i];
+    TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.dim() == 4,
+                "weight_prep_multi: fp32 contiguous 4-D weights");
+    const int64_t a = w.size(0), b = w.size(1), kh = w.size(2), kw = w.size(3);
+    TORCH_CHECK(xp[i] >= (swap[i] ? b : a) && yp[i] >= (swap[i] ? a : b), "weight_prep_multi: padding");
+    Tensor out = at::empty({xp[i], kh, kw, yp[i]}, w.options().dtype(at::kBFloat16));
+    outs.push_back(out);
+    W.push_back(w.data_ptr<float>());
+    O.push_back(out.data_ptr());
+    A.push_back((int)a);
+    B.push_back((int)b);
+    T.push_back((int)(kh * kw));
+    S.push_back((int)swap[i]);
+    X.push_back((int)xp[i]);
+    Y.push_back((int)yp[i]);
+    if ((int)W.size() == maxT) flush();
+  }
+  flush();
+  return outs;
 }
 
 // ------------------------------------------------------------------ norms
@@ -593,6 +633,7 @@ TORCH_LIBRARY(p2p, m) {
   m.def("conv_wgrad(Tensor p1, Tensor? p2, int p_act, Tensor q1, Tensor? q2, int q_act, int KH, int KW, "
         "int stride, int pad, int reflect, int up, Tensor(a!) dw, float scale, int accumulate) -> ()");
   m.def("weight_prep(Tensor w, int swap, int Xp, int Yp, Tensor? scale) -> Tensor");
+  m.def("weight_prep_multi(Tensor[] w, int[] swap, int[] xp, int[] yp) -> Tensor[]");
   m.def("norm_fwd(Tensor x, float eps, Tensor? gamma, Tensor? beta, Tensor? prelu_w, int act, "
         "Tensor(a!)? run_mean, Tensor(b!)? run_var, float momentum, bool batch) -> Tensor[]");
   m.def("norm_apply(Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? prelu_w, "
@@ -615,6 +656,7 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("conv_fwd", conv_fwd);
   m.impl("conv_wgrad", conv_wgrad);
   m.impl("weight_prep", weight_prep);
+  m.impl("weight_prep_multi", weight_prep_multi);
   m.impl("norm_fwd", norm_fwd);
   m.impl("norm_apply", norm_apply);
   m.impl("norm_bwd", norm_bwd);

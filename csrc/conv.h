@@ -72,6 +72,10 @@ int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int KW, int C, 
 int p2p_col2im(int mode, const void* col, int ldc, int N, int H, int W, int OH, int OW, int KH, int KW,
                int s, int p, int Cv, int Coutp, const float* bias, int act_out, const void* xb,
                int act_bwd, void* y, hipStream_t stream);
+int p2p_weight_prep_max();
+int p2p_weight_prep_multi(int count, const float* const* w, void* const* out, const int* A, const int* B,
+                          const int* T, const int* swap, const int* Xp, const int* Yp,
+                          hipStream_t stream);
 int p2p_weight_prep(const float* w, int A, int B, int KH, int KW, int swap, int Xp, int Yp,
                     const float* scale, void* out, hipStream_t stream);
 }

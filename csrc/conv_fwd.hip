@@ -406,66 +406,59 @@ extern "C" int p2p_weight_prep(const float* w, int A, int B, int KH, int KW, int
 //   MODE 1 (convT): input i = (o + p - t) / s        (if divisible and inside)
 // then bias, output activation, optional act'(xb) (dgrad) and zero padded channels.
 namespace p2p {
+// one thread per output pixel; only the taps that hit it are visited (MODE 1: the
+// ceil(K/s)^2 taps of its parity class, found arithmetically -- no per-tap divisibility
+// loop), each tap's Cv values are contiguous in col.
 template <int MODE>
 __global__ void __launch_bounds__(256) col2im_kernel(const bf16* __restrict__ col, int ldc, int N, int H,
                                                      int W, int OH, int OW, int KH, int KW, int s, int p,
                                                      int Cv, int Coutp, const float* __restrict__ bias,
                                                      int act_out, const bf16* __restrict__ xb, int act_bwd,
                                                      bf16* __restrict__ y) {
-  const int groups = Coutp / 8;
-  const long total = (long)N * OH * OW * groups;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-    const int gq = (int)(e % groups);
-    const long o = e / groups;
+  constexpr int MAXC = 16;
+  const long total = (long)N * OH * OW;
+  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
     const int ox = (int)(o % OW);
     const long t1 = o / OW;
     const int oy = (int)(t1 % OH);
     const int n = (int)(t1 / OH);
-    float acc[8];
+    float acc[MAXC];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    for (int ky = 0; ky < KH; ++ky) {
-      int iy;
-      if (MODE == 0) {
-        iy = oy * s - p + ky;
-      } else {
-        const int num = oy + p - ky;
-        if (num < 0 || num % s) continue;
-        iy = num / s;
-      }
+    for (int j = 0; j < MAXC; ++j) acc[j] = 0.f;
+    int ky = 0, kx0 = 0, kstep = 1;
+    if (MODE == 1) {
+      ky = (oy + p) % s;
+      kx0 = (ox + p) % s;
+      kstep = s;
+    }
+    for (; ky < KH; ky += kstep) {
+      const int iy = MODE == 0 ? oy * s - p + ky : (oy + p - ky) / s;
       if ((unsigned)iy >= (unsigned)H) continue;
-      for (int kx = 0; kx < KW; ++kx) {
-        int ix;
-        if (MODE == 0) {
-          ix = ox * s - p + kx;
-        } else {
-          const int num = ox + p - kx;
-          if (num < 0 || num % s) continue;
-          ix = num / s;
-        }
+      for (int kx = kx0; kx < KW; kx += kstep) {
+        const int ix = MODE == 0 ? ox * s - p + kx : (ox + p - kx) / s;
         if ((unsigned)ix >= (unsigned)W) continue;
         const bf16* src = col + ((long)(n * H + iy) * W + ix) * ldc + (ky * KW + kx) * Cv;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int co = gq * 8 + j;
-          if (co < Cv) acc[j] += (float)src[co];
-        }
+        for (int j = 0; j < MAXC; ++j)
+          if (j < Cv) acc[j] += (float)src[j];
       }
     }
-    bf16x8 out;
-    bf16x8 xv;
-    if (act_bwd) xv = *reinterpret_cast<const bf16x8*>(xb + o * Coutp + gq * 8);
+    for (int g0 = 0; g0 < Coutp; g0 += 8) {
+      bf16x8 out;
+      bf16x8 xv;
+      if (act_bwd) xv = *reinterpret_cast<const bf16x8*>(xb + o * Coutp + g0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int co = gq * 8 + j;
-      float v = 0.f;
-      if (co < Cv) {
-        v = act_fwd(acc[j] + (bias ? bias[co] : 0.f), act_out);
+      for (int j = 0; j < 8; ++j) {
+        const int co = g0 + j;
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < MAXC; ++q)
+          if (q == co && co < Cv) v = act_fwd(acc[q] + (bias ? bias[co] : 0.f), act_out);
         if (act_bwd) v *= act_grad_from_input((float)xv[j], act_bwd);
+        out[j] = (bf16)v;
       }
-      out[j] = (bf16)v;
+      *reinterpret_cast<bf16x8*>(y + o * Coutp + g0) = out;
     }
-    *reinterpret_cast<bf16x8*>(y + o * Coutp + gq * 8) = out;
   }
 }
 }  // namespace p2p
@@ -473,9 +466,9 @@ __global__ void __launch_bounds__(256) col2im_kernel(const bf16* __restrict__ co
 extern "C" int p2p_col2im(int mode, const void* col, int ldc, int N, int H, int W, int OH, int OW, int KH,
                           int KW, int s, int p, int Cv, int Coutp, const float* bias, int act_out,
                           const void* xb, int act_bwd, void* y, hipStream_t st) {
-  const long total = (long)N * OH * OW * (Coutp / 8);
+  const long total = (long)N * OH * OW;
   long blocks = (total + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
+  if (blocks > 16384) blocks = 16384;
   if (blocks < 1) blocks = 1;
   const p2p::bf16* c = static_cast<const p2p::bf16*>(col);
   const p2p::bf16* x = static_cast<const p2p::bf16*>(xb);
@@ -486,5 +479,67 @@ extern "C" int p2p_col2im(int mode, const void* col, int ldc, int N, int H, int 
   else
     hipLaunchKernelGGL(p2p::col2im_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, st, c, ldc, N, H, W, OH,
                        OW, KH, KW, s, p, Cv, Coutp, bias, act_out, x, act_bwd, o);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Multi-tensor weight preparation: every conv of a network in ONE launch (blockIdx.y =
+// tensor, descriptors in the kernel-argument block), instead of one small launch per
+// layout per layer.
+namespace p2p {
+constexpr int WP_MAX = 24;
+struct WPrepList {
+  const float* w[WP_MAX];
+  bf16* out[WP_MAX];
+  int A[WP_MAX], B[WP_MAX], T[WP_MAX], swap[WP_MAX], Xp[WP_MAX], Yp[WP_MAX];
+  int count;
+};
+
+__global__ void __launch_bounds__(256) weight_prep_multi_kernel(WPrepList L) {
+  const int t = blockIdx.y;
+  const float* __restrict__ w = L.w[t];
+  bf16* __restrict__ out = L.out[t];
+  const int A = L.A[t], B = L.B[t], T = L.T[t], swap = L.swap[t], Yp = L.Yp[t];
+  const long total = (long)L.Xp[t] * T * Yp;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int yv = (int)(e % Yp);
+    const long r = e / Yp;
+    const int tap = (int)(r % T);
+    const int xv = (int)(r / T);
+    const int a = swap ? yv : xv, b = swap ? xv : yv;
+    float v = 0.f;
+    if (a < A && b < B) v = w[((long)a * B + b) * T + tap];
+    out[e] = (bf16)v;
+  }
+}
+}  // namespace p2p
+
+extern "C" int p2p_weight_prep_max() { return p2p::WP_MAX; }
+
+// descriptors: w[i] fp32 [A][B][T], out[i] bf16 [Xp][T][Yp]
+extern "C" int p2p_weight_prep_multi(int count, const float* const* w, void* const* out, const int* A,
+                                     const int* B, const int* T, const int* swap, const int* Xp,
+                                     const int* Yp, hipStream_t st) {
+  using namespace p2p;
+  if (count <= 0) return 0;
+  if (count > WP_MAX) return -1;
+  WPrepList L;
+  L.count = count;
+  long maxel = 0;
+  for (int i = 0; i < count; ++i) {
+    L.w[i] = w[i];
+    L.out[i] = static_cast<bf16*>(out[i]);
+    L.A[i] = A[i];
+    L.B[i] = B[i];
+    L.T[i] = T[i];
+    L.swap[i] = swap[i];
+    L.Xp[i] = Xp[i];
+    L.Yp[i] = Yp[i];
+    const long el = (long)Xp[i] * T[i] * Yp[i];
+    maxel = el > maxel ? el : maxel;
+  }
+  long bx = (maxel + 255) / 256;
+  if (bx > 1024) bx = 1024;
+  hipLaunchKernelGGL(weight_prep_multi_kernel, dim3((unsigned)bx, count), dim3(256), 0, st, L);
   return (int)hipGetLastError();
 }

@@ -28,7 +28,10 @@ __device__ __forceinline__ void glds16(const void* g, bf16* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(lds_wave_base), 16, 0, 0);
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, int STAGES>
+// FASTK: every channel group a multiple of 64 (one tap per 64-deep K tile, wave-uniform);
+// otherwise (packed 8 / 16 / 24-channel image inputs) each lane splits its own chunk's k
+// into (tap, channel) and k >= Kc reads zeros.
+template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK>
 __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs a) {
   constexpr int NT = WM * WN * 64;
   constexpr int TM = BM / WM / 16;
@@ -108,51 +111,104 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
 
   auto issue = [&](int kt, int stage) {
     const int k0 = kt * BK;
-    const int tap = (int)fdiv((uint32_t)k0, fd_c);
-    const int ci0 = k0 - tap * C;
-    const int t_y = (int)fdiv((uint32_t)tap, fd_ti);
-    const int t_x = tap - t_y * g.Ti;
-    const bool s1 = ci0 < C1;
-    const bf16* src = s1 ? x1 : x2;
-    const int cs = s1 ? C1 : C2;
-    const int cio = s1 ? ci0 : ci0 - C1;
     bf16* Ast = As + stage * BM * BK;
-#pragma unroll
-    for (int i = 0; i < AROWS; ++i) {
-      int iy, ix;
-      bool inb;
-      if (MODE == 0) {
-        int uy = r_y[i] + t_y, ux = r_x[i] + t_x;
-        if (a.reflect && r_y[i] > -(1 << 27)) {
-          uy = reflect_idx(uy, Hu);
-          ux = reflect_idx(ux, Wu);
-        }
-        inb = (unsigned)uy < (unsigned)Hu && (unsigned)ux < (unsigned)Wu;
-        iy = uy >> ush;
-        ix = ux >> ush;
-      } else {
-        iy = r_y[i] - t_y;
-        ix = r_x[i] - t_x;
-        inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-      }
-      // branch-free: the address is formed unconditionally, the pointer selected
-      const long off = (long)(r_img[i] + iy * a.W + ix) * cs + cio + r_c[i];
-      const bf16* gp = inb ? src + off : zero;
-      glds16(gp, Ast + (wid * 8 + RPP * i) * BK);
-    }
-    long woff;
-    if (MODE == 0) {
-      woff = k0;
-    } else {
-      const int ky = g.ky0 + a.stride * t_y, kx = g.kx0 + a.stride * t_x;
-      woff = (long)(ky * a.KW + kx) * C + ci0;
-    }
     bf16* Bst = Bs + stage * BN * BK;
+    if constexpr (FASTK) {
+      const int tap = (int)fdiv((uint32_t)k0, fd_c);
+      const int ci0 = k0 - tap * C;
+      const int t_y = (int)fdiv((uint32_t)tap, fd_ti);
+      const int t_x = tap - t_y * g.Ti;
+      const bool s1 = ci0 < C1;
+      const bf16* src = s1 ? x1 : x2;
+      const int cs = s1 ? C1 : C2;
+      const int cio = s1 ? ci0 : ci0 - C1;
 #pragma unroll
-    for (int i = 0; i < BROWS; ++i) {
-      const int co = n0 + wid * 8 + rsub + RPP * i;
-      const bf16* gp = b_ok[i] ? w + co * wrow + woff + b_off[i] : zero;
-      glds16(gp, Bst + (wid * 8 + RPP * i) * BK);
+      for (int i = 0; i < AROWS; ++i) {
+        int iy, ix;
+        bool inb;
+        if (MODE == 0) {
+          int uy = r_y[i] + t_y, ux = r_x[i] + t_x;
+          if (a.reflect && r_y[i] > -(1 << 27)) {
+            uy = reflect_idx(uy, Hu);
+            ux = reflect_idx(ux, Wu);
+          }
+          inb = (unsigned)uy < (unsigned)Hu && (unsigned)ux < (unsigned)Wu;
+          iy = uy >> ush;
+          ix = ux >> ush;
+        } else {
+          iy = r_y[i] - t_y;
+          ix = r_x[i] - t_x;
+          inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+        }
+        // branch-free: the address is formed unconditionally, the pointer selected
+        const long off = (long)(r_img[i] + iy * a.W + ix) * cs + cio + r_c[i];
+        const bf16* gp = inb ? src + off : zero;
+        glds16(gp, Ast + (wid * 8 + RPP * i) * BK);
+      }
+      long woff;
+      if (MODE == 0) {
+        woff = k0;
+      } else {
+        const int ky = g.ky0 + a.stride * t_y, kx = g.kx0 + a.stride * t_x;
+        woff = (long)(ky * a.KW + kx) * C + ci0;
+      }
+#pragma unroll
+      for (int i = 0; i < BROWS; ++i) {
+        const int co = n0 + wid * 8 + rsub + RPP * i;
+        const bf16* gp = b_ok[i] ? w + co * wrow + woff + b_off[i] : zero;
+        glds16(gp, Bst + (wid * 8 + RPP * i) * BK);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AROWS; ++i) {
+        const int k = k0 + r_c[i];
+        const int tap = (int)fdiv((uint32_t)k, fd_c);
+        const int ci = k - tap * C;
+        const int t_y = (int)fdiv((uint32_t)tap, fd_ti);
+        const int t_x = tap - t_y * g.Ti;
+        const bool s1 = ci < C1;
+        const bf16* src = s1 ? x1 : x2;
+        const int cs = s1 ? C1 : C2;
+        const int cio = s1 ? ci : ci - C1;
+        int iy, ix;
+        bool inb;
+        if (MODE == 0) {
+          int uy = r_y[i] + t_y, ux = r_x[i] + t_x;
+          if (a.reflect && r_y[i] > -(1 << 27)) {
+            uy = reflect_idx(uy, Hu);
+            ux = reflect_idx(ux, Wu);
+          }
+          inb = (unsigned)uy < (unsigned)Hu && (unsigned)ux < (unsigned)Wu;
+          iy = uy >> ush;
+          ix = ux >> ush;
+        } else {
+          iy = r_y[i] - t_y;
+          ix = r_x[i] - t_x;
+          inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+        }
+        inb = inb && k < g.Kc;
+        const long off = (long)(r_img[i] + iy * a.W + ix) * cs + cio;
+        const bf16* gp = inb ? src + off : zero;
+        glds16(gp, Ast + (wid * 8 + RPP * i) * BK);
+      }
+#pragma unroll
+      for (int i = 0; i < BROWS; ++i) {
+        const int co = n0 + wid * 8 + rsub + RPP * i;
+        const int k = k0 + b_off[i];
+        long woff;
+        if (MODE == 0) {
+          woff = k;
+        } else {
+          const int tap = (int)fdiv((uint32_t)k, fd_c);
+          const int ci = k - tap * C;
+          const int t_y = (int)fdiv((uint32_t)tap, fd_ti);
+          const int t_x = tap - t_y * g.Ti;
+          const int ky = g.ky0 + a.stride * t_y, kx = g.kx0 + a.stride * t_x;
+          woff = (long)(ky * a.KW + kx) * C + ci;
+        }
+        const bf16* gp = (b_ok[i] && k < g.Kc) ? w + co * wrow + woff : zero;
+        glds16(gp, Bst + (wid * 8 + RPP * i) * BK);
+      }
     }
   };
 
@@ -210,7 +266,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
   conv_epilogue<BM, BN, WM, WN, MODE, NT>(a, g, acc, m0, n0, smem, fd_hwq, fd_wq);
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, int STAGES>
+template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK>
 static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int pipe = STAGES * (BM + BN) * BK * 2;
   constexpr int epi = BM * (BN + 8) * 2;
@@ -218,7 +274,7 @@ static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES>),
+        reinterpret_cast<const void*>(&conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK>),
         hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
@@ -237,30 +293,36 @@ static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   const long mtiles = (mmax + BM - 1) / BM;
   const long ntiles = (a.Cout + BN - 1) / BN;
   dim3 grid((unsigned)(mtiles * ntiles), 1, (unsigned)(classes * a.splits));
-  hipLaunchKernelGGL((conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES>), grid, dim3(WM * WN * 64), smem,
+  hipLaunchKernelGGL((conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK>), grid, dim3(WM * WN * 64), smem,
                      st, a);
   return (int)hipGetLastError();
 }
 
-template <int MODE>
-static int dispatch_glds(const ConvFwdArgs& a, int variant, hipStream_t st) {
+template <int MODE, bool FASTK>
+static int dispatch_glds2(const ConvFwdArgs& a, int variant, hipStream_t st) {
   // variant: 2 = 2-stage 128-row tile, 3 = 3-stage 128-row tile, 4 = 3-stage 256x128 8 waves
   if (a.Cout > 64) {
-    if (variant == 2) return launch_glds<128, 128, 2, 2, MODE, 2>(a, st);
-    if (variant == 3) return launch_glds<128, 128, 2, 2, MODE, 3>(a, st);
-    if (variant == 4) return launch_glds<256, 128, 4, 2, MODE, 3>(a, st);
+    if (variant == 2) return launch_glds<128, 128, 2, 2, MODE, 2, FASTK>(a, st);
+    if (variant == 3) return launch_glds<128, 128, 2, 2, MODE, 3, FASTK>(a, st);
+    if (variant == 4) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK>(a, st);
   } else if (a.Cout > 32) {
-    if (variant == 2) return launch_glds<128, 64, 2, 2, MODE, 2>(a, st);
-    if (variant == 3) return launch_glds<128, 64, 2, 2, MODE, 3>(a, st);
-    if (variant == 4) return launch_glds<256, 64, 4, 2, MODE, 3>(a, st);
+    if (variant == 2) return launch_glds<128, 64, 2, 2, MODE, 2, FASTK>(a, st);
+    if (variant == 3) return launch_glds<128, 64, 2, 2, MODE, 3, FASTK>(a, st);
+    if (variant == 4) return launch_glds<256, 64, 4, 2, MODE, 3, FASTK>(a, st);
   }
   return -2;
+}
+
+template <int MODE>
+static int dispatch_glds(const ConvFwdArgs& a, int variant, hipStream_t st) {
+  const bool fastk = a.C1 % BK == 0 && a.C2 % BK == 0;
+  return fastk ? dispatch_glds2<MODE, true>(a, variant, st) : dispatch_glds2<MODE, false>(a, variant, st);
 }
 
 }  // namespace p2p
 
 extern "C" int p2p_conv_fwd_glds(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t st) {
-  if (a->C1 % p2p::BK || a->C2 % p2p::BK || !a->zero) return -2;
+  if (!a->zero) return -2;
   if (a->act_in != p2p::ACT_NONE && a->act_in != p2p::ACT_RELU) return -2;
   return mode == 0 ? p2p::dispatch_glds<0>(*a, variant, st) : p2p::dispatch_glds<1>(*a, variant, st);
 }

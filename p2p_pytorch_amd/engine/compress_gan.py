@@ -1,0 +1,139 @@
+"""Family-R training step: the reference's compression + bit-depth-expansion GAN
+(/root/reference/train.py:291-414), phase for phase.
+
+  compressed = quantize(C(real_b), 3)                     train.py:297
+  fake_b     = G(compressed.detach())                     :300
+  D loss     : LSGAN(D(pool(cat(a, fake.detach()))), 0) + LSGAN(D(cat(a, b)), 1), x0.5
+  G loss     : LSGAN(D(cat(a, fake)), 1)                  :336-338
+               + 10 * sum_scales sum_layers (1/3)(4/4) L1(feat_fake, feat_real.detach())
+               + 10 * VGG(fake_b, real_b) + TV(fake_b)     :344-380
+  step G, then step D (D's grads from the G loss are discarded: zero_grad first)
+  C phase    : G(compressed) forward (updates G's BN running stats) and
+               locc = MSE(G(compressed), b) + 10 * VGG(compressed, b)   :392-397
+
+Reference semantics kept by default: optimizer_c is built over
+D's parameters (A1) and round() has no gradient (A2), so the C phase changes no
+parameter -- its loss is computed and logged, its backward is skipped because it is
+provably a no-op (``c_phase_backward=True`` runs it anyway for cost parity).
+``train_c=True`` fixes both quirks: a straight-through quantiser and an Adam over C.
+
+All three D passes go through the fused ops (virtual concat of (a, b) on the native
+path; spectral-norm 1/sigma on the weight image).  Losses stay on the device.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native, ops
+from ..models.losses import GANLoss, calc_tv_Loss
+from ..models.vgg import VGGLoss
+from .optim import make_adam
+
+
+class _STEQuantize(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bits):
+        return ops.quantize(x, bits)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+def set_requires_grad(nets, flag):
+    for n in nets:
+        for p in n.parameters():
+            p.requires_grad_(flag)
+
+
+class CompressGANStep:
+    def __init__(self, net_g, net_d, net_c, lr=2e-4, beta1=0.5, bits=3, lambda_feat=10.0,
+                 lambda_vgg=10.0, lambda_tv=1.0, n_layers_d=3, num_d=3, image_pool=None,
+                 train_c=False, c_phase_backward=False, vgg=None, reducer_g=None,
+                 reducer_d=None):
+        self.net_g, self.net_d, self.net_c = net_g, net_d, net_c
+        self.criterionGAN = GANLoss()                      # LSGAN, reference default
+        self.criterionVGG = vgg if vgg is not None else VGGLoss()
+        dev = next(net_g.parameters()).device
+        self.criterionVGG.to(dev)
+        self.bits = bits
+        self.lambda_feat, self.lambda_vgg, self.lambda_tv = lambda_feat, lambda_vgg, lambda_tv
+        self.feat_weights = 4.0 / (n_layers_d + 1)
+        self.d_weights = 1.0 / num_d
+        self.opt_g = make_adam(net_g.parameters(), lr=lr, betas=(beta1, 0.999))
+        self.opt_d = make_adam(net_d.parameters(), lr=lr, betas=(beta1, 0.999))
+        self.train_c = train_c
+        self.opt_c = make_adam(net_c.parameters(), lr=lr, betas=(beta1, 0.999)) if train_c else None
+        self.c_phase_backward = c_phase_backward
+        self.image_pool = image_pool
+        self.reducer_g, self.reducer_d = reducer_g, reducer_d
+
+    def _d_in(self, a, b):
+        if a.is_cuda and _native.get_backend() == "native":
+            return (a, b)
+        return torch.cat((a, b), 1)
+
+    def _quant(self, x):
+        return _STEQuantize.apply(x, self.bits) if self.train_c else ops.quantize(x, self.bits)
+
+    def _zero(self, opt, reducer):
+        if reducer is not None:
+            reducer.zero_grad()
+        else:
+            opt.zero_grad(set_to_none=True)
+
+    def step(self, real_a, real_b):
+        G, D, C = self.net_g, self.net_d, self.net_c
+        if real_a.is_cuda and _native.get_backend() == "native":
+            from ..ops import hip
+            hip.begin_step()
+            hip.prepare_weights(G, D, C)
+        compressed = self._quant(C(real_b))
+        fake_b = G(compressed.detach())
+        # ---- D losses (reference computes all losses before any update)
+        fake_in = self._d_in(real_a, fake_b.detach())
+        if self.image_pool is not None and self.image_pool.pool_size > 0:
+            fake_in = self.image_pool.query(torch.cat((real_a, fake_b.detach()), 1))
+        pred_fake = D(fake_in)
+        loss_d_fake = self.criterionGAN(pred_fake, False)
+        pred_real = D(self._d_in(real_a, real_b.detach()))
+        loss_d_real = self.criterionGAN(pred_real, True)
+        loss_d = (loss_d_fake + loss_d_real) * 0.5
+        # ---- G losses
+        pred_fake_g = D(self._d_in(real_a, fake_b))
+        loss_g_gan = self.criterionGAN(pred_fake_g, True)
+        loss_feat = 0.0
+        for i in range(len(pred_fake_g)):
+            for j in range(len(pred_fake_g[i]) - 1):
+                loss_feat = loss_feat + self.d_weights * self.feat_weights * ops.l1(
+                    pred_fake_g[i][j], pred_real[i][j].detach()) * self.lambda_feat
+        content = self.criterionVGG(fake_b, real_b) * self.lambda_vgg
+        tv = calc_tv_Loss(fake_b)
+        loss_g = loss_g_gan + loss_feat + content + tv * self.lambda_tv
+        # ---- updates: G first (its backward also reaches D; those grads are dropped)
+        self._zero(self.opt_g, self.reducer_g)
+        loss_g.backward()
+        if self.reducer_g is not None:
+            self.reducer_g.finish()
+        self.opt_g.step()
+        self._zero(self.opt_d, self.reducer_d)
+        loss_d.backward()
+        if self.reducer_d is not None:
+            self.reducer_d.finish()
+        self.opt_d.step()
+        # ---- C phase
+        need_graph = self.train_c or self.c_phase_backward
+        with torch.set_grad_enabled(need_graph):
+            fake_ac = G(compressed)     # also advances G's BN running stats, as the reference
+            loss_c = ops.mse(fake_ac, real_b) + self.criterionVGG(compressed, real_b) * \
+                self.lambda_vgg
+        if self.train_c:
+            self.opt_c.zero_grad(set_to_none=True)
+            self.opt_g.zero_grad(set_to_none=True)
+            loss_c.backward()
+            self.opt_c.step()
+        elif self.c_phase_backward:
+            loss_c.backward()   # reference: grads land on G (zeroed next step) -- no effect
+        return {"D": loss_d.detach(), "G_GAN": loss_g_gan.detach(),
+                "C": loss_c.detach(), "G_GAN_Feat": torch.as_tensor(loss_feat).detach(),
+                "VGG": content.detach(), "TV": tv.detach(), "G": loss_g.detach()}

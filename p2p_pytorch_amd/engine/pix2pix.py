@@ -72,6 +72,7 @@ class Pix2PixStep:
             from ..ops import hip
             hip.begin_step()      # weight images re-cast once per step (graph-safe)
             hip.advance_rng()     # new dropout masks
+            hip.prepare_weights(netG, netD)   # all bf16 weight images, one launch each
         with self._ctx(real_A.device):
             fake_B = netG(real_A)
             # ---- D
@@ -97,6 +98,9 @@ class Pix2PixStep:
         if self.reducer_d is not None:
             self.reducer_d.finish()
         self.opt_D.step()
+        if real_A.is_cuda and _native.get_backend() == "native":
+            from ..ops import hip
+            hip.prepare_weights(netD)         # D moved: fresh images for the G phase
         # ---- G
         set_requires_grad(netD, False)
         with self._ctx(real_A.device):

@@ -189,10 +189,13 @@ class SpectralNorm(nn.Module):
         w = getattr(m, self.name + "_bar")
         h = w.shape[0]
         w2 = w.reshape(h, -1)
-        with torch.no_grad():
-            for _ in range(self.power_iterations):
-                v.copy_(l2normalize(torch.mv(w2.detach().t(), u)))
-                u.copy_(l2normalize(torch.mv(w2.detach(), v)))
+        # ``.data`` assignment like the reference (networks.py:543-546): it swaps storage
+        # without bumping the version counter, so a backward through an EARLIER forward of
+        # this step sees the newest u / v (what the reference computes) instead of
+        # raising an in-place-modification error.
+        for _ in range(self.power_iterations):
+            v.data = l2normalize(torch.mv(w2.detach().t(), u.data))
+            u.data = l2normalize(torch.mv(w2.detach(), v.data))
         sigma = torch.dot(u, torch.mv(w2, v))
         return w / sigma
 
@@ -258,6 +261,8 @@ class MultiscaleDiscriminator(nn.Module):
                 setattr(self, f"layer{i}", d.model)
 
     def downsample(self, x):
+        if isinstance(x, (tuple, list)):  # virtual concat: pool each half
+            return tuple(ops.avg_pool3_s2(t) for t in x)
         return ops.avg_pool3_s2(x)
 
     def _single(self, i, x):

@@ -101,6 +101,45 @@ def _weight_image(w: torch.Tensor, swap: int, xp: int, yp: int, scale=None) -> t
     return img
 
 
+def prepare_weights(*modules):
+    """Cast every conv weight image (forward and dgrad layouts) of ``modules`` in one
+    multi-tensor launch per 24 tensors and seed the per-parameter cache, instead of one
+    weight_prep launch per layout per layer on first use."""
+    from ..models.layers import Conv2d, ConvTranspose2d
+    ws, sw, xp, yp, keys = [], [], [], [], []
+    for mod in modules:
+        for m in mod.modules():
+            w = getattr(m, "weight", None)
+            if not isinstance(w, torch.Tensor) or not w.is_cuda or w.dim() != 4:
+                continue
+            if isinstance(m, ConvTranspose2d):
+                cin, cout = w.shape[0], w.shape[1]
+                layouts = [(1, _pad8(cout), _pad8(cin)), (0, _pad8(cin), _pad8(cout))]
+            elif isinstance(m, Conv2d):
+                cout, cin = w.shape[0], w.shape[1]
+                layouts = [(0, _pad8(cout), _pad8(cin)), (1, _pad8(cin), _pad8(cout))]
+            else:
+                continue
+            wc = w.detach()
+            if wc.dtype != torch.float32 or not wc.is_contiguous():
+                continue
+            for (s_, x_, y_) in layouts:
+                ws.append(wc)
+                sw.append(s_)
+                xp.append(x_)
+                yp.append(y_)
+                keys.append((w, (s_, x_, y_, None)))
+    if not ws:
+        return
+    imgs = P().weight_prep_multi(ws, sw, xp, yp)
+    for (w, key), img in zip(keys, imgs):
+        cache = getattr(w, "_p2p_cache", None)
+        if cache is None:
+            cache = {}
+            w._p2p_cache = cache
+        cache[key] = (w._version, _gen[0], img)
+
+
 def _bias_padded(b, coutp):
     if b is None:
         return None

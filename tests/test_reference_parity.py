@@ -179,3 +179,74 @@ def test_scheduler_lambda_rule(refnet):
         s1.step()
         s2.step()
         assert o1.param_groups[0]["lr"] == pytest.approx(o2.param_groups[0]["lr"])
+
+
+def test_compress_gan_step_matches_reference_loop(refnet):
+    """One family-R training iteration: the reference's own loop body (train.py:291-402,
+    transcribed with the reference modules; GANLoss' hard-coded CUDA tensor type pointed
+    at CPU) vs CompressGANStep on our modules with copied weights -- same losses, same
+    updated G / D parameters."""
+    from p2p_pytorch_amd.engine.compress_gan import CompressGANStep
+    from p2p_pytorch_amd.models import (CompressionNetwork, ExpandNetwork,
+                                        MultiscaleDiscriminator, VGGLoss)
+    torch.manual_seed(5)
+    rg, rd, rc = (refnet.ExpandNetwork(),
+                  refnet.MultiscaleDiscriminator(6, 64, 3, None, False, 3, True),
+                  refnet.CompressionNetwork())
+    g, d, c = ExpandNetwork(), MultiscaleDiscriminator(6, 64, 3, None, False, 3, True), \
+        CompressionNetwork()
+    _copy(g, rg)
+    _copy(d, rd)
+    _copy(c, rc)
+    rvgg = refnet.VGGLoss("cpu")
+    vgg = VGGLoss()
+    _copy(vgg.vgg, rvgg.vgg)
+    a = torch.rand(1, 3, 32, 32) * 2 - 1
+    b = torch.rand(1, 3, 32, 32) * 2 - 1
+
+    # ---- reference loop body
+    def compress(t, bit):
+        m = 2 ** bit - 1
+        return torch.round(torch.clamp(t, 0.0, 1.0) * m) / m
+
+    gan = refnet.GANLoss()
+    gan.Tensor = torch.FloatTensor
+    l1 = nn.L1Loss()
+    opt_g = torch.optim.Adam(rg.parameters(), lr=2e-4, betas=(0.5, 0.999))
+    opt_d = torch.optim.Adam(rd.parameters(), lr=2e-4, betas=(0.5, 0.999))
+    compressed = compress(rc(b), 3)
+    fake_b = rg(compressed.detach())
+    pred_fake = rd.forward(torch.cat((a, fake_b.detach()), 1))
+    loss_d_fake = gan(pred_fake, False)
+    pred_real = rd.forward(torch.cat((a, b.detach()), 1))
+    loss_d_real = gan(pred_real, True)
+    loss_d = (loss_d_fake + loss_d_real) * 0.5
+    pred_fake = rd.forward(torch.cat((a, fake_b), 1))
+    loss_g_gan = gan(pred_fake, True)
+    feat = 0
+    for i in range(3):
+        for j in range(len(pred_fake[i]) - 1):
+            feat += (1.0 / 3) * (4.0 / 4) * l1(pred_fake[i][j], pred_real[i][j].detach()) * 10.0
+    content = rvgg(fake_b, b) * 10.0
+    tv = torch.mean(torch.abs(fake_b[:, :, :, :-1] - fake_b[:, :, :, 1:])) + \
+        torch.mean(torch.abs(fake_b[:, :, :-1, :] - fake_b[:, :, 1:, :]))
+    loss_g = loss_g_gan + feat + content + tv
+    opt_g.zero_grad()
+    loss_g.backward()
+    opt_g.step()
+    opt_d.zero_grad()
+    loss_d.backward()
+    opt_d.step()
+    locc = torch.nn.functional.mse_loss(rg(compressed), b) + rvgg(compressed, b) * 10.0
+
+    # ---- ours
+    step = CompressGANStep(g, d, c, vgg=vgg)
+    out = step.step(a, b)
+    assert out["D"].item() == pytest.approx(loss_d.item(), rel=1e-4)
+    assert out["G"].item() == pytest.approx(loss_g.item(), rel=1e-4)
+    assert out["C"].item() == pytest.approx(locc.item(), rel=1e-4)
+    for (n1, t1), (n2, t2) in zip(rg.state_dict().items(), g.state_dict().items()):
+        assert n1 == n2
+        assert torch.allclose(t1.float(), t2.float(), atol=1e-5, rtol=1e-4), n1
+    for (n1, t1), (n2, t2) in zip(rd.state_dict().items(), d.state_dict().items()):
+        assert torch.allclose(t1, t2, atol=1e-5, rtol=1e-4), n1
