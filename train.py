@@ -1,0 +1,308 @@
+#!/usr/bin/env python
+"""Training entry point -- flag-compatible with the reference ``train.py``
+(/root/reference/train.py:133-157: every reference flag keeps its name and default).
+
+Two model families behind one CLI:
+  * reference family (default, ``--netG expand``): CompressionNetwork C + ExpandNetwork G
+    + 3-scale spectral-norm PatchGAN D, LSGAN + feature matching + VGG19 + TV
+    (engine/compress_gan.py, reference train.py:291-414);
+  * pix2pix family (``--netG unet_256`` / ``unet_128`` / ``unet_<levels>``): U-Net + PatchGAN
+    (``--netD basic | n_layers | pixel``), GAN + lamb * L1 (engine/pix2pix.py).
+
+MI355X additions: one process per GPU (launch with ``torchrun --nproc-per-node N``), RCCL
+gradient all-reduce bucketed and overlapped with backward (parallel/ddp.py), the HIP
+kernels (``--backend native``, default on GPU), optional whole-step hipGraph capture on
+one GPU (``--graph``), the dataset decoded once into HBM (``--device_cache``) or
+synthetic pairs (``--synthetic``), JSONL metrics (``--log_json``), and checkpoints that
+really resume (``--epoch_count N`` or ``--resume``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+
+def build_parser():
+    p = argparse.ArgumentParser(description="pix2pix-pytorch-implementation")
+    # ---- reference flags (train.py:134-156), same names and defaults
+    p.add_argument("--dataset", default=None, help="facades (dataset/<name>/{train,test}/{a,b})")
+    p.add_argument("--name", default="run", help="training name")
+    p.add_argument("--epoch_count", type=int, default=1, help="the starting epoch count")
+    p.add_argument("--nepoch", type=int, default=50, help="# of epoch")
+    p.add_argument("--niter", type=int, default=100, help="# of iter at starting learning rate")
+    p.add_argument("--niter_decay", type=int, default=100,
+                   help="# of iter to linearly decay learning rate to zero")
+    p.add_argument("--cuda", action="store_true", help="use cuda?")
+    p.add_argument("--epochsave", type=int, default=50, help="checkpoint every N epochs")
+    p.add_argument("--batch_size", type=int, default=1, help="training batch size (per GPU)")
+    p.add_argument("--test_batch_size", type=int, default=1, help="testing batch size")
+    p.add_argument("--direction", type=str, default="b2a", help="a2b or b2a")
+    p.add_argument("--input_nc", type=int, default=3, help="input image channels")
+    p.add_argument("--output_nc", type=int, default=3, help="output image channels")
+    p.add_argument("--ngf", type=int, default=64, help="generator filters in first conv layer")
+    p.add_argument("--ndf", type=int, default=64, help="discriminator filters in first conv layer")
+    p.add_argument("--lr", type=float, default=0.0002, help="initial learning rate for adam")
+    p.add_argument("--lr_policy", type=str, default="lambda",
+                   help="learning rate policy: lambda|step|plateau|cosine")
+    p.add_argument("--lr_decay_iters", type=int, default=50,
+                   help="multiply by a gamma every lr_decay_iters iterations")
+    p.add_argument("--beta1", type=float, default=0.5, help="beta1 for adam. default=0.5")
+    p.add_argument("--threads", type=int, default=4, help="number of threads for data loader")
+    p.add_argument("--seed", type=int, default=123, help="random seed to use. Default=123")
+    p.add_argument("--lamb", type=float, default=10, help="weight on L1 term in objective")
+    # ---- new
+    p.add_argument("--netG", default="expand", help="expand | unet_256 | unet_128 | unet_<levels>")
+    p.add_argument("--netD", default=None, help="multiscale | basic | n_layers | pixel")
+    p.add_argument("--n_layers_D", type=int, default=3)
+    p.add_argument("--norm", default="instance", help="instance | batch | none (pix2pix family)")
+    p.add_argument("--no_dropout", action="store_true", help="pix2pix U-Net without dropout")
+    p.add_argument("--gan_mode", default=None, help="lsgan | vanilla | bce (default per family)")
+    p.add_argument("--backend", default=None, choices=["native", "torch"],
+                   help="GPU kernels: native HIP (default) or stock PyTorch eager")
+    p.add_argument("--synthetic", action="store_true", help="synthetic paired images, no dataset")
+    p.add_argument("--image_size", type=int, default=256, help="synthetic image size")
+    p.add_argument("--steps_per_epoch", type=int, default=100, help="synthetic steps per epoch")
+    p.add_argument("--device_cache", action="store_true",
+                   help="decode the training set once into GPU memory (uint8) and batch there")
+    p.add_argument("--graph", action="store_true", help="capture the training step in a hipGraph")
+    p.add_argument("--bucket_mb", type=float, default=64.0, help="gradient all-reduce bucket size")
+    p.add_argument("--train_c", action="store_true",
+                   help="reference family: really train C (straight-through quantiser)")
+    p.add_argument("--c_phase_backward", action="store_true",
+                   help="reference family: run the C-phase backward the reference runs (no effect)")
+    p.add_argument("--bits", type=int, default=3, help="quantiser bits (reference: 3)")
+    p.add_argument("--checkpoint_dir", default="checkpoint")
+    p.add_argument("--resume", action="store_true", help="resume from the newest checkpoint")
+    p.add_argument("--log_every", type=int, default=50)
+    p.add_argument("--log_json", default=None, help="append JSONL metrics here (rank 0)")
+    p.add_argument("--no_eval", action="store_true")
+    p.add_argument("--max_eval", type=int, default=0, help="limit eval images (0 = all)")
+    return p
+
+
+def main(argv=None):
+    opt = build_parser().parse_args(argv)
+    import p2p_pytorch_amd as p2p
+    from p2p_pytorch_amd.data import (DevicePairCache, SyntheticPairs, get_test_set,
+                                      get_training_set)
+    from p2p_pytorch_amd.engine.checkpoint import (checkpoint_path, latest_checkpoint,
+                                                   load_checkpoint, save_checkpoint)
+    from p2p_pytorch_amd.engine.metrics import psnr, ssim
+    from p2p_pytorch_amd.models import (define_C, define_D, define_G, get_scheduler,
+                                        update_learning_rate)
+    from p2p_pytorch_amd.parallel import dist as pdist
+
+    world, rank, local_rank = pdist.init_from_env()
+    use_cuda = (opt.cuda or world > 1 or opt.backend == "native") and torch.cuda.is_available()
+    if opt.cuda and not torch.cuda.is_available():
+        raise Exception("No GPU found, please run without --cuda")
+    device = torch.device("cuda", local_rank) if use_cuda else torch.device("cpu")
+    if use_cuda:
+        torch.cuda.set_device(device)
+    p2p.set_backend(opt.backend or "native")
+    if rank == 0:
+        print(opt)
+    torch.manual_seed(opt.seed)
+    random.seed(opt.seed + rank)
+    if use_cuda:
+        torch.cuda.manual_seed(opt.seed)
+    pix2pix = opt.netG.startswith("unet")
+    act_dtype = torch.bfloat16 if (use_cuda and p2p.get_backend() == "native") else torch.float32
+
+    # ---- data
+    if opt.synthetic:
+        train_src = SyntheticPairs(opt.batch_size, opt.image_size, device, seed=opt.seed + rank,
+                                   dtype=act_dtype, bits=opt.bits, direction=opt.direction)
+        test_set = None
+    else:
+        if not opt.dataset:
+            raise SystemExit("--dataset is required unless --synthetic")
+        root = os.path.join("dataset", opt.dataset)
+        train_set = get_training_set(root, opt.direction)
+        test_set = get_test_set(root, opt.direction)
+        if opt.device_cache and use_cuda:
+            train_src = DevicePairCache(train_set, device, rank, world, seed=opt.seed)
+        else:
+            sampler = (torch.utils.data.distributed.DistributedSampler(
+                train_set, num_replicas=world, rank=rank, shuffle=True, seed=opt.seed)
+                if world > 1 else None)
+            train_src = torch.utils.data.DataLoader(
+                train_set, batch_size=opt.batch_size, shuffle=sampler is None, sampler=sampler,
+                num_workers=opt.threads, drop_last=world > 1 or opt.graph)
+
+    # ---- models
+    if rank == 0:
+        print("===> Building models")
+    if pix2pix:
+        net_g = define_G(netG=opt.netG, input_nc=opt.input_nc, output_nc=opt.output_nc,
+                         ngf=opt.ngf, norm=opt.norm, use_dropout=not opt.no_dropout,
+                         gpu_id=device, verbose=rank == 0)
+        net_d = define_D(opt.input_nc + opt.output_nc, opt.ndf, norm=opt.norm,
+                         netD=opt.netD or "basic", n_layers_D=opt.n_layers_D, gpu_id=device,
+                         verbose=rank == 0)
+        net_c = None
+    else:
+        net_g = define_G("normal", 0.02, gpu_id=device, verbose=rank == 0)
+        net_d = define_D(opt.input_nc + opt.output_nc, opt.ndf, gpu_id=device,
+                         netD=opt.netD or "multiscale", n_layers_D=opt.n_layers_D,
+                         verbose=rank == 0)
+        net_c = define_C("normal", 0.02, gpu_id=device, verbose=rank == 0)
+    for net in (net_g, net_d, net_c):
+        if net is not None:
+            pdist.broadcast_module(net)
+    reducer_g = reducer_d = None
+    if world > 1:
+        from p2p_pytorch_amd.parallel import GradReducer
+        reducer_g = GradReducer(net_g, bucket_mb=opt.bucket_mb)
+        reducer_d = GradReducer(net_d, bucket_mb=opt.bucket_mb)
+
+    if pix2pix:
+        from p2p_pytorch_amd.engine.pix2pix import Pix2PixStep
+        trainer = Pix2PixStep(net_g, net_d, lr=opt.lr, beta1=opt.beta1,
+                              gan_mode=opt.gan_mode or "vanilla", lambda_L1=opt.lamb,
+                              reducer_g=reducer_g, reducer_d=reducer_d,
+                              autocast_dtype=torch.bfloat16 if (use_cuda and p2p.get_backend() == "torch") else None)
+        opt_g, opt_d = trainer.opt_G, trainer.opt_D
+    else:
+        from p2p_pytorch_amd.engine.compress_gan import CompressGANStep
+        from p2p_pytorch_amd.models import ImagePool
+        trainer = CompressGANStep(net_g, net_d, net_c, lr=opt.lr, beta1=opt.beta1, bits=opt.bits,
+                                  n_layers_d=opt.n_layers_D, image_pool=ImagePool(0),
+                                  train_c=opt.train_c, c_phase_backward=opt.c_phase_backward,
+                                  reducer_g=reducer_g, reducer_d=reducer_d)
+        opt_g, opt_d = trainer.opt_g, trainer.opt_d
+    sched_g = get_scheduler(opt_g, opt)
+    sched_d = get_scheduler(opt_d, opt)
+
+    # ---- resume
+    start_epoch = opt.epoch_count
+    losslogger = []
+    ck_path = None
+    if opt.resume:
+        ck_path, ep = latest_checkpoint(opt.checkpoint_dir, opt.dataset or "synthetic", opt.name)
+        if ck_path:
+            start_epoch = ep + 1
+    elif opt.epoch_count > 1:
+        ck_path = checkpoint_path(opt.checkpoint_dir, opt.dataset or "synthetic", opt.name,
+                                  opt.epoch_count - 1)
+        if not os.path.exists(ck_path):
+            raise SystemExit(f"=> No checkpoint found at '{ck_path}'")
+    if ck_path:
+        if rank == 0:
+            print(f"=> Loading checkpoint '{ck_path}'")
+        start_epoch, losslogger = load_checkpoint(ck_path, net_g, net_c, net_d, opt_g, opt_d,
+                                                  sched_g, sched_d, device=device)
+
+    step_fn = trainer.step
+    num_epoch = opt.nepoch + 1
+    logf = open(opt.log_json, "a") if (opt.log_json and rank == 0) else None
+    for epoch in range(start_epoch, num_epoch):
+        net_g.train()
+        net_d.train()
+        sums, count, t0 = {}, 0, time.perf_counter()
+        if hasattr(train_src, "sampler") and hasattr(train_src.sampler, "set_epoch"):
+            train_src.sampler.set_epoch(epoch)
+        if isinstance(train_src, DevicePairCache):
+            train_src.new_epoch()
+            n_it = train_src.batches_per_epoch(opt.batch_size)
+            batches = (train_src.next_batch(opt.batch_size, act_dtype) for _ in range(n_it))
+        elif isinstance(train_src, SyntheticPairs):
+            n_it = opt.steps_per_epoch
+            batches = (train_src.next_batch() for _ in range(n_it))
+        else:
+            n_it = len(train_src)
+            batches = iter(train_src)
+        for iteration, batch in enumerate(batches, 1):
+            real_a = batch[0].to(device, act_dtype).contiguous(memory_format=torch.channels_last)
+            real_b = batch[1].to(device, act_dtype).contiguous(memory_format=torch.channels_last)
+            if opt.graph and use_cuda and world == 1 and step_fn is trainer.step:
+                from p2p_pytorch_amd.engine.graph import CapturedStep
+                step_fn = CapturedStep(trainer.step, real_a, real_b)
+            losses = step_fn(real_a, real_b)
+            for k, v in losses.items():   # device-side running sums, no host sync
+                sums[k] = sums.get(k, 0) + v.detach().float()
+            count += 1
+            if iteration % opt.log_every == 0 or iteration == n_it:
+                keys = sorted(sums)
+                vals = torch.stack([torch.as_tensor(sums[k], device=device).float() for k in keys])
+                pdist.all_reduce_mean_([vals])
+                if rank == 0:
+                    means = {k: float(v) / count for k, v in zip(keys, vals.tolist())}
+                    dt = time.perf_counter() - t0
+                    ips = count * opt.batch_size * world / max(dt, 1e-9)
+                    print("itr: %d/%d [%3d/%3d] " % (iteration, n_it, epoch, num_epoch - 1) +
+                          " ".join(f"[{k}: {means[k]:.6f}]" for k in keys) +
+                          f" [{ips:.1f} img/s]", flush=True)
+                    if logf:
+                        logf.write(json.dumps({"epoch": epoch, "iter": iteration, "img_s": ips,
+                                               **means}) + "\n")
+                        logf.flush()
+        update_learning_rate(sched_g, opt_g, verbose=rank == 0)
+        update_learning_rate(sched_d, opt_d, verbose=rank == 0)
+        for o in (opt_g, opt_d):
+            if hasattr(o, "sync_lr"):
+                o.sync_lr()
+
+        # ---- eval (train.py:450-502), no autograd
+        if test_set is not None and not opt.no_eval:
+            net_g.eval()
+            net_d.eval()
+            if net_c is not None:
+                net_c.eval()
+            ps, ss = [], []
+            n_eval = len(test_set) if not opt.max_eval else min(opt.max_eval, len(test_set))
+            with torch.no_grad():
+                for i in range(rank, n_eval, world):
+                    inp, tgt = test_set[i]
+                    inp = inp.unsqueeze(0).to(device, act_dtype).contiguous(memory_format=torch.channels_last)
+                    tgt = tgt.unsqueeze(0).to(device, act_dtype).contiguous(memory_format=torch.channels_last)
+                    if net_c is not None:
+                        from p2p_pytorch_amd import ops
+                        pred = net_g(ops.quantize(net_c(tgt), opt.bits))
+                    else:
+                        pred = net_g(inp)
+                    ps.append(psnr(tgt, pred).clamp(max=60.0))
+                    ss.append(ssim(pred, tgt))
+            if ps:
+                pt, st = torch.cat(ps), torch.cat(ss)
+                stats = torch.stack([pt.sum(), st.sum(), torch.tensor(float(len(pt)), device=pt.device),
+                                     pt.max(), st.max()])
+            else:
+                stats = torch.zeros(5, device=device)
+            if world > 1:
+                import torch.distributed as dist
+                agg = stats[:3].clone()
+                dist.all_reduce(agg)
+                mx = stats[3:].clone()
+                dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+                stats = torch.cat([agg, mx])
+            if rank == 0:
+                n = max(float(stats[2]), 1.0)
+                print("===> Avg. PSNR: {:.4f} dB".format(float(stats[0]) / n))
+                print("===> Avg. SSIM: {:.4f}".format(float(stats[1]) / n))
+                print("===> Max PSNR: {:.4f} dB".format(float(stats[3])))
+                print("===> Max SSIM: {:.4f}".format(float(stats[4])))
+
+        if epoch % opt.epochsave == 0:
+            path = checkpoint_path(opt.checkpoint_dir, opt.dataset or "synthetic", opt.name, epoch)
+            save_checkpoint(path, epoch, net_g, net_c, net_d, opt_g, opt_d, sched_g, sched_d,
+                            losslogger, rank=rank)
+            pdist.barrier()
+            if rank == 0:
+                print("Checkpoint saved to {}".format(path))
+    if logf:
+        logf.close()
+    pdist.destroy()
+
+
+if __name__ == "__main__":
+    main()
