@@ -276,7 +276,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
 void conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, const Tensor& q1,
                 const optional<Tensor>& q2, int64_t q_act, int64_t KH, int64_t KW, int64_t stride,
                 int64_t pad, int64_t reflect, int64_t up, Tensor dw, double scale,
-                int64_t accumulate) {
+                int64_t accumulate, int64_t flip) {
   check_act(p1, "conv_wgrad p1");
   check_act(q1, "conv_wgrad q1");
   const int64_t N = p1.size(0), OH = p1.size(2), OW = p1.size(3);
@@ -296,7 +296,8 @@ void conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, con
   const int64_t R = p1.size(1) + R2, C = q1.size(1) + C2;
   TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == at::kFloat && dw.is_contiguous() && dw.dim() == 4,
               "conv_wgrad: dw must be contiguous fp32 [R][C][KH][KW]");
-  const int64_t Rr = dw.size(0), Cr = dw.size(1);
+  // flip: dw is [C][R][KH][KW] with flipped taps (stride-1 conv wgrad in transposed form)
+  const int64_t Rr = flip ? dw.size(1) : dw.size(0), Cr = flip ? dw.size(0) : dw.size(1);
   TORCH_CHECK(Rr <= R && Cr <= C && dw.size(2) == KH && dw.size(3) == KW, "conv_wgrad: dw shape");
   // the conv geometry over q must produce the p grid
   const int64_t Hu = H * up, Wu = W * up;
@@ -344,8 +345,9 @@ void conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, con
   a.ws = ws.data_ptr<float>();
   hipStream_t st = cur_stream(p1);
   check_rc(p2p_conv_wgrad(&a, st), "conv_wgrad");
-  check_rc(p2p_wgrad_reduce(a.ws, a.splits, a.R, a.KH, a.KW, a.C, (int)Rr, (int)Cr,
-                            dw.data_ptr<float>(), (float)scale, (int)accumulate, st),
+  check_rc(p2p_wgrad_reduce(a.ws, a.splits, a.R, a.KH, a.KW, a.C, flip ? (int)Cr : (int)Rr,
+                            flip ? (int)Rr : (int)Cr, dw.data_ptr<float>(), (float)scale,
+                            (int)accumulate, (int)flip, st),
            "wgrad_reduce");
 }
 
@@ -631,7 +633,8 @@ TORCH_LIBRARY(p2p, m) {
         "int pad, int reflect, int up, int act_in, int OH, int OW, int Cout, int act_out, int Csplit, "
         "Tensor? xb1, Tensor? xb2, int act_bwd, int Cvalid=0) -> Tensor[]");
   m.def("conv_wgrad(Tensor p1, Tensor? p2, int p_act, Tensor q1, Tensor? q2, int q_act, int KH, int KW, "
-        "int stride, int pad, int reflect, int up, Tensor(a!) dw, float scale, int accumulate) -> ()");
+        "int stride, int pad, int reflect, int up, Tensor(a!) dw, float scale, int accumulate, "
+        "int flip=0) -> ()");
   m.def("weight_prep(Tensor w, int swap, int Xp, int Yp, Tensor? scale) -> Tensor");
   m.def("weight_prep_multi(Tensor[] w, int[] swap, int[] xp, int[] yp) -> Tensor[]");
   m.def("norm_fwd(Tensor x, float eps, Tensor? gamma, Tensor? beta, Tensor? prelu_w, int act, "

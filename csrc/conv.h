@@ -68,7 +68,7 @@ int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t stream);
 int p2p_conv_wgrad_tile_rows(int R);
 int p2p_conv_wgrad_tile(const p2p::ConvWgradArgs* a, int* tile_r, int* tile_q);
 int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int KW, int C, int Rr, int Cr,
-                     float* dw, float scale, int accumulate, hipStream_t stream);
+                     float* dw, float scale, int accumulate, int flip, hipStream_t stream);
 int p2p_col2im(int mode, const void* col, int ldc, int N, int H, int W, int OH, int OW, int KH, int KW,
                int s, int p, int Cv, int Coutp, const float* bias, int act_out, const void* xb,
                int act_bwd, void* y, hipStream_t stream);

@@ -495,21 +495,47 @@ struct WPrepList {
   int count;
 };
 
+// One thread per (x, y-pair) of the image: it reads the two source rows w[a][b][0..T)
+// (contiguous fp32 runs) and writes the T taps as packed bf16 pairs, so for every tap a
+// wave stores 256 contiguous bytes (the element-per-thread form re-read each 64-B source
+// line T times at stride T and issued 2-byte stores).
 __global__ void __launch_bounds__(256) weight_prep_multi_kernel(WPrepList L) {
   const int t = blockIdx.y;
   const float* __restrict__ w = L.w[t];
   bf16* __restrict__ out = L.out[t];
   const int A = L.A[t], B = L.B[t], T = L.T[t], swap = L.swap[t], Yp = L.Yp[t];
-  const long total = (long)L.Xp[t] * T * Yp;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-    const int yv = (int)(e % Yp);
-    const long r = e / Yp;
-    const int tap = (int)(r % T);
-    const int xv = (int)(r / T);
-    const int a = swap ? yv : xv, b = swap ? xv : yv;
-    float v = 0.f;
-    if (a < A && b < B) v = w[((long)a * B + b) * T + tap];
-    out[e] = (bf16)v;
+  if (Yp & 1) {
+    const long total = (long)L.Xp[t] * T * Yp;
+    for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+      const int yv = (int)(e % Yp);
+      const long r = e / Yp;
+      const int tap = (int)(r % T);
+      const int xv = (int)(r / T);
+      const int a = swap ? yv : xv, b = swap ? xv : yv;
+      float v = 0.f;
+      if (a < A && b < B) v = w[((long)a * B + b) * T + tap];
+      out[e] = (bf16)v;
+    }
+    return;
+  }
+  const int Yh = Yp >> 1;
+  const long pairs = (long)L.Xp[t] * Yh;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < pairs; e += (long)gridDim.x * 256) {
+    const int y0 = (int)(e % Yh) * 2;
+    const int xv = (int)(e / Yh);
+    const int a0 = swap ? y0 : xv, b0 = swap ? xv : y0;
+    const int a1 = swap ? y0 + 1 : xv, b1 = swap ? xv : y0 + 1;
+    const bool ok0 = a0 < A && b0 < B, ok1 = a1 < A && b1 < B;
+    const float* r0 = w + ((long)a0 * B + b0) * T;
+    const float* r1 = w + ((long)a1 * B + b1) * T;
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + (long)xv * T * Yp + y0);
+    for (int tap = 0; tap < T; ++tap) {
+      const float v0 = ok0 ? r0[tap] : 0.f;
+      const float v1 = ok1 ? r1[tap] : 0.f;
+      const uint32_t lo = __builtin_bit_cast(uint16_t, (bf16)v0);
+      const uint32_t hi = __builtin_bit_cast(uint16_t, (bf16)v1);
+      o[(long)tap * Yh] = lo | (hi << 16);
+    }
   }
 }
 }  // namespace p2p
@@ -535,7 +561,7 @@ extern "C" int p2p_weight_prep_multi(int count, const float* const* w, void* con
     L.swap[i] = swap[i];
     L.Xp[i] = Xp[i];
     L.Yp[i] = Yp[i];
-    const long el = (long)Xp[i] * T[i] * Yp[i];
+    const long el = (Yp[i] & 1) ? (long)Xp[i] * T[i] * Yp[i] : (long)Xp[i] * (Yp[i] / 2);
     maxel = el > maxel ? el : maxel;
   }
   long bx = (maxel + 255) / 256;

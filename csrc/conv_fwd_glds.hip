@@ -31,7 +31,7 @@ __device__ __forceinline__ void glds16(const void* g, bf16* lds_wave_base) {
 // FASTK: every channel group a multiple of 64 (one tap per 64-deep K tile, wave-uniform);
 // otherwise (packed 8 / 16 / 24-channel image inputs) each lane splits its own chunk's k
 // into (tap, channel) and k >= Kc reads zeros.
-template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK>
+template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU>
 __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs a) {
   constexpr int NT = WM * WN * 64;
   constexpr int TM = BM / WM / 16;
@@ -108,6 +108,16 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
     b_off[i] = (slot ^ ((row >> 1) & 7)) * 8;
   }
   const FastDiv fd_c = make_fastdiv((uint32_t)C), fd_ti = make_fastdiv((uint32_t)g.Ti);
+  // FASTK A-row pointers of the current channel segment (one tap x one source tensor):
+  // formed once per segment, then advanced by BK per k-tile (out-of-image rows walk the
+  // zero page, which covers a whole segment: host guarantees C1, C2 <= 1024).
+  const bf16* a_ptr[AROWS];
+  const bf16* b_base[BROWS];
+#pragma unroll
+  for (int i = 0; i < BROWS; ++i) {
+    const int co = n0 + wid * 8 + rsub + RPP * i;
+    b_base[i] = w + (long)(b_ok[i] ? co : 0) * wrow + b_off[i];
+  }
 
   auto issue = [&](int kt, int stage) {
     const int k0 = kt * BK;
@@ -118,33 +128,38 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
       const int ci0 = k0 - tap * C;
       const int t_y = (int)fdiv((uint32_t)tap, fd_ti);
       const int t_x = tap - t_y * g.Ti;
-      const bool s1 = ci0 < C1;
-      const bf16* src = s1 ? x1 : x2;
-      const int cs = s1 ? C1 : C2;
-      const int cio = s1 ? ci0 : ci0 - C1;
+      if (kt == kt0 || ci0 == 0 || ci0 == C1) {
+        const bool s1 = ci0 < C1;
+        const bf16* src = s1 ? x1 : x2;
+        const int cs = s1 ? C1 : C2;
+        const int cio = s1 ? ci0 : ci0 - C1;
 #pragma unroll
-      for (int i = 0; i < AROWS; ++i) {
-        int iy, ix;
-        bool inb;
-        if (MODE == 0) {
-          int uy = r_y[i] + t_y, ux = r_x[i] + t_x;
-          if (a.reflect && r_y[i] > -(1 << 27)) {
-            uy = reflect_idx(uy, Hu);
-            ux = reflect_idx(ux, Wu);
+        for (int i = 0; i < AROWS; ++i) {
+          int iy, ix;
+          bool inb;
+          if (MODE == 0) {
+            int uy = r_y[i] + t_y, ux = r_x[i] + t_x;
+            if (a.reflect && r_y[i] > -(1 << 27)) {
+              uy = reflect_idx(uy, Hu);
+              ux = reflect_idx(ux, Wu);
+            }
+            inb = (unsigned)uy < (unsigned)Hu && (unsigned)ux < (unsigned)Wu;
+            iy = uy >> ush;
+            ix = ux >> ush;
+          } else {
+            iy = r_y[i] - t_y;
+            ix = r_x[i] - t_x;
+            inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
           }
-          inb = (unsigned)uy < (unsigned)Hu && (unsigned)ux < (unsigned)Wu;
-          iy = uy >> ush;
-          ix = ux >> ush;
-        } else {
-          iy = r_y[i] - t_y;
-          ix = r_x[i] - t_x;
-          inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+          const long off = (long)(r_img[i] + iy * a.W + ix) * cs + cio + r_c[i];
+          a_ptr[i] = inb ? src + off : zero;
         }
-        // branch-free: the address is formed unconditionally, the pointer selected
-        const long off = (long)(r_img[i] + iy * a.W + ix) * cs + cio + r_c[i];
-        const bf16* gp = inb ? src + off : zero;
-        glds16(gp, Ast + (wid * 8 + RPP * i) * BK);
+      } else {
+#pragma unroll
+        for (int i = 0; i < AROWS; ++i) a_ptr[i] += BK;
       }
+#pragma unroll
+      for (int i = 0; i < AROWS; ++i) glds16(a_ptr[i], Ast + (wid * 8 + RPP * i) * BK);
       long woff;
       if (MODE == 0) {
         woff = k0;
@@ -154,8 +169,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
       }
 #pragma unroll
       for (int i = 0; i < BROWS; ++i) {
-        const int co = n0 + wid * 8 + rsub + RPP * i;
-        const bf16* gp = b_ok[i] ? w + co * wrow + woff + b_off[i] : zero;
+        const bf16* gp = b_ok[i] ? b_base[i] + woff : zero;
         glds16(gp, Bst + (wid * 8 + RPP * i) * BK);
       }
     } else {
@@ -223,7 +237,6 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
   for (int s = 0; s < STAGES - 1; ++s)
     if (kt0 + s < kt1) issue(kt0 + s, s);
 
-  const bool relu_a = a.act_in == ACT_RELU;
   int stage = 0;
   for (int kt = kt0; kt < kt1; ++kt) {
     // retire tile kt (this wave's share), then the barrier makes every wave's share visible
@@ -238,27 +251,35 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
     }
     const bf16* A = As + stage * BM * BK;
     const bf16* B = Bs + stage * BN * BK;
+    // fragments of both 32-deep halves are read up front (double-buffered registers) so
+    // the second half's LDS latency hides behind the first half's MFMAs
+    bf16x8 af[2][TM], bfr[2][TN];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int chunk = kk * 4 + (lane >> 4);
-      bf16x8 af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * TM * 16 + i * 16 + (lane & 15);
-        u32x4 v = *reinterpret_cast<const u32x4*>(A + swz(row, chunk));
-        if (relu_a) v = relu8(v);
-        af[i] = __builtin_bit_cast(bf16x8, v);
+        af[kk][i] = *reinterpret_cast<const bf16x8*>(A + swz(row, chunk));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * TN * 16 + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(B + swz(row, chunk));
+        bfr[kk][j] = *reinterpret_cast<const bf16x8*>(B + swz(row, chunk));
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      if constexpr (RELU) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[kk][i] = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, af[kk][i])));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
     }
     stage = stage + 1 == STAGES ? 0 : stage + 1;
   }
@@ -266,7 +287,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
   conv_epilogue<BM, BN, WM, WN, MODE, NT>(a, g, acc, m0, n0, smem, fd_hwq, fd_wq);
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK>
+template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU>
 static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int pipe = STAGES * (BM + BN) * BK * 2;
   constexpr int epi = BM * (BN + 8) * 2;
@@ -274,7 +295,7 @@ static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK>),
+        reinterpret_cast<const void*>(&conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU>),
         hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
@@ -293,22 +314,22 @@ static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   const long mtiles = (mmax + BM - 1) / BM;
   const long ntiles = (a.Cout + BN - 1) / BN;
   dim3 grid((unsigned)(mtiles * ntiles), 1, (unsigned)(classes * a.splits));
-  hipLaunchKernelGGL((conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK>), grid, dim3(WM * WN * 64), smem,
+  hipLaunchKernelGGL((conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU>), grid, dim3(WM * WN * 64), smem,
                      st, a);
   return (int)hipGetLastError();
 }
 
-template <int MODE, bool FASTK>
+template <int MODE, bool FASTK, bool RELU>
 static int dispatch_glds2(const ConvFwdArgs& a, int variant, hipStream_t st) {
   // variant: 2 = 2-stage 128-row tile, 3 = 3-stage 128-row tile, 4 = 3-stage 256x128 8 waves
   if (a.Cout > 64) {
-    if (variant == 2) return launch_glds<128, 128, 2, 2, MODE, 2, FASTK>(a, st);
-    if (variant == 3) return launch_glds<128, 128, 2, 2, MODE, 3, FASTK>(a, st);
-    if (variant == 4) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK>(a, st);
+    if (variant == 2) return launch_glds<128, 128, 2, 2, MODE, 2, FASTK, RELU>(a, st);
+    if (variant == 3) return launch_glds<128, 128, 2, 2, MODE, 3, FASTK, RELU>(a, st);
+    if (variant == 4) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU>(a, st);
   } else if (a.Cout > 32) {
-    if (variant == 2) return launch_glds<128, 64, 2, 2, MODE, 2, FASTK>(a, st);
-    if (variant == 3) return launch_glds<128, 64, 2, 2, MODE, 3, FASTK>(a, st);
-    if (variant == 4) return launch_glds<256, 64, 4, 2, MODE, 3, FASTK>(a, st);
+    if (variant == 2) return launch_glds<128, 64, 2, 2, MODE, 2, FASTK, RELU>(a, st);
+    if (variant == 3) return launch_glds<128, 64, 2, 2, MODE, 3, FASTK, RELU>(a, st);
+    if (variant == 4) return launch_glds<256, 64, 4, 2, MODE, 3, FASTK, RELU>(a, st);
   }
   return -2;
 }
@@ -316,13 +337,16 @@ static int dispatch_glds2(const ConvFwdArgs& a, int variant, hipStream_t st) {
 template <int MODE>
 static int dispatch_glds(const ConvFwdArgs& a, int variant, hipStream_t st) {
   const bool fastk = a.C1 % BK == 0 && a.C2 % BK == 0;
-  return fastk ? dispatch_glds2<MODE, true>(a, variant, st) : dispatch_glds2<MODE, false>(a, variant, st);
+  if (a.act_in == ACT_RELU)
+    return fastk ? dispatch_glds2<MODE, true, true>(a, variant, st) : dispatch_glds2<MODE, false, true>(a, variant, st);
+  return fastk ? dispatch_glds2<MODE, true, false>(a, variant, st) : dispatch_glds2<MODE, false, false>(a, variant, st);
 }
 
 }  // namespace p2p
 
 extern "C" int p2p_conv_fwd_glds(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t st) {
   if (!a->zero) return -2;
+  if (a->C1 > 1024 || a->C2 > 1024) return -2;  // zero-page walk bound (see a_ptr)
   if (a->act_in != p2p::ACT_NONE && a->act_in != p2p::ACT_RELU) return -2;
   return mode == 0 ? p2p::dispatch_glds<0>(*a, variant, st) : p2p::dispatch_glds<1>(*a, variant, st);
 }

@@ -221,6 +221,39 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
     }
 }
 
+// Transposing fragment read for a [64][PW] sub-tile (PW = 128: the swz_t image above;
+// PW = 64: 128-B rows with the same XOR pattern on the 8 chunks of a row).
+template <int PW>
+__device__ __forceinline__ int wg_xor(int row) {
+  const int x = (row & 3) | (((row >> 3) & 1) << 2);
+  return PW == 128 ? x << 1 : x;
+}
+
+template <int PW>
+__device__ __forceinline__ int wg_off(int row, int chunk) {
+  return row * PW + ((chunk ^ wg_xor<PW>(row)) << 3);
+}
+
+template <int PW>
+__device__ __forceinline__ bf16x8 tr_frag_w(const bf16* tile, int kbase, int cbase, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int chunk = (cbase >> 3) + (p >> 1);
+  s16x4 lo, hi;
+  {
+    const int row = kbase + 8 * g + q;
+    const bf16* ptr = tile + wg_off<PW>(row, chunk) + (p & 1) * 4;
+    lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(ptr));
+  }
+  {
+    const int row = kbase + 8 * g + 4 + q;
+    const bf16* ptr = tile + wg_off<PW>(row, chunk) + (p & 1) * 4;
+    hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(ptr));
+  }
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 // ---------------------------------------------------------------------------------------
 // LDS-DMA (global_load_lds) pipelined variant for the big layers: 8 waves, a 256x128 or
 // 128x256 (R x Kq) output tile, a STAGES-deep ring of 64-row reduction stages.  Both
@@ -234,20 +267,25 @@ __device__ __forceinline__ void wg_wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int TBR, int TBQ, int WM, int WN, int STAGES>
+// RM: bit 0 = ReLU on the P fragments, bit 1 = ReLU on the Q fragments (compile-time, so
+// the fragment reads stay branch-free and can be batched ahead of the MFMAs).
+template <int TBR, int TBQ, int WM, int WN, int STAGES, int RM>
 __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgradArgs a) {
   constexpr int NT = WM * WN * 64;
   constexpr int TM = TBR / WM / 16, TN = TBQ / WN / 16;
-  constexpr int PSUB = TBR / 128, QSUB = TBQ / 128;
+  constexpr int PW = TBR >= 128 ? 128 : TBR;          // P sub-tile width (elements)
+  constexpr int PSUB = TBR / PW, QSUB = TBQ / 128;
+  constexpr int PCPR = PW / 8;                        // 16-B chunks per P row
   constexpr int PL = WBM * (TBR / 8) / NT;   // glds per thread per stage
   constexpr int QL = WBM * (TBQ / 8) / NT;
   constexpr int LOADS = PL + QL;
-  constexpr int SUBE = WBM * WROW;           // elements per [64][128] sub-tile
+  constexpr int PSUBE = WBM * PW;            // elements per P sub-tile
+  constexpr int SUBE = WBM * WROW;           // elements per [64][128] Q sub-tile
   static_assert(PL >= 1 && QL >= 1 && (WBM * (TBR / 8)) % NT == 0 && (WBM * (TBQ / 8)) % NT == 0,
                 "every wave issues the same glds count");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* Ps = reinterpret_cast<bf16*>(smem);          // [STAGES][PSUB][64][128]
-  bf16* Qs = Ps + STAGES * PSUB * SUBE;              // [STAGES][QSUB][64][128]
+  bf16* Ps = reinterpret_cast<bf16*>(smem);          // [STAGES][PSUB][64][PW]
+  bf16* Qs = Ps + STAGES * PSUB * PSUBE;             // [STAGES][QSUB][64][128]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -274,15 +312,14 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
 #pragma unroll
   for (int i = 0; i < PL; ++i) {
     const int q = tid + NT * i;
-    const int sub = q >> 10, rem = q & 1023;
-    const int row = rem >> 4, slot = rem & 15;
-    const int x = ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
-    const int col = r0 + sub * 128 + ((slot ^ x) << 3);
+    const int sub = q / (64 * PCPR), rem = q % (64 * PCPR);
+    const int row = rem / PCPR, slot = rem % PCPR;
+    const int col = r0 + sub * PW + ((slot ^ wg_xor<PW>(row)) << 3);
     const bool first = col < a.R1;
     p_row[i] = col < a.R ? row : -1;
     p_base[i] = first ? p1 + col : p2 + (col - a.R1);
     p_ld[i] = first ? a.R1 : a.R2;
-    p_lds[i] = sub * SUBE + ((q & ~63) & 1023) * 8;   // wave-uniform LDS element offset
+    p_lds[i] = sub * PSUBE + ((q & ~63) % (64 * PCPR)) * 8;   // wave-uniform LDS offset
   }
   int q_row[QL], q_lds[QL], q_kh[QL], q_kw[QL], q_ld[QL];
   const bf16* q_base[QL];
@@ -291,8 +328,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
     const int q = tid + NT * i;
     const int sub = q >> 10, rem = q & 1023;
     const int row = rem >> 4, slot = rem & 15;
-    const int x = ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
-    const int kq = q0 + sub * 128 + ((slot ^ x) << 3);
+    const int kq = q0 + sub * 128 + ((slot ^ wg_xor<128>(row)) << 3);
     int tap = 0, ci = 0;
     const bool ok = kq < a.Kq;
     if (ok) {
@@ -313,7 +349,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
   const FastDiv fd_ohw = make_fastdiv((uint32_t)OHW), fd_ow = make_fastdiv((uint32_t)a.OW);
 
   auto issue = [&](int st, int stage) {
-    bf16* Pst = Ps + stage * PSUB * SUBE;
+    bf16* Pst = Ps + stage * PSUB * PSUBE;
     bf16* Qst = Qs + stage * QSUB * SUBE;
 #pragma unroll
     for (int i = 0; i < PL; ++i) {
@@ -355,7 +391,6 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
   for (int sgi = 0; sgi < STAGES - 1; ++sgi)
     if (s0 + sgi < s1) issue(s0 + sgi, sgi);
 
-  const bool p_relu = a.p_act == ACT_RELU, q_relu = a.q_act == ACT_RELU;
   int stage = 0;
   for (int st = s0; st < s1; ++st) {
     if (st + STAGES - 2 < s1) wg_wait_vmcnt<LOADS * (STAGES - 2)>();
@@ -367,30 +402,39 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
       if (ns >= STAGES) ns -= STAGES;
       issue(st + STAGES - 1, ns);
     }
-    const bf16* P = Ps + stage * PSUB * SUBE;
+    const bf16* P = Ps + stage * PSUB * PSUBE;
     const bf16* Q = Qs + stage * QSUB * SUBE;
+    bf16x8 af[2][TM], bfr[2][TN];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int cb = wm * (TBR / WM) + i * 16;
-        bf16x8 v = tr_frag(P + (cb >> 7) * SUBE, kk * 32, cb & 127, lane);
-        if (p_relu) v = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, v)));
-        af[i] = v;
+        af[kk][i] = tr_frag_w<PW>(P + (cb / PW) * PSUBE, kk * 32, cb % PW, lane);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int cb = wn * (TBQ / WN) + j * 16;
-        bf16x8 v = tr_frag(Q + (cb >> 7) * SUBE, kk * 32, cb & 127, lane);
-        if (q_relu) v = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, v)));
-        bfr[j] = v;
+        bfr[kk][j] = tr_frag_w<128>(Q + (cb >> 7) * SUBE, kk * 32, cb & 127, lane);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      if constexpr (RM & 1) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[kk][i] = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, af[kk][i])));
+      }
+      if constexpr (RM & 2) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bfr[kk][j] = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, bfr[kk][j])));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
     }
     stage = stage + 1 == STAGES ? 0 : stage + 1;
   }
@@ -417,7 +461,7 @@ template <int G>
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, int splits,
                                                            int R, int KH, int KW, int C, int Rr,
                                                            int Cr, float* __restrict__ dw,
-                                                           float scale, int accumulate) {
+                                                           float scale, int accumulate, int flip) {
   constexpr int EPB = 256 / G;
   const int Kq = KH * KW * C;
   const long total = (long)R * Kq;
@@ -437,16 +481,34 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   const int kq = (int)(e - (long)r * Kq);
   const int tap = kq / C;
   const int ci = kq - tap * C;
-  if (r >= Rr || ci >= Cr) return;  // padded rows / channels of the GEMM view
-  const long o = ((long)r * Cr + ci) * KH * KW + tap;
+  long o;
+  if (!flip) {
+    if (r >= Rr || ci >= Cr) return;  // padded rows / channels of the GEMM view
+    o = ((long)r * Cr + ci) * KH * KW + tap;
+  } else {
+    // stride-1 conv wgrad computed in transposed-conv form: rows r = input channels,
+    // (tap, ci) = (flipped tap, output channel) -> dw[ci][r][KH-1-kh][KW-1-kw]
+    if (ci >= Rr || r >= Cr) return;
+    const int kh = tap / KW, kw = tap - kh * KW;
+    o = ((long)ci * Cr + r) * KH * KW + (KH - 1 - kh) * KW + (KW - 1 - kw);
+  }
   dw[o] = accumulate ? dw[o] + s : s;
 }
 
 }  // namespace p2p
 
-// glds variant geometry: 0 = none (fall back), 1 = 256(R) x 128(Kq), 2 = 128(R) x 256(Kq)
+// glds variant geometry: 0 = none (fall back), 1 = 256(R) x 128(Kq), 2 = 128(R) x 256(Kq),
+// 3 = 64(R) x 128(Kq) with 4 waves (first-layer wgrads, R = 64 output channels)
 static int wgrad_glds_shape(const p2p::ConvWgradArgs* a) {
-  if (!a->zero || a->R % 128 || a->Kq % 128) return 0;
+  if (!a->zero || a->Kq % 128) return 0;
+  if (a->R == 64) {
+    if ((a->p_act != p2p::ACT_NONE && a->p_act != p2p::ACT_RELU) ||
+        (a->q_act != p2p::ACT_NONE && a->q_act != p2p::ACT_RELU))
+      return 0;
+    const char* v0 = std::getenv("P2P_CONV_VARIANT");
+    return (v0 && v0[0] == 'v') ? 0 : 3;
+  }
+  if (a->R % 128) return 0;
   // fragments get ReLU only (LeakyReLU inputs are stored pre-activated by the models)
   if ((a->p_act != p2p::ACT_NONE && a->p_act != p2p::ACT_RELU) ||
       (a->q_act != p2p::ACT_NONE && a->q_act != p2p::ACT_RELU))
@@ -461,6 +523,7 @@ extern "C" int p2p_conv_wgrad_tile(const p2p::ConvWgradArgs* a, int* tr, int* tq
   const int shape = wgrad_glds_shape(a);
   if (shape == 1) { *tr = 256; *tq = 128; return shape; }
   if (shape == 2) { *tr = 128; *tq = 256; return shape; }
+  if (shape == 3) { *tr = 64; *tq = 128; return shape; }
   *tr = a->R <= 16 ? 16 : (a->R <= 64 ? 64 : 128);
   *tq = 128;
   return 0;
@@ -468,31 +531,43 @@ extern "C" int p2p_conv_wgrad_tile(const p2p::ConvWgradArgs* a, int* tr, int* tq
 
 extern "C" int p2p_conv_wgrad_tile_rows(int R) { return R <= 16 ? 16 : (R <= 64 ? 64 : 128); }
 
+template <int TBR, int TBQ, int WM, int WN, int STG, int RM>
+static int wg_launch(const p2p::ConvWgradArgs& a, dim3 grid, int smem, hipStream_t st) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&p2p::conv_wgrad_glds_kernel<TBR, TBQ, WM, WN, STG, RM>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((p2p::conv_wgrad_glds_kernel<TBR, TBQ, WM, WN, STG, RM>), grid, dim3(WM * WN * 64), smem,
+                     st, a);
+  return (int)hipGetLastError();
+}
+
+template <int TBR, int TBQ, int WM, int WN, int STG>
+static int wg_launch_rm(int rm, const p2p::ConvWgradArgs& a, dim3 grid, int smem, hipStream_t st) {
+  switch (rm) {
+    case 1: return wg_launch<TBR, TBQ, WM, WN, STG, 1>(a, grid, smem, st);
+    case 2: return wg_launch<TBR, TBQ, WM, WN, STG, 2>(a, grid, smem, st);
+    case 3: return wg_launch<TBR, TBQ, WM, WN, STG, 3>(a, grid, smem, st);
+    default: return wg_launch<TBR, TBQ, WM, WN, STG, 0>(a, grid, smem, st);
+  }
+}
+
 extern "C" int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t st) {
   using namespace p2p;
   const int shape = wgrad_glds_shape(a);
   if (shape) {
     constexpr int STG = 3;
-    const int tr = shape == 1 ? 256 : 128, tq = shape == 1 ? 128 : 256;
+    const int tr = shape == 1 ? 256 : (shape == 2 ? 128 : 64);
+    const int tq = shape == 2 ? 256 : 128;
     const int smem = STG * (tr + tq) * WBM * 2;
     dim3 grid(((a->R + tr - 1) / tr) * ((a->Kq + tq - 1) / tq), a->splits, 1);
-    static bool set1 = false, set2 = false;
-    if (shape == 1) {
-      if (!set1) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_glds_kernel<256, 128, 4, 2, STG>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-        set1 = true;
-      }
-      hipLaunchKernelGGL((conv_wgrad_glds_kernel<256, 128, 4, 2, STG>), grid, dim3(512), smem, st, *a);
-    } else {
-      if (!set2) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_glds_kernel<128, 256, 2, 4, STG>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-        set2 = true;
-      }
-      hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 256, 2, 4, STG>), grid, dim3(512), smem, st, *a);
-    }
-    return (int)hipGetLastError();
+    const int rm = (a->p_act == ACT_RELU ? 1 : 0) | (a->q_act == ACT_RELU ? 2 : 0);
+    if (shape == 1) return wg_launch_rm<256, 128, 4, 2, STG>(rm, *a, grid, smem, st);
+    if (shape == 2) return wg_launch_rm<128, 256, 2, 4, STG>(rm, *a, grid, smem, st);
+    return wg_launch_rm<64, 128, 1, 4, STG>(rm, *a, grid, smem, st);
   }
   constexpr int smem = 2 * 2 * WBM * WROW * 2;  // 64 KB
   const int tbr = p2p_conv_wgrad_tile_rows(a->R);
@@ -509,7 +584,8 @@ extern "C" int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t st) {
 }
 
 extern "C" int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int KW, int C, int Rr,
-                                int Cr, float* dw, float scale, int accumulate, hipStream_t st) {
+                                int Cr, float* dw, float scale, int accumulate, int flip,
+                                hipStream_t st) {
   const long total = (long)R * KH * KW * C;
   int G = 1;
   while (G < 32 && splits > 8 * G) G *= 2;   // <= ~8 slab reads per thread
@@ -518,7 +594,7 @@ extern "C" int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int 
 #define P2P_RED(g)                                                                              \
   case g:                                                                                        \
     hipLaunchKernelGGL(p2p::wgrad_reduce_kernel<g>, dim3(blocks), dim3(256), 0, st, ws, splits, R, \
-                       KH, KW, C, Rr, Cr, dw, scale, accumulate);                                \
+                       KH, KW, C, Rr, Cr, dw, scale, accumulate, flip);                          \
     break;
   switch (G) {
     P2P_RED(1)

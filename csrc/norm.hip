@@ -52,7 +52,6 @@ __global__ void __launch_bounds__(256) norm_partial_kernel(const bf16* __restric
   const int p1 = min(g.HW, p0 + g.chunk);
   const bf16* base = x + (long)n * g.HW * g.C;
   float piv[8], s1[8], s2[8];
-  int cnt = 0;
   {
     u32x4 v = *reinterpret_cast<const u32x4*>(base + (long)p0 * g.C + cg * 8);
     unpack8(v, piv);
@@ -60,17 +59,26 @@ __global__ void __launch_bounds__(256) norm_partial_kernel(const bf16* __restric
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
   if (tr < RP) {
-    for (int p = p0 + tr; p < p1; p += RP) {
+    auto acc1 = [&](u32x4 v) {
       float f[8];
-      unpack8(*reinterpret_cast<const u32x4*>(base + (long)p * g.C + cg * 8), f);
+      unpack8(v, f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float d = f[j] - piv[j];
         s1[j] += d;
         s2[j] += d * d;
       }
-      ++cnt;
+    };
+    int p = p0 + tr;
+    for (; p + 3 * RP < p1; p += 4 * RP) {   // 4 independent 16-B loads in flight
+      u32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        v[u] = *reinterpret_cast<const u32x4*>(base + (long)(p + u * RP) * g.C + cg * 8);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc1(v[u]);
     }
+    for (; p < p1; p += RP) acc1(*reinterpret_cast<const u32x4*>(base + (long)p * g.C + cg * 8));
   }
   // block reduce over rows sharing a channel chunk: LDS [RP][C] x 2
   __shared__ float red1[2048], red2[2048];
@@ -108,7 +116,6 @@ __global__ void __launch_bounds__(256) norm_partial_kernel(const bf16* __restric
     ws[o] = mb;
     ws[(long)g.N * g.nchunks * g.C + o] = m2;
   }
-  (void)cnt;
 }
 
 // stats: [N][C] mean, [N][C] rstd (fp32).  bn: running stats update (N == 1).
@@ -172,18 +179,28 @@ __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict_
   }
   const float pw = prelu_w ? prelu_w[0] : 0.f;
   const long base = (long)n * g.HW * g.C + cg * 8;
-  for (int p = p0 + tr; p < p1; p += RP) {
+  auto one = [&](u32x4 v) -> u32x4 {
     float f[8];
-    unpack8(*reinterpret_cast<const u32x4*>(x + base + (long)p * g.C), f);
+    unpack8(v, f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float v = f[j] * sc[j] + sh[j];
-      if (prelu_w) v = v > 0.f ? v : pw * v;
-      else v = act_fwd(v, act);
-      f[j] = v;
+      float t = f[j] * sc[j] + sh[j];
+      if (prelu_w) t = t > 0.f ? t : pw * t;
+      else t = act_fwd(t, act);
+      f[j] = t;
     }
-    *reinterpret_cast<u32x4*>(y + base + (long)p * g.C) = pack8(f);
+    return pack8(f);
+  };
+  int p = p0 + tr;
+  for (; p + 3 * RP < p1; p += 4 * RP) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const u32x4*>(x + base + (long)(p + u * RP) * g.C);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) *reinterpret_cast<u32x4*>(y + base + (long)(p + u * RP) * g.C) = one(v[u]);
   }
+  for (; p < p1; p += RP)
+    *reinterpret_cast<u32x4*>(y + base + (long)p * g.C) = one(*reinterpret_cast<const u32x4*>(x + base + (long)p * g.C));
 }
 
 // ---------------------------------------------------------------- backward
@@ -256,10 +273,10 @@ __global__ void __launch_bounds__(256) norm_bwd_partial_kernel(
     s1[j] = s2[j] = 0.f;
   }
   if (tr < RP) {
-    for (int p = p0 + tr; p < p1; p += RP) {
+    auto acc2 = [&](u32x4 vx, u32x4 vd) {
       float fx[8], fd[8];
-      unpack8(*reinterpret_cast<const u32x4*>(x + off + (long)p * g.C), fx);
-      unpack8(*reinterpret_cast<const u32x4*>(dy + off + (long)p * g.C), fd);
+      unpack8(vx, fx);
+      unpack8(vd, fd);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float xh = (fx[j] - mu[j]) * rs[j];
@@ -267,7 +284,21 @@ __global__ void __launch_bounds__(256) norm_bwd_partial_kernel(
         s1[j] += d;
         s2[j] += d * xh;
       }
+    };
+    int p = p0 + tr;
+    for (; p + 3 * RP < p1; p += 4 * RP) {
+      u32x4 vx[4], vd[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        vx[u] = *reinterpret_cast<const u32x4*>(x + off + (long)(p + u * RP) * g.C);
+        vd[u] = *reinterpret_cast<const u32x4*>(dy + off + (long)(p + u * RP) * g.C);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc2(vx[u], vd[u]);
     }
+    for (; p < p1; p += RP)
+      acc2(*reinterpret_cast<const u32x4*>(x + off + (long)p * g.C),
+           *reinterpret_cast<const u32x4*>(dy + off + (long)p * g.C));
   }
   __shared__ float red1[2048], red2[2048];
   __shared__ float o1[2048], o2[2048];
@@ -324,22 +355,23 @@ __global__ void __launch_bounds__(256) norm_param_grad_kernel(const float* __res
   dbeta[c] += sdy;
 }
 
-// dx = A*dy_eff + B + Cc*xhat; optionally also block partial column sums of the (bf16)
-// dx -- the bias gradient of the conv that produced x, fused here instead of a re-read.
+// dx = A*dy_eff + B + Cc*xhat.  (The column sums of dx -- the bias gradient of the conv
+// that produced x -- are exactly zero for a normalised group: sum_p dx = Cc * sum_p xhat = 0,
+// so the host returns that exact zero instead of re-reading dx.)
 __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ dy, NormGeom g,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
-    const float* __restrict__ beta, int act, const float* __restrict__ coef, bf16* __restrict__ dx,
-    float* __restrict__ dsum_ws) {
+    const float* __restrict__ beta, int act, const float* __restrict__ coef, bf16* __restrict__ dx) {
   const int n = blockIdx.y, cb = blockIdx.x;
   const int CP = g.C >> 3;
   const int RP = 256 / CP;
   const int tid = threadIdx.x;
   const int cg = tid % CP, tr = tid / CP;
+  if (tr >= RP) return;
   const int p0 = cb * g.chunk;
   const int p1 = min(g.HW, p0 + g.chunk);
   const long NC = (long)g.N * g.C;
-  float mu[8], rs[8], ga[8], be[8], ca[8], cx[8], c0[8], ds[8];
+  float mu[8], rs[8], ga[8], be[8], ca[8], cx[8], c0[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const long ci = (long)n * g.C + cg * 8 + j;
@@ -350,55 +382,36 @@ __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
     ca[j] = coef[ci];
     cx[j] = coef[2 * NC + ci];
     c0[j] = coef[NC + ci];
-    ds[j] = 0.f;
   }
   const long base = (long)n * g.HW * g.C + cg * 8;
-  if (tr < RP) {
-    for (int p = p0 + tr; p < p1; p += RP) {
-      float fx[8], fd[8];
-      unpack8(*reinterpret_cast<const u32x4*>(x + base + (long)p * g.C), fx);
-      unpack8(*reinterpret_cast<const u32x4*>(dy + base + (long)p * g.C), fd);
+  auto one = [&](u32x4 vx, u32x4 vd) -> u32x4 {
+    float fx[8], fd[8];
+    unpack8(vx, fx);
+    unpack8(vd, fd);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xh = (fx[j] - mu[j]) * rs[j];
-        const float d = fd[j] * act_gate(xh * ga[j] + be[j], act);
-        fd[j] = ca[j] * d + c0[j] + cx[j] * xh;
-      }
-      const u32x4 o = pack8(fd);
-      *reinterpret_cast<u32x4*>(dx + base + (long)p * g.C) = o;
-      if (dsum_ws) {
-        float fo[8];
-        unpack8(o, fo);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ds[j] += fo[j];
-      }
+    for (int j = 0; j < 8; ++j) {
+      const float xh = (fx[j] - mu[j]) * rs[j];
+      const float d = act ? fd[j] * act_gate(xh * ga[j] + be[j], act) : fd[j];
+      fd[j] = ca[j] * d + c0[j] + cx[j] * xh;
     }
+    return pack8(fd);
+  };
+  int p = p0 + tr;
+  for (; p + 3 * RP < p1; p += 4 * RP) {
+    u32x4 vx[4], vd[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      vx[u] = *reinterpret_cast<const u32x4*>(x + base + (long)(p + u * RP) * g.C);
+      vd[u] = *reinterpret_cast<const u32x4*>(dy + base + (long)(p + u * RP) * g.C);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      *reinterpret_cast<u32x4*>(dx + base + (long)(p + u * RP) * g.C) = one(vx[u], vd[u]);
   }
-  if (dsum_ws) {
-    __shared__ float red1[2048];
-    __shared__ float o1[2048];
-    block_rows_reduce(ds, nullptr, g.C, cg, tr, RP, red1, nullptr, o1, nullptr);
-    __syncthreads();
-    for (int c = tid; c < g.C; c += 256) dsum_ws[((long)n * g.nchunks + cb) * g.C + c] = o1[c];
-  }
-}
-
-// out[c] = sum over all blocks of dsum_ws[b][c] (fixed order), G threads per channel
-template <int G>
-__global__ void __launch_bounds__(256) dsum_final_kernel(const float* __restrict__ ws, int nb, int C,
-                                                         float* __restrict__ out) {
-  constexpr int EPB = 256 / G;
-  const int le = threadIdx.x % EPB, sg = threadIdx.x / EPB;
-  const int c = blockIdx.x * EPB + le;
-  float a = 0.f;
-  if (c < C)
-    for (int b = sg; b < nb; b += G) a += ws[(long)b * C + c];
-  __shared__ float red[256];
-  red[threadIdx.x] = a;
-  __syncthreads();
-  if (sg != 0 || c >= C) return;
-  for (int q = 1; q < G; ++q) a += red[q * EPB + le];
-  out[c] = a;
+  for (; p < p1; p += RP)
+    *reinterpret_cast<u32x4*>(dx + base + (long)p * g.C) =
+        one(*reinterpret_cast<const u32x4*>(x + base + (long)p * g.C),
+            *reinterpret_cast<const u32x4*>(dy + base + (long)p * g.C));
 }
 
 static inline NormGeom make_geom(int N, int HW, int C) {
@@ -406,11 +419,13 @@ static inline NormGeom make_geom(int N, int HW, int C) {
   g.N = N;
   g.HW = HW;
   g.C = C;
-  // ~ 2048 blocks of work; at least 64 pixels per block
-  long total_px = (long)N * HW;
-  int chunk = (int)((total_px + 2047) / 2048);
-  chunk = chunk < 64 ? 64 : chunk;
-  chunk = ((chunk + 31) / 32) * 32;
+  // ~2048 blocks of work: every thread walks `iters` pixels (4..64) of its 8-channel
+  // column, RP = 256 / (C/8) columns' worth of pixel rows per pass
+  const long total_px = (long)N * HW;
+  const int RP = C >= 2048 ? 1 : 256 / (C >> 3);
+  long iters = total_px / ((long)RP * 2048);
+  iters = iters < 4 ? 4 : (iters > 64 ? 64 : iters);
+  int chunk = (int)(RP * iters);
   if (chunk > HW) chunk = HW;
   g.chunk = chunk;
   g.nchunks = (HW + chunk - 1) / chunk;
@@ -424,7 +439,7 @@ extern "C" {
 // workspace floats needed by p2p_norm_fwd / p2p_norm_bwd (incl. the fused bias-grad partials)
 long p2p_norm_ws_floats(int N, int HW, int C) {
   p2p::NormGeom g = p2p::make_geom(N, HW, C);
-  return 3L * N * g.nchunks * C + 3L * N * C;
+  return 2L * N * g.nchunks * C + 3L * N * C;
 }
 
 int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* gamma,
@@ -456,15 +471,14 @@ int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const
   return (int)hipGetLastError();
 }
 
-// act: ReLU / LeakyReLU fused by the forward (0 = none); dsum (optional, [C] fp32): column
-// sums of dx -- the bias gradient of the producing conv.
+// act: ReLU / LeakyReLU fused by the forward (0 = none); dsum (optional, [C] fp32): the
+// column sums of dx (bias gradient of the producing conv), which are exactly zero.
 int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const float* mean,
                  const float* rstd, const float* gamma, const float* beta, int act, float* dgamma,
                  float* dbeta, float* ws, void* dx, float* dsum, hipStream_t st) {
   using namespace p2p;
   NormGeom g = make_geom(N, HW, C);
   float* coef = ws + 2L * N * g.nchunks * C;
-  float* dsum_ws = coef + 3L * N * C;
   const bf16* xb = static_cast<const bf16*>(x);
   const bf16* db = static_cast<const bf16*>(dy);
   if (dgamma) {
@@ -479,11 +493,8 @@ int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const floa
     hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, ws, g,
                        rstd, gamma, coef);
     hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st, xb, db, g, mean,
-                       rstd, gamma, beta, act, coef, static_cast<bf16*>(dx),
-                       dsum ? dsum_ws : (float*)nullptr);
-    if (dsum)
-      hipLaunchKernelGGL(dsum_final_kernel<32>, dim3((C + 7) / 8), dim3(256), 0, st, dsum_ws,
-                         N * g.nchunks, C, dsum);
+                       rstd, gamma, beta, act, coef, static_cast<bf16*>(dx));
+    if (dsum) (void)hipMemsetAsync(dsum, 0, sizeof(float) * C, st);
   }
   return (int)hipGetLastError();
 }

@@ -48,10 +48,11 @@ def begin_step():
     _colsum_stash.clear()
 
 
-# Bias gradients fused into the norm backward: NormFn.backward computes the column sums of
-# the dx it returns (the producing conv's dY) in the same pass and parks them here keyed by
-# that tensor; ConvFn.backward picks them up instead of re-reading dY.  Holding the tensor
-# keeps its storage alive, so a key can never alias a recycled allocation.
+# Bias gradients handed from the norm backward to the producing conv: for a conv feeding a
+# training-mode instance / batch norm, sum_p dY = sum_p dx_norm = Cc * sum_p xhat == 0
+# exactly, so NormFn.backward parks that exact zero here keyed by the dx it returns and
+# ConvFn.backward takes it instead of re-reading dY.  Holding the tensor keeps its storage
+# alive, so a key can never alias a recycled allocation.
 _colsum_stash: dict = {}
 
 
@@ -271,6 +272,13 @@ class ConvFn(torch.autograd.Function):
             act_in = _act_code(cfg.act_in)
             if cfg.transposed:
                 P().conv_wgrad(q1, q2, act_in, gyp, None, 0, KH, KW, s, p, 0, 1, gw, 1.0, 0)
+            elif (s == 1 and Coutp <= 16 and Cp >= 128 and KH == KW and not cfg.reflect
+                  and cfg.up == 1):
+                # tiny-Cout stride-1 conv (PatchGAN logits): the GEMM's R = Cout would waste
+                # the MFMA tile, so compute it in transposed-conv form -- rows = input
+                # channels, the dY gather with pad K-1-p, taps flipped by the reduce
+                P().conv_wgrad(q1, q2, act_in, gyp, None, 0, KH, KW, 1, KH - 1 - p, 0, 1, gw,
+                               1.0, 0, 1)
             else:
                 P().conv_wgrad(gyp, None, 0, q1, q2, act_in, KH, KW, s, p, int(cfg.reflect),
                                cfg.up, gw, 1.0, 0)

@@ -198,9 +198,9 @@ def test_conv_instance_norm_act_chain(act):
     assert rel_err(y, ry) < 3e-2
     assert rel_err(hx.grad, rx.grad) < 4e-2
     assert rel_err(hw.grad, rw.grad) < 4e-2
-    # bias before an instance norm has an exactly-zero true gradient: the HIP value is the
-    # column sum of bf16 dY (rounding noise), small against the weight-gradient scale
-    assert hb.grad.abs().max() < 0.05 * hw.grad.abs().max() * 64
+    # bias before an instance norm has an exactly-zero true gradient (sum_p dx_norm = 0):
+    # the HIP path returns that exact zero; fp32 autograd returns rounding noise around it
+    assert torch.count_nonzero(hb.grad) == 0
     assert rb.grad.abs().max() < 1e-3
 
 
@@ -283,6 +283,32 @@ def test_losses(kind):
     (v * 3.0).backward()
     (r * 3.0).backward()
     assert rel_err(ha.grad, ra.grad) < 2e-2
+
+
+def test_weight_prep_multi_matches_single():
+    """Multi-tensor weight cast (one launch) == per-tensor cast == bf16(permuted fp32)."""
+    P = torch.ops.p2p
+    torch.manual_seed(0)
+    shapes = [(64, 3, 4, 4), (128, 64, 4, 4), (6, 512, 4, 4), (64, 64, 3, 3), (3, 64, 7, 7),
+              (512, 256, 1, 1)]
+    ws, sw, xp, yp, refs = [], [], [], [], []
+    for (a, b, kh, kw) in shapes:
+        w = torch.randn(a, b, kh, kw, device=DEV)
+        for swap in (0, 1):
+            X, Y = (b, a) if swap else (a, b)
+            Xp, Yp = (X + 7) // 8 * 8 + (8 if swap else 0), (Y + 7) // 8 * 8
+            ws.append(w)
+            sw.append(swap)
+            xp.append(Xp)
+            yp.append(Yp)
+            img = torch.zeros(Xp, kh, kw, Yp, device=DEV)
+            src = w.permute(1, 2, 3, 0) if swap else w.permute(0, 2, 3, 1)
+            img[:X, :, :, :Y] = src
+            refs.append(img.to(torch.bfloat16))
+    outs = P.weight_prep_multi(ws, sw, xp, yp)
+    for o, r, w, s_, x_, y_ in zip(outs, refs, ws, sw, xp, yp):
+        assert torch.equal(o, r)
+        assert torch.equal(P.weight_prep(w, s_, x_, y_, None), r)
 
 
 def test_fused_adam_matches_torch():
