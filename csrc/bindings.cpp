@@ -34,6 +34,20 @@ int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const floa
 int p2p_act(const void* a, const void* b, long n, int act, int mode, void* out, hipStream_t st);
 int p2p_dropout(const void* x, long n, float p, const int64_t* seed, unsigned salt, void* y,
                 hipStream_t st);
+int p2p_misc_nblocks(long n);
+int p2p_prelu_fwd(const void* x, long n, const float* w, void* y, hipStream_t st);
+int p2p_prelu_bwd(const void* x, const void* dy, long n, const float* w, void* dx, float* ws, float* gw,
+                  int accumulate, hipStream_t st);
+int p2p_tv_fwd(const void* x, int N, int H, int W, int C, float* ws, float* out, hipStream_t st);
+int p2p_tv_bwd(const void* x, int N, int H, int W, int C, const float* gout, void* dx, hipStream_t st);
+int p2p_quantize(const void* x, long n, int bits, void* y, hipStream_t st);
+int p2p_avgpool3s2(const void* x, int N, int H, int W, int C, int OH, int OW, void* y, int bwd, hipStream_t st);
+int p2p_maxpool2(const void* x, const void* gy, int N, int H, int W, int C, void* out, hipStream_t st);
+int p2p_l2norm(const void* x, const void* gy, long P, int C, float eps, void* out, hipStream_t st);
+int p2p_pixel_shuffle(const void* in, int N, int OH, int OW, int OC, int r, int dir, void* out,
+                      hipStream_t st);
+int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, int reflect,
+                 const void* xb, int act, void* dx, hipStream_t st);
 int p2p_pad_channels(const void* a, int Ca, const void* b, int Cb, long P, int Co, void* out,
                      hipStream_t st);
 int p2p_slice_channels(const void* in, int Ci, int c0, long P, int C, void* out, hipStream_t st);
@@ -47,8 +61,8 @@ int p2p_loss_bwd(const void* a, const void* b, int is_f32, long n, int kind, flo
                  const float* gout, void* ga, void* gb, hipStream_t st);
 int p2p_adam_max_tensors();
 int p2p_adam(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
-             const long* n, const float* lr, const float* step, float b1, float b2, float eps,
-             float wd, hipStream_t st);
+             const long* n, const float* lr, const float* step, const float* skip, float b1, float b2,
+             float eps, float wd, hipStream_t st);
 }
 
 namespace {
@@ -85,11 +99,19 @@ const void* zero_page(const Tensor& like) {
 // rings) | unset = auto: g4 (256x128 tile, 8 waves, 3-stage ring) for Cout > 64, g2
 // (128x64, 2-stage) below -- the per-layer winners of tools/conv_bench.py on MI355X
 // (profiles/conv_variants_r1.jsonl).
-int conv_variant(int64_t Cout) {
+// glds tile variant: 4 = 256x128 3-stage (one 144 KB block per CU), 2 = 128-row 2-stage
+// (two blocks per CU).  A GEMM with only a few K tiles (packed 8-channel inputs / dgrads
+// of the image layers) spends most of a block's life in prologue and epilogue, which only
+// overlap across blocks when two fit on a CU.
+// 5 = 256x256 2-stage (Cout > 128 only; 8 waves of 128x64 -> a quarter less LDS fragment
+// traffic and half the A re-reads per MFMA of variant 4).
+int conv_variant(int64_t Cout, int64_t kmax) {
   const char* v = std::getenv("P2P_CONV_VARIANT");
   if (v && v[0] == 'v') return 1;
+  const int autov = (Cout > 64 && kmax > 256) ? 4 : 2;
   if (v && v[0] == 'g' && v[1] >= '2' && v[1] <= '4') return v[1] - '0';
-  return Cout > 64 ? 4 : 2;
+  if (v && v[0] == 'g' && v[1] == '5') return (Cout > 128 && kmax > 256) ? 5 : autov;
+  return autov;
 }
 
 Tensor empty_nhwc(int64_t N, int64_t C, int64_t H, int64_t W, const Tensor& like) {
@@ -171,12 +193,14 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   const int64_t Cv = Cvalid > 0 ? Cvalid : Cout;
   if (Cout <= 16 && Cv <= 16 && Csplit == Cout && !reflect && up == 1 && C1 % 64 == 0 &&
       C2 % 64 == 0) {
+    // col[i][t*Cvp + co]: each tap's outputs padded to Cvp (4 / 8 / 16) so col2im reads
+    // one aligned vector per tap
     const int64_t T = KH * KW;
-    const int64_t Ncol = ((T * Cv + 7) / 8) * 8;
-    Tensor wv = w.reshape({-1}).narrow(0, 0, Cout * T * C).view({Cout, T, C}).narrow(0, 0, Cv).transpose(0, 1)
-                    .reshape({T * Cv, C});
-    if (Ncol != T * Cv) wv = at::cat({wv, at::zeros({Ncol - T * Cv, C}, wv.options())});
-    wv = wv.contiguous();
+    const int64_t Cvp = Cv <= 2 ? Cv : (Cv <= 4 ? 4 : (Cv <= 8 ? 8 : 16));
+    const int64_t Ncol = ((T * Cvp + 7) / 8) * 8;
+    Tensor wv = at::zeros({Ncol, C}, w.options());
+    wv.narrow(0, 0, T * Cvp).view({T, Cvp, C}).narrow(1, 0, Cv).copy_(
+        w.reshape({-1}).narrow(0, 0, Cout * T * C).view({Cout, T, C}).narrow(0, 0, Cv).transpose(0, 1));
     Tensor col = empty_nhwc(N, Ncol, H, W, x1);
     p2p::ConvFwdArgs g = a;
     g.KH = g.KW = 1;
@@ -193,9 +217,15 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     g.xb1 = g.xb2 = nullptr;
     g.y1 = col.data_ptr();
     g.y2 = nullptr;
-    const int gbn = Ncol <= 16 ? 16 : (Ncol <= 32 ? 32 : (Ncol <= 64 ? 64 : 128));
-    const int gbm = gbn <= 32 ? 256 : 128;
-    check_rc(p2p_conv_fwd(&g, 0, gbm, gbn, st), "conv_fwd(col gemm)");
+    int grc = -2;
+    if (Ncol > 32 && (act_in == 0 || act_in == 1))
+      grc = p2p_conv_fwd_glds(&g, 0, conv_variant(Ncol, C), st);
+    if (grc == -2) {
+      const int gbn = Ncol <= 16 ? 16 : (Ncol <= 32 ? 32 : (Ncol <= 64 ? 64 : 128));
+      const int gbm = gbn <= 32 ? 256 : 128;
+      grc = p2p_conv_fwd(&g, 0, gbm, gbn, st);
+    }
+    check_rc(grc, "conv_fwd(col gemm)");
     check_rc(p2p_col2im((int)mode, col.data_ptr(), (int)Ncol, (int)N, (int)H, (int)W, (int)OH, (int)OW,
                         (int)KH, (int)KW, (int)stride, (int)pad, (int)Cv, (int)Cout, a.bias,
                         (int)act_out, act_bwd ? xb1->data_ptr() : nullptr, (int)act_bwd, y1.data_ptr(),
@@ -222,12 +252,12 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     mmax = std::max(mmax, N * hq * wq);
     kmax = std::max(kmax, taps * C);
   }
-  const int variant = conv_variant(Cout);
+  const int variant = conv_variant(Cout, kmax);
   const bool glds_ok = variant > 1 && Cout > 32 && (act_in == 0 || act_in == 1);
   int bm, bn;
   if (glds_ok) {
-    bn = Cout > 64 ? 128 : 64;
-    bm = variant == 4 ? 256 : 128;
+    bn = variant == 5 ? 256 : (Cout > 64 ? 128 : 64);
+    bm = (variant == 4 || variant == 5) ? 256 : 128;
   } else if (Cout <= 16) {
     bn = 16;
     bm = mmax >= 4096 ? 256 : 64;
@@ -505,6 +535,142 @@ Tensor dropout(const Tensor& x, double p, const Tensor& seed, int64_t salt) {
   return y;
 }
 
+// ------------------------------------------------------------------ family-R fringe ops
+static void check_nhwc(const Tensor& x, const char* what) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4, what, ": bf16 4-D CUDA");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), what, ": NHWC (channels_last) input");
+}
+
+Tensor prelu_fwd(const Tensor& x, const Tensor& w) {
+  check_nhwc(x, "prelu");
+  TORCH_CHECK(w.numel() == 1 && w.scalar_type() == at::kFloat, "prelu: one fp32 slope");
+  Tensor y = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  check_rc(p2p_prelu_fwd(x.data_ptr(), x.numel(), w.data_ptr<float>(), y.data_ptr(), cur_stream(x)), "prelu");
+  return y;
+}
+
+std::vector<Tensor> prelu_bwd(const Tensor& x, const Tensor& gy, const Tensor& w, bool need_x) {
+  check_nhwc(x, "prelu_bwd x");
+  check_nhwc(gy, "prelu_bwd gy");
+  Tensor gx;
+  if (need_x) gx = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor ws = at::empty({p2p_misc_nblocks(x.numel())}, x.options().dtype(at::kFloat));
+  Tensor gw = at::empty({1}, x.options().dtype(at::kFloat));
+  check_rc(p2p_prelu_bwd(x.data_ptr(), gy.data_ptr(), x.numel(), w.data_ptr<float>(),
+                         need_x ? gx.data_ptr() : nullptr, ws.data_ptr<float>(), gw.data_ptr<float>(), 0,
+                         cur_stream(x)),
+           "prelu_bwd");
+  if (!need_x) return {gw};
+  return {gw, gx};
+}
+
+Tensor tv_fwd(const Tensor& x) {
+  check_nhwc(x, "tv");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  Tensor ws = at::empty({p2p_misc_nblocks(x.numel())}, x.options().dtype(at::kFloat));
+  Tensor out = at::empty({}, x.options().dtype(at::kFloat));
+  check_rc(p2p_tv_fwd(x.data_ptr(), N, H, W, C, ws.data_ptr<float>(), out.data_ptr<float>(), cur_stream(x)),
+           "tv");
+  return out;
+}
+
+Tensor tv_bwd(const Tensor& x, const Tensor& gout) {
+  check_nhwc(x, "tv_bwd");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  Tensor g = gout.to(at::kFloat).reshape({1}).contiguous();
+  Tensor gx = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  check_rc(p2p_tv_bwd(x.data_ptr(), N, H, W, C, g.data_ptr<float>(), gx.data_ptr(), cur_stream(x)), "tv_bwd");
+  return gx;
+}
+
+Tensor quantize(const Tensor& x, int64_t bits) {
+  check_nhwc(x, "quantize");
+  TORCH_CHECK(bits >= 1 && bits <= 16, "quantize: bits");
+  Tensor y = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  check_rc(p2p_quantize(x.data_ptr(), x.numel(), (int)bits, y.data_ptr(), cur_stream(x)), "quantize");
+  return y;
+}
+
+// bwd = 0: x (N,C,H,W) -> pooled; bwd = 1: x = gy (N,C,OH,OW) -> gx (N,C,H,W)
+Tensor avgpool3s2(const Tensor& x, int64_t bwd, int64_t H, int64_t W) {
+  check_nhwc(x, "avgpool3s2");
+  const int64_t N = x.size(0), C = x.size(1);
+  int64_t h = x.size(2), w = x.size(3);
+  if (!bwd) {
+    H = h;
+    W = w;
+  }
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  if (bwd) TORCH_CHECK(h == OH && w == OW, "avgpool3s2 bwd: geometry");
+  Tensor y = bwd ? empty_nhwc(N, C, H, W, x) : empty_nhwc(N, C, OH, OW, x);
+  check_rc(p2p_avgpool3s2(x.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)OH, (int)OW, y.data_ptr(),
+                          (int)bwd, cur_stream(x)),
+           "avgpool3s2");
+  return y;
+}
+
+Tensor maxpool2(const Tensor& x, const optional<Tensor>& gy) {
+  check_nhwc(x, "maxpool2");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  Tensor out = gy ? empty_nhwc(N, C, H, W, x) : empty_nhwc(N, C, H / 2, W / 2, x);
+  if (gy) check_nhwc(*gy, "maxpool2 gy");
+  check_rc(p2p_maxpool2(x.data_ptr(), gy ? gy->data_ptr() : nullptr, (int)N, (int)H, (int)W, (int)C,
+                        out.data_ptr(), cur_stream(x)),
+           "maxpool2");
+  return out;
+}
+
+Tensor l2norm(const Tensor& x, const optional<Tensor>& gy, double eps) {
+  check_nhwc(x, "l2norm");
+  if (gy) check_nhwc(*gy, "l2norm gy");
+  Tensor out = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t C = x.size(1);
+  check_rc(p2p_l2norm(x.data_ptr(), gy ? gy->data_ptr() : nullptr, x.numel() / C, (int)C, (float)eps,
+                      out.data_ptr(), cur_stream(x)),
+           "l2norm");
+  return out;
+}
+
+// dir 0: unshuffle (C,H,W) -> (C*r*r, H/r, W/r); dir 1: shuffle (C,H,W) -> (C/(r*r), H*r, W*r)
+Tensor pixel_shuffle(const Tensor& x, int64_t r, int64_t dir) {
+  check_nhwc(x, "pixel_shuffle");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  int64_t OC, OH, OW;
+  if (dir == 0) {
+    TORCH_CHECK(H % r == 0 && W % r == 0, "pixel_unshuffle: H, W % r");
+    OC = C * r * r;
+    OH = H / r;
+    OW = W / r;
+  } else {
+    TORCH_CHECK(C % (r * r) == 0, "pixel_shuffle: C % r^2");
+    OC = C / (r * r);
+    OH = H * r;
+    OW = W * r;
+  }
+  Tensor out = empty_nhwc(N, OC, OH, OW, x);
+  check_rc(p2p_pixel_shuffle(x.data_ptr(), (int)N, (int)OH, (int)OW, (int)OC, (int)r, (int)dir, out.data_ptr(),
+                             cur_stream(x)),
+           "pixel_shuffle");
+  return out;
+}
+
+// pad_fold: gradient of a virtual reflect/zero-padded + nearest-upsampled input -> real input
+Tensor pad_fold(const Tensor& dxp, int64_t H, int64_t W, int64_t pad, int64_t up, int64_t reflect,
+                const optional<Tensor>& xb, int64_t act) {
+  TORCH_CHECK(dxp.is_cuda() && dxp.scalar_type() == at::kBFloat16 && dxp.dim() == 4, "pad_fold: dxp");
+  TORCH_CHECK(dxp.is_contiguous(at::MemoryFormat::ChannelsLast), "pad_fold: NHWC input");
+  const int64_t N = dxp.size(0), C = dxp.size(1);
+  TORCH_CHECK(C % 8 == 0, "pad_fold: C % 8");
+  TORCH_CHECK(dxp.size(2) == H * up + 2 * pad && dxp.size(3) == W * up + 2 * pad, "pad_fold: geometry");
+  TORCH_CHECK(!act || (xb && xb->is_contiguous(at::MemoryFormat::ChannelsLast) && xb->size(1) == C),
+              "pad_fold: xb");
+  Tensor dx = empty_nhwc(N, C, H, W, dxp);
+  check_rc(p2p_pad_fold(dxp.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)pad, (int)up, (int)reflect,
+                        act ? xb->data_ptr() : nullptr, (int)act, dx.data_ptr(), cur_stream(dxp)),
+           "pad_fold");
+  return dx;
+}
+
 // pad_channels: NHWC a (Ca) [+ b (Cb)] -> Co channels, zero filled
 Tensor pad_channels(const Tensor& a, const optional<Tensor>& b, int64_t Co) {
   TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && a.dim() == 4, "pad_channels: a");
@@ -594,8 +760,9 @@ std::vector<Tensor> loss_bwd(const Tensor& a, const optional<Tensor>& b, int64_t
 
 // ------------------------------------------------------------------ optimizer
 void adam(at::TensorList p, at::TensorList g, at::TensorList m, at::TensorList v, const Tensor& lr,
-          const Tensor& step, double b1, double b2, double eps, double wd) {
+          const Tensor& step, double b1, double b2, double eps, double wd, const optional<Tensor>& skip) {
   const size_t n = p.size();
+  TORCH_CHECK(!skip || skip->scalar_type() == at::kFloat, "adam: skip flag fp32");
   TORCH_CHECK(g.size() == n && m.size() == n && v.size() == n, "adam: list sizes");
   TORCH_CHECK(lr.scalar_type() == at::kFloat && step.scalar_type() == at::kFloat, "adam: lr/step fp32");
   const int maxT = p2p_adam_max_tensors();
@@ -606,7 +773,8 @@ void adam(at::TensorList p, at::TensorList g, at::TensorList m, at::TensorList v
   auto flush = [&]() {
     if (P.empty()) return;
     check_rc(p2p_adam((int)P.size(), P.data(), G.data(), M.data(), V.data(), Nn.data(),
-                      lr.data_ptr<float>(), step.data_ptr<float>(), (float)b1, (float)b2, (float)eps,
+                      lr.data_ptr<float>(), step.data_ptr<float>(), skip ? skip->data_ptr<float>() : nullptr,
+                      (float)b1, (float)b2, (float)eps,
                       (float)wd, st),
              "adam");
     P.clear(); G.clear(); M.clear(); V.clear(); Nn.clear();
@@ -636,6 +804,16 @@ TORCH_LIBRARY(p2p, m) {
         "int stride, int pad, int reflect, int up, Tensor(a!) dw, float scale, int accumulate, "
         "int flip=0) -> ()");
   m.def("weight_prep(Tensor w, int swap, int Xp, int Yp, Tensor? scale) -> Tensor");
+  m.def("prelu_fwd(Tensor x, Tensor w) -> Tensor");
+  m.def("prelu_bwd(Tensor x, Tensor gy, Tensor w, bool need_x) -> Tensor[]");
+  m.def("tv_fwd(Tensor x) -> Tensor");
+  m.def("tv_bwd(Tensor x, Tensor gout) -> Tensor");
+  m.def("quantize(Tensor x, int bits) -> Tensor");
+  m.def("avgpool3s2(Tensor x, int bwd, int H, int W) -> Tensor");
+  m.def("maxpool2(Tensor x, Tensor? gy) -> Tensor");
+  m.def("l2norm(Tensor x, Tensor? gy, float eps) -> Tensor");
+  m.def("pixel_shuffle(Tensor x, int r, int dir) -> Tensor");
+  m.def("pad_fold(Tensor dxp, int H, int W, int pad, int up, int reflect, Tensor? xb, int act) -> Tensor");
   m.def("weight_prep_multi(Tensor[] w, int[] swap, int[] xp, int[] yp) -> Tensor[]");
   m.def("norm_fwd(Tensor x, float eps, Tensor? gamma, Tensor? beta, Tensor? prelu_w, int act, "
         "Tensor(a!)? run_mean, Tensor(b!)? run_var, float momentum, bool batch) -> Tensor[]");
@@ -652,7 +830,7 @@ TORCH_LIBRARY(p2p, m) {
   m.def("loss_bwd(Tensor a, Tensor? b, int kind, float t, float scale, Tensor gout, bool need_a, "
         "bool need_b) -> Tensor[]");
   m.def("adam(Tensor(a!)[] p, Tensor[] g, Tensor(b!)[] m, Tensor(c!)[] v, Tensor lr, Tensor step, "
-        "float b1, float b2, float eps, float wd) -> ()");
+        "float b1, float b2, float eps, float wd, Tensor? skip=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
@@ -666,6 +844,16 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("act", act);
   m.impl("dropout", dropout);
   m.impl("pad_channels", pad_channels);
+  m.impl("pad_fold", pad_fold);
+  m.impl("prelu_fwd", prelu_fwd);
+  m.impl("prelu_bwd", prelu_bwd);
+  m.impl("tv_fwd", tv_fwd);
+  m.impl("tv_bwd", tv_bwd);
+  m.impl("quantize", quantize);
+  m.impl("avgpool3s2", avgpool3s2);
+  m.impl("maxpool2", maxpool2);
+  m.impl("l2norm", l2norm);
+  m.impl("pixel_shuffle", pixel_shuffle);
   m.impl("slice_channels", slice_channels);
   m.impl("colsum", colsum);
   m.impl("loss_fwd", loss_fwd);

@@ -408,23 +408,27 @@ extern "C" int p2p_weight_prep(const float* w, int A, int B, int KH, int KW, int
 namespace p2p {
 // one thread per output pixel; only the taps that hit it are visited (MODE 1: the
 // ceil(K/s)^2 taps of its parity class, found arithmetically -- no per-tap divisibility
-// loop), each tap's Cv values are contiguous in col.
-template <int MODE>
+// loop).  Each tap's values are CVP (4 / 8 / 16, >= Cv, zero-padded by the GEMM) contiguous
+// bf16 in col, read as one 8 / 16 / 32-byte vector per tap.
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+template <int MODE, int CVP>
 __global__ void __launch_bounds__(256) col2im_kernel(const bf16* __restrict__ col, int ldc, int N, int H,
                                                      int W, int OH, int OW, int KH, int KW, int s, int p,
                                                      int Cv, int Coutp, const float* __restrict__ bias,
                                                      int act_out, const bf16* __restrict__ xb, int act_bwd,
                                                      bf16* __restrict__ y) {
-  constexpr int MAXC = 16;
+  constexpr int NW = CVP / 2;  // 32-bit words per tap
   const long total = (long)N * OH * OW;
   for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
     const int ox = (int)(o % OW);
     const long t1 = o / OW;
     const int oy = (int)(t1 % OH);
     const int n = (int)(t1 / OH);
-    float acc[MAXC];
+    float acc[CVP];
 #pragma unroll
-    for (int j = 0; j < MAXC; ++j) acc[j] = 0.f;
+    for (int j = 0; j < CVP; ++j) acc[j] = 0.f;
     int ky = 0, kx0 = 0, kstep = 1;
     if (MODE == 1) {
       ky = (oy + p) % s;
@@ -437,27 +441,59 @@ __global__ void __launch_bounds__(256) col2im_kernel(const bf16* __restrict__ co
       for (int kx = kx0; kx < KW; kx += kstep) {
         const int ix = MODE == 0 ? ox * s - p + kx : (ox + p - kx) / s;
         if ((unsigned)ix >= (unsigned)W) continue;
-        const bf16* src = col + ((long)(n * H + iy) * W + ix) * ldc + (ky * KW + kx) * Cv;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(
+            col + ((long)(n * H + iy) * W + ix) * ldc + (ky * KW + kx) * CVP);
+        if constexpr (CVP == 1) {
+          acc[0] += (float)*reinterpret_cast<const bf16*>(src);
+          continue;
+        }
+        uint32_t wv[NW > 0 ? NW : 1];
+        if constexpr (NW == 1) {
+          wv[0] = src[0];
+        } else if constexpr (NW == 2) {
+          const uint2 v = *reinterpret_cast<const uint2*>(src);
+          wv[0] = v.x;
+          wv[1] = v.y;
+        } else {
 #pragma unroll
-        for (int j = 0; j < MAXC; ++j)
-          if (j < Cv) acc[j] += (float)src[j];
+          for (int q = 0; q < NW / 4; ++q) {
+            const uint4 v = *reinterpret_cast<const uint4*>(src + 4 * q);
+            wv[4 * q] = v.x;
+            wv[4 * q + 1] = v.y;
+            wv[4 * q + 2] = v.z;
+            wv[4 * q + 3] = v.w;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+          acc[2 * q] += bf_lo(wv[q]);
+          acc[2 * q + 1] += bf_hi(wv[q]);
+        }
       }
     }
     for (int g0 = 0; g0 < Coutp; g0 += 8) {
-      bf16x8 out;
-      bf16x8 xv;
-      if (act_bwd) xv = *reinterpret_cast<const bf16x8*>(xb + o * Coutp + g0);
+      uint4 xv = make_uint4(0, 0, 0, 0);
+      if (act_bwd) xv = *reinterpret_cast<const uint4*>(xb + o * Coutp + g0);
+      const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w};
+      uint32_t ow[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int co = g0 + j;
-        float v = 0.f;
+      for (int q = 0; q < 4; ++q) {
+        float v2[2];
 #pragma unroll
-        for (int q = 0; q < MAXC; ++q)
-          if (q == co && co < Cv) v = act_fwd(acc[q] + (bias ? bias[co] : 0.f), act_out);
-        if (act_bwd) v *= act_grad_from_input((float)xv[j], act_bwd);
-        out[j] = (bf16)v;
+        for (int h = 0; h < 2; ++h) {
+          const int co = g0 + 2 * q + h;
+          float v = 0.f;
+#pragma unroll
+          for (int k = 0; k < CVP; ++k)
+            if (k == co && co < Cv) v = act_fwd(acc[k] + (bias ? bias[co] : 0.f), act_out);
+          if (act_bwd) v *= act_grad_from_input(h ? bf_hi(xw[q]) : bf_lo(xw[q]), act_bwd);
+          v2[h] = v;
+        }
+        const uint32_t lo = __builtin_bit_cast(uint16_t, (bf16)v2[0]);
+        const uint32_t hi = __builtin_bit_cast(uint16_t, (bf16)v2[1]);
+        ow[q] = lo | (hi << 16);
       }
-      *reinterpret_cast<bf16x8*>(y + o * Coutp + g0) = out;
+      *reinterpret_cast<uint4*>(y + o * Coutp + g0) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
     }
   }
 }
@@ -473,12 +509,25 @@ extern "C" int p2p_col2im(int mode, const void* col, int ldc, int N, int H, int 
   const p2p::bf16* c = static_cast<const p2p::bf16*>(col);
   const p2p::bf16* x = static_cast<const p2p::bf16*>(xb);
   p2p::bf16* o = static_cast<p2p::bf16*>(y);
-  if (mode == 0)
-    hipLaunchKernelGGL(p2p::col2im_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, st, c, ldc, N, H, W, OH,
-                       OW, KH, KW, s, p, Cv, Coutp, bias, act_out, x, act_bwd, o);
-  else
-    hipLaunchKernelGGL(p2p::col2im_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, st, c, ldc, N, H, W, OH,
-                       OW, KH, KW, s, p, Cv, Coutp, bias, act_out, x, act_bwd, o);
+  const int cvp = Cv <= 2 ? Cv : (Cv <= 4 ? 4 : (Cv <= 8 ? 8 : 16));
+  if (Cv > 16 || Cv < 1 || ldc % cvp) return -1;
+#define P2P_COL2IM(M, V)                                                                              \
+  hipLaunchKernelGGL((p2p::col2im_kernel<M, V>), dim3((unsigned)blocks), dim3(256), 0, st, c, ldc, N, H, W, \
+                     OH, OW, KH, KW, s, p, Cv, Coutp, bias, act_out, x, act_bwd, o)
+  if (mode == 0) {
+    if (cvp == 1) P2P_COL2IM(0, 1);
+    else if (cvp == 2) P2P_COL2IM(0, 2);
+    else if (cvp == 4) P2P_COL2IM(0, 4);
+    else if (cvp == 8) P2P_COL2IM(0, 8);
+    else P2P_COL2IM(0, 16);
+  } else {
+    if (cvp == 1) P2P_COL2IM(1, 1);
+    else if (cvp == 2) P2P_COL2IM(1, 2);
+    else if (cvp == 4) P2P_COL2IM(1, 4);
+    else if (cvp == 8) P2P_COL2IM(1, 8);
+    else P2P_COL2IM(1, 16);
+  }
+#undef P2P_COL2IM
   return (int)hipGetLastError();
 }
 
@@ -529,6 +578,23 @@ __global__ void __launch_bounds__(256) weight_prep_multi_kernel(WPrepList L) {
     const float* r0 = w + ((long)a0 * B + b0) * T;
     const float* r1 = w + ((long)a1 * B + b1) * T;
     uint32_t* o = reinterpret_cast<uint32_t*>(out + (long)xv * T * Yp + y0);
+    if (T == 16) {  // 4x4 kernels: two 64-B rows as 16-B vector loads
+      float4 f0[4], f1[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f0[q] = ok0 ? reinterpret_cast<const float4*>(r0)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        f1[q] = ok1 ? reinterpret_cast<const float4*>(r1)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      const float* a0 = reinterpret_cast<const float*>(f0);
+      const float* a1 = reinterpret_cast<const float*>(f1);
+#pragma unroll
+      for (int tap = 0; tap < 16; ++tap) {
+        const uint32_t lo = __builtin_bit_cast(uint16_t, (bf16)a0[tap]);
+        const uint32_t hi = __builtin_bit_cast(uint16_t, (bf16)a1[tap]);
+        o[(long)tap * Yh] = lo | (hi << 16);
+      }
+      continue;
+    }
     for (int tap = 0; tap < T; ++tap) {
       const float v0 = ok0 ? r0[tap] : 0.f;
       const float v1 = ok1 ? r1[tap] : 0.f;

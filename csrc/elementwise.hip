@@ -97,6 +97,70 @@ __global__ void __launch_bounds__(256) pad_channels_kernel(const bf16* __restric
   }
 }
 
+// dgrad of a conv whose input was reflect/zero padded by `pad` and nearest-upsampled by
+// `up` inside the conv's gather (family-R ConvLayer / UpsampleConvLayer): the MODE-1 dgrad
+// wrote the gradient of the VIRTUAL padded input dxp[N][Hp][Wp][C] (Hp = H*up + 2*pad);
+// here every real input pixel sums the padded positions that read it (reflection maps up
+// to 3 padded rows onto one, the upsample 2x2 up-pixels onto one), then the input
+// activation's derivative is applied (act_bwd with the saved input xb).
+// One thread per (pixel, 8-channel chunk).
+__device__ __forceinline__ int fold_taps(int u, int pad, int Hu, bool reflect, int* q) {
+  int n = 0;
+  const int c[3] = {u + pad, pad - u, 2 * (Hu - 1) + pad - u};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int qq = c[i];
+    if (qq < 0 || qq >= Hu + 2 * pad) continue;
+    const int src = reflect ? reflect_idx(qq - pad, Hu) : qq - pad;
+    if (src != u) continue;
+    bool dup = false;
+    for (int j = 0; j < n; ++j) dup = dup || q[j] == qq;
+    if (!dup) q[n++] = qq;
+  }
+  return n;
+}
+
+__global__ void __launch_bounds__(256) pad_fold_kernel(const bf16* __restrict__ dxp, int N, int H, int W,
+                                                       int C, int pad, int up, int reflect,
+                                                       const bf16* __restrict__ xb, int act,
+                                                       bf16* __restrict__ dx) {
+  const int CP = C >> 3;
+  const int Hu = H * up, Wu = W * up;
+  const int Hp = Hu + 2 * pad, Wp = Wu + 2 * pad;
+  const long total = (long)N * H * W * CP;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int cg = (int)(e % CP);
+    const long pix = e / CP;
+    const int x = (int)(pix % W);
+    const long t = pix / W;
+    const int y = (int)(t % H);
+    const int n = (int)(t / H);
+    int qy[6], qx[6];
+    int ny = 0, nx = 0;
+    for (int k = 0; k < up; ++k) {
+      ny += fold_taps(y * up + k, pad, Hu, reflect != 0, qy + ny);
+      nx += fold_taps(x * up + k, pad, Wu, reflect != 0, qx + nx);
+    }
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int i = 0; i < ny; ++i)
+      for (int k = 0; k < nx; ++k) {
+        float f[8];
+        unpack8e(*reinterpret_cast<const u32x4*>(dxp + (((long)n * Hp + qy[i]) * Wp + qx[k]) * C + cg * 8), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += f[j];
+      }
+    if (act) {
+      float xf[8];
+      unpack8e(*reinterpret_cast<const u32x4*>(xb + pix * C + cg * 8), xf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] *= act_grad_from_input(xf[j], act);
+    }
+    *reinterpret_cast<u32x4*>(dx + pix * C + cg * 8) = pack8e(acc);
+  }
+}
+
 // out[p][0:C] = in[p][c0:c0+C]   (in has Ci channels); one thread per pixel
 __global__ void __launch_bounds__(256) slice_channels_kernel(const bf16* __restrict__ in, int Ci, int c0,
                                                              long P, int C, bf16* __restrict__ out) {
@@ -271,6 +335,15 @@ int p2p_pad_channels(const void* a, int Ca, const void* b, int Cb, long P, int C
   hipLaunchKernelGGL(pad_channels_kernel, dim3(egrid(P)), dim3(256), 0, st,
                      static_cast<const bf16*>(a), Ca, static_cast<const bf16*>(b), Cb, P, Co,
                      static_cast<bf16*>(out));
+  return (int)hipGetLastError();
+}
+
+int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, int reflect,
+                 const void* xb, int act, void* dx, hipStream_t st) {
+  using namespace p2p;
+  const long total = (long)N * H * W * (C / 8);
+  hipLaunchKernelGGL(pad_fold_kernel, dim3(egrid(total)), dim3(256), 0, st, static_cast<const bf16*>(dxp), N,
+                     H, W, C, pad, up, reflect, static_cast<const bf16*>(xb), act, static_cast<bf16*>(dx));
   return (int)hipGetLastError();
 }
 

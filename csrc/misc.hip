@@ -1,0 +1,375 @@
+// Family-R (compression GAN) fringe ops on bf16 NHWC tensors (gfx950): shared-scalar
+// PReLU, anisotropic TV loss, the 3-bit quantiser, AvgPool(3, s2, p1, no-pad-count) of the
+// multiscale discriminator, 2x2 max-pool (VGG19), per-pixel L2 normalisation over channels
+// (compression network head) and pixel (un)shuffle.  All memory-bound: one thread per
+// output element (or pixel), backward passes written as gathers so no atomics are needed
+// and every result is bitwise reproducible; reductions are two-stage (block partials ->
+// one finishing block, fixed order).
+//   reference: networks.py:173-236 (C), :452 (PReLU), :732 (AvgPool), train.py:123-126
+//   (TV), generate_dataset.py:29-34 (quantiser), torchvision VGG19 (max-pool).
+#include "common.h"
+
+namespace p2p {
+
+static inline unsigned mgrid(long work) {
+  long b = (work + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+__device__ __forceinline__ float block_sum256(float s, float* red) {
+  s = warp_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+// ------------------------------------------------------------------ PReLU (one slope)
+__global__ void __launch_bounds__(256) prelu_fwd_kernel(const bf16* __restrict__ x, long n,
+                                                        const float* __restrict__ w, bf16* __restrict__ y) {
+  const float a = w[0];
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const float v = (float)x[e];
+    y[e] = (bf16)(v > 0.f ? v : a * v);
+  }
+}
+
+// dx = dy * (x > 0 ? 1 : a); ws[block] = sum dy * x * [x <= 0]
+__global__ void __launch_bounds__(256) prelu_bwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                        long n, const float* __restrict__ w,
+                                                        bf16* __restrict__ dx, float* __restrict__ ws) {
+  const float a = w[0];
+  float s = 0.f;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const float v = (float)x[e], g = (float)dy[e];
+    if (dx) dx[e] = (bf16)(v > 0.f ? g : a * g);
+    if (v <= 0.f) s += g * v;
+  }
+  __shared__ float red[4];
+  const float t = block_sum256(s, red);
+  if (threadIdx.x == 0) ws[blockIdx.x] = t;
+}
+
+__global__ void __launch_bounds__(256) sum_final_kernel(const float* __restrict__ ws, int nb, float scale,
+                                                        int accumulate, float* __restrict__ out) {
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 256) s += ws[i];
+  __shared__ float red[4];
+  const float t = block_sum256(s, red) * scale;
+  if (threadIdx.x == 0) out[0] = accumulate ? out[0] + t : t;
+}
+
+// ------------------------------------------------------------------ TV loss
+// mean|x[..., w] - x[..., w+1]| + mean|x[h, :] - x[h+1, :]|  over NHWC (N, H, W, C)
+__global__ void __launch_bounds__(256) tv_partial_kernel(const bf16* __restrict__ x, int N, int H, int W, int C,
+                                                         float ih, float iv, float* __restrict__ ws) {
+  const long n = (long)N * H * W * C;
+  float s = 0.f;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const long pix = e / C;
+    const int w = (int)(pix % W);
+    const int h = (int)((pix / W) % H);
+    const float v = (float)x[e];
+    if (w + 1 < W) s += fabsf(v - (float)x[e + C]) * ih;
+    if (h + 1 < H) s += fabsf(v - (float)x[e + (long)W * C]) * iv;
+  }
+  __shared__ float red[4];
+  const float t = block_sum256(s, red);
+  if (threadIdx.x == 0) ws[blockIdx.x] = t;
+}
+
+__device__ __forceinline__ float sgnf(float d) { return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); }
+
+__global__ void __launch_bounds__(256) tv_grad_kernel(const bf16* __restrict__ x, int N, int H, int W, int C,
+                                                      float ih, float iv, const float* __restrict__ gout,
+                                                      bf16* __restrict__ dx) {
+  const long n = (long)N * H * W * C;
+  const float g = gout[0];
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const long pix = e / C;
+    const int w = (int)(pix % W);
+    const int h = (int)((pix / W) % H);
+    const float v = (float)x[e];
+    float d = 0.f;
+    if (w + 1 < W) d += sgnf(v - (float)x[e + C]) * ih;
+    if (w > 0) d -= sgnf((float)x[e - C] - v) * ih;
+    if (h + 1 < H) d += sgnf(v - (float)x[e + (long)W * C]) * iv;
+    if (h > 0) d -= sgnf((float)x[e - (long)W * C] - v) * iv;
+    dx[e] = (bf16)(g * d);
+  }
+}
+
+// ------------------------------------------------------------------ quantiser
+__global__ void __launch_bounds__(256) quantize_kernel(const bf16* __restrict__ x, long n, float m,
+                                                       bf16* __restrict__ y) {
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const float v = fminf(fmaxf((float)x[e], 0.f), 1.f);
+    y[e] = (bf16)(rintf(v * m) / m);
+  }
+}
+
+// ------------------------------------------------------------------ AvgPool 3x3 s2 p1, count_include_pad=False
+__device__ __forceinline__ int pool_count(int o, int n) {  // valid taps of window 2o-1 .. 2o+1
+  const int lo = max(2 * o - 1, 0), hi = min(2 * o + 1, n - 1);
+  return hi - lo + 1;
+}
+
+__global__ void __launch_bounds__(256) avgpool_fwd_kernel(const bf16* __restrict__ x, int N, int H, int W, int C,
+                                                          int OH, int OW, bf16* __restrict__ y) {
+  const long n = (long)N * OH * OW * C;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int c = (int)(e % C);
+    const long p = e / C;
+    const int ow = (int)(p % OW);
+    const int oh = (int)((p / OW) % OH);
+    const int b = (int)(p / ((long)OW * OH));
+    float s = 0.f;
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int ih = 2 * oh + dy;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int iw = 2 * ow + dx;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        s += (float)x[(((long)b * H + ih) * W + iw) * C + c];
+      }
+    }
+    y[e] = (bf16)(s / (float)(pool_count(oh, H) * pool_count(ow, W)));
+  }
+}
+
+__global__ void __launch_bounds__(256) avgpool_bwd_kernel(const bf16* __restrict__ gy, int N, int H, int W, int C,
+                                                          int OH, int OW, bf16* __restrict__ gx) {
+  const long n = (long)N * H * W * C;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int c = (int)(e % C);
+    const long p = e / C;
+    const int iw = (int)(p % W);
+    const int ih = (int)((p / W) % H);
+    const int b = (int)(p / ((long)W * H));
+    float s = 0.f;
+    // outputs whose window 2o-1..2o+1 contains i: o in [ceil((i-1)/2), floor((i+1)/2)]
+    for (int oh = (ih > 0 ? ih : ih + 1) / 2; oh <= (ih + 1) / 2; ++oh) {
+      if (oh >= OH) continue;
+      for (int ow = (iw > 0 ? iw : iw + 1) / 2; ow <= (iw + 1) / 2; ++ow) {
+        if (ow >= OW) continue;
+        s += (float)gy[(((long)b * OH + oh) * OW + ow) * C + c] /
+             (float)(pool_count(oh, H) * pool_count(ow, W));
+      }
+    }
+    gx[e] = (bf16)s;
+  }
+}
+
+// ------------------------------------------------------------------ MaxPool 2x2 s2
+// PyTorch semantics: the gradient goes to the FIRST maximum of the window in row-major
+// order (strict '>' scan; NaN wins).
+__device__ __forceinline__ int max2x2_arg(const bf16* x, long base, long rowst, int C, float* mv) {
+  int arg = 0;
+  float m = (float)x[base];
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    const float v = (float)x[base + (k >> 1) * rowst + (k & 1) * C];
+    if (v > m || v != v) {
+      m = v;
+      arg = k;
+    }
+  }
+  *mv = m;
+  return arg;
+}
+
+__global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16* __restrict__ x, int N, int H, int W, int C,
+                                                          bf16* __restrict__ y) {
+  const int OH = H / 2, OW = W / 2;
+  const long n = (long)N * OH * OW * C;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int c = (int)(e % C);
+    const long p = e / C;
+    const int ow = (int)(p % OW);
+    const int oh = (int)((p / OW) % OH);
+    const int b = (int)(p / ((long)OW * OH));
+    float m;
+    max2x2_arg(x, (((long)b * H + 2 * oh) * W + 2 * ow) * C + c, (long)W * C, C, &m);
+    y[e] = (bf16)m;
+  }
+}
+
+__global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ gy,
+                                                          int N, int H, int W, int C, bf16* __restrict__ gx) {
+  const int OH = H / 2, OW = W / 2;
+  const long n = (long)N * H * W * C;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int c = (int)(e % C);
+    const long p = e / C;
+    const int iw = (int)(p % W);
+    const int ih = (int)((p / W) % H);
+    const int b = (int)(p / ((long)W * H));
+    const int oh = ih >> 1, ow = iw >> 1;
+    float g = 0.f;
+    if (oh < OH && ow < OW) {
+      float m;
+      const int arg = max2x2_arg(x, (((long)b * H + 2 * oh) * W + 2 * ow) * C + c, (long)W * C, C, &m);
+      if (arg == ((ih & 1) << 1 | (iw & 1))) g = (float)gy[(((long)b * OH + oh) * OW + ow) * C + c];
+    }
+    gx[e] = (bf16)g;
+  }
+}
+
+// ------------------------------------------------------------------ L2 normalise over channels
+// y = x / max(||x||, eps);  dx = (dy - y * <dy, y>) / max(||x||, eps)  (norm > eps),
+// dx = dy / eps otherwise (F.normalize's clamp_min has zero gradient below eps)
+__global__ void __launch_bounds__(256) l2norm_fwd_kernel(const bf16* __restrict__ x, long P, int C, float eps,
+                                                         bf16* __restrict__ y) {
+  for (long p = blockIdx.x * 256L + threadIdx.x; p < P; p += (long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float v = (float)x[p * C + c];
+      s += v * v;
+    }
+    const float inv = 1.f / fmaxf(sqrtf(s), eps);
+    for (int c = 0; c < C; ++c) y[p * C + c] = (bf16)((float)x[p * C + c] * inv);
+  }
+}
+
+__global__ void __launch_bounds__(256) l2norm_bwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ gy,
+                                                         long P, int C, float eps, bf16* __restrict__ gx) {
+  for (long p = blockIdx.x * 256L + threadIdx.x; p < P; p += (long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float v = (float)x[p * C + c];
+      s += v * v;
+    }
+    const float nrm = sqrtf(s);
+    const float d = fmaxf(nrm, eps);
+    float dot = 0.f;
+    if (nrm > eps)
+      for (int c = 0; c < C; ++c) dot += (float)gy[p * C + c] * (float)x[p * C + c];
+    const float k = nrm > eps ? dot / (d * d * d) : 0.f;
+    for (int c = 0; c < C; ++c)
+      gx[p * C + c] = (bf16)((float)gy[p * C + c] / d - (float)x[p * C + c] * k);
+  }
+}
+
+// ------------------------------------------------------------------ pixel (un)shuffle, NHWC
+// unshuffle: out[n][h][w][c*r*r + i*r + j] = in[n][h*r+i][w*r+j][c]   (out H/r x W/r x C*r*r)
+// shuffle is the inverse map.  dir 0 = unshuffle, 1 = shuffle; shapes are the OUTPUT's.
+__global__ void __launch_bounds__(256) pixel_shuffle_kernel(const bf16* __restrict__ in, int N, int OH, int OW,
+                                                            int OC, int r, int dir, bf16* __restrict__ out) {
+  const long n = (long)N * OH * OW * OC;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int oc = (int)(e % OC);
+    const long p = e / OC;
+    const int ow = (int)(p % OW);
+    const int oh = (int)((p / OW) % OH);
+    const int b = (int)(p / ((long)OW * OH));
+    long src;
+    if (dir == 0) {  // input (OH*r, OW*r, OC/(r*r))
+      const int C = OC / (r * r);
+      const int c = oc / (r * r), ij = oc % (r * r), i = ij / r, j = ij % r;
+      src = (((long)b * OH * r + oh * r + i) * (OW * r) + ow * r + j) * C + c;
+    } else {         // input (OH/r, OW/r, OC*r*r)
+      const int IH = OH / r, IW = OW / r, IC = OC * r * r;
+      const int ih = oh / r, i = oh % r, iw = ow / r, j = ow % r;
+      src = (((long)b * IH + ih) * IW + iw) * IC + oc * r * r + i * r + j;
+    }
+    out[e] = in[src];
+  }
+}
+
+}  // namespace p2p
+
+extern "C" {
+
+int p2p_misc_nblocks(long n) { return (int)p2p::mgrid(n); }
+
+int p2p_prelu_fwd(const void* x, long n, const float* w, void* y, hipStream_t st) {
+  hipLaunchKernelGGL(p2p::prelu_fwd_kernel, dim3(p2p::mgrid(n)), dim3(256), 0, st,
+                     static_cast<const p2p::bf16*>(x), n, w, static_cast<p2p::bf16*>(y));
+  return (int)hipGetLastError();
+}
+
+// ws >= p2p_misc_nblocks(n) floats; gw: [1] fp32 (accumulated when accumulate != 0)
+int p2p_prelu_bwd(const void* x, const void* dy, long n, const float* w, void* dx, float* ws, float* gw,
+                  int accumulate, hipStream_t st) {
+  const unsigned nb = p2p::mgrid(n);
+  hipLaunchKernelGGL(p2p::prelu_bwd_kernel, dim3(nb), dim3(256), 0, st, static_cast<const p2p::bf16*>(x),
+                     static_cast<const p2p::bf16*>(dy), n, w, static_cast<p2p::bf16*>(dx), ws);
+  hipLaunchKernelGGL(p2p::sum_final_kernel, dim3(1), dim3(256), 0, st, ws, (int)nb, 1.f, accumulate, gw);
+  return (int)hipGetLastError();
+}
+
+int p2p_tv_fwd(const void* x, int N, int H, int W, int C, float* ws, float* out, hipStream_t st) {
+  const long n = (long)N * H * W * C;
+  const unsigned nb = p2p::mgrid(n);
+  const float ih = W > 1 ? 1.f / ((float)N * C * H * (W - 1)) : 0.f;
+  const float iv = H > 1 ? 1.f / ((float)N * C * (H - 1) * W) : 0.f;
+  hipLaunchKernelGGL(p2p::tv_partial_kernel, dim3(nb), dim3(256), 0, st, static_cast<const p2p::bf16*>(x), N, H,
+                     W, C, ih, iv, ws);
+  hipLaunchKernelGGL(p2p::sum_final_kernel, dim3(1), dim3(256), 0, st, ws, (int)nb, 1.f, 0, out);
+  return (int)hipGetLastError();
+}
+
+int p2p_tv_bwd(const void* x, int N, int H, int W, int C, const float* gout, void* dx, hipStream_t st) {
+  const long n = (long)N * H * W * C;
+  const float ih = W > 1 ? 1.f / ((float)N * C * H * (W - 1)) : 0.f;
+  const float iv = H > 1 ? 1.f / ((float)N * C * (H - 1) * W) : 0.f;
+  hipLaunchKernelGGL(p2p::tv_grad_kernel, dim3(p2p::mgrid(n)), dim3(256), 0, st,
+                     static_cast<const p2p::bf16*>(x), N, H, W, C, ih, iv, gout, static_cast<p2p::bf16*>(dx));
+  return (int)hipGetLastError();
+}
+
+int p2p_quantize(const void* x, long n, int bits, void* y, hipStream_t st) {
+  const float m = (float)((1 << bits) - 1);
+  hipLaunchKernelGGL(p2p::quantize_kernel, dim3(p2p::mgrid(n)), dim3(256), 0, st,
+                     static_cast<const p2p::bf16*>(x), n, m, static_cast<p2p::bf16*>(y));
+  return (int)hipGetLastError();
+}
+
+int p2p_avgpool3s2(const void* x, int N, int H, int W, int C, int OH, int OW, void* y, int bwd, hipStream_t st) {
+  if (!bwd) {
+    const long n = (long)N * OH * OW * C;
+    hipLaunchKernelGGL(p2p::avgpool_fwd_kernel, dim3(p2p::mgrid(n)), dim3(256), 0, st,
+                       static_cast<const p2p::bf16*>(x), N, H, W, C, OH, OW, static_cast<p2p::bf16*>(y));
+  } else {  // x = gy (OH x OW), y = gx (H x W)
+    const long n = (long)N * H * W * C;
+    hipLaunchKernelGGL(p2p::avgpool_bwd_kernel, dim3(p2p::mgrid(n)), dim3(256), 0, st,
+                       static_cast<const p2p::bf16*>(x), N, H, W, C, OH, OW, static_cast<p2p::bf16*>(y));
+  }
+  return (int)hipGetLastError();
+}
+
+int p2p_maxpool2(const void* x, const void* gy, int N, int H, int W, int C, void* out, hipStream_t st) {
+  if (!gy) {
+    const long n = (long)N * (H / 2) * (W / 2) * C;
+    hipLaunchKernelGGL(p2p::maxpool_fwd_kernel, dim3(p2p::mgrid(n)), dim3(256), 0, st,
+                       static_cast<const p2p::bf16*>(x), N, H, W, C, static_cast<p2p::bf16*>(out));
+  } else {
+    const long n = (long)N * H * W * C;
+    hipLaunchKernelGGL(p2p::maxpool_bwd_kernel, dim3(p2p::mgrid(n)), dim3(256), 0, st,
+                       static_cast<const p2p::bf16*>(x), static_cast<const p2p::bf16*>(gy), N, H, W, C,
+                       static_cast<p2p::bf16*>(out));
+  }
+  return (int)hipGetLastError();
+}
+
+int p2p_l2norm(const void* x, const void* gy, long P, int C, float eps, void* out, hipStream_t st) {
+  if (!gy)
+    hipLaunchKernelGGL(p2p::l2norm_fwd_kernel, dim3(p2p::mgrid(P)), dim3(256), 0, st,
+                       static_cast<const p2p::bf16*>(x), P, C, eps, static_cast<p2p::bf16*>(out));
+  else
+    hipLaunchKernelGGL(p2p::l2norm_bwd_kernel, dim3(p2p::mgrid(P)), dim3(256), 0, st,
+                       static_cast<const p2p::bf16*>(x), static_cast<const p2p::bf16*>(gy), P, C, eps,
+                       static_cast<p2p::bf16*>(out));
+  return (int)hipGetLastError();
+}
+
+int p2p_pixel_shuffle(const void* in, int N, int OH, int OW, int OC, int r, int dir, void* out,
+                      hipStream_t st) {
+  const long n = (long)N * OH * OW * OC;
+  hipLaunchKernelGGL(p2p::pixel_shuffle_kernel, dim3(p2p::mgrid(n)), dim3(256), 0, st,
+                     static_cast<const p2p::bf16*>(in), N, OH, OW, OC, r, dir, static_cast<p2p::bf16*>(out));
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

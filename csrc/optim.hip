@@ -21,9 +21,13 @@ struct AdamList {
   int count;
 };
 
+// skip_p (optional): a device flag set by the NaN/Inf guard -- when non-zero the whole
+// update (parameters AND moments) is skipped, with no host round trip.
 __global__ void __launch_bounds__(256) adam_kernel(AdamList L, const float* __restrict__ lr_p,
-                                                   const float* __restrict__ step_p, float b1, float b2,
+                                                   const float* __restrict__ step_p,
+                                                   const float* __restrict__ skip_p, float b1, float b2,
                                                    float eps, float wd) {
+  if (skip_p && skip_p[0] != 0.f) return;
   const int blk = blockIdx.x;
   int t = 0;
   while (t + 1 < L.count && L.chunk_start[t + 1] <= blk) ++t;
@@ -79,8 +83,8 @@ extern "C" {
 int p2p_adam_max_tensors() { return p2p::MT_MAX; }
 
 int p2p_adam(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
-             const long* n, const float* lr, const float* step, float b1, float b2, float eps,
-             float wd, hipStream_t st) {
+             const long* n, const float* lr, const float* step, const float* skip, float b1, float b2,
+             float eps, float wd, hipStream_t st) {
   using namespace p2p;
   if (count <= 0) return 0;
   if (count > MT_MAX) return -1;
@@ -97,7 +101,7 @@ int p2p_adam(int count, float* const* p, const float* const* g, float* const* m,
     chunks += (int)((n[i] + MT_CHUNK - 1) / MT_CHUNK);
   }
   L.chunk_start[count] = chunks;
-  hipLaunchKernelGGL(adam_kernel, dim3(chunks), dim3(256), 0, st, L, lr, step, b1, b2, eps, wd);
+  hipLaunchKernelGGL(adam_kernel, dim3(chunks), dim3(256), 0, st, L, lr, step, skip, b1, b2, eps, wd);
   return (int)hipGetLastError();
 }
 

@@ -27,7 +27,8 @@ import torch
 from .. import _native, ops
 from ..models.losses import GANLoss, calc_tv_Loss
 from ..models.vgg import VGGLoss
-from .optim import make_adam
+from ..utils.tracing import trace_range
+from .optim import guarded_step, make_adam
 
 
 class _STEQuantize(torch.autograd.Function):
@@ -50,7 +51,7 @@ class CompressGANStep:
     def __init__(self, net_g, net_d, net_c, lr=2e-4, beta1=0.5, bits=3, lambda_feat=10.0,
                  lambda_vgg=10.0, lambda_tv=1.0, n_layers_d=3, num_d=3, image_pool=None,
                  train_c=False, c_phase_backward=False, vgg=None, reducer_g=None,
-                 reducer_d=None):
+                 reducer_d=None, nan_guard=True):
         self.net_g, self.net_d, self.net_c = net_g, net_d, net_c
         self.criterionGAN = GANLoss()                      # LSGAN, reference default
         self.criterionVGG = vgg if vgg is not None else VGGLoss()
@@ -67,6 +68,14 @@ class CompressGANStep:
         self.c_phase_backward = c_phase_backward
         self.image_pool = image_pool
         self.reducer_g, self.reducer_d = reducer_g, reducer_d
+        self.nan_guard = nan_guard
+        self.skipped = None
+
+    def _opt_step(self, opt, reducer, *losses):
+        if not self.nan_guard:
+            opt.step()
+        else:
+            self.skipped = guarded_step(opt, reducer, self.skipped, *losses)
 
     def _d_in(self, a, b):
         if a.is_cuda and _native.get_backend() == "native":
@@ -111,16 +120,18 @@ class CompressGANStep:
         tv = calc_tv_Loss(fake_b)
         loss_g = loss_g_gan + loss_feat + content + tv * self.lambda_tv
         # ---- updates: G first (its backward also reaches D; those grads are dropped)
-        self._zero(self.opt_g, self.reducer_g)
-        loss_g.backward()
-        if self.reducer_g is not None:
-            self.reducer_g.finish()
-        self.opt_g.step()
-        self._zero(self.opt_d, self.reducer_d)
-        loss_d.backward()
-        if self.reducer_d is not None:
-            self.reducer_d.finish()
-        self.opt_d.step()
+        with trace_range("G_bwd_opt"):
+            self._zero(self.opt_g, self.reducer_g)
+            loss_g.backward()
+            if self.reducer_g is not None:
+                self.reducer_g.finish()
+            self._opt_step(self.opt_g, self.reducer_g, loss_g)
+        with trace_range("D_bwd_opt"):
+            self._zero(self.opt_d, self.reducer_d)
+            loss_d.backward()
+            if self.reducer_d is not None:
+                self.reducer_d.finish()
+            self._opt_step(self.opt_d, self.reducer_d, loss_d)
         # ---- C phase
         need_graph = self.train_c or self.c_phase_backward
         with torch.set_grad_enabled(need_graph):

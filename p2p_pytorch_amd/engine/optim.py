@@ -33,7 +33,9 @@ class FusedAdam(torch.optim.Optimizer):
             t.fill_(float(g["lr"]))
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, skip=None):
+        """``skip``: optional device flag (fp32 scalar tensor, non-zero = skip this update,
+        e.g. from ``utils.guards.nonfinite``); decided on the device, no host sync."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -59,10 +61,14 @@ class FusedAdam(torch.optim.Optimizer):
                 continue
             if not capturing:
                 self._lr_t[gi].fill_(float(group["lr"]))
-            self._step_t[gi].add_(1.0)
+            if skip is None:
+                self._step_t[gi].add_(1.0)
+            else:
+                self._step_t[gi].add_(1.0 - skip.reshape(1))
             b1, b2 = group["betas"]
             hip.adam_(params, grads, m1, m2, self._lr_t[gi], self._step_t[gi], b1, b2,
-                      group["eps"], group["weight_decay"])
+                      group["eps"], group["weight_decay"],
+                      None if skip is None else skip.reshape(1).float().contiguous())
         return loss
 
     def state_dict(self):
@@ -77,6 +83,24 @@ class FusedAdam(torch.optim.Optimizer):
         if steps:
             for t, v in zip(self._step_t, steps):
                 t.fill_(v)
+
+
+def guarded_step(opt, reducer, skipped, *losses):
+    """Optimizer step behind the NaN/Inf guard: a non-finite loss skips the update on the
+    device (FusedAdam: no host sync; agreed across ranks by a 4-byte MAX all-reduce) and is
+    added to the ``skipped`` device counter, which is returned (created on first use)."""
+    from ..utils.guards import nonfinite
+    flag = nonfinite(*losses)
+    if reducer is not None:
+        reducer.all_reduce_max_(flag)
+    if skipped is None:
+        skipped = torch.zeros((), device=flag.device)
+    skipped.add_(flag)
+    if isinstance(opt, FusedAdam):
+        opt.step(skip=flag)
+    elif float(flag) == 0.0:   # stock optimizer: host decision (eager baseline / CPU)
+        opt.step()
+    return skipped
 
 
 def make_adam(params, lr=2e-4, betas=(0.5, 0.999), eps=1e-8):

@@ -24,7 +24,8 @@ from .. import _native
 from ..models.compress_gan import MultiscaleDiscriminator
 from ..models.losses import GANLoss
 from ..ops import l1
-from .optim import make_adam
+from ..utils.tracing import trace_range
+from .optim import guarded_step, make_adam
 
 
 def set_requires_grad(nets, flag: bool):
@@ -35,7 +36,8 @@ def set_requires_grad(nets, flag: bool):
 
 class Pix2PixStep:
     def __init__(self, netG, netD, lr=2e-4, beta1=0.5, gan_mode="vanilla", lambda_L1=100.0,
-                 reducer_g=None, reducer_d=None, autocast_dtype=None, fuse_d_batch=None):
+                 reducer_g=None, reducer_d=None, autocast_dtype=None, fuse_d_batch=None,
+                 nan_guard=True):
         self.netG, self.netD = netG, netD
         self.criterionGAN = GANLoss(gan_mode=gan_mode)
         self.lambda_L1 = float(lambda_L1)
@@ -46,6 +48,16 @@ class Pix2PixStep:
         # D(fake.detach()) and D(real) as ONE 2B-batch forward/backward (D is per-sample:
         # instance norm, no batch statistics), halving D launches and doubling GEMM M.
         self.fuse_d_batch = fuse_d_batch
+        # NaN/Inf guard: a non-finite loss skips that network's update on the device (no
+        # host sync; agreed across ranks with one 4-byte MAX all-reduce) and is counted
+        self.nan_guard = nan_guard
+        self.skipped = None
+
+    def _guarded_step(self, opt, reducer, *losses):
+        if not self.nan_guard:
+            opt.step()
+            return
+        self.skipped = guarded_step(opt, reducer, self.skipped, *losses)
 
     def _ctx(self, device):
         if self.autocast_dtype is not None:
@@ -73,8 +85,9 @@ class Pix2PixStep:
             hip.begin_step()      # weight images re-cast once per step (graph-safe)
             hip.advance_rng()     # new dropout masks
             hip.prepare_weights(netG, netD)   # all bf16 weight images, one launch each
-        with self._ctx(real_A.device):
+        with self._ctx(real_A.device), trace_range("G_fwd"):
             fake_B = netG(real_A)
+        with self._ctx(real_A.device), trace_range("D_fwd"):
             # ---- D
             set_requires_grad(netD, True)
             fuse = self.fuse_d_batch
@@ -93,25 +106,27 @@ class Pix2PixStep:
                 pred_real = netD(self._d_input(real_A, real_B))
                 loss_D_real = self.criterionGAN(pred_real, True)
             loss_D = (loss_D_fake + loss_D_real) * 0.5
-        self._zero(self.opt_D, self.reducer_d)
-        loss_D.backward()
-        if self.reducer_d is not None:
-            self.reducer_d.finish()
-        self.opt_D.step()
+        with trace_range("D_bwd_opt"):
+            self._zero(self.opt_D, self.reducer_d)
+            loss_D.backward()
+            if self.reducer_d is not None:
+                self.reducer_d.finish()
+            self._guarded_step(self.opt_D, self.reducer_d, loss_D)
         if real_A.is_cuda and _native.get_backend() == "native":
             from ..ops import hip
             hip.prepare_weights(netD)         # D moved: fresh images for the G phase
         # ---- G
         set_requires_grad(netD, False)
-        with self._ctx(real_A.device):
+        with self._ctx(real_A.device), trace_range("G_loss_fwd"):
             pred_fake = netD(self._d_input(real_A, fake_B))
             loss_G_GAN = self.criterionGAN(pred_fake, True)
             loss_G_L1 = l1(fake_B, real_B) * self.lambda_L1
             loss_G = loss_G_GAN + loss_G_L1
-        self._zero(self.opt_G, self.reducer_g)
-        loss_G.backward()
-        if self.reducer_g is not None:
-            self.reducer_g.finish()
-        self.opt_G.step()
+        with trace_range("G_bwd_opt"):
+            self._zero(self.opt_G, self.reducer_g)
+            loss_G.backward()
+            if self.reducer_g is not None:
+                self.reducer_g.finish()
+            self._guarded_step(self.opt_G, self.reducer_g, loss_G)
         return {"D": loss_D.detach(), "G_GAN": loss_G_GAN.detach(), "G_L1": loss_G_L1.detach(),
                 "G": loss_G.detach()}

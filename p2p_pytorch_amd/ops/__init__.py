@@ -126,8 +126,18 @@ def l2_normalize_channels(x, eps=1e-12):
 
 
 def pixel_shuffle(x, r):
+    if _native.use_native(x):
+        return _hip().pixel_shuffle(x, r)
     return torch.nn.functional.pixel_shuffle(x, r)
 
 
 def pixel_unshuffle(x, r):
+    if _native.use_native(x):
+        return _hip().pixel_unshuffle(x, r)
     return torch.nn.functional.pixel_unshuffle(x, r)
+
+
+def max_pool2(x):
+    if _native.use_native(x):
+        return _hip().max_pool2(x)
+    return torch.nn.functional.max_pool2d(x, 2, 2)

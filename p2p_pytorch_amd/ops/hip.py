@@ -240,12 +240,20 @@ class ConvFn(torch.autograd.Function):
         KH, KW, s, p = cfg.KH, cfg.KW, cfg.stride, cfg.pad
         gx1 = gx2 = gw = gb = None
         if need_x1 or need_x2:
-            if cfg.reflect or cfg.up != 1:
-                raise NotImplementedError("dgrad of reflect-pad / upsample convs (family R) "
-                                          "is not implemented on the HIP path yet")
             act_in = _act_code(cfg.act_in)
             split = C1 if (q2 is not None) else Cp
-            if cfg.transposed:
+            if cfg.reflect or cfg.up != 1:
+                # family-R ConvLayer / UpsampleConvLayer: dgrad onto the virtual padded,
+                # upsampled input (a plain pad-0 transposed conv), then fold it back
+                if q2 is not None:
+                    raise NotImplementedError("virtual concat with reflect/upsample gather")
+                Hp, Wp = H * cfg.up + 2 * p, W * cfg.up + 2 * p
+                wimg = _weight_image(weight, 1, Cp, Coutp)
+                dxp = P().conv_fwd(gyp, None, wimg, None, 1, KH, KW, s, 0, 0, 1, 0, Hp, Wp, Cp,
+                                   0, Cp, None, None, 0, C1)[0]
+                outs = [P().pad_fold(dxp, H, W, p, cfg.up, int(cfg.reflect),
+                                     q1 if act_in else None, act_in)]
+            elif cfg.transposed:
                 wimg = _weight_image(weight, 0, Cp, Coutp)
                 outs = P().conv_fwd(gyp, None, wimg, None, 0, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
                                     split, q1 if act_in else None,
@@ -403,16 +411,65 @@ def _norm_recompute(x, mean, rstd, gamma, beta, batch):
     return z
 
 
+class _PadCFn(torch.autograd.Function):
+    """Zero-pad the channel dim to a multiple of 8 (norm kernels move 8-channel vectors)."""
+
+    @staticmethod
+    def forward(ctx, x, cp):
+        x = to_nhwc_bf16(x)
+        ctx.c = x.shape[1]
+        return P().pad_channels(x, None, cp)
+
+    @staticmethod
+    def backward(ctx, g):
+        return P().slice_channels(to_nhwc_bf16(g), 0, ctx.c), None
+
+
+class _SliceCFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, c):
+        ctx.cp = x.shape[1]
+        return P().slice_channels(x, 0, c)
+
+    @staticmethod
+    def backward(ctx, g):
+        return P().pad_channels(to_nhwc_bf16(g), None, ctx.cp), None
+
+
+def _norm_any_c(x, gamma, beta, prelu_w, run_mean, run_var, eps, momentum, act, batch, training):
+    C = x.shape[1]
+    if C % 8 == 0:
+        return NormFn.apply(x, gamma, beta, prelu_w, run_mean, run_var, eps, momentum, act, batch,
+                            training)
+    # odd channel counts (family-R tail BN(3)): pad to 8 with identity channels, slice back
+    cp = _pad8(C)
+    pad = cp - C
+    g8 = b8 = rm8 = rv8 = None
+    if gamma is not None:
+        g8 = torch.cat((gamma, gamma.new_ones(pad)))
+        b8 = torch.cat((beta, beta.new_zeros(pad)))
+    if run_mean is not None:
+        rm8 = torch.cat((run_mean, run_mean.new_zeros(pad)))
+        rv8 = torch.cat((run_var, run_var.new_ones(pad)))
+    y8 = NormFn.apply(_PadCFn.apply(x, cp), g8, b8, prelu_w, rm8, rv8, eps, momentum, act, batch,
+                      training)
+    if run_mean is not None and training:
+        with torch.no_grad():
+            run_mean.copy_(rm8[:C])
+            run_var.copy_(rv8[:C])
+    return _SliceCFn.apply(y8, C)
+
+
 def instance_norm(x, eps=1e-5, act=None, weight=None, bias=None):
-    return NormFn.apply(x, weight, bias, None, None, None, eps, 0.0, act, False, True)
+    return _norm_any_c(x, weight, bias, None, None, None, eps, 0.0, act, False, True)
 
 
 def batch_norm(x, running_mean, running_var, weight, bias, training, momentum=0.1, eps=1e-5,
                act=None, prelu_weight=None):
     if not training and running_mean is None:
         training = True
-    return NormFn.apply(x, weight, bias, prelu_weight, running_mean, running_var, eps, momentum,
-                        act, True, training)
+    return _norm_any_c(x, weight, bias, prelu_weight, running_mean, running_var, eps, momentum,
+                       act, True, training)
 
 
 # ============================================================== elementwise
@@ -529,34 +586,130 @@ def mse(a, b):
 
 
 # ============================================================== optimizer
-def adam_(params, grads, exp_avg, exp_avg_sq, lr_t, step_t, b1, b2, eps, wd):
+def adam_(params, grads, exp_avg, exp_avg_sq, lr_t, step_t, b1, b2, eps, wd, skip=None):
     P().adam(params, grads, exp_avg, exp_avg_sq, lr_t, step_t, float(b1), float(b2), float(eps),
-             float(wd))
+             float(wd), skip)
 
 
-# ============================================================== not yet native
-# Family-R helpers outside the family-P hot path.  They run as explicit stock-PyTorch ops
-# on the GPU until their HIP kernels land; listed here so
-# the routing is visible rather than a silent fallback.
+# ============================================================== family-R fringe ops
+# csrc/misc.hip: shared-slope PReLU, TV loss, quantiser, multiscale-D avg-pool, VGG
+# max-pool, channel L2 normalisation, pixel (un)shuffle -- all NHWC bf16.
+def _nhwc(x):
+    return to_nhwc_bf16(x)
+
+
+class PReLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        x = _nhwc(x)
+        wf = w.detach().float().reshape(1).contiguous()
+        ctx.wshape = w.shape
+        ctx.save_for_backward(x, wf)
+        return P().prelu_fwd(x, wf)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, wf = ctx.saved_tensors
+        outs = P().prelu_bwd(x, _nhwc(gy), wf, bool(ctx.needs_input_grad[0]))
+        gx = outs[1] if ctx.needs_input_grad[0] else None
+        gw = outs[0].reshape(ctx.wshape) if ctx.needs_input_grad[1] else None
+        return gx, gw
+
+
 def prelu(x, weight):
-    return torch.nn.functional.prelu(x, weight.to(x.dtype))
+    if weight.numel() != 1:
+        # per-channel PReLU is not used by either model family; explicit stock-PyTorch op
+        return torch.nn.functional.prelu(x, weight.to(x.dtype))
+    return PReLUFn.apply(x, weight)
+
+
+class TVFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = _nhwc(x)
+        ctx.save_for_backward(x)
+        return P().tv_fwd(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        return P().tv_bwd(x, g)
 
 
 def tv(x):
-    from . import reference
-    return reference.tv(x)
+    return TVFn.apply(x)
 
 
 def quantize(x, bits):
-    from . import reference
-    return reference.quantize(x, bits)
+    """Forward value only: round() has zero gradient (the reference's quantiser)."""
+    return P().quantize(_nhwc(x.detach()), int(bits))
+
+
+class AvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = _nhwc(x)
+        ctx.hw = (x.shape[2], x.shape[3])
+        return P().avgpool3s2(x, 0, 0, 0)
+
+    @staticmethod
+    def backward(ctx, gy):
+        return P().avgpool3s2(_nhwc(gy), 1, ctx.hw[0], ctx.hw[1])
 
 
 def avg_pool3_s2(x):
-    from . import reference
-    return reference.avg_pool3_s2(x).contiguous(memory_format=CL)
+    return AvgPoolFn.apply(x)
+
+
+class MaxPool2Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = _nhwc(x)
+        ctx.save_for_backward(x)
+        return P().maxpool2(x, None)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        return P().maxpool2(x, _nhwc(gy))
+
+
+def max_pool2(x):
+    return MaxPool2Fn.apply(x)
+
+
+class L2NormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, eps):
+        x = _nhwc(x)
+        ctx.eps = eps
+        ctx.save_for_backward(x)
+        return P().l2norm(x, None, eps)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        return P().l2norm(x, _nhwc(gy), ctx.eps), None
 
 
 def l2_normalize_channels(x, eps=1e-12):
-    from . import reference
-    return reference.l2_normalize_channels(x, eps)
+    return L2NormFn.apply(x, float(eps))
+
+
+class PixelShuffleFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, r, direction):
+        ctx.r, ctx.dir = r, direction
+        return P().pixel_shuffle(_nhwc(x), r, direction)
+
+    @staticmethod
+    def backward(ctx, gy):
+        return P().pixel_shuffle(_nhwc(gy), ctx.r, 1 - ctx.dir), None, None
+
+
+def pixel_shuffle(x, r):
+    return PixelShuffleFn.apply(x, int(r), 1)
+
+
+def pixel_unshuffle(x, r):
+    return PixelShuffleFn.apply(x, int(r), 0)

@@ -119,6 +119,13 @@ class GradReducer:
             b.work = None
             b.pending = len(b.params)
 
+    def all_reduce_max_(self, t: torch.Tensor):
+        """In-place MAX over ranks of a small device tensor (e.g. the NaN-guard flag), so
+        every rank takes the same skip decision."""
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.pg)
+        return t
+
     def zero_grad(self):
         for b in self.buckets:
             b.flat.zero_()

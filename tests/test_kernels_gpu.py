@@ -130,15 +130,37 @@ def test_conv_transpose2d_fwd_bwd(case):
         assert rel_err(hb.grad, rb.grad) < 3e-2, name
 
 
-@pytest.mark.parametrize("pad_mode,up", [("reflect", 1), ("zeros", 2), ("reflect", 2)])
-def test_conv_reflect_upsample_fwd(pad_mode, up):
-    x = rand_img(2, 32, 12, 12, seed=7)
-    w = torch.randn(64, 32, 3, 3, device=DEV) * 0.05
-    b = torch.randn(64, device=DEV) * 0.1
-    y = ops.conv2d(x, w, b, 1, 1, pad_mode=pad_mode, upsample=up)
-    ry = ref.conv2d(x.float(), w.to(torch.bfloat16).float(), b, 1, 1, pad_mode=pad_mode,
-                    upsample=up)
-    assert rel_err(y, ry) < 2e-2
+REFLECT_CASES = [
+    # (name, N, Cin, H, Cout, k, s, pad_mode, up, act_in)  -- family-R ConvLayer shapes
+    ("res3x3", 2, 64, 16, 64, 3, 1, "reflect", 1, None),
+    ("head9x9_c12", 2, 12, 24, 32, 9, 1, "reflect", 1, None),
+    ("down3x3_s2", 2, 32, 20, 64, 3, 2, "reflect", 1, "relu"),
+    ("c5x5_c3", 2, 3, 16, 64, 5, 1, "reflect", 1, None),
+    ("up2_3x3", 2, 64, 8, 32, 3, 1, "reflect", 2, None),
+    ("up2_zeros", 2, 32, 12, 64, 3, 1, "zeros", 2, None),
+    ("tail9x9_c3", 2, 32, 16, 3, 9, 1, "reflect", 1, None),
+]
+
+
+@pytest.mark.parametrize("case", REFLECT_CASES, ids=[c[0] for c in REFLECT_CASES])
+def test_conv_reflect_upsample_fwd_bwd(case):
+    name, N, Cin, H, Cout, k, s, pad_mode, up, act_in = case
+    x = rand_img(N, Cin, H, H, seed=7)
+    w = torch.randn(Cout, Cin, k, k, device=DEV) * (1.0 / (Cin * k * k) ** 0.5)
+    b = torch.randn(Cout, device=DEV) * 0.1
+    hx, hw, hb = _leaf(x), _leaf(w), _leaf(b)
+    y = ops.conv2d(hx, hw, hb, s, k // 2, pad_mode=pad_mode, upsample=up, act_in=act_in)
+    gy = rand_img(*y.shape, seed=8)
+    y.backward(gy)
+    rx, rw, rb = _leaf(x.float()), _leaf(w), _leaf(b)
+    ry = ref.conv2d(rx, rw.to(torch.bfloat16).float(), rb, s, k // 2, pad_mode=pad_mode,
+                    upsample=up, act_in=act_in)
+    ry.backward(gy.float())
+    assert y.shape == ry.shape
+    assert rel_err(y, ry) < 2e-2, name
+    assert rel_err(hx.grad, rx.grad) < 3e-2, name
+    assert rel_err(hw.grad, rw.grad) < 3e-2, name
+    assert rel_err(hb.grad, rb.grad) < 3e-2, name
 
 
 def test_conv_wgrad_large_m():
@@ -372,5 +394,125 @@ def test_unet_patchgan_step_matches_oracle():
         assert torch.isfinite(gh[n]).all(), n
         eh, ee = rel_err(gh[n], g32[n]), rel_err(g16[n], g32[n])
         if eh > 1.5 * ee + 0.03:
+            worse.append((n, eh, ee))
+    assert not worse, worse
+
+
+# ---------------------------------------------------------------- family-R fringe ops
+def _grad_pair(fn_h, fn_r, x, gy_seed=21):
+    """HIP op on the GPU vs the same op in fp32 on the CPU (the oracle must not depend on
+    the GPU library path: MIOpen's pooling backward is not the PyTorch definition)."""
+    hx = _leaf(x)
+    rx = _leaf(x.float().cpu())
+    yh = fn_h(hx)
+    yr = fn_r(rx)
+    if yh.dim() == 0:
+        yh.backward(torch.tensor(1.7, device=DEV))
+        yr.backward(torch.tensor(1.7))
+    else:
+        gy = rand_img(*yh.shape, seed=gy_seed)
+        yh.backward(gy)
+        yr.backward(gy.float().cpu())
+    return yh.cpu(), yr, hx.grad.cpu(), rx.grad
+
+
+def test_prelu_shared_slope():
+    x = rand_img(2, 32, 16, 16, seed=11)
+    wh = torch.nn.Parameter(torch.tensor([0.25], device=DEV))
+    wr = torch.nn.Parameter(torch.tensor([0.25]))
+    yh, yr, gh, gr = _grad_pair(lambda t: ops.prelu(t, wh), lambda t: F.prelu(t, wr), x)
+    assert rel_err(yh, yr) < 1e-2 and rel_err(gh, gr) < 1e-2
+    assert abs(wh.grad.item() - wr.grad.item()) <= 2e-2 * abs(wr.grad.item()) + 1e-3
+    assert wh.grad.shape == wh.shape
+
+
+def test_tv_loss():
+    x = rand_img(2, 3, 20, 24, seed=12)
+    yh, yr, gh, gr = _grad_pair(ops.tv, ref.tv, x)
+    assert abs(yh.item() - yr.item()) <= 1e-3 * abs(yr.item())
+    assert rel_err(gh, gr) < 1e-2
+
+
+def test_quantize_3bit():
+    x = rand_img(2, 3, 16, 16, seed=13)
+    y = ops.quantize(x, 3)
+    r = ref.quantize(x.float(), 3)
+    assert rel_err(y, r) < 1e-2
+
+
+@pytest.mark.parametrize("C,H,W", [(3, 32, 32), (6, 33, 20), (8, 7, 9)])
+def test_avg_pool3_s2(C, H, W):
+    x = rand_img(2, C, H, W, seed=14)
+    yh, yr, gh, gr = _grad_pair(ops.avg_pool3_s2, ref.avg_pool3_s2, x)
+    assert yh.shape == yr.shape
+    assert rel_err(yh, yr) < 1e-2 and rel_err(gh, gr) < 1e-2
+
+
+def test_max_pool2_ties_route_to_first():
+    x = bf(torch.relu(torch.randn(2, 64, 16, 16, device=DEV)))  # many exact-zero ties
+    yh, yr, gh, gr = _grad_pair(ops.max_pool2, lambda t: F.max_pool2d(t, 2, 2), x)
+    assert torch.equal(yh.float(), yr)
+    assert rel_err(gh, gr) < 1e-2
+    assert torch.equal(gh != 0, gr != 0)
+
+
+def test_l2_normalize_channels():
+    x = rand_img(2, 12, 16, 16, seed=15)
+    yh, yr, gh, gr = _grad_pair(ops.l2_normalize_channels, ref.l2_normalize_channels, x)
+    assert rel_err(yh, yr) < 1e-2 and rel_err(gh, gr) < 2e-2
+
+
+@pytest.mark.parametrize("r", [2])
+def test_pixel_shuffle_roundtrip(r):
+    x = rand_img(2, 12, 8, 6, seed=16)
+    yh, yr, gh, gr = _grad_pair(lambda t: ops.pixel_shuffle(t, r),
+                                lambda t: F.pixel_shuffle(t, r), x)
+    assert torch.equal(yh.float(), yr) and torch.equal(gh.float(), gr)
+    x = rand_img(2, 3, 8, 6, seed=17)
+    yh, yr, gh, gr = _grad_pair(lambda t: ops.pixel_unshuffle(t, r),
+                                lambda t: F.pixel_unshuffle(t, r), x)
+    assert torch.equal(yh.float(), yr) and torch.equal(gh.float(), gr)
+
+
+def test_family_r_networks_match_oracle():
+    """Compression network C + ExpandNetwork G + multiscale SN PatchGAN forward/backward on
+    the HIP path vs the fp32 oracle (bound relative to eager bf16 autocast, per parameter)."""
+    from p2p_pytorch_amd.models.factory import define_C, define_D, define_G
+    torch.manual_seed(0)
+    C = define_C(gpu_id=DEV, verbose=False)
+    G = define_G(gpu_id=DEV, verbose=False)
+    D = define_D(6, 64, gpu_id=DEV, verbose=False)
+    B = bf(torch.rand(2, 3, 32, 32, device=DEV) * 2 - 1)
+
+    def run(backend, dtype=None):
+        _native.set_backend(backend)
+        for m in (C, G, D):
+            m.zero_grad(set_to_none=True)
+        try:
+            ctx = torch.autocast("cuda", dtype) if dtype else torch.autocast("cuda", enabled=False)
+            b = B if backend == "native" else B.float()
+            with ctx:
+                comp = C(b)
+                fake = G(comp)
+                pred = D(torch.cat((comp, fake.to(comp.dtype)), 1))
+                loss = sum(ops.mse_const(p[-1], 1.0) for p in pred) + 10 * ops.l1(fake, b) + \
+                    ops.tv(fake)
+            loss.backward()
+        finally:
+            _native.set_backend("native")
+        grads = {n: p.grad.detach().float().clone() for n, p in G.named_parameters()
+                 if p.grad is not None}
+        return loss.detach().float(), fake.detach().float(), grads
+
+    l32, f32, g32 = run("torch")
+    l16, f16, g16 = run("torch", torch.bfloat16)
+    lh, fh, gh = run("native")
+    assert torch.isfinite(lh) and abs(lh.item() - l32.item()) < 5e-2 * abs(l32.item())
+    assert rel_err(fh, f32) < 1e-1
+    worse = []
+    for n in g32:
+        assert torch.isfinite(gh[n]).all(), n
+        eh, ee = rel_err(gh[n], g32[n]), rel_err(g16[n], g32[n])
+        if eh > 1.5 * ee + 0.05:
             worse.append((n, eh, ee))
     assert not worse, worse

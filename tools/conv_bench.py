@@ -21,6 +21,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 # (name, kind, Cin1, Cin2, H_in, Cout, k, stride, pad, act_in)
 LAYERS = [
+    ("e1", "conv", 3, 0, 256, 64, 4, 2, 1, None),
     ("e2", "conv", 64, 0, 128, 128, 4, 2, 1, None),
     ("e3", "conv", 128, 0, 64, 256, 4, 2, 1, None),
     ("e4", "conv", 256, 0, 32, 512, 4, 2, 1, None),
@@ -30,6 +31,7 @@ LAYERS = [
     ("d3", "convT", 256, 256, 32, 128, 4, 2, 1, "relu"),
     ("d2", "convT", 128, 128, 64, 64, 4, 2, 1, "relu"),
     ("d1", "convT", 64, 64, 128, 3, 4, 2, 1, "relu"),
+    ("c1", "conv", 3, 3, 256, 64, 4, 2, 1, None),
     ("c2", "conv", 64, 0, 128, 128, 4, 2, 1, None),
     ("c3", "conv", 128, 0, 64, 256, 4, 2, 1, None),
     ("c4", "conv", 256, 0, 32, 512, 4, 1, 1, None),

@@ -19,7 +19,6 @@ really resume (``--epoch_count N`` or ``--resume``).
 from __future__ import annotations
 
 import argparse
-import json
 import os
 import random
 import sys
@@ -85,6 +84,11 @@ def build_parser():
     p.add_argument("--log_every", type=int, default=50)
     p.add_argument("--log_json", default=None, help="append JSONL metrics here (rank 0)")
     p.add_argument("--no_eval", action="store_true")
+    p.add_argument("--no_nan_guard", action="store_true",
+                   help="apply updates even when a loss is NaN/Inf (default: skip on device)")
+    p.add_argument("--watchdog_s", type=float, default=None,
+                   help="abort (exit 124) when no step finishes for this long; default 1800 s "
+                        "for multi-GPU runs, off for one GPU")
     p.add_argument("--max_eval", type=int, default=0, help="limit eval images (0 = all)")
     return p
 
@@ -170,7 +174,8 @@ def main(argv=None):
         trainer = Pix2PixStep(net_g, net_d, lr=opt.lr, beta1=opt.beta1,
                               gan_mode=opt.gan_mode or "vanilla", lambda_L1=opt.lamb,
                               reducer_g=reducer_g, reducer_d=reducer_d,
-                              autocast_dtype=torch.bfloat16 if (use_cuda and p2p.get_backend() == "torch") else None)
+                              autocast_dtype=torch.bfloat16 if (use_cuda and p2p.get_backend() == "torch") else None,
+                              nan_guard=not opt.no_nan_guard)
         opt_g, opt_d = trainer.opt_G, trainer.opt_D
     else:
         from p2p_pytorch_amd.engine.compress_gan import CompressGANStep
@@ -178,7 +183,8 @@ def main(argv=None):
         trainer = CompressGANStep(net_g, net_d, net_c, lr=opt.lr, beta1=opt.beta1, bits=opt.bits,
                                   n_layers_d=opt.n_layers_D, image_pool=ImagePool(0),
                                   train_c=opt.train_c, c_phase_backward=opt.c_phase_backward,
-                                  reducer_g=reducer_g, reducer_d=reducer_d)
+                                  reducer_g=reducer_g, reducer_d=reducer_d,
+                                  nan_guard=not opt.no_nan_guard)
         opt_g, opt_d = trainer.opt_g, trainer.opt_d
     sched_g = get_scheduler(opt_g, opt)
     sched_d = get_scheduler(opt_d, opt)
@@ -202,9 +208,12 @@ def main(argv=None):
         start_epoch, losslogger = load_checkpoint(ck_path, net_g, net_c, net_d, opt_g, opt_d,
                                                   sched_g, sched_d, device=device)
 
+    from p2p_pytorch_amd.utils import JsonlLogger, StepWatchdog
     step_fn = trainer.step
     num_epoch = opt.nepoch + 1
-    logf = open(opt.log_json, "a") if (opt.log_json and rank == 0) else None
+    jlog = JsonlLogger(opt.log_json, rank)
+    wd_s = opt.watchdog_s if opt.watchdog_s is not None else (1800.0 if world > 1 else 0.0)
+    watchdog = StepWatchdog(wd_s).start()
     for epoch in range(start_epoch, num_epoch):
         net_g.train()
         net_d.train()
@@ -228,6 +237,7 @@ def main(argv=None):
                 from p2p_pytorch_amd.engine.graph import CapturedStep
                 step_fn = CapturedStep(trainer.step, real_a, real_b)
             losses = step_fn(real_a, real_b)
+            watchdog.beat()
             for k, v in losses.items():   # device-side running sums, no host sync
                 sums[k] = sums.get(k, 0) + v.detach().float()
             count += 1
@@ -242,10 +252,10 @@ def main(argv=None):
                     print("itr: %d/%d [%3d/%3d] " % (iteration, n_it, epoch, num_epoch - 1) +
                           " ".join(f"[{k}: {means[k]:.6f}]" for k in keys) +
                           f" [{ips:.1f} img/s]", flush=True)
-                    if logf:
-                        logf.write(json.dumps({"epoch": epoch, "iter": iteration, "img_s": ips,
-                                               **means}) + "\n")
-                        logf.flush()
+                    skipped = getattr(trainer, "skipped", None)
+                    jlog.log(epoch=epoch, iter=iteration, img_s=ips,
+                             skipped_updates=float(skipped) if skipped is not None else 0.0,
+                             **means)
         update_learning_rate(sched_g, opt_g, verbose=rank == 0)
         update_learning_rate(sched_d, opt_d, verbose=rank == 0)
         for o in (opt_g, opt_d):
@@ -299,8 +309,8 @@ def main(argv=None):
             pdist.barrier()
             if rank == 0:
                 print("Checkpoint saved to {}".format(path))
-    if logf:
-        logf.close()
+    watchdog.stop()
+    jlog.close()
     pdist.destroy()
 
 
