@@ -21,6 +21,10 @@
 
 extern "C" {
 long p2p_norm_ws_floats(int N, int HW, int C);
+int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, const float* partials,
+                          float eps, const float* gamma, const float* beta, const float* prelu_w,
+                          int act, float* mean, float* rstd, float* run_mean, float* run_var,
+                          float momentum, void* y, hipStream_t st);
 int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* gamma,
                  const float* beta, const float* prelu_w, int act, float* mean, float* rstd,
                  float* run_mean, float* run_var, float momentum, float* ws, void* y,
@@ -105,13 +109,16 @@ const void* zero_page(const Tensor& like) {
 // overlap across blocks when two fit on a CU.
 // 5 = 256x256 2-stage (Cout > 128 only; 8 waves of 128x64 -> a quarter less LDS fragment
 // traffic and half the A re-reads per MFMA of variant 4).
-int conv_variant(int64_t Cout, int64_t kmax) {
+// Auto: 5 when it still yields >= 256 tiles (one per CU; measured: it wins on every such
+// U-Net / PatchGAN layer and loses below, profiles/conv_layers_r1d.jsonl), else 4 / 2.
+int conv_variant(int64_t Cout, int64_t kmax, int64_t tiles256 = 0) {
   const char* v = std::getenv("P2P_CONV_VARIANT");
   if (v && v[0] == 'v') return 1;
-  const int autov = (Cout > 64 && kmax > 256) ? 4 : 2;
+  const int v4 = (Cout > 64 && kmax > 256) ? 4 : 2;
+  const bool big = Cout > 128 && kmax > 256;
   if (v && v[0] == 'g' && v[1] >= '2' && v[1] <= '4') return v[1] - '0';
-  if (v && v[0] == 'g' && v[1] == '5') return (Cout > 128 && kmax > 256) ? 5 : autov;
-  return autov;
+  if (v && v[0] == 'g' && v[1] == '5') return big ? 5 : v4;
+  return (big && tiles256 >= 256) ? 5 : v4;
 }
 
 Tensor empty_nhwc(int64_t N, int64_t C, int64_t H, int64_t W, const Tensor& like) {
@@ -124,7 +131,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                              int64_t stride, int64_t pad, int64_t reflect, int64_t up,
                              int64_t act_in, int64_t OH, int64_t OW, int64_t Cout, int64_t act_out,
                              int64_t Csplit, const optional<Tensor>& xb1,
-                             const optional<Tensor>& xb2, int64_t act_bwd, int64_t Cvalid) {
+                             const optional<Tensor>& xb2, int64_t act_bwd, int64_t Cvalid,
+                             bool want_stats) {
   check_act(x1, "conv_fwd x1");
   const int64_t N = x1.size(0), H = x1.size(2), W = x1.size(3);
   int64_t C2 = 0;
@@ -187,6 +195,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   a.ws = nullptr;
   a.splits = 1;
   a.zero = zero_page(x1);
+  a.stats = nullptr;
+  a.stats_nchunks = 0;
 
   hipStream_t st = cur_stream(x1);
   // ---- tiny-Cout "col" path: dense GEMM over the input pixels (N = taps x Cvalid) + col2im
@@ -252,7 +262,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     mmax = std::max(mmax, N * hq * wq);
     kmax = std::max(kmax, taps * C);
   }
-  const int variant = conv_variant(Cout, kmax);
+  const int variant = conv_variant(Cout, kmax, ((mmax + 255) / 256) * ((Cout + 255) / 256) * classes);
   const bool glds_ok = variant > 1 && Cout > 32 && (act_in == 0 || act_in == 1);
   int bm, bn;
   if (glds_ok) {
@@ -284,8 +294,29 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     a.ws = ws.data_ptr<float>();
     a.splits = splits;
   }
+  // fused norm statistics: only on the glds path with whole tiles inside one image/class
+  Tensor stats;
+  if (want_stats && glds_ok && splits == 1 && Csplit == Cout && act_out == 0 && !act_bwd) {
+    bool ok = true;
+    int64_t hwq = OH * OW;
+    if (mode == 1) {
+      ok = OH % stride == 0 && OW % stride == 0;
+      hwq = (OH / stride) * (OW / stride);
+    }
+    ok = ok && hwq % bm == 0;
+    if (ok) {
+      const int64_t nch = classes * (hwq / bm);
+      stats = at::empty({2, N, nch, Cout}, x1.options().dtype(at::kFloat));
+      a.stats = stats.data_ptr<float>();
+      a.stats_nchunks = (int)nch;
+    }
+  }
   int rc = -2;
   if (glds_ok) rc = p2p_conv_fwd_glds(&a, (int)mode, variant, st);
+  if (rc == -2 && a.stats) {  // glds refused after all: no fused statistics
+    a.stats = nullptr;
+    stats = Tensor();
+  }
   if (rc == -2) {
     // register-staged kernel: its own tile table
     int vbm = bm, vbn = bn;
@@ -299,6 +330,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   if (splits > 1) check_rc(p2p_conv_finalize(&a, st), "conv_finalize");
   std::vector<Tensor> out{y1};
   if (y2.defined()) out.push_back(y2);
+  if (stats.defined()) out.push_back(stats);
   return out;
 }
 
@@ -441,7 +473,8 @@ std::vector<Tensor> weight_prep_multi(at::TensorList ws, at::IntArrayRef swap, a
 std::vector<Tensor> norm_fwd(const Tensor& x, double eps, const optional<Tensor>& gamma,
                              const optional<Tensor>& beta, const optional<Tensor>& prelu_w,
                              int64_t act, const optional<Tensor>& run_mean,
-                             const optional<Tensor>& run_var, double momentum, bool batch) {
+                             const optional<Tensor>& run_var, double momentum, bool batch,
+                             const optional<Tensor>& partials) {
   check_act(x, "norm_fwd x");
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
   TORCH_CHECK(C <= 2048, "norm_fwd: C > 2048 unsupported");
@@ -449,6 +482,24 @@ std::vector<Tensor> norm_fwd(const Tensor& x, double eps, const optional<Tensor>
   const int gHW = batch ? (int)(N * HW) : (int)HW;
   Tensor mean = at::empty({gN, C}, x.options().dtype(at::kFloat));
   Tensor rstd = at::empty({gN, C}, x.options().dtype(at::kFloat));
+  if (partials) {
+    // [2][N][nch][C] from the producing conv's epilogue (BN: all N*nch chunks of one group)
+    TORCH_CHECK(partials->dim() == 4 && partials->size(0) == 2 && partials->size(1) == N &&
+                    partials->size(3) == C && partials->scalar_type() == at::kFloat,
+                "norm_fwd: partials shape");
+    const int nch = (int)(batch ? N * partials->size(2) : partials->size(2));
+    Tensor y = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+    check_rc(p2p_norm_fwd_partials(x.data_ptr(), gN, gHW, (int)C, nch, partials->data_ptr<float>(),
+                                   (float)eps, gamma ? gamma->data_ptr<float>() : nullptr,
+                                   beta ? beta->data_ptr<float>() : nullptr,
+                                   prelu_w ? prelu_w->data_ptr<float>() : nullptr, (int)act,
+                                   mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                                   run_mean ? run_mean->data_ptr<float>() : nullptr,
+                                   run_var ? run_var->data_ptr<float>() : nullptr, (float)momentum,
+                                   y.data_ptr(), cur_stream(x)),
+             "norm_fwd(partials)");
+    return {y, mean, rstd};
+  }
   Tensor ws = at::empty({p2p_norm_ws_floats(gN, gHW, (int)C)}, x.options().dtype(at::kFloat));
   Tensor y = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   check_rc(p2p_norm_fwd(x.data_ptr(), gN, gHW, (int)C, (float)eps,
@@ -799,7 +850,7 @@ void adam(at::TensorList p, at::TensorList g, at::TensorList m, at::TensorList v
 TORCH_LIBRARY(p2p, m) {
   m.def("conv_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, int mode, int KH, int KW, int stride, "
         "int pad, int reflect, int up, int act_in, int OH, int OW, int Cout, int act_out, int Csplit, "
-        "Tensor? xb1, Tensor? xb2, int act_bwd, int Cvalid=0) -> Tensor[]");
+        "Tensor? xb1, Tensor? xb2, int act_bwd, int Cvalid=0, bool want_stats=False) -> Tensor[]");
   m.def("conv_wgrad(Tensor p1, Tensor? p2, int p_act, Tensor q1, Tensor? q2, int q_act, int KH, int KW, "
         "int stride, int pad, int reflect, int up, Tensor(a!) dw, float scale, int accumulate, "
         "int flip=0) -> ()");
@@ -816,7 +867,7 @@ TORCH_LIBRARY(p2p, m) {
   m.def("pad_fold(Tensor dxp, int H, int W, int pad, int up, int reflect, Tensor? xb, int act) -> Tensor");
   m.def("weight_prep_multi(Tensor[] w, int[] swap, int[] xp, int[] yp) -> Tensor[]");
   m.def("norm_fwd(Tensor x, float eps, Tensor? gamma, Tensor? beta, Tensor? prelu_w, int act, "
-        "Tensor(a!)? run_mean, Tensor(b!)? run_var, float momentum, bool batch) -> Tensor[]");
+        "Tensor(a!)? run_mean, Tensor(b!)? run_var, float momentum, bool batch, Tensor? partials=None) -> Tensor[]");
   m.def("norm_apply(Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? prelu_w, "
         "int act, bool batch) -> Tensor");
   m.def("norm_bwd(Tensor x, Tensor dy, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, int act, "

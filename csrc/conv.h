@@ -31,6 +31,12 @@ struct ConvFwdArgs {
   float* ws;       // split-K fp32 accumulator [N*OH*OW][Cout] (pre-zeroed) when splits > 1
   int splits;
   const void* zero;  // >= 16 zero bytes in global memory (global_load_lds padding source)
+  // Normalisation statistics fused into the epilogue (null = off): every BM-row tile (all
+  // rows inside one image and one parity class -- host-checked) writes the per-channel
+  // (mean, M2) of its bf16 outputs to stats[{0,1}][n][chunk][Cout], chunk = class * (Hq*Wq
+  // / BM) + tile-in-class; the norm then only merges them (norm.hip finalize).
+  float* stats;
+  int stats_nchunks;  // chunks per image
 };
 
 // Weight gradient: C[R][Kq] = sum_m P[m][R] * im2col(Q)[m][Kq], written to per-split

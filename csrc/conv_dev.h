@@ -103,6 +103,40 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
   }
   __syncthreads();
 
+  if (a.stats) {
+    // per-column (mean, M2) of the tile's BM bf16 outputs, shifted by the tile's first row
+    // (no E[x^2] - E[x]^2 cancellation); NT / BN threads per column, combined in LDS
+    constexpr int TPC = NT / BN;
+    static_assert(NT % BN == 0 && BM % TPC == 0, "stats partition");
+    float* red = reinterpret_cast<float*>(smem + BM * LDC * 2);
+    const int col = tid % BN, part = tid / BN;
+    const float piv = (float)Cs[col];
+    float s1 = 0.f, s2 = 0.f;
+    for (int r = part * (BM / TPC); r < (part + 1) * (BM / TPC); ++r) {
+      const float d = (float)Cs[r * LDC + col] - piv;
+      s1 += d;
+      s2 += d * d;
+    }
+    red[tid] = s1;
+    red[NT + tid] = s2;
+    __syncthreads();
+    const int co = n0 + col;
+    if (part == 0 && co < a.Cout) {
+      float S1 = 0.f, S2 = 0.f;
+#pragma unroll
+      for (int q = 0; q < TPC; ++q) {
+        S1 += red[q * BN + col];
+        S2 += red[NT + q * BN + col];
+      }
+      const float inv = 1.f / (float)BM;
+      const int img = m0 / HWq;
+      const int chunk = g.ry * s * (HWq / BM) + g.rx * (HWq / BM) + (m0 - img * HWq) / BM;
+      const long o = ((long)img * a.stats_nchunks + chunk) * a.Cout + co;
+      a.stats[o] = piv + S1 * inv;
+      a.stats[(long)a.N * a.stats_nchunks * a.Cout + o] = fmaxf(S2 - S1 * S1 * inv, 0.f);
+    }
+  }
+
   constexpr int CPR = BN / 8;  // 8-channel chunks per row
   for (int c = tid; c < BM * CPR; c += NT) {
     const int row = c / CPR, cc = c - row * CPR;

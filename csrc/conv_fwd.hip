@@ -42,7 +42,7 @@ namespace p2p {
 template <int BM, int BN>
 struct FwdSmem {
   static constexpr int pipe = 2 * (BM + BN) * BK * 2;
-  static constexpr int epi = BM * (BN + 8) * 2;
+  static constexpr int epi = BM * (BN + 8) * 2 + 2 * 256 * 4;  // + stats scratch
   static constexpr int bytes = pipe > epi ? pipe : epi;
 };
 

@@ -290,7 +290,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
 template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU>
 static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int pipe = STAGES * (BM + BN) * BK * 2;
-  constexpr int epi = BM * (BN + 8) * 2;
+  constexpr int epi = BM * (BN + 8) * 2 + 2 * (WM * WN * 64) * 4;  // + stats scratch
   constexpr int smem = pipe > epi ? pipe : epi;
   static bool attr_set = false;
   if (!attr_set) {

@@ -254,6 +254,45 @@ __device__ __forceinline__ bf16x8 tr_frag_w(const bf16* tile, int kbase, int cba
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// The same transposing read as inline asm, for the LDS-DMA kernel: hipcc treats the
+// ds_read_tr16 intrinsic as possibly aliasing the in-flight global_load_lds writes and
+// puts an s_waitcnt vmcnt(0) in front of it -- draining the whole prefetch ring every
+// stage.  The asm form is invisible to that analysis; the RAW order on the staged tile
+// is given explicitly (counted vmcnt + barrier), the fragment readiness by lgkm_wait8.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)p));
+}
+
+template <int PW>
+__device__ __forceinline__ bf16x8 tr_frag_w_asm(const bf16* tile, int kbase, int cbase, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int chunk = (cbase >> 3) + (p >> 1);
+  const uint32_t a0 = lds_addr(tile + wg_off<PW>(kbase + 8 * g + q, chunk) + (p & 1) * 4);
+  const uint32_t a1 = lds_addr(tile + wg_off<PW>(kbase + 8 * g + 4 + q, chunk) + (p & 1) * 4);
+  uint64_t lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a1));
+  u32x4 v = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// s_waitcnt lgkmcnt(N) that the compiler must order before any use of the fragments
+template <int N>
+__device__ __forceinline__ void lgkm_wait(bf16x8& f0, bf16x8& f1) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(f0), "+v"(f1) : "n"(N));
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait(bf16x8& f0, bf16x8& f1, bf16x8& f2, bf16x8& f3) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3) : "n"(N));
+}
+template <int N, int CNT>
+__device__ __forceinline__ void lgkm_wait_arr(bf16x8 (&f)[CNT]) {
+  static_assert(CNT == 2 || CNT == 4, "fragment count");
+  if constexpr (CNT == 2) lgkm_wait<N>(f[0], f[1]);
+  else lgkm_wait<N>(f[0], f[1], f[2], f[3]);
+}
+
 // ---------------------------------------------------------------------------------------
 // LDS-DMA (global_load_lds) pipelined variant for the big layers: 8 waves, a 256x128 or
 // 128x256 (R x Kq) output tile, a STAGES-deep ring of 64-row reduction stages.  Both
@@ -348,6 +387,23 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
   const int OHW = a.OH * a.OW;
   const FastDiv fd_ohw = make_fastdiv((uint32_t)OHW), fd_ow = make_fastdiv((uint32_t)a.OW);
 
+  // Q rows walk the output pixels in steps of WBM per stage: keep each load's (n, oh, ow)
+  // and advance it by the constant (dn, dh, dw) decomposition of WBM with two carries
+  // instead of two magic-number divisions per load per stage (the loader, not the MFMA,
+  // bounded this kernel: ~150 VALU per 32 MFMA).  Stages are issued in order from s0.
+  int q_n[QL], q_oh[QL], q_ow[QL];
+#pragma unroll
+  for (int i = 0; i < QL; ++i) {
+    const int m = s0 * WBM + (q_row[i] >= 0 ? q_row[i] : 0);
+    q_n[i] = (int)fdiv((uint32_t)m, fd_ohw);
+    const int rem = m - q_n[i] * OHW;
+    q_oh[i] = (int)fdiv((uint32_t)rem, fd_ow);
+    q_ow[i] = rem - q_oh[i] * a.OW;
+  }
+  const int d_n = WBM / OHW, d_rem = WBM % OHW;
+  const int d_h = d_rem / a.OW, d_w = d_rem % a.OW;
+  const long p_step = (long)WBM;
+
   auto issue = [&](int st, int stage) {
     bf16* Pst = Ps + stage * PSUB * PSUBE;
     bf16* Qst = Qs + stage * QSUB * SUBE;
@@ -359,23 +415,34 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
       __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)(Pst + p_lds[i]),
                                        16, 0, 0);
     }
+    (void)p_step;
 #pragma unroll
     for (int i = 0; i < QL; ++i) {
+      if (st != s0) {
+        int ow = q_ow[i] + d_w, oh = q_oh[i] + d_h, n = q_n[i] + d_n;
+        if (ow >= a.OW) {
+          ow -= a.OW;
+          ++oh;
+        }
+        if (oh >= a.OH) {
+          oh -= a.OH;
+          ++n;
+        }
+        q_ow[i] = ow;
+        q_oh[i] = oh;
+        q_n[i] = n;
+      }
       const int m = st * WBM + (q_row[i] >= 0 ? q_row[i] : 0);
-      const int n = (int)fdiv((uint32_t)m, fd_ohw);
-      const int rem = m - n * OHW;
-      const int oh = (int)fdiv((uint32_t)rem, fd_ow);
-      const int ow = rem - oh * a.OW;
-      int uy = oh * a.stride - a.pad + q_kh[i];
-      int ux = ow * a.stride - a.pad + q_kw[i];
+      int uy = q_oh[i] * a.stride - a.pad + q_kh[i];
+      int ux = q_ow[i] * a.stride - a.pad + q_kw[i];
       if (a.reflect) {
         uy = reflect_idx(uy, Hu);
         ux = reflect_idx(ux, Wu);
       }
       const bool ok = q_row[i] >= 0 && m < a.M && (unsigned)uy < (unsigned)Hu &&
                       (unsigned)ux < (unsigned)Wu;
-      const long pix = ((long)n * a.H + (uy >> ush)) * a.W + (ux >> ush);
-      const bf16* gp = ok ? q_base[i] + pix * q_ld[i] : zero;
+      const int pix = (q_n[i] * a.H + (uy >> ush)) * a.W + (ux >> ush);
+      const bf16* gp = ok ? q_base[i] + (long)pix * q_ld[i] : zero;
       __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)(Qst + q_lds[i]),
                                        16, 0, 0);
     }
@@ -405,21 +472,32 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
     const bf16* P = Ps + stage * PSUB * PSUBE;
     const bf16* Q = Qs + stage * QSUB * SUBE;
     bf16x8 af[2][TM], bfr[2][TN];
+    constexpr int RD_HALF = 2 * (TM + TN);   // ds_read_b64_tr per 32-deep half
+    constexpr int WAIT0 = RD_HALF < 15 ? RD_HALF : 15;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int cb = wm * (TBR / WM) + i * 16;
-        af[kk][i] = tr_frag_w<PW>(P + (cb / PW) * PSUBE, kk * 32, cb % PW, lane);
+        af[kk][i] = tr_frag_w_asm<PW>(P + (cb / PW) * PSUBE, kk * 32, cb % PW, lane);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int cb = wn * (TBQ / WN) + j * 16;
-        bfr[kk][j] = tr_frag_w<128>(Q + (cb >> 7) * SUBE, kk * 32, cb & 127, lane);
+        bfr[kk][j] = tr_frag_w_asm<128>(Q + (cb >> 7) * SUBE, kk * 32, cb & 127, lane);
       }
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
+      // reads return in order: lgkmcnt(min(RD_HALF, 15)) retires the first half (the
+      // counter holds at most 15, so the reads past that issued only as earlier ones returned)
+      if (kk == 0) {
+        lgkm_wait_arr<WAIT0>(af[0]);
+        lgkm_wait_arr<WAIT0>(bfr[0]);
+      } else {
+        lgkm_wait_arr<0>(af[1]);
+        lgkm_wait_arr<0>(bfr[1]);
+      }
       if constexpr (RM & 1) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)

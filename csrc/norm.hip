@@ -459,6 +459,29 @@ int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* ga
   return (int)hipGetLastError();
 }
 
+// forward from per-chunk (mean, M2) partials produced by the conv epilogue (conv_dev.h):
+// partials [2][N][nchunks][C], every chunk HW / nchunks pixels -- the read-only stats pass
+// over x is gone; finalize merges, apply normalises.
+int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, const float* partials,
+                          float eps, const float* gamma, const float* beta, const float* prelu_w,
+                          int act, float* mean, float* rstd, float* run_mean, float* run_var,
+                          float momentum, void* y, hipStream_t st) {
+  using namespace p2p;
+  if (nchunks <= 0 || HW % nchunks) return -1;
+  NormGeom pg;
+  pg.N = N;
+  pg.HW = HW;
+  pg.C = C;
+  pg.chunk = HW / nchunks;
+  pg.nchunks = nchunks;
+  hipLaunchKernelGGL(norm_finalize_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, partials, pg, eps,
+                     mean, rstd, run_mean, run_var, momentum);
+  NormGeom g = make_geom(N, HW, C);
+  hipLaunchKernelGGL(norm_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st, static_cast<const bf16*>(x), g,
+                     mean, rstd, gamma, beta, prelu_w, act, static_cast<bf16*>(y));
+  return (int)hipGetLastError();
+}
+
 // apply only (eval-mode BN with running stats: host passes mean/rstd computed from them)
 int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const float* rstd,
                    const float* gamma, const float* beta, const float* prelu_w, int act, void* y,

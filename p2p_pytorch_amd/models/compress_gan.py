@@ -193,11 +193,13 @@ class SpectralNorm(nn.Module):
         # without bumping the version counter, so a backward through an EARLIER forward of
         # this step sees the newest u / v (what the reference computes) instead of
         # raising an in-place-modification error.
-        for _ in range(self.power_iterations):
-            v.data = l2normalize(torch.mv(w2.detach().t(), u.data))
-            u.data = l2normalize(torch.mv(w2.detach(), v.data))
-        sigma = torch.dot(u, torch.mv(w2, v))
-        return w / sigma
+        # fp32 always (also under an autocast region: sigma is a norm, and u / v are state)
+        with torch.autocast(device_type=w.device.type, enabled=False):
+            for _ in range(self.power_iterations):
+                v.data = l2normalize(torch.mv(w2.detach().t(), u.data))
+                u.data = l2normalize(torch.mv(w2.detach(), v.data))
+            sigma = torch.dot(u, torch.mv(w2, v))
+            return w / sigma
 
     def forward(self, x):
         m = self.module

@@ -23,10 +23,12 @@ class Conv2d(nn.Conv2d):
         self.upsample = upsample
         self.act_in = act_in
         self.act_out = act_out
+        self.norm_stats = False   # set by link_norm(): a norm consumes the output
 
     def forward(self, x):  # noqa: D401
         return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.pad_mode,
-                          self.upsample, self.act_in, self.act_out)
+                          self.upsample, self.act_in, self.act_out,
+                          stats=self.norm_stats and self.training)
 
 
 class ConvTranspose2d(nn.ConvTranspose2d):
@@ -39,10 +41,19 @@ class ConvTranspose2d(nn.ConvTranspose2d):
                          bias=bias)
         self.act_in = act_in
         self.act_out = act_out
+        self.norm_stats = False
 
     def forward(self, x):
         return ops.conv_transpose2d(x, self.weight, self.bias, self.stride[0], self.padding[0],
-                                    self.act_in, self.act_out)
+                                    self.act_in, self.act_out,
+                                    stats=self.norm_stats and self.training)
+
+
+def link_norm(conv, norm):
+    """Mark ``conv`` as feeding ``norm`` directly: on the HIP path the conv epilogue then
+    emits the per-tile (mean, M2) partials and the norm skips its own statistics pass."""
+    if isinstance(norm, (InstanceNorm2d, BatchNorm2d)) and hasattr(conv, "norm_stats"):
+        conv.norm_stats = True
 
 
 class InstanceNorm2d(nn.Module):

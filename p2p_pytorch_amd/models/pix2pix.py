@@ -28,7 +28,7 @@ from __future__ import annotations
 
 import torch.nn as nn
 
-from .layers import Conv2d, ConvTranspose2d, Dropout, norm_layer
+from .layers import Conv2d, ConvTranspose2d, Dropout, link_norm, norm_layer
 
 
 class UnetGenerator(nn.Module):
@@ -65,6 +65,8 @@ class UnetGenerator(nn.Module):
             self.up_norms.append(norm_layer(norm, cout, act="relu") if i > 0 else nn.Identity())
         self.dropouts = nn.ModuleList(
             [Dropout(0.5) if i in self.drop_levels else nn.Identity() for i in range(n)])
+        for c, m in list(zip(self.downs, self.down_norms)) + list(zip(self.ups, self.up_norms)):
+            link_norm(c, m)
 
     def forward(self, x):
         n = self.num_downs
@@ -103,6 +105,8 @@ class NLayerDiscriminator(nn.Module):
         norms.append(nn.Identity())
         self.convs = nn.ModuleList(layers)
         self.norms = nn.ModuleList(norms)
+        for c, m in zip(self.convs, self.norms):
+            link_norm(c, m)
 
     def forward(self, x):
         for conv, norm in zip(self.convs, self.norms):

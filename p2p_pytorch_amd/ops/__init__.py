@@ -25,15 +25,18 @@ def _hip():
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, pad_mode="zeros", upsample=1,
-           act_in=None, act_out=None):
+           act_in=None, act_out=None, stats=False):
+    """``stats=True``: the output feeds a norm -- the HIP conv emits its statistics."""
     if _native.use_native(_first(x)):
-        return _hip().conv2d(x, weight, bias, stride, padding, pad_mode, upsample, act_in, act_out)
+        return _hip().conv2d(x, weight, bias, stride, padding, pad_mode, upsample, act_in, act_out,
+                             stats)
     return ref.conv2d(x, weight, bias, stride, padding, pad_mode, upsample, act_in, act_out)
 
 
-def conv_transpose2d(x, weight, bias=None, stride=2, padding=1, act_in=None, act_out=None):
+def conv_transpose2d(x, weight, bias=None, stride=2, padding=1, act_in=None, act_out=None,
+                     stats=False):
     if _native.use_native(_first(x)):
-        return _hip().conv_transpose2d(x, weight, bias, stride, padding, act_in, act_out)
+        return _hip().conv_transpose2d(x, weight, bias, stride, padding, act_in, act_out, stats)
     return ref.conv_transpose2d(x, weight, bias, stride, padding, act_in, act_out)
 
 

@@ -46,6 +46,7 @@ def begin_step():
     """Start a new step generation: weight images are re-cast on first use (graph-safe)."""
     _gen[0] += 1
     _colsum_stash.clear()
+    _stats_stash.clear()
 
 
 # Bias gradients handed from the norm backward to the producing conv: for a conv feeding a
@@ -58,6 +59,21 @@ _colsum_stash: dict = {}
 
 def _stash_colsum(dx, colsum):
     _colsum_stash[(dx.data_ptr(), tuple(dx.shape))] = (dx, colsum)
+
+
+_stats_stash: dict = {}
+
+
+def _stash_stats(y, st):
+    # the entry keeps y alive, so its address cannot be reused while the entry exists
+    if len(_stats_stash) >= 256:
+        _stats_stash.pop(next(iter(_stats_stash)))
+    _stats_stash[(y.data_ptr(), tuple(y.shape))] = (y, st)
+
+
+def _take_stats(x):
+    ent = _stats_stash.pop((x.data_ptr(), tuple(x.shape)), None)
+    return None if ent is None else ent[1]
 
 
 def _take_colsum(gy):
@@ -167,9 +183,11 @@ def advance_rng(device=None):
 
 # ============================================================== convolution
 class _ConvCfg:
-    __slots__ = ("transposed", "KH", "KW", "stride", "pad", "reflect", "up", "act_in", "act_out")
+    __slots__ = ("transposed", "KH", "KW", "stride", "pad", "reflect", "up", "act_in", "act_out",
+                 "stats")
 
-    def __init__(self, transposed, KH, KW, stride, pad, reflect, up, act_in, act_out):
+    def __init__(self, transposed, KH, KW, stride, pad, reflect, up, act_in, act_out, stats=False):
+        self.stats = stats
         self.transposed = transposed
         self.KH, self.KW = KH, KW
         self.stride, self.pad = stride, pad
@@ -211,9 +229,13 @@ class ConvFn(torch.autograd.Function):
             mode, swap = 0, 0
         Coutp = _pad8(Cout)
         wimg = _weight_image(weight, swap, Coutp, Cp)
-        y = P().conv_fwd(q1, q2, wimg, _bias_padded(bias, Coutp), mode, KH, KW, s, p,
-                         int(cfg.reflect), cfg.up, _act_code(cfg.act_in), OH, OW, Coutp,
-                         _act_code(cfg.act_out), Coutp, None, None, 0, Cout)[0]
+        want = bool(cfg.stats) and Coutp == Cout
+        outs = P().conv_fwd(q1, q2, wimg, _bias_padded(bias, Coutp), mode, KH, KW, s, p,
+                            int(cfg.reflect), cfg.up, _act_code(cfg.act_in), OH, OW, Coutp,
+                            _act_code(cfg.act_out), Coutp, None, None, 0, Cout, want)
+        y = outs[0]
+        if want and len(outs) == 2:
+            _stash_stats(y, outs[1])
         if Coutp != Cout:
             y = P().slice_channels(y, 0, Cout)
         ctx.cfg = cfg
@@ -311,21 +333,22 @@ def _pair(v):
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, pad_mode="zeros", upsample=1,
-           act_in=None, act_out=None):
+           act_in=None, act_out=None, stats=False):
     s, s2 = _pair(stride)
     p, p2 = _pair(padding)
     if s != s2 or p != p2:
         raise NotImplementedError("anisotropic stride/padding")
     x1, x2 = _split_input(x)
     cfg = _ConvCfg(False, weight.shape[2], weight.shape[3], s, p, pad_mode == "reflect" and p > 0,
-                   int(upsample or 1), act_in, act_out)
+                   int(upsample or 1), act_in, act_out, stats)
     return ConvFn.apply(x1, x2, weight, bias, cfg)
 
 
-def conv_transpose2d(x, weight, bias=None, stride=2, padding=1, act_in=None, act_out=None):
+def conv_transpose2d(x, weight, bias=None, stride=2, padding=1, act_in=None, act_out=None,
+                     stats=False):
     x1, x2 = _split_input(x)
     cfg = _ConvCfg(True, weight.shape[2], weight.shape[3], int(stride), int(padding), False, 1,
-                   act_in, act_out)
+                   act_in, act_out, stats)
     return ConvFn.apply(x1, x2, weight, bias, cfg)
 
 
@@ -341,7 +364,7 @@ class NormFn(torch.autograd.Function):
         if training:
             y, mean, rstd = P().norm_fwd(x, eps, g, b, pw, _act_code(act),
                                          run_mean if batch else None, run_var if batch else None,
-                                         momentum, batch)
+                                         momentum, batch, _take_stats(x))
         else:
             mean = run_mean.float().view(1, -1)
             rstd = torch.rsqrt(run_var.float() + eps).view(1, -1)

@@ -508,7 +508,7 @@ def test_family_r_networks_match_oracle():
     l16, f16, g16 = run("torch", torch.bfloat16)
     lh, fh, gh = run("native")
     assert torch.isfinite(lh) and abs(lh.item() - l32.item()) < 5e-2 * abs(l32.item())
-    assert rel_err(fh, f32) < 1e-1
+    assert rel_err(fh, f32) < 1.5 * rel_err(f16, f32) + 0.05
     worse = []
     for n in g32:
         assert torch.isfinite(gh[n]).all(), n
@@ -516,3 +516,34 @@ def test_family_r_networks_match_oracle():
         if eh > 1.5 * ee + 0.05:
             worse.append((n, eh, ee))
     assert not worse, worse
+
+
+@pytest.mark.parametrize("kind,N,C,H,Cout", [("conv", 16, 64, 128, 128), ("convT", 16, 128, 32, 256),
+                                             ("conv_s1", 2, 256, 17, 512)])
+@pytest.mark.parametrize("norm", ["instance", "batch"])
+def test_conv_epilogue_norm_stats(kind, N, C, H, Cout, norm):
+    """Norm statistics emitted by the conv epilogue == the norm's own statistics pass."""
+    from p2p_pytorch_amd.ops import hip
+    x = rand_img(N, C, H, H, seed=31)
+    if kind == "convT":
+        w = torch.randn(C, Cout, 4, 4, device=DEV) * 0.05
+        f = lambda st: ops.conv_transpose2d(x, w, None, 2, 1, "relu", None, stats=st)  # noqa: E731
+    else:
+        w = torch.randn(Cout, C, 4, 4, device=DEV) * 0.05
+        s = 1 if kind == "conv_s1" else 2
+        f = lambda st: ops.conv2d(x, w, None, s, 1, stats=st)  # noqa: E731
+    outs = []
+    for st in (False, True):
+        hip.begin_step()
+        y = f(st)
+        if st and kind != "conv_s1":
+            assert len(hip._stats_stash) == 1, "epilogue statistics expected for this shape"
+        if norm == "instance":
+            z = ops.instance_norm(y, act="lrelu")
+        else:
+            rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+            z = ops.batch_norm(y, rm, rv, torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV),
+                               True, act="relu")
+        outs.append(z.float())
+        assert not hip._stats_stash
+    assert rel_err(outs[1], outs[0]) < 1e-2
