@@ -50,6 +50,9 @@ int p2p_maxpool2(const void* x, const void* gy, int N, int H, int W, int C, void
 int p2p_l2norm(const void* x, const void* gy, long P, int C, float eps, void* out, hipStream_t st);
 int p2p_pixel_shuffle(const void* in, int N, int OH, int OW, int OC, int r, int dir, void* out,
                       hipStream_t st);
+int p2p_weight_prep_pairs(int count, const float* const* w, void* const* out0, void* const* out1,
+                          const int* A, const int* B, const int* T, const int* Xa, const int* Xb,
+                          hipStream_t st);
 int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, int reflect,
                  const void* xb, int act, void* dx, hipStream_t st);
 int p2p_pad_channels(const void* a, int Ca, const void* b, int Cb, long P, int Co, void* out,
@@ -98,6 +101,7 @@ const void* zero_page(const Tensor& like) {
   if (!pages[d].defined()) pages[d] = at::zeros({4096}, like.options().dtype(at::kByte));
   return pages[d].data_ptr();
 }
+
 
 // conv kernel variant: P2P_CONV_VARIANT = v1 (register-staged) | g2 | g3 | g4 (LDS-DMA
 // rings) | unset = auto: g4 (256x128 tile, 8 waves, 3-stage ring) for Cout > 64, g2
@@ -429,6 +433,47 @@ Tensor weight_prep(const Tensor& w, int64_t swap, int64_t Xp, int64_t Yp,
 }
 
 // all weight images of a network in one launch per WP_MAX tensors
+// both images of each weight (T <= 16) in one launch: returns [out0_0, out1_0, out0_1, ...]
+std::vector<Tensor> weight_prep_pairs(at::TensorList ws, at::IntArrayRef xa, at::IntArrayRef xb) {
+  const size_t n = ws.size();
+  TORCH_CHECK(xa.size() == n && xb.size() == n, "weight_prep_pairs: list sizes");
+  std::vector<Tensor> outs;
+  outs.reserve(2 * n);
+  std::vector<const float*> W;
+  std::vector<void*> O0, O1;
+  std::vector<int> A, B, T, XA, XB;
+  auto flush = [&]() {
+    if (W.empty()) return;
+    check_rc(p2p_weight_prep_pairs((int)W.size(), W.data(), O0.data(), O1.data(), A.data(), B.data(),
+                                   T.data(), XA.data(), XB.data(), cur_stream(ws[0])),
+             "weight_prep_pairs");
+    W.clear(); O0.clear(); O1.clear(); A.clear(); B.clear(); T.clear(); XA.clear(); XB.clear();
+  };
+  for (size_t i = 0; i < n; ++i) {
+    const Tensor& w = ws[i];
+    TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.dim() == 4,
+                "weight_prep_pairs: fp32 contiguous 4-D weights");
+    const int64_t a = w.size(0), b = w.size(1), kh = w.size(2), kw = w.size(3);
+    TORCH_CHECK(kh * kw <= 16 && xa[i] >= a && xb[i] >= b && xa[i] % 2 == 0 && xb[i] % 2 == 0,
+                "weight_prep_pairs: T <= 16, even padded sizes");
+    Tensor o0 = at::empty({xa[i], kh, kw, xb[i]}, w.options().dtype(at::kBFloat16));
+    Tensor o1 = at::empty({xb[i], kh, kw, xa[i]}, w.options().dtype(at::kBFloat16));
+    outs.push_back(o0);
+    outs.push_back(o1);
+    W.push_back(w.data_ptr<float>());
+    O0.push_back(o0.data_ptr());
+    O1.push_back(o1.data_ptr());
+    A.push_back((int)a);
+    B.push_back((int)b);
+    T.push_back((int)(kh * kw));
+    XA.push_back((int)xa[i]);
+    XB.push_back((int)xb[i]);
+    if (W.size() == 24) flush();
+  }
+  flush();
+  return outs;
+}
+
 std::vector<Tensor> weight_prep_multi(at::TensorList ws, at::IntArrayRef swap, at::IntArrayRef xp,
                                       at::IntArrayRef yp) {
   const size_t n = ws.size();
@@ -865,6 +910,7 @@ TORCH_LIBRARY(p2p, m) {
   m.def("l2norm(Tensor x, Tensor? gy, float eps) -> Tensor");
   m.def("pixel_shuffle(Tensor x, int r, int dir) -> Tensor");
   m.def("pad_fold(Tensor dxp, int H, int W, int pad, int up, int reflect, Tensor? xb, int act) -> Tensor");
+  m.def("weight_prep_pairs(Tensor[] w, int[] xa, int[] xb) -> Tensor[]");
   m.def("weight_prep_multi(Tensor[] w, int[] swap, int[] xp, int[] yp) -> Tensor[]");
   m.def("norm_fwd(Tensor x, float eps, Tensor? gamma, Tensor? beta, Tensor? prelu_w, int act, "
         "Tensor(a!)? run_mean, Tensor(b!)? run_var, float momentum, bool batch, Tensor? partials=None) -> Tensor[]");
@@ -889,6 +935,7 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("conv_wgrad", conv_wgrad);
   m.impl("weight_prep", weight_prep);
   m.impl("weight_prep_multi", weight_prep_multi);
+  m.impl("weight_prep_pairs", weight_prep_pairs);
   m.impl("norm_fwd", norm_fwd);
   m.impl("norm_apply", norm_apply);
   m.impl("norm_bwd", norm_bwd);

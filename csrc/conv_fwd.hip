@@ -349,15 +349,6 @@ extern "C" int p2p_conv_fwd(const p2p::ConvFwdArgs* a, int mode, int bm, int bn,
   return mode == 0 ? p2p::dispatch_fwd<0>(*a, bm, bn, st) : p2p::dispatch_fwd<1>(*a, bm, bn, st);
 }
 
-extern "C" int p2p_conv_finalize(const p2p::ConvFwdArgs* a, hipStream_t st) {
-  const long P = (long)a->N * a->OH * a->OW;
-  const long nchunks = P * (a->Cout / 8);
-  long blocks = (nchunks + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(p2p::conv_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, st, *a, P);
-  return (int)hipGetLastError();
-}
 
 // ---------------------------------------------------------------------------------------
 // Weight preparation: fp32 master weight [A][B][KH][KW] (PyTorch Conv2d: [Cout][Cin][..],
@@ -606,7 +597,148 @@ __global__ void __launch_bounds__(256) weight_prep_multi_kernel(WPrepList L) {
 }
 }  // namespace p2p
 
+extern "C" int p2p_conv_finalize(const p2p::ConvFwdArgs* a, hipStream_t st) {
+  const long P = (long)a->N * a->OH * a->OW;
+  const long nchunks = P * (a->Cout / 8);
+  long blocks = (nchunks + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(p2p::conv_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, st, *a, P);
+  return (int)hipGetLastError();
+}
+
 extern "C" int p2p_weight_prep_max() { return p2p::WP_MAX; }
+
+// ---------------------------------------------------------------------------------------
+// Both GEMM images of a weight in ONE pass (T = KH*KW <= 16): out0 [Xa][T][Xb] (w[a][b][t])
+// and out1 [Xb][T][Xa] (w[b-major]) with Xa >= A, Xb >= B zero-padded.  A 32(a) x 32(b) x T
+// block is read once with coalesced runs (each a-row's b x t slab is contiguous), staged
+// as bf16 in LDS, and written out as 4-byte pairs along the contiguous axis of each image
+// -- the transposed image no longer gathers across 64 KB-strided source rows.
+namespace p2p {
+constexpr int WPP_MAX = 24;
+struct WPairList {
+  const float* w[WPP_MAX];
+  bf16* out0[WPP_MAX];
+  bf16* out1[WPP_MAX];
+  int A[WPP_MAX], B[WPP_MAX], T[WPP_MAX], Xa[WPP_MAX], Xb[WPP_MAX];
+};
+
+// TT = 16: the 4x4-kernel fast path (all index math shifts, float4 source loads);
+// TT = 0: any T <= 16 with runtime division.
+template <int TT>
+__global__ void __launch_bounds__(256) weight_prep_pair_kernel(WPairList L) {
+  constexpr int TA = 32, TB = 32, TMAX = 16, TS = TMAX + 2;  // +2: breaks the 32-B row stride
+  __shared__ bf16 tile[TA][TB][TS];
+  const int k = blockIdx.y;
+  const float* __restrict__ w = L.w[k];
+  const int A = L.A[k], B = L.B[k], Xa = L.Xa[k], Xb = L.Xb[k];
+  const int T = TT ? TT : L.T[k];
+  if (TT && L.T[k] != TT) return;
+  if (!TT && L.T[k] == 16) return;
+  const int ta = (Xa + TA - 1) / TA, tb = (Xb + TB - 1) / TB;
+  const int tid = threadIdx.x;
+  for (int tile_id = blockIdx.x; tile_id < ta * tb; tile_id += gridDim.x) {
+    const int a0 = (tile_id / tb) * TA, b0 = (tile_id % tb) * TB;
+    if constexpr (TT == 16) {
+      // per a-row the [b0, b0+32) x 16 run is 128 float4s
+      for (int idx = tid; idx < TA * 128; idx += 256) {
+        const int al = idx >> 7, bl = (idx >> 2) & 31, t4 = (idx & 3) * 4;
+        const int a = a0 + al, b = b0 + bl;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (a < A && b < B) v = *reinterpret_cast<const float4*>(w + ((long)a * B + b) * 16 + t4);
+        bf16* d = &tile[al][bl][t4];
+        d[0] = (bf16)v.x;
+        d[1] = (bf16)v.y;
+        d[2] = (bf16)v.z;
+        d[3] = (bf16)v.w;
+      }
+    } else {
+      const int run = TB * T;
+      for (int idx = tid; idx < TA * run; idx += 256) {
+        const int al = idx / run, r = idx - al * run;
+        const int bl = r / T, t = r - bl * T;
+        const int a = a0 + al, b = b0 + bl;
+        float v = 0.f;
+        if (a < A && b < B) v = w[((long)a * B + b) * T + t];
+        tile[al][bl][t] = (bf16)v;
+      }
+    }
+    __syncthreads();
+    // out0[a][t][b]: bf16 pairs along b
+    const int n0 = TA * T * (TB / 2);
+    for (int idx = tid; idx < n0; idx += 256) {
+      int al, t, bl;
+      if constexpr (TT == 16) {
+        al = idx >> 8;
+        t = (idx >> 4) & 15;
+        bl = (idx & 15) * 2;
+      } else {
+        al = idx / (T * (TB / 2));
+        const int r = idx - al * (T * (TB / 2));
+        t = r / (TB / 2);
+        bl = (r - t * (TB / 2)) * 2;
+      }
+      const int a = a0 + al, b = b0 + bl;
+      if (a < Xa && b < Xb) {
+        const uint32_t lo = __builtin_bit_cast(uint16_t, tile[al][bl][t]);
+        const uint32_t hi = __builtin_bit_cast(uint16_t, tile[al][bl + 1][t]);
+        *reinterpret_cast<uint32_t*>(L.out0[k] + ((long)a * T + t) * Xb + b) = lo | (hi << 16);
+      }
+    }
+    // out1[b][t][a]: bf16 pairs along a
+    for (int idx = tid; idx < n0; idx += 256) {
+      int bl, t, al;
+      if constexpr (TT == 16) {
+        bl = idx >> 8;
+        t = (idx >> 4) & 15;
+        al = (idx & 15) * 2;
+      } else {
+        bl = idx / (T * (TA / 2));
+        const int r = idx - bl * (T * (TA / 2));
+        t = r / (TA / 2);
+        al = (r - t * (TA / 2)) * 2;
+      }
+      const int a = a0 + al, b = b0 + bl;
+      if (b < Xb && a < Xa) {
+        const uint32_t lo = __builtin_bit_cast(uint16_t, tile[al][bl][t]);
+        const uint32_t hi = __builtin_bit_cast(uint16_t, tile[al + 1][bl][t]);
+        *reinterpret_cast<uint32_t*>(L.out1[k] + ((long)b * T + t) * Xa + a) = lo | (hi << 16);
+      }
+    }
+    __syncthreads();
+  }
+}
+}  // namespace p2p
+
+extern "C" int p2p_weight_prep_pairs(int count, const float* const* w, void* const* out0, void* const* out1,
+                                     const int* A, const int* B, const int* T, const int* Xa, const int* Xb,
+                                     hipStream_t st) {
+  using namespace p2p;
+  if (count <= 0) return 0;
+  if (count > WPP_MAX) return -1;
+  WPairList L;
+  int maxt = 1;
+  for (int i = 0; i < count; ++i) {
+    if (T[i] > 16 || (Xa[i] & 1) || (Xb[i] & 1)) return -1;
+    L.w[i] = w[i];
+    L.out0[i] = static_cast<bf16*>(out0[i]);
+    L.out1[i] = static_cast<bf16*>(out1[i]);
+    L.A[i] = A[i];
+    L.B[i] = B[i];
+    L.T[i] = T[i];
+    L.Xa[i] = Xa[i];
+    L.Xb[i] = Xb[i];
+    const int tiles = ((Xa[i] + 31) / 32) * ((Xb[i] + 31) / 32);
+    maxt = tiles > maxt ? tiles : maxt;
+  }
+  bool any16 = false, other = false;
+  for (int i = 0; i < count; ++i) (T[i] == 16 ? any16 : other) = true;
+  const dim3 grid((unsigned)(maxt < 2048 ? maxt : 2048), count);
+  if (any16) hipLaunchKernelGGL(weight_prep_pair_kernel<16>, grid, dim3(256), 0, st, L);
+  if (other) hipLaunchKernelGGL(weight_prep_pair_kernel<0>, grid, dim3(256), 0, st, L);
+  return (int)hipGetLastError();
+}
 
 // descriptors: w[i] fp32 [A][B][T], out[i] bf16 [Xp][T][Yp]
 extern "C" int p2p_weight_prep_multi(int count, const float* const* w, void* const* out, const int* A,

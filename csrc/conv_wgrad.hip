@@ -288,9 +288,15 @@ __device__ __forceinline__ void lgkm_wait(bf16x8& f0, bf16x8& f1, bf16x8& f2, bf
 }
 template <int N, int CNT>
 __device__ __forceinline__ void lgkm_wait_arr(bf16x8 (&f)[CNT]) {
-  static_assert(CNT == 2 || CNT == 4, "fragment count");
-  if constexpr (CNT == 2) lgkm_wait<N>(f[0], f[1]);
-  else lgkm_wait<N>(f[0], f[1], f[2], f[3]);
+  static_assert(CNT == 2 || CNT == 4 || CNT == 8, "fragment count");
+  if constexpr (CNT == 2) {
+    lgkm_wait<N>(f[0], f[1]);
+  } else if constexpr (CNT == 4) {
+    lgkm_wait<N>(f[0], f[1], f[2], f[3]);
+  } else {
+    lgkm_wait<N>(f[0], f[1], f[2], f[3]);
+    lgkm_wait<N>(f[4], f[5], f[6], f[7]);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -471,48 +477,60 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
     }
     const bf16* P = Ps + stage * PSUB * PSUBE;
     const bf16* Q = Qs + stage * QSUB * SUBE;
-    bf16x8 af[2][TM], bfr[2][TN];
-    constexpr int RD_HALF = 2 * (TM + TN);   // ds_read_b64_tr per 32-deep half
-    constexpr int WAIT0 = RD_HALF < 15 ? RD_HALF : 15;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    // fragment reads of one 32-deep half; both halves are read up front (register double
+    // buffer) unless the wide 256x256 tile's accumulators leave no room (TM * TN > 16)
+    auto read_half = [&](int kk, bf16x8 (&af)[TM], bf16x8 (&bfr)[TN]) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int cb = wm * (TBR / WM) + i * 16;
-        af[kk][i] = tr_frag_w_asm<PW>(P + (cb / PW) * PSUBE, kk * 32, cb % PW, lane);
+        af[i] = tr_frag_w_asm<PW>(P + (cb / PW) * PSUBE, kk * 32, cb % PW, lane);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int cb = wn * (TBQ / WN) + j * 16;
-        bfr[kk][j] = tr_frag_w_asm<128>(Q + (cb >> 7) * SUBE, kk * 32, cb & 127, lane);
+        bfr[j] = tr_frag_w_asm<128>(Q + (cb >> 7) * SUBE, kk * 32, cb & 127, lane);
       }
-    }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      // reads return in order: lgkmcnt(min(RD_HALF, 15)) retires the first half (the
-      // counter holds at most 15, so the reads past that issued only as earlier ones returned)
-      if (kk == 0) {
-        lgkm_wait_arr<WAIT0>(af[0]);
-        lgkm_wait_arr<WAIT0>(bfr[0]);
-      } else {
-        lgkm_wait_arr<0>(af[1]);
-        lgkm_wait_arr<0>(bfr[1]);
-      }
+    };
+    auto mma_half = [&](bf16x8 (&af)[TM], bf16x8 (&bfr)[TN]) {
       if constexpr (RM & 1) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
-          af[kk][i] = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, af[kk][i])));
+          af[i] = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, af[i])));
       }
       if constexpr (RM & 2) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          bfr[kk][j] = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, bfr[kk][j])));
+          bfr[j] = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, bfr[j])));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    };
+    constexpr int RD_HALF = 2 * (TM + TN);   // ds_read_b64_tr per 32-deep half
+    if constexpr (TM * TN <= 16) {
+      bf16x8 af0[TM], bf0[TN], af1[TM], bf1[TN];
+      constexpr int WAIT0 = RD_HALF < 15 ? RD_HALF : 15;
+      read_half(0, af0, bf0);
+      read_half(1, af1, bf1);
+      // reads return in order: lgkmcnt(min(RD_HALF, 15)) retires the first half (the
+      // counter holds at most 15, so the reads past that issued only as earlier ones returned)
+      lgkm_wait_arr<WAIT0>(af0);
+      lgkm_wait_arr<WAIT0>(bf0);
+      mma_half(af0, bf0);
+      lgkm_wait_arr<0>(af1);
+      lgkm_wait_arr<0>(bf1);
+      mma_half(af1, bf1);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[TM], bfr[TN];
+        read_half(kk, af, bfr);
+        lgkm_wait_arr<0>(af);
+        lgkm_wait_arr<0>(bfr);
+        mma_half(af, bfr);
+      }
     }
     stage = stage + 1 == STAGES ? 0 : stage + 1;
   }
@@ -593,6 +611,8 @@ static int wgrad_glds_shape(const p2p::ConvWgradArgs* a) {
     return 0;
   const char* v = std::getenv("P2P_CONV_VARIANT");
   if (v && v[0] == 'v') return 0;
+  // 4 = 256x256 (half the VALU + LDS fragment traffic per MFMA of 1 / 2)
+  if (v && v[0] == 'g' && v[1] == '5' && a->R % 256 == 0 && a->Kq % 256 == 0) return 4;
   if (a->R >= 256) return 1;
   return a->Kq >= 256 ? 2 : 0;
 }
@@ -602,6 +622,7 @@ extern "C" int p2p_conv_wgrad_tile(const p2p::ConvWgradArgs* a, int* tr, int* tq
   if (shape == 1) { *tr = 256; *tq = 128; return shape; }
   if (shape == 2) { *tr = 128; *tq = 256; return shape; }
   if (shape == 3) { *tr = 64; *tq = 128; return shape; }
+  if (shape == 4) { *tr = 256; *tq = 256; return shape; }
   *tr = a->R <= 16 ? 16 : (a->R <= 64 ? 64 : 128);
   *tq = 128;
   return 0;
@@ -643,6 +664,11 @@ extern "C" int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t st) {
     const int smem = STG * (tr + tq) * WBM * 2;
     dim3 grid(((a->R + tr - 1) / tr) * ((a->Kq + tq - 1) / tq), a->splits, 1);
     const int rm = (a->p_act == ACT_RELU ? 1 : 0) | (a->q_act == ACT_RELU ? 2 : 0);
+    if (shape == 4) {  // 256x256, 2-stage ring (128 KB LDS)
+      const int smem4 = 2 * (256 + 256) * WBM * 2;
+      dim3 grid4(((a->R + 255) / 256) * ((a->Kq + 255) / 256), a->splits, 1);
+      return wg_launch_rm<256, 256, 2, 4, 2>(rm, *a, grid4, smem4, st);
+    }
     if (shape == 1) return wg_launch_rm<256, 128, 4, 2, STG>(rm, *a, grid, smem, st);
     if (shape == 2) return wg_launch_rm<128, 256, 2, 4, STG>(rm, *a, grid, smem, st);
     return wg_launch_rm<64, 128, 1, 4, STG>(rm, *a, grid, smem, st);

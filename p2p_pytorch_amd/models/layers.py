@@ -24,11 +24,14 @@ class Conv2d(nn.Conv2d):
         self.act_in = act_in
         self.act_out = act_out
         self.norm_stats = False   # set by link_norm(): a norm consumes the output
+        self.grad_gate = None     # set by link_gate(): apply the producer's act' in dgrad
+        self.out_gated = False    # set by link_gate(): consumers apply act_out' for us
 
     def forward(self, x):  # noqa: D401
         return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.pad_mode,
                           self.upsample, self.act_in, self.act_out,
-                          stats=self.norm_stats and self.training)
+                          stats=self.norm_stats and self.training, grad_gate=self.grad_gate,
+                          out_gated=self.out_gated)
 
 
 class ConvTranspose2d(nn.ConvTranspose2d):
@@ -42,11 +45,14 @@ class ConvTranspose2d(nn.ConvTranspose2d):
         self.act_in = act_in
         self.act_out = act_out
         self.norm_stats = False
+        self.grad_gate = None
+        self.out_gated = False
 
     def forward(self, x):
         return ops.conv_transpose2d(x, self.weight, self.bias, self.stride[0], self.padding[0],
                                     self.act_in, self.act_out,
-                                    stats=self.norm_stats and self.training)
+                                    stats=self.norm_stats and self.training,
+                                    grad_gate=self.grad_gate, out_gated=self.out_gated)
 
 
 def link_norm(conv, norm):
@@ -54,6 +60,25 @@ def link_norm(conv, norm):
     emits the per-tile (mean, M2) partials and the norm skips its own statistics pass."""
     if isinstance(norm, (InstanceNorm2d, BatchNorm2d)) and hasattr(conv, "norm_stats"):
         conv.norm_stats = True
+
+
+def link_gate(producer, consumers):
+    """Fuse ``producer``'s output-activation derivative (ReLU / LeakyReLU, whose sign test
+    reads the same from the stored output as from the input) into the dgrad epilogues of
+    its ``consumers`` -- only when EVERY consumer of the output is listed here and either
+    gates (``grad_gate``) or already applies an equivalent input ReLU (``act_in``)."""
+    act = getattr(producer, "act_out", None)
+    if act not in ("relu", "lrelu"):
+        return
+    for c in consumers:
+        if getattr(c, "act_in", None) == "relu":
+            continue   # relu'(act(x)) * act'(x) == relu'(act(x)) for relu / lrelu
+        if getattr(c, "act_in", None) is not None or not hasattr(c, "grad_gate"):
+            return
+    for c in consumers:
+        if getattr(c, "act_in", None) is None:
+            c.grad_gate = act
+    producer.out_gated = True
 
 
 class InstanceNorm2d(nn.Module):

@@ -28,7 +28,7 @@ from __future__ import annotations
 
 import torch.nn as nn
 
-from .layers import Conv2d, ConvTranspose2d, Dropout, link_norm, norm_layer
+from .layers import Conv2d, ConvTranspose2d, Dropout, link_gate, link_norm, norm_layer
 
 
 class UnetGenerator(nn.Module):
@@ -67,6 +67,9 @@ class UnetGenerator(nn.Module):
             [Dropout(0.5) if i in self.drop_levels else nn.Identity() for i in range(n)])
         for c, m in list(zip(self.downs, self.down_norms)) + list(zip(self.ups, self.up_norms)):
             link_norm(c, m)
+        # outermost encoder output feeds downs[1] and (skip) ups[0]; innermost feeds ups[n-1]
+        link_gate(self.downs[0], [self.downs[1], self.ups[0]])
+        link_gate(self.downs[n - 1], [self.ups[n - 1]])
 
     def forward(self, x):
         n = self.num_downs
@@ -107,6 +110,7 @@ class NLayerDiscriminator(nn.Module):
         self.norms = nn.ModuleList(norms)
         for c, m in zip(self.convs, self.norms):
             link_norm(c, m)
+        link_gate(self.convs[0], [self.convs[1]])
 
     def forward(self, x):
         for conv, norm in zip(self.convs, self.norms):
@@ -127,6 +131,9 @@ class PixelDiscriminator(nn.Module):
         ])
         self.norms = nn.ModuleList([nn.Identity(), norm_layer(norm, ndf * 2, act="lrelu"),
                                     nn.Identity()])
+        for c, m in zip(self.convs, self.norms):
+            link_norm(c, m)
+        link_gate(self.convs[0], [self.convs[1]])
 
     def forward(self, x):
         for conv, norm in zip(self.convs, self.norms):

@@ -119,37 +119,47 @@ def _weight_image(w: torch.Tensor, swap: int, xp: int, yp: int, scale=None) -> t
 
 
 def prepare_weights(*modules):
-    """Cast every conv weight image (forward and dgrad layouts) of ``modules`` in one
-    multi-tensor launch per 24 tensors and seed the per-parameter cache, instead of one
-    weight_prep launch per layout per layer on first use."""
+    """Cast every conv weight image (forward and dgrad layouts) of ``modules`` and seed the
+    per-parameter cache: kernels up to 4x4 in one launch writing BOTH images from a single
+    read (weight_prep_pairs), larger kernels (family R 5x5 / 7x7 / 9x9) through the
+    per-layout multi-tensor cast -- instead of one launch per layout per layer on first use."""
     from ..models.layers import Conv2d, ConvTranspose2d
+    pw, pa, pb, pkeys = [], [], [], []
     ws, sw, xp, yp, keys = [], [], [], [], []
     for mod in modules:
         for m in mod.modules():
             w = getattr(m, "weight", None)
             if not isinstance(w, torch.Tensor) or not w.is_cuda or w.dim() != 4:
                 continue
-            if isinstance(m, ConvTranspose2d):
-                cin, cout = w.shape[0], w.shape[1]
-                layouts = [(1, _pad8(cout), _pad8(cin)), (0, _pad8(cin), _pad8(cout))]
-            elif isinstance(m, Conv2d):
-                cout, cin = w.shape[0], w.shape[1]
-                layouts = [(0, _pad8(cout), _pad8(cin)), (1, _pad8(cin), _pad8(cout))]
-            else:
+            if not isinstance(m, (Conv2d, ConvTranspose2d)):
                 continue
             wc = w.detach()
             if wc.dtype != torch.float32 or not wc.is_contiguous():
                 continue
-            for (s_, x_, y_) in layouts:
+            # dim0 = A, dim1 = B for both module kinds: image 0 = [A][T][B], image 1 = [B][T][A]
+            xa, xb = _pad8(w.shape[0]), _pad8(w.shape[1])
+            if w.shape[2] * w.shape[3] <= 16:
+                pw.append(wc)
+                pa.append(xa)
+                pb.append(xb)
+                pkeys.append(w)
+                continue
+            for (s_, x_, y_) in ((0, xa, xb), (1, xb, xa)):
                 ws.append(wc)
                 sw.append(s_)
                 xp.append(x_)
                 yp.append(y_)
                 keys.append((w, (s_, x_, y_, None)))
-    if not ws:
-        return
-    imgs = P().weight_prep_multi(ws, sw, xp, yp)
-    for (w, key), img in zip(keys, imgs):
+    entries = []
+    if pw:
+        imgs = P().weight_prep_pairs(pw, pa, pb)
+        for i, w in enumerate(pkeys):
+            entries.append((w, (0, pa[i], pb[i], None), imgs[2 * i]))
+            entries.append((w, (1, pb[i], pa[i], None), imgs[2 * i + 1]))
+    if ws:
+        imgs = P().weight_prep_multi(ws, sw, xp, yp)
+        entries.extend((w, key, img) for (w, key), img in zip(keys, imgs))
+    for w, key, img in entries:
         cache = getattr(w, "_p2p_cache", None)
         if cache is None:
             cache = {}
@@ -183,11 +193,18 @@ def advance_rng(device=None):
 
 # ============================================================== convolution
 class _ConvCfg:
+    """``grad_gate``: activation derivative (from the input value) applied to the input
+    gradient in the dgrad epilogue -- the producer of this conv's input stored
+    ``act(x)`` and set ``out_gated`` so it skips its own gate pass (valid only when every
+    consumer of that output gates; the models wire both ends)."""
     __slots__ = ("transposed", "KH", "KW", "stride", "pad", "reflect", "up", "act_in", "act_out",
-                 "stats")
+                 "stats", "grad_gate", "out_gated")
 
-    def __init__(self, transposed, KH, KW, stride, pad, reflect, up, act_in, act_out, stats=False):
+    def __init__(self, transposed, KH, KW, stride, pad, reflect, up, act_in, act_out, stats=False,
+                 grad_gate=None, out_gated=False):
         self.stats = stats
+        self.grad_gate = grad_gate
+        self.out_gated = out_gated
         self.transposed = transposed
         self.KH, self.KW = KH, KW
         self.stride, self.pad = stride, pad
@@ -242,7 +259,7 @@ class ConvFn(torch.autograd.Function):
         ctx.geo = (C1, C2, Cp, packed, Cout, Coutp, H, W)
         ctx.has_x2 = x2 is not None
         ctx.has_bias = bias is not None
-        keep_y = cfg.act_out not in (None, "none")
+        keep_y = cfg.act_out not in (None, "none") and not cfg.out_gated
         ctx.save_for_backward(q1, q2, weight, y if keep_y else None)
         return y
 
@@ -256,13 +273,14 @@ class ConvFn(torch.autograd.Function):
         need_w = ctx.needs_input_grad[2]
         need_b = ctx.has_bias and ctx.needs_input_grad[3]
         gy = to_nhwc_bf16(gy)
-        if cfg.act_out not in (None, "none"):
+        if cfg.act_out not in (None, "none") and not cfg.out_gated:
             gy = P().act(gy, y, _act_code(cfg.act_out), 2)
         gyp = gy if Coutp == Cout else P().pad_channels(gy, None, Coutp)
         KH, KW, s, p = cfg.KH, cfg.KW, cfg.stride, cfg.pad
         gx1 = gx2 = gw = gb = None
         if need_x1 or need_x2:
-            act_in = _act_code(cfg.act_in)
+            # input-gradient gate: the input activation's derivative, or the producer's
+            act_in = _act_code(cfg.act_in) or _act_code(cfg.grad_gate)
             split = C1 if (q2 is not None) else Cp
             if cfg.reflect or cfg.up != 1:
                 # family-R ConvLayer / UpsampleConvLayer: dgrad onto the virtual padded,
@@ -333,22 +351,22 @@ def _pair(v):
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, pad_mode="zeros", upsample=1,
-           act_in=None, act_out=None, stats=False):
+           act_in=None, act_out=None, stats=False, grad_gate=None, out_gated=False):
     s, s2 = _pair(stride)
     p, p2 = _pair(padding)
     if s != s2 or p != p2:
         raise NotImplementedError("anisotropic stride/padding")
     x1, x2 = _split_input(x)
     cfg = _ConvCfg(False, weight.shape[2], weight.shape[3], s, p, pad_mode == "reflect" and p > 0,
-                   int(upsample or 1), act_in, act_out, stats)
+                   int(upsample or 1), act_in, act_out, stats, grad_gate, out_gated)
     return ConvFn.apply(x1, x2, weight, bias, cfg)
 
 
 def conv_transpose2d(x, weight, bias=None, stride=2, padding=1, act_in=None, act_out=None,
-                     stats=False):
+                     stats=False, grad_gate=None, out_gated=False):
     x1, x2 = _split_input(x)
     cfg = _ConvCfg(True, weight.shape[2], weight.shape[3], int(stride), int(padding), False, 1,
-                   act_in, act_out, stats)
+                   act_in, act_out, stats, grad_gate, out_gated)
     return ConvFn.apply(x1, x2, weight, bias, cfg)
 
 
@@ -445,7 +463,12 @@ class _PadCFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        return P().slice_channels(to_nhwc_bf16(g), 0, ctx.c), None
+        g = to_nhwc_bf16(g)
+        out = P().slice_channels(g, 0, ctx.c)
+        cs = _take_colsum(g)   # the norm's exact-zero bias gradient follows the slice
+        if cs is not None:
+            _stash_colsum(out, cs[:ctx.c])
+        return out, None
 
 
 class _SliceCFn(torch.autograd.Function):
