@@ -133,7 +133,7 @@ def main():
     img_s = world * B * args.steps / dt_max
     base = EAGER_BASELINE_IMG_S_PER_GPU
     out = {
-        "metric": "train images/sec (whole node), 256x256 pix2pix U-Net+PatchGAN",
+        "metric": f"train images/sec (whole node), {S}x{S} pix2pix U-Net+PatchGAN",
         "value": round(img_s, 2),
         "unit": "images/sec",
         "n_gpus": world,

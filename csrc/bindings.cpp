@@ -122,6 +122,7 @@ int conv_variant(int64_t Cout, int64_t kmax, int64_t tiles256 = 0) {
   const bool big = Cout > 128 && kmax > 256;
   if (v && v[0] == 'g' && v[1] >= '2' && v[1] <= '4') return v[1] - '0';
   if (v && v[0] == 'g' && v[1] == '5') return big ? 5 : v4;
+  if (v && v[0] == 'g' && v[1] == '6') return (Cout <= 64 && kmax > 256) ? 6 : ((big && tiles256 >= 256) ? 5 : v4);
   return (big && tiles256 >= 256) ? 5 : v4;
 }
 
@@ -271,7 +272,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   int bm, bn;
   if (glds_ok) {
     bn = variant == 5 ? 256 : (Cout > 64 ? 128 : 64);
-    bm = (variant == 4 || variant == 5) ? 256 : 128;
+    bm = (variant == 4 || variant == 5 || variant == 6) ? 256 : 128;
   } else if (Cout <= 16) {
     bn = 16;
     bm = mmax >= 4096 ? 256 : 64;

@@ -322,7 +322,8 @@ static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
 template <int MODE, bool FASTK, bool RELU>
 static int dispatch_glds2(const ConvFwdArgs& a, int variant, hipStream_t st) {
   // variant: 2 = 2-stage 128-row tile, 3 = 3-stage 128-row tile, 4 = 3-stage 256x128 8 waves,
-  // 5 = 2-stage 256x256 (8 waves of 128x64: half the LDS fragment traffic per MFMA of 4)
+  // 5 = 2-stage 256x256 (8 waves of 128x64: half the LDS fragment traffic per MFMA of 4),
+  // 6 = 2-stage 256x64 on 4 waves of 64x64 (N <= 64 layers)
   if (a.Cout > 128 && variant == 5) return launch_glds<256, 256, 2, 4, MODE, 2, FASTK, RELU>(a, st);
   if (a.Cout > 64) {
     if (variant == 5) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU>(a, st);
@@ -330,6 +331,7 @@ static int dispatch_glds2(const ConvFwdArgs& a, int variant, hipStream_t st) {
     if (variant == 3) return launch_glds<128, 128, 2, 2, MODE, 3, FASTK, RELU>(a, st);
     if (variant == 4) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU>(a, st);
   } else if (a.Cout > 32) {
+    if (variant == 6) return launch_glds<256, 64, 4, 1, MODE, 2, FASTK, RELU>(a, st);
     if (variant == 2) return launch_glds<128, 64, 2, 2, MODE, 2, FASTK, RELU>(a, st);
     if (variant == 3) return launch_glds<128, 64, 2, 2, MODE, 3, FASTK, RELU>(a, st);
     if (variant == 4) return launch_glds<256, 64, 4, 2, MODE, 3, FASTK, RELU>(a, st);

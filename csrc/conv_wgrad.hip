@@ -18,6 +18,7 @@
 // wgrad_reduce_kernel sums the slabs in a fixed order (bitwise deterministic, no
 // atomics) while permuting into PyTorch's [R][C][KH][KW] weight layout.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "conv.h"
@@ -277,6 +278,26 @@ __device__ __forceinline__ bf16x8 tr_frag_w_asm(const bf16* tile, int kbase, int
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// transposed fragment from a precomputed per-lane LDS byte address: the lo / hi 4-row
+// groups and the 32-deep half are immediate offsets (row + 4 keeps the XOR pattern, the
+// half only moves whole rows), so a fragment costs no per-read address arithmetic
+template <int PW, int KK>
+__device__ __forceinline__ bf16x8 tr_frag_at(uint32_t addr) {
+  constexpr int OLO = KK * 32 * PW * 2, OHI = (KK * 32 + 4) * PW * 2;
+  uint64_t lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(addr), "i"(OLO));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(addr), "i"(OHI));
+  u32x4 v = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int PW>
+__device__ __forceinline__ uint32_t tr_lane_addr(const bf16* tile, int cbase, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int chunk = (cbase >> 3) + (p >> 1);
+  return lds_addr(tile + wg_off<PW>(8 * g + q, chunk) + (p & 1) * 4);
+}
+
 // s_waitcnt lgkmcnt(N) that the compiler must order before any use of the fragments
 template <int N>
 __device__ __forceinline__ void lgkm_wait(bf16x8& f0, bf16x8& f1) {
@@ -454,6 +475,20 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
     }
   };
 
+  // per-lane LDS byte addresses of every fragment in stage 0 (stage / half / row-group
+  // displacements are added per read as uniform / immediate offsets)
+  uint32_t fa_lane[TM], fb_lane[TN];
+#pragma unroll
+  for (int i2 = 0; i2 < TM; ++i2) {
+    const int cb = wm * (TBR / WM) + i2 * 16;
+    fa_lane[i2] = tr_lane_addr<PW>(Ps + (cb / PW) * PSUBE, cb % PW, lane);
+  }
+#pragma unroll
+  for (int j2 = 0; j2 < TN; ++j2) {
+    const int cb = wn * (TBQ / WN) + j2 * 16;
+    fb_lane[j2] = tr_lane_addr<128>(Qs + (cb >> 7) * SUBE, cb & 127, lane);
+  }
+
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -475,21 +510,15 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
       if (ns >= STAGES) ns -= STAGES;
       issue(st + STAGES - 1, ns);
     }
-    const bf16* P = Ps + stage * PSUB * PSUBE;
-    const bf16* Q = Qs + stage * QSUB * SUBE;
+    const uint32_t p_st = (uint32_t)(stage * PSUB * PSUBE * 2), q_st = (uint32_t)(stage * QSUB * SUBE * 2);
     // fragment reads of one 32-deep half; both halves are read up front (register double
     // buffer) unless the wide 256x256 tile's accumulators leave no room (TM * TN > 16)
-    auto read_half = [&](int kk, bf16x8 (&af)[TM], bf16x8 (&bfr)[TN]) {
+    auto read_half = [&](auto kkc, bf16x8 (&af)[TM], bf16x8 (&bfr)[TN]) {
+      constexpr int KK = decltype(kkc)::value;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int cb = wm * (TBR / WM) + i * 16;
-        af[i] = tr_frag_w_asm<PW>(P + (cb / PW) * PSUBE, kk * 32, cb % PW, lane);
-      }
+      for (int i = 0; i < TM; ++i) af[i] = tr_frag_at<PW, KK>(fa_lane[i] + p_st);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int cb = wn * (TBQ / WN) + j * 16;
-        bfr[j] = tr_frag_w_asm<128>(Q + (cb >> 7) * SUBE, kk * 32, cb & 127, lane);
-      }
+      for (int j = 0; j < TN; ++j) bfr[j] = tr_frag_at<128, KK>(fb_lane[j] + q_st);
     };
     auto mma_half = [&](bf16x8 (&af)[TM], bf16x8 (&bfr)[TN]) {
       if constexpr (RM & 1) {
@@ -512,8 +541,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
     if constexpr (TM * TN <= 16) {
       bf16x8 af0[TM], bf0[TN], af1[TM], bf1[TN];
       constexpr int WAIT0 = RD_HALF < 15 ? RD_HALF : 15;
-      read_half(0, af0, bf0);
-      read_half(1, af1, bf1);
+      read_half(std::integral_constant<int, 0>{}, af0, bf0);
+      read_half(std::integral_constant<int, 1>{}, af1, bf1);
       // reads return in order: lgkmcnt(min(RD_HALF, 15)) retires the first half (the
       // counter holds at most 15, so the reads past that issued only as earlier ones returned)
       lgkm_wait_arr<WAIT0>(af0);
@@ -523,10 +552,16 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
       lgkm_wait_arr<0>(bf1);
       mma_half(af1, bf1);
     } else {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
+      {
         bf16x8 af[TM], bfr[TN];
-        read_half(kk, af, bfr);
+        read_half(std::integral_constant<int, 0>{}, af, bfr);
+        lgkm_wait_arr<0>(af);
+        lgkm_wait_arr<0>(bfr);
+        mma_half(af, bfr);
+      }
+      {
+        bf16x8 af[TM], bfr[TN];
+        read_half(std::integral_constant<int, 1>{}, af, bfr);
         lgkm_wait_arr<0>(af);
         lgkm_wait_arr<0>(bfr);
         mma_half(af, bfr);
