@@ -49,6 +49,9 @@ def parse():
     p.add_argument("--no_graph", action="store_true", help="(native) disable hipGraph capture")
     p.add_argument("--graph", action="store_true",
                    help="(native) force hipGraph capture also for N>1 (default: N == 1 only)")
+    p.add_argument("--precision", default=os.environ.get("P2P_PRECISION", "bf16"), choices=["bf16", "fp8"],
+                   help="(native) conv GEMM operands: bf16, or fp8 (e4m3 fwd / e5m2 dgrad, bf16 wgrad; "
+                        "BASELINE config 5)")
     p.add_argument("--json_out", default=None)
     return p.parse_args()
 
@@ -61,6 +64,10 @@ def main():
     from p2p_pytorch_amd.engine.pix2pix import Pix2PixStep
     from p2p_pytorch_amd.parallel import dist as pdist
     p2p.set_backend(args.impl)
+    from p2p_pytorch_amd.ops import fp8 as _fp8
+    if args.precision == "fp8" and args.impl != "native":
+        raise SystemExit("--precision fp8 needs --impl native")
+    _fp8.set_precision(args.precision)
 
     world, rank, local_rank = pdist.init_from_env()
     if world != args.gpus:
@@ -143,13 +150,15 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": round(img_s / (base * world), 3) if base else None,
-        "dtype": "bf16",
+        "dtype": "fp8+bf16" if args.precision == "fp8" else "bf16",
         "data": "synthetic (random paired images, random-init weights)",
         "config": {"model": f"pix2pix {args.netG} + PatchGAN {args.netD} (70x70)",
                    "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
                    "image_size": S, "parallelism": f"dp{world}", "impl": args.impl,
                    "gan_mode": args.gan_mode, "lambda_L1": args.lamb,
-                   "hipgraph": bool(use_graph)},
+                   "hipgraph": bool(use_graph),
+                   "conv_precision": ("fp8 e4m3 fwd / e5m2 dgrad, bf16 wgrad + first/last layers"
+                                      if args.precision == "fp8" else "bf16")},
         "losses_finite": finite,
         "losses": loss_vals,
     }

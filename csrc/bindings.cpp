@@ -81,9 +81,11 @@ hipStream_t cur_stream(const Tensor& t) {
   return c10::hip::getCurrentHIPStream(t.device().index()).stream();
 }
 
-void check_act(const Tensor& t, const char* name) {
+void check_act(const Tensor& t, const char* name, bool allow_fp8 = false) {
   TORCH_CHECK(t.is_cuda(), name, ": expected a GPU tensor");
-  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, ": expected bf16, got ", t.scalar_type());
+  const auto dt = t.scalar_type();
+  TORCH_CHECK(dt == at::kBFloat16 || (allow_fp8 && (dt == at::kFloat8_e4m3fn || dt == at::kFloat8_e5m2)), name,
+              ": expected bf16", allow_fp8 ? " or fp8" : "", ", got ", dt);
   TORCH_CHECK(t.dim() == 4, name, ": expected NCHW-shaped tensor");
   TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), name,
               ": expected channels_last (NHWC) memory");
@@ -137,17 +139,30 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                              int64_t act_in, int64_t OH, int64_t OW, int64_t Cout, int64_t act_out,
                              int64_t Csplit, const optional<Tensor>& xb1,
                              const optional<Tensor>& xb2, int64_t act_bwd, int64_t Cvalid,
-                             bool want_stats) {
-  check_act(x1, "conv_fwd x1");
+                             bool want_stats, const optional<Tensor>& qs_x1,
+                             const optional<Tensor>& qs_x2, const optional<Tensor>& qs_w) {
+  check_act(x1, "conv_fwd x1", true);
+  // fp8 operands: x e4m3 (activations) or e5m2 (gradients), weight image e4m3, each with
+  // an fp8 scale site (csrc/fp8.hip); outputs stay bf16
+  const int fp8 = x1.scalar_type() == at::kFloat8_e4m3fn ? 1 : (x1.scalar_type() == at::kFloat8_e5m2 ? 2 : 0);
+  const Tensor obf = fp8 ? at::empty({0}, x1.options().dtype(at::kBFloat16)) : x1;
   const int64_t N = x1.size(0), H = x1.size(2), W = x1.size(3);
   int64_t C2 = 0;
   if (x2) {
-    check_act(*x2, "conv_fwd x2");
+    check_act(*x2, "conv_fwd x2", true);
+    TORCH_CHECK(x2->scalar_type() == x1.scalar_type(), "conv_fwd: concat halves must share a dtype");
     TORCH_CHECK(x2->size(0) == N && x2->size(2) == H && x2->size(3) == W, "conv_fwd: concat shape");
     C2 = x2->size(1);
   }
   const int64_t C1 = x1.size(1), C = C1 + C2;
-  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous(), "conv_fwd: weight");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == (fp8 ? at::kFloat8_e4m3fn : at::kBFloat16) && w.is_contiguous(),
+              "conv_fwd: weight (bf16, or e4m3 with fp8 activations)");
+  if (fp8) {
+    auto site_ok = [](const optional<Tensor>& t) {
+      return t.has_value() && t->is_cuda() && t->scalar_type() == at::kInt && t->numel() >= 4 && t->is_contiguous();
+    };
+    TORCH_CHECK(site_ok(qs_x1) && site_ok(qs_w) && (!x2 || site_ok(qs_x2)), "conv_fwd: fp8 needs scale sites");
+  }
   TORCH_CHECK(w.numel() >= Cout * KH * KW * C, "conv_fwd: weight too small for the GEMM view");
   TORCH_CHECK(Cout % 8 == 0 && Csplit % 8 == 0 && Csplit > 0 && Csplit <= Cout, "conv_fwd: Cout/Csplit");
   TORCH_CHECK(mode == 0 || mode == 1, "conv_fwd: mode");
@@ -165,9 +180,9 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       TORCH_CHECK(xb2->size(1) == Cout - Csplit, "xb2 shape");
     }
   }
-  Tensor y1 = empty_nhwc(N, Csplit, OH, OW, x1);
+  Tensor y1 = empty_nhwc(N, Csplit, OH, OW, obf);
   Tensor y2;
-  if (Csplit < Cout) y2 = empty_nhwc(N, Cout - Csplit, OH, OW, x1);
+  if (Csplit < Cout) y2 = empty_nhwc(N, Cout - Csplit, OH, OW, obf);
 
   p2p::ConvFwdArgs a{};
   a.x1 = x1.data_ptr();
@@ -202,12 +217,17 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   a.zero = zero_page(x1);
   a.stats = nullptr;
   a.stats_nchunks = 0;
+  a.fp8 = fp8;
+  a.qs_x1 = fp8 ? qs_x1->data_ptr<int>() : nullptr;
+  a.qs_x2 = (fp8 && x2) ? qs_x2->data_ptr<int>() : nullptr;
+  a.qs_w = fp8 ? qs_w->data_ptr<int>() : nullptr;
 
   hipStream_t st = cur_stream(x1);
   // ---- tiny-Cout "col" path: dense GEMM over the input pixels (N = taps x Cvalid) + col2im
   const int64_t Cv = Cvalid > 0 ? Cvalid : Cout;
   if (Cout <= 16 && Cv <= 16 && Csplit == Cout && !reflect && up == 1 && C1 % 64 == 0 &&
       C2 % 64 == 0) {
+    TORCH_CHECK(!fp8, "conv_fwd: fp8 is not supported on the tiny-Cout col path");
     // col[i][t*Cvp + co]: each tap's outputs padded to Cvp (4 / 8 / 16) so col2im reads
     // one aligned vector per tap
     const int64_t T = KH * KW;
@@ -216,7 +236,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     Tensor wv = at::zeros({Ncol, C}, w.options());
     wv.narrow(0, 0, T * Cvp).view({T, Cvp, C}).narrow(1, 0, Cv).copy_(
         w.reshape({-1}).narrow(0, 0, Cout * T * C).view({Cout, T, C}).narrow(0, 0, Cv).transpose(0, 1));
-    Tensor col = empty_nhwc(N, Ncol, H, W, x1);
+    Tensor col = empty_nhwc(N, Ncol, H, W, obf);
     p2p::ConvFwdArgs g = a;
     g.KH = g.KW = 1;
     g.stride = 1;
@@ -287,7 +307,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     bm = mmax >= 16384 ? 128 : 64;
   }
   const int64_t tiles = ((mmax + bm - 1) / bm) * ((Cout + bn - 1) / bn) * classes;
-  const int64_t ktiles = (kmax + 63) / 64;
+  const int64_t ktiles = (kmax + (fp8 ? 127 : 63)) / (fp8 ? 128 : 64);
   int splits = 1;
   if (tiles < 256 && ktiles >= 8) {
     splits = (int)std::min<int64_t>((512 + tiles - 1) / tiles, ktiles / 4);
@@ -295,7 +315,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   }
   Tensor ws;
   if (splits > 1) {
-    ws = at::zeros({N * OH * OW, Cout}, x1.options().dtype(at::kFloat));
+    ws = at::zeros({N * OH * OW, Cout}, obf.options().dtype(at::kFloat));
     a.ws = ws.data_ptr<float>();
     a.splits = splits;
   }
@@ -322,6 +342,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     a.stats = nullptr;
     stats = Tensor();
   }
+  TORCH_CHECK(!(fp8 && rc == -2), "conv_fwd: no fp8 kernel for this geometry (Cout ", Cout, ", C1 ", C1, ", C2 ",
+              C2, ", act_in ", act_in, ")");
   if (rc == -2) {
     // register-staged kernel: its own tile table
     int vbm = bm, vbn = bn;
@@ -799,6 +821,54 @@ Tensor slice_channels(const Tensor& x, int64_t c0, int64_t C) {
 }
 
 // out[c] (+)= scale * sum over all pixels of x[..., c]   (bias gradient)
+// ------------------------------------------------------------------ fp8 (csrc/fp8.hip)
+void check_site(const Tensor& site) {
+  TORCH_CHECK(site.is_cuda() && site.scalar_type() == at::kInt && site.numel() >= 4 && site.is_contiguous(),
+              "fp8: a scale site is a contiguous int32 GPU tensor of 4 words");
+}
+
+Tensor fp8_quant(const Tensor& x, Tensor site, int64_t fmt, int64_t use_cur) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16, "fp8_quant: bf16 input");
+  TORCH_CHECK(x.is_contiguous() || x.is_contiguous(at::MemoryFormat::ChannelsLast), "fp8_quant: dense input");
+  TORCH_CHECK(x.numel() % 8 == 0, "fp8_quant: numel % 8");
+  TORCH_CHECK(fmt == 0 || fmt == 1, "fp8_quant: fmt 0 (e4m3) or 1 (e5m2)");
+  check_site(site);
+  Tensor q = at::empty_like(x, x.options().dtype(fmt == 0 ? at::kFloat8_e4m3fn : at::kFloat8_e5m2),
+                            at::MemoryFormat::Preserve);
+  check_rc(p2p_fp8_quant(x.data_ptr(), x.numel(), site.data_ptr<int>(), (int)use_cur, (int)fmt, q.data_ptr(),
+                         cur_stream(x)),
+           "fp8_quant");
+  return q;
+}
+
+void fp8_amax(const Tensor& x, Tensor site, int64_t slot) {
+  TORCH_CHECK(x.is_cuda() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat), "fp8_amax: input");
+  TORCH_CHECK(x.is_contiguous() || x.is_contiguous(at::MemoryFormat::ChannelsLast), "fp8_amax: dense input");
+  TORCH_CHECK(slot >= 0 && slot < 4, "fp8_amax: slot");
+  check_site(site);
+  check_rc(p2p_fp8_amax(x.data_ptr(), x.scalar_type() == at::kFloat, x.numel(), site.data_ptr<int>(), (int)slot,
+                        cur_stream(x)),
+           "fp8_amax");
+}
+
+void fp8_roll(Tensor sites) {
+  TORCH_CHECK(sites.is_cuda() && sites.scalar_type() == at::kInt && sites.is_contiguous() && sites.numel() % 4 == 0,
+              "fp8_roll: int32 [n][4] pool");
+  check_rc(p2p_fp8_roll(sites.data_ptr<int>(), (int)(sites.numel() / 4), cur_stream(sites)), "fp8_roll");
+}
+
+Tensor fp8_dequant(const Tensor& q, const Tensor& site) {
+  const auto dt = q.scalar_type();
+  TORCH_CHECK(q.is_cuda() && (dt == at::kFloat8_e4m3fn || dt == at::kFloat8_e5m2), "fp8_dequant: fp8 input");
+  TORCH_CHECK(q.is_contiguous() || q.is_contiguous(at::MemoryFormat::ChannelsLast), "fp8_dequant: dense input");
+  check_site(site);
+  Tensor y = at::empty_like(q, q.options().dtype(at::kBFloat16), at::MemoryFormat::Preserve);
+  check_rc(p2p_fp8_dequant(q.data_ptr(), q.numel(), site.data_ptr<int>(), dt == at::kFloat8_e5m2 ? 1 : 0,
+                           y.data_ptr(), cur_stream(q)),
+           "fp8_dequant");
+  return y;
+}
+
 void colsum(const Tensor& x, Tensor out, double scale, bool accumulate) {
   check_act(x, "colsum x");
   const int64_t C = x.size(1), M = x.numel() / C;
@@ -896,7 +966,12 @@ void adam(at::TensorList p, at::TensorList g, at::TensorList m, at::TensorList v
 TORCH_LIBRARY(p2p, m) {
   m.def("conv_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, int mode, int KH, int KW, int stride, "
         "int pad, int reflect, int up, int act_in, int OH, int OW, int Cout, int act_out, int Csplit, "
-        "Tensor? xb1, Tensor? xb2, int act_bwd, int Cvalid=0, bool want_stats=False) -> Tensor[]");
+        "Tensor? xb1, Tensor? xb2, int act_bwd, int Cvalid=0, bool want_stats=False, Tensor? qs_x1=None, "
+        "Tensor? qs_x2=None, Tensor? qs_w=None) -> Tensor[]");
+  m.def("fp8_quant(Tensor x, Tensor(a!) site, int fmt, int use_cur=0) -> Tensor");
+  m.def("fp8_amax(Tensor x, Tensor(a!) site, int slot) -> ()");
+  m.def("fp8_roll(Tensor(a!) sites) -> ()");
+  m.def("fp8_dequant(Tensor q, Tensor site) -> Tensor");
   m.def("conv_wgrad(Tensor p1, Tensor? p2, int p_act, Tensor q1, Tensor? q2, int q_act, int KH, int KW, "
         "int stride, int pad, int reflect, int up, Tensor(a!) dw, float scale, int accumulate, "
         "int flip=0) -> ()");
@@ -933,6 +1008,10 @@ TORCH_LIBRARY(p2p, m) {
 
 TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("conv_fwd", conv_fwd);
+  m.impl("fp8_quant", fp8_quant);
+  m.impl("fp8_amax", fp8_amax);
+  m.impl("fp8_roll", fp8_roll);
+  m.impl("fp8_dequant", fp8_dequant);
   m.impl("conv_wgrad", conv_wgrad);
   m.impl("weight_prep", weight_prep);
   m.impl("weight_prep_multi", weight_prep_multi);

@@ -37,6 +37,12 @@ struct ConvFwdArgs {
   // / BM) + tile-in-class; the norm then only merges them (norm.hip finalize).
   float* stats;
   int stats_nchunks;  // chunks per image
+  // fp8 operands (0 = bf16): 1 = x e4m3, 2 = x e5m2 (gradients); weights always e4m3.
+  // qs_*: fp8 scale sites (csrc/fp8.hip) whose word [2] is the E8M0 dequant exponent.
+  int fp8;
+  const int* qs_x1;
+  const int* qs_x2;
+  const int* qs_w;
 };
 
 // Weight gradient: C[R][Kq] = sum_m P[m][R] * im2col(Q)[m][Kq], written to per-split
@@ -71,6 +77,10 @@ int p2p_conv_finalize(const p2p::ConvFwdArgs* a, hipStream_t stream);
 // configuration is not supported so the caller can fall back to p2p_conv_fwd.
 int p2p_conv_fwd_glds(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t stream);
 int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t stream);
+int p2p_fp8_quant(const void* x, long n, int* site, int use_cur, int fmt, void* q, hipStream_t st);
+int p2p_fp8_amax(const void* x, int is_f32, long n, int* site, int slot, hipStream_t st);
+int p2p_fp8_roll(int* sites, int nsites, hipStream_t st);
+int p2p_fp8_dequant(const void* q, long n, const int* site, int fmt, void* y, hipStream_t st);
 int p2p_conv_wgrad_tile_rows(int R);
 int p2p_conv_wgrad_tile(const p2p::ConvWgradArgs* a, int* tile_r, int* tile_q);
 int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int KW, int C, int Rr, int Cr,

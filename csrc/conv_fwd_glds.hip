@@ -24,15 +24,46 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-__device__ __forceinline__ void glds16(const void* g, bf16* lds_wave_base) {
+__device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(lds_wave_base), 16, 0, 0);
+}
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ i32x8 cat8(u32x4 lo, u32x4 hi) {
+  return __builtin_shufflevector(__builtin_bit_cast(i32x4, lo), __builtin_bit_cast(i32x4, hi), 0, 1, 2, 3, 4, 5,
+                                 6, 7);
+}
+
+// ReLU on 16 packed fp8 (e4m3 / e5m2: sign = bit 7 of each byte): zero the negative bytes
+__device__ __forceinline__ uint32_t relu_fp8x4(uint32_t w) {
+  const uint32_t neg = (w >> 7) & 0x01010101u;
+  return w & ~(neg * 0xffu);
+}
+__device__ __forceinline__ u32x4 relu_fp8x16(u32x4 v) {
+  u32x4 o;
+  o.x = relu_fp8x4(v.x);
+  o.y = relu_fp8x4(v.y);
+  o.z = relu_fp8x4(v.z);
+  o.w = relu_fp8x4(v.w);
+  return o;
 }
 
 // FASTK: every channel group a multiple of 64 (one tap per 64-deep K tile, wave-uniform);
 // otherwise (packed 8 / 16 / 24-channel image inputs) each lane splits its own chunk's k
 // into (tap, channel) and k >= Kc reads zeros.
-template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU>
+// F8 = 0: bf16 operands, v_mfma_f32_16x16x32_bf16 (two per 64-deep K tile).
+// F8 = 1 / 2: fp8 operands -- A e4m3 / e5m2 (activations / gradients), B e4m3 (weights) --
+// one v_mfma_scale_f32_16x16x128_f8f6f4 per 128-deep K tile.  The LDS image is byte-for-byte
+// the bf16 one ([rows][128 B], 16-B chunks, same swizzle), so per K tile the staging, LDS
+// traffic and MFMA cycles are unchanged while the tile carries twice the MACs.  Dequant:
+// per-source power-of-two scales as the MFMA's E8M0 scale operands (csrc/fp8.hip).
+template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU, int F8>
 __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs a) {
+  using T = typename std::conditional<F8 != 0, uint8_t, bf16>::type;
+  constexpr int EPC = 16 / (int)sizeof(T);  // elements per 16-B chunk
+  constexpr int BKE = 8 * EPC;              // K elements per tile (128 B per row)
   constexpr int NT = WM * WN * 64;
   constexpr int TM = BM / WM / 16;
   constexpr int TN = BN / WN / 16;
@@ -42,8 +73,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
   constexpr int LOADS = AROWS + BROWS;   // glds instructions per thread per tile
   static_assert(BM % RPP == 0 && BN % RPP == 0, "every wave issues the same glds count");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* As = reinterpret_cast<bf16*>(smem);
-  bf16* Bs = As + STAGES * BM * BK;
+  T* As = reinterpret_cast<T*>(smem);
+  T* Bs = As + STAGES * BM * BKE;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -57,17 +88,21 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
   const int m0 = mt * BM, n0 = nt * BN;
   if (m0 >= g.Mc) return;
 
-  const int ktiles = (g.Kc + BK - 1) / BK;
+  const int ktiles = (g.Kc + BKE - 1) / BKE;
   const int kps = (ktiles + a.splits - 1) / a.splits;
   const int kt0 = split * kps;
   const int kt1 = min(ktiles, kt0 + kps);
   if (kt0 >= kt1 && a.splits > 1) return;
 
-  const bf16* __restrict__ x1 = static_cast<const bf16*>(a.x1);
-  const bf16* __restrict__ x2 = static_cast<const bf16*>(a.x2);
-  const bf16* __restrict__ w = static_cast<const bf16*>(a.w);
-  const bf16* zero = static_cast<const bf16*>(a.zero);
+  const T* __restrict__ x1 = static_cast<const T*>(a.x1);
+  const T* __restrict__ x2 = static_cast<const T*>(a.x2);
+  const T* __restrict__ w = static_cast<const T*>(a.w);
+  const T* zero = static_cast<const T*>(a.zero);
   const int C = a.C, C1 = a.C1, C2 = a.C2;
+  // fp8: E8M0 dequant exponents of the two A sources and of the weights (fp8 scale sites)
+  const int ex1 = (F8 && a.qs_x1) ? a.qs_x1[2] : 127;
+  const int ex2 = (F8 && a.qs_x2) ? a.qs_x2[2] : 127;
+  const int ew = (F8 && a.qs_w) ? a.qs_w[2] : 127;
   const int slot = lane & 7;
   const int rsub = lane >> 3;            // row within this wave's 8-row glds group
   const int ush = a.up == 2 ? 1 : 0;
@@ -95,7 +130,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
       r_x[i] = qx + g.dx;
     }
     if (m >= g.Mc) r_y[i] = -(1 << 28);
-    r_c[i] = (slot ^ ((row >> 1) & 7)) * 8;   // source-side swizzle
+    r_c[i] = (slot ^ ((row >> 1) & 7)) * EPC;   // source-side swizzle
   }
   int b_off[BROWS];
   bool b_ok[BROWS];
@@ -105,14 +140,14 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
     const int row = wid * 8 + rsub + RPP * i;
     const int co = n0 + row;
     b_ok[i] = co < a.Cout;
-    b_off[i] = (slot ^ ((row >> 1) & 7)) * 8;
+    b_off[i] = (slot ^ ((row >> 1) & 7)) * EPC;
   }
   const FastDiv fd_c = make_fastdiv((uint32_t)C), fd_ti = make_fastdiv((uint32_t)g.Ti);
   // FASTK A-row pointers of the current channel segment (one tap x one source tensor):
   // formed once per segment, then advanced by BK per k-tile (out-of-image rows walk the
   // zero page, which covers a whole segment: host guarantees C1, C2 <= 1024).
-  const bf16* a_ptr[AROWS];
-  const bf16* b_base[BROWS];
+  const T* a_ptr[AROWS];
+  const T* b_base[BROWS];
 #pragma unroll
   for (int i = 0; i < BROWS; ++i) {
     const int co = n0 + wid * 8 + rsub + RPP * i;
@@ -120,9 +155,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
   }
 
   auto issue = [&](int kt, int stage) {
-    const int k0 = kt * BK;
-    bf16* Ast = As + stage * BM * BK;
-    bf16* Bst = Bs + stage * BN * BK;
+    const int k0 = kt * BKE;
+    T* Ast = As + stage * BM * BKE;
+    T* Bst = Bs + stage * BN * BKE;
     if constexpr (FASTK) {
       const int tap = (int)fdiv((uint32_t)k0, fd_c);
       const int ci0 = k0 - tap * C;
@@ -130,7 +165,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
       const int t_x = tap - t_y * g.Ti;
       if (kt == kt0 || ci0 == 0 || ci0 == C1) {
         const bool s1 = ci0 < C1;
-        const bf16* src = s1 ? x1 : x2;
+        const T* src = s1 ? x1 : x2;
         const int cs = s1 ? C1 : C2;
         const int cio = s1 ? ci0 : ci0 - C1;
 #pragma unroll
@@ -156,10 +191,10 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
         }
       } else {
 #pragma unroll
-        for (int i = 0; i < AROWS; ++i) a_ptr[i] += BK;
+        for (int i = 0; i < AROWS; ++i) a_ptr[i] += BKE;
       }
 #pragma unroll
-      for (int i = 0; i < AROWS; ++i) glds16(a_ptr[i], Ast + (wid * 8 + RPP * i) * BK);
+      for (int i = 0; i < AROWS; ++i) glds16(a_ptr[i], Ast + (wid * 8 + RPP * i) * BKE);
       long woff;
       if (MODE == 0) {
         woff = k0;
@@ -169,8 +204,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
       }
 #pragma unroll
       for (int i = 0; i < BROWS; ++i) {
-        const bf16* gp = b_ok[i] ? b_base[i] + woff : zero;
-        glds16(gp, Bst + (wid * 8 + RPP * i) * BK);
+        const T* gp = b_ok[i] ? b_base[i] + woff : zero;
+        glds16(gp, Bst + (wid * 8 + RPP * i) * BKE);
       }
     } else {
 #pragma unroll
@@ -181,7 +216,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
         const int t_y = (int)fdiv((uint32_t)tap, fd_ti);
         const int t_x = tap - t_y * g.Ti;
         const bool s1 = ci < C1;
-        const bf16* src = s1 ? x1 : x2;
+        const T* src = s1 ? x1 : x2;
         const int cs = s1 ? C1 : C2;
         const int cio = s1 ? ci : ci - C1;
         int iy, ix;
@@ -202,8 +237,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
         }
         inb = inb && k < g.Kc;
         const long off = (long)(r_img[i] + iy * a.W + ix) * cs + cio;
-        const bf16* gp = inb ? src + off : zero;
-        glds16(gp, Ast + (wid * 8 + RPP * i) * BK);
+        const T* gp = inb ? src + off : zero;
+        glds16(gp, Ast + (wid * 8 + RPP * i) * BKE);
       }
 #pragma unroll
       for (int i = 0; i < BROWS; ++i) {
@@ -220,8 +255,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
           const int ky = g.ky0 + a.stride * t_y, kx = g.kx0 + a.stride * t_x;
           woff = (long)(ky * a.KW + kx) * C + ci;
         }
-        const bf16* gp = (b_ok[i] && k < g.Kc) ? w + co * wrow + woff : zero;
-        glds16(gp, Bst + (wid * 8 + RPP * i) * BK);
+        const T* gp = (b_ok[i] && k < g.Kc) ? w + co * wrow + woff : zero;
+        glds16(gp, Bst + (wid * 8 + RPP * i) * BKE);
       }
     }
   };
@@ -249,6 +284,46 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
       if (ns >= STAGES) ns -= STAGES;
       issue(kt + STAGES - 1, ns);
     }
+    if constexpr (F8 != 0) {
+      const T* A = As + stage * BM * BKE;
+      const T* B = Bs + stage * BN * BKE;
+      // this lane's 32-deep k block comes from one source tensor (host: C1 % 32 == 0):
+      // its E8M0 dequant exponent is the MFMA's scale_a
+      int sa = ex1;
+      if (C2 > 0) {
+        const int k = FASTK ? kt * BKE : kt * BKE + 32 * (lane >> 4);
+        const int tap = (int)fdiv((uint32_t)k, fd_c);
+        sa = (k - tap * C) < C1 ? ex1 : ex2;
+      }
+      // operand layout of the 16x16x128 f8 MFMA: lane group q = lane>>4 holds K [16q, 16q+16)
+      // in its low 16 bytes and K [64+16q, 64+16q+16) in its high 16 bytes (LDS chunks q and
+      // q+4), and its scale operand covers K block [32q, 32q+32) -- probes/mfma_fp8_scale.hip
+      const int c0 = lane >> 4;
+      i32x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * TM * 16 + i * 16 + (lane & 15);
+        u32x4 lo = *reinterpret_cast<const u32x4*>(A + 2 * swz(row, c0));
+        u32x4 hi = *reinterpret_cast<const u32x4*>(A + 2 * swz(row, c0 + 4));
+        if constexpr (RELU) {
+          lo = relu_fp8x16(lo);
+          hi = relu_fp8x16(hi);
+        }
+        af[i] = cat8(lo, hi);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * TN * 16 + j * 16 + (lane & 15);
+        bfr[j] = cat8(*reinterpret_cast<const u32x4*>(B + 2 * swz(row, c0)),
+                      *reinterpret_cast<const u32x4*>(B + 2 * swz(row, c0 + 4)));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], F8 - 1, 0, 0, sa,
+                                                                       0, ew);
+    } else {
     const bf16* A = As + stage * BM * BK;
     const bf16* B = Bs + stage * BN * BK;
     // fragments of both 32-deep halves are read up front (double-buffered registers) so
@@ -281,13 +356,14 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
     }
+    }
     stage = stage + 1 == STAGES ? 0 : stage + 1;
   }
   __syncthreads();  // every wave done with the ring before the epilogue reuses the LDS
   conv_epilogue<BM, BN, WM, WN, MODE, NT>(a, g, acc, m0, n0, smem, fd_hwq, fd_wq);
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU>
+template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU, int F8>
 static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int pipe = STAGES * (BM + BN) * BK * 2;
   constexpr int epi = BM * (BN + 8) * 2 + 2 * (WM * WN * 64) * 4;  // + stats scratch
@@ -295,7 +371,7 @@ static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU>),
+        reinterpret_cast<const void*>(&conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU, F8>),
         hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
@@ -314,37 +390,59 @@ static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   const long mtiles = (mmax + BM - 1) / BM;
   const long ntiles = (a.Cout + BN - 1) / BN;
   dim3 grid((unsigned)(mtiles * ntiles), 1, (unsigned)(classes * a.splits));
-  hipLaunchKernelGGL((conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU>), grid, dim3(WM * WN * 64), smem,
+  hipLaunchKernelGGL((conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU, F8>), grid, dim3(WM * WN * 64), smem,
                      st, a);
   return (int)hipGetLastError();
 }
 
-template <int MODE, bool FASTK, bool RELU>
+template <int MODE, bool FASTK, bool RELU, int F8>
 static int dispatch_glds2(const ConvFwdArgs& a, int variant, hipStream_t st) {
+  if constexpr (F8 != 0) {
+    // fp8: the bf16 winners only (256x256 / 256x128 for wide layers, 128x64 below)
+    if (a.Cout > 128 && variant == 5) return launch_glds<256, 256, 2, 4, MODE, 2, FASTK, RELU, F8>(a, st);
+    if (a.Cout > 64) {
+      if (variant == 2) return launch_glds<128, 128, 2, 2, MODE, 2, FASTK, RELU, F8>(a, st);
+      return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU, F8>(a, st);
+    }
+    if (a.Cout > 32) return launch_glds<128, 64, 2, 2, MODE, 2, FASTK, RELU, F8>(a, st);
+    return -2;
+  } else {
   // variant: 2 = 2-stage 128-row tile, 3 = 3-stage 128-row tile, 4 = 3-stage 256x128 8 waves,
   // 5 = 2-stage 256x256 (8 waves of 128x64: half the LDS fragment traffic per MFMA of 4),
   // 6 = 2-stage 256x64 on 4 waves of 64x64 (N <= 64 layers)
-  if (a.Cout > 128 && variant == 5) return launch_glds<256, 256, 2, 4, MODE, 2, FASTK, RELU>(a, st);
+  if (a.Cout > 128 && variant == 5) return launch_glds<256, 256, 2, 4, MODE, 2, FASTK, RELU, F8>(a, st);
   if (a.Cout > 64) {
-    if (variant == 5) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU>(a, st);
-    if (variant == 2) return launch_glds<128, 128, 2, 2, MODE, 2, FASTK, RELU>(a, st);
-    if (variant == 3) return launch_glds<128, 128, 2, 2, MODE, 3, FASTK, RELU>(a, st);
-    if (variant == 4) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU>(a, st);
+    if (variant == 5) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU, F8>(a, st);
+    if (variant == 2) return launch_glds<128, 128, 2, 2, MODE, 2, FASTK, RELU, F8>(a, st);
+    if (variant == 3) return launch_glds<128, 128, 2, 2, MODE, 3, FASTK, RELU, F8>(a, st);
+    if (variant == 4) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU, F8>(a, st);
   } else if (a.Cout > 32) {
-    if (variant == 6) return launch_glds<256, 64, 4, 1, MODE, 2, FASTK, RELU>(a, st);
-    if (variant == 2) return launch_glds<128, 64, 2, 2, MODE, 2, FASTK, RELU>(a, st);
-    if (variant == 3) return launch_glds<128, 64, 2, 2, MODE, 3, FASTK, RELU>(a, st);
-    if (variant == 4) return launch_glds<256, 64, 4, 2, MODE, 3, FASTK, RELU>(a, st);
+    if (variant == 6) return launch_glds<256, 64, 4, 1, MODE, 2, FASTK, RELU, F8>(a, st);
+    if (variant == 2) return launch_glds<128, 64, 2, 2, MODE, 2, FASTK, RELU, F8>(a, st);
+    if (variant == 3) return launch_glds<128, 64, 2, 2, MODE, 3, FASTK, RELU, F8>(a, st);
+    if (variant == 4) return launch_glds<256, 64, 4, 2, MODE, 3, FASTK, RELU, F8>(a, st);
   }
   return -2;
+  }
 }
 
-template <int MODE>
+template <int MODE, int F8>
 static int dispatch_glds(const ConvFwdArgs& a, int variant, hipStream_t st) {
-  const bool fastk = a.C1 % BK == 0 && a.C2 % BK == 0;
-  if (a.act_in == ACT_RELU)
-    return fastk ? dispatch_glds2<MODE, true, true>(a, variant, st) : dispatch_glds2<MODE, false, true>(a, variant, st);
-  return fastk ? dispatch_glds2<MODE, true, false>(a, variant, st) : dispatch_glds2<MODE, false, false>(a, variant, st);
+  constexpr int BKE = F8 ? 2 * BK : BK;
+  const bool fastk = a.C1 % BKE == 0 && a.C2 % BKE == 0;
+  if (a.act_in == ACT_RELU) {
+    if constexpr (F8 == 2) return -2;  // gradients (e5m2) never carry an input activation
+    else
+      return fastk ? dispatch_glds2<MODE, true, true, F8>(a, variant, st)
+                   : dispatch_glds2<MODE, false, true, F8>(a, variant, st);
+  }
+  return fastk ? dispatch_glds2<MODE, true, false, F8>(a, variant, st)
+               : dispatch_glds2<MODE, false, false, F8>(a, variant, st);
+}
+
+template <int F8>
+static int dispatch_mode(const ConvFwdArgs& a, int mode, int variant, hipStream_t st) {
+  return mode == 0 ? dispatch_glds<0, F8>(a, variant, st) : dispatch_glds<1, F8>(a, variant, st);
 }
 
 }  // namespace p2p
@@ -353,5 +451,10 @@ extern "C" int p2p_conv_fwd_glds(const p2p::ConvFwdArgs* a, int mode, int varian
   if (!a->zero) return -2;
   if (a->C1 > 1024 || a->C2 > 1024) return -2;  // zero-page walk bound (see a_ptr)
   if (a->act_in != p2p::ACT_NONE && a->act_in != p2p::ACT_RELU) return -2;
-  return mode == 0 ? p2p::dispatch_glds<0>(*a, variant, st) : p2p::dispatch_glds<1>(*a, variant, st);
+  if (a->fp8 == 0) return p2p::dispatch_mode<0>(*a, mode, variant, st);
+  // fp8: every 32-deep k block of a lane inside one source tensor and one tap
+  if (a->C1 % 32 || a->C2 % 32 || a->splits > 1 && a->ws == nullptr) return -2;
+  if (a->fp8 == 1) return p2p::dispatch_mode<1>(*a, mode, variant, st);
+  if (a->fp8 == 2) return p2p::dispatch_mode<2>(*a, mode, variant, st);
+  return -2;
 }

@@ -1,0 +1,142 @@
+"""FP8 conv path (BASELINE config 5: "256x256 pix2pix with fp8 conv MFMA path").
+
+Recipe (MI355X-first, see ``csrc/fp8.hip``):
+
+* conv forward:  x in OCP e4m3 x weight e4m3 -> bf16 output (bias / act / norm stats fused
+  as on the bf16 path);
+* conv dgrad:    dY in e5m2 (gradient range) x weight e4m3 -> bf16 dX;
+* conv wgrad:    stays bf16 (it reads the saved bf16 activations, so no fp8 copy has to
+  live until backward);
+* first / last layers stay bf16: their channel counts (3 / 6-channel images, 1-channel
+  PatchGAN logits) are below the fp8 kernel's 32-channel granularity, which is also the
+  usual "keep the image-facing layers in high precision" rule for GANs.
+
+Every fp8 tensor carries a per-tensor *power-of-two* scale, so dequantisation is an E8M0
+exponent handed to the MFMA's own block-scale operands -- free in the matrix core, and the
+two halves of a U-Net skip concat keep independent scales.  Scales live on the device in
+"sites" (4 int32 words: amax_ref, amax_cur, e8m0, amax_last):
+
+* activations / gradients: *delayed* scaling -- quantised with the amax of the previous two
+  steps (``fp8_roll`` shifts the window once per step, one launch for the whole pool); a
+  site's first use measures the tensor itself (bootstrap);
+* weights: *current* scaling -- exact amax of this step's weight image, then the cast.
+
+Sites are keyed by (consumer weight, operand role), so they are stable across steps and the
+whole step stays capturable in one hipGraph (no host sync anywhere).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .. import _native
+
+E4M3, E5M2 = 0, 1
+_POOL_SITES = 4096
+
+_precision = [os.environ.get("P2P_PRECISION", "bf16").lower()]
+if _precision[0] not in ("bf16", "fp8"):
+    raise ValueError(f"P2P_PRECISION must be 'bf16' or 'fp8', got {_precision[0]!r}")
+
+
+def set_precision(name: str) -> None:
+    """Conv GEMM operand precision on the HIP path: 'bf16' (default) or 'fp8'."""
+    name = name.lower()
+    if name not in ("bf16", "fp8"):
+        raise ValueError(name)
+    _precision[0] = name
+
+
+def get_precision() -> str:
+    return _precision[0]
+
+
+def enabled() -> bool:
+    return _precision[0] == "fp8"
+
+
+class _Pool:
+    def __init__(self, device):
+        self.sites = torch.zeros(_POOL_SITES, 4, dtype=torch.int32, device=device)
+        self.index: dict = {}
+        self.fresh: set = set()
+
+    def site(self, key):
+        i = self.index.get(key)
+        if i is None:
+            i = len(self.index)
+            if i >= _POOL_SITES:
+                raise RuntimeError("fp8: scale-site pool exhausted")
+            self.index[key] = i
+            self.fresh.add(i)
+        return i
+
+
+_pools: dict = {}
+# per-step cache of quantised activations: (ptr, shape, version, site) -> (x, q)
+_qcache: dict = {}
+
+
+def _pool(device) -> _Pool:
+    p = _pools.get(device)
+    if p is None:
+        p = _Pool(device)
+        _pools[device] = p
+    return p
+
+
+def site_tensor(device, key) -> torch.Tensor:
+    p = _pool(device)
+    return p.sites[p.site(key)]
+
+
+def begin_step() -> None:
+    """Shift every delayed-scaling window (one launch per device) and drop the per-step
+    quantisation cache."""
+    _qcache.clear()
+    P = _native.ops()
+    for p in _pools.values():
+        if p.index:
+            P.fp8_roll(p.sites[: len(p.index)])
+
+
+def quant(x: torch.Tensor, key, fmt: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """Delayed-scaled fp8 copy of the bf16 NHWC tensor ``x`` (site ``key``); returns (q, site).
+    The same tensor quantised twice for the same site in one step is reused."""
+    P = _native.ops()
+    pool = _pool(x.device)
+    i = pool.site(key)
+    site = pool.sites[i]
+    ck = (x.data_ptr(), tuple(x.shape), x._version, i)
+    ent = _qcache.get(ck)
+    if ent is not None:
+        return ent[1], site
+    if i in pool.fresh:
+        # bootstrap: the first quantisation of a site measures the tensor itself
+        pool.fresh.discard(i)
+        site[0].zero_()
+        P.fp8_amax(x, site, 0)
+    q = P.fp8_quant(x, site, fmt, 0)
+    _qcache[ck] = (x, q)   # the entry holds x: its address cannot be recycled this step
+    return q, site
+
+
+def quant_weight(img: torch.Tensor, key) -> tuple[torch.Tensor, torch.Tensor]:
+    """Current-scaled e4m3 copy of a bf16 weight image: exact amax, then the cast."""
+    P = _native.ops()
+    pool = _pool(img.device)
+    i = pool.site(key)
+    pool.fresh.discard(i)
+    site = pool.sites[i]
+    site[0].zero_()
+    P.fp8_amax(img, site, 0)
+    return P.fp8_quant(img, site, E4M3, 0), site
+
+
+def conv_ok(C1: int, C2: int, Cout: int, act_in: int) -> bool:
+    """Geometries the fp8 kernels take: the LDS-DMA conv with every 32-deep k block inside
+    one source tensor, N tile >= 64, input activation none / ReLU."""
+    if os.environ.get("P2P_CONV_VARIANT", "").startswith("v"):
+        return False
+    return Cout > 32 and C1 % 32 == 0 and C2 % 32 == 0 and act_in in (0, 1) and C1 <= 1024 and C2 <= 1024

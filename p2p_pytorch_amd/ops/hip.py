@@ -29,6 +29,7 @@ import itertools
 import torch
 
 from .. import _native
+from . import fp8 as _f8
 
 ACT = {None: 0, "none": 0, "relu": 1, "lrelu": 2, "tanh": 3, "sigmoid": 4}
 CL = torch.channels_last
@@ -47,6 +48,8 @@ def begin_step():
     _gen[0] += 1
     _colsum_stash.clear()
     _stats_stash.clear()
+    if _f8._pools:
+        _f8.begin_step()
 
 
 # Bias gradients handed from the norm backward to the producing conv: for a conv feeding a
@@ -116,6 +119,40 @@ def _weight_image(w: torch.Tensor, swap: int, xp: int, yp: int, scale=None) -> t
     img = P().weight_prep(w.detach().contiguous().float(), swap, xp, yp, scale)
     cache[key] = (ver, _gen[0], img)
     return img
+
+
+def _weight_image_fp8(w: torch.Tensor, swap: int, xp: int, yp: int):
+    """e4m3 copy (current scaling) of the bf16 GEMM-operand image, cached like the bf16 one;
+    returns (image, scale site)."""
+    cache = getattr(w, "_p2p_cache", None)
+    key = (swap, xp, yp, "fp8")
+    ver = w._version
+    ent = cache.get(key) if cache is not None else None
+    if ent is not None and ent[0] == ver and ent[1] == _gen[0]:
+        return ent[2]
+    img = _weight_image(w, swap, xp, yp)
+    out = _f8.quant_weight(img, (id(w), "w", swap))
+    w._p2p_cache[key] = (ver, _gen[0], out)
+    return out
+
+
+def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout, act_out,
+               Csplit, xb1, xb2, act_bwd, Cvalid, want, weight=None, swap=0, xp=0, yp=0, role="x"):
+    """conv_fwd on bf16 operands, or -- fp8 precision and a geometry the fp8 kernel takes --
+    on fp8 ones: x (role 'x': activations, e4m3; 'gy': gradients, e5m2) quantised with
+    delayed scaling, the weight image with current scaling."""
+    C1 = x1.shape[1]
+    C2 = 0 if x2 is None else x2.shape[1]
+    if weight is not None and _f8.enabled() and _f8.conv_ok(C1, C2, Cout, act_in):
+        fmt = _f8.E5M2 if role == "gy" else _f8.E4M3
+        w8, sw = _weight_image_fp8(weight, swap, xp, yp)
+        k = id(weight)
+        a1, s1 = _f8.quant(x1, (k, role, 1), fmt)
+        a2, s2 = _f8.quant(x2, (k, role, 2), fmt) if x2 is not None else (None, None)
+        return P().conv_fwd(a1, a2, w8, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout,
+                            act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, s1, s2, sw)
+    return P().conv_fwd(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout,
+                        act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want)
 
 
 def prepare_weights(*modules):
@@ -247,9 +284,10 @@ class ConvFn(torch.autograd.Function):
         Coutp = _pad8(Cout)
         wimg = _weight_image(weight, swap, Coutp, Cp)
         want = bool(cfg.stats) and Coutp == Cout
-        outs = P().conv_fwd(q1, q2, wimg, _bias_padded(bias, Coutp), mode, KH, KW, s, p,
-                            int(cfg.reflect), cfg.up, _act_code(cfg.act_in), OH, OW, Coutp,
-                            _act_code(cfg.act_out), Coutp, None, None, 0, Cout, want)
+        outs = _conv_call(q1, q2, wimg, _bias_padded(bias, Coutp), mode, KH, KW, s, p,
+                          int(cfg.reflect), cfg.up, _act_code(cfg.act_in), OH, OW, Coutp,
+                          _act_code(cfg.act_out), Coutp, None, None, 0, Cout, want,
+                          weight, swap, Coutp, Cp)
         y = outs[0]
         if want and len(outs) == 2:
             _stash_stats(y, outs[1])
@@ -289,20 +327,22 @@ class ConvFn(torch.autograd.Function):
                     raise NotImplementedError("virtual concat with reflect/upsample gather")
                 Hp, Wp = H * cfg.up + 2 * p, W * cfg.up + 2 * p
                 wimg = _weight_image(weight, 1, Cp, Coutp)
-                dxp = P().conv_fwd(gyp, None, wimg, None, 1, KH, KW, s, 0, 0, 1, 0, Hp, Wp, Cp,
-                                   0, Cp, None, None, 0, C1)[0]
+                dxp = _conv_call(gyp, None, wimg, None, 1, KH, KW, s, 0, 0, 1, 0, Hp, Wp, Cp,
+                                 0, Cp, None, None, 0, C1, False, weight, 1, Cp, Coutp, "gy")[0]
                 outs = [P().pad_fold(dxp, H, W, p, cfg.up, int(cfg.reflect),
                                      q1 if act_in else None, act_in)]
             elif cfg.transposed:
                 wimg = _weight_image(weight, 0, Cp, Coutp)
-                outs = P().conv_fwd(gyp, None, wimg, None, 0, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
-                                    split, q1 if act_in else None,
-                                    q2 if (act_in and q2 is not None) else None, act_in, C1 + C2)
+                outs = _conv_call(gyp, None, wimg, None, 0, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
+                                  split, q1 if act_in else None,
+                                  q2 if (act_in and q2 is not None) else None, act_in, C1 + C2,
+                                  False, weight, 0, Cp, Coutp, "gy")
             else:
                 wimg = _weight_image(weight, 1, Cp, Coutp)
-                outs = P().conv_fwd(gyp, None, wimg, None, 1, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
-                                    split, q1 if act_in else None,
-                                    q2 if (act_in and q2 is not None) else None, act_in, C1 + C2)
+                outs = _conv_call(gyp, None, wimg, None, 1, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
+                                  split, q1 if act_in else None,
+                                  q2 if (act_in and q2 is not None) else None, act_in, C1 + C2,
+                                  False, weight, 1, Cp, Coutp, "gy")
             if q2 is not None:
                 gx1, gx2 = outs[0], outs[1]
             elif packed:
