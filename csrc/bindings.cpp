@@ -24,17 +24,18 @@ long p2p_norm_ws_floats(int N, int HW, int C);
 int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, const float* partials,
                           float eps, const float* gamma, const float* beta, const float* prelu_w,
                           int act, float* mean, float* rstd, float* run_mean, float* run_var,
-                          float momentum, void* y, hipStream_t st);
+                          float momentum, void* y, void* q, int* qsite, int qfmt, hipStream_t st);
 int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* gamma,
                  const float* beta, const float* prelu_w, int act, float* mean, float* rstd,
                  float* run_mean, float* run_var, float momentum, float* ws, void* y,
-                 hipStream_t st);
+                 void* q, int* qsite, int qfmt, hipStream_t st);
 int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const float* rstd,
                    const float* gamma, const float* beta, const float* prelu_w, int act, void* y,
                    hipStream_t st);
 int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const float* mean,
                  const float* rstd, const float* gamma, const float* beta, int act, float* dgamma,
-                 float* dbeta, float* ws, void* dx, float* dsum, hipStream_t st);
+                 float* dbeta, float* ws, void* dx, float* dsum, void* q, int* qsite, int qfmt,
+                 hipStream_t st);
 int p2p_act(const void* a, const void* b, long n, int act, int mode, void* out, hipStream_t st);
 int p2p_dropout(const void* x, long n, float p, const int64_t* seed, unsigned salt, void* y,
                 hipStream_t st);
@@ -52,7 +53,7 @@ int p2p_pixel_shuffle(const void* in, int N, int OH, int OW, int OC, int r, int 
                       hipStream_t st);
 int p2p_weight_prep_pairs(int count, const float* const* w, void* const* out0, void* const* out1,
                           const int* A, const int* B, const int* T, const int* Xa, const int* Xb,
-                          hipStream_t st);
+                          int* const* site, hipStream_t st);
 int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, int reflect,
                  const void* xb, int act, void* dx, hipStream_t st);
 int p2p_pad_channels(const void* a, int Ca, const void* b, int Cb, long P, int Co, void* out,
@@ -128,6 +129,11 @@ int conv_variant(int64_t Cout, int64_t kmax, int64_t tiles256 = 0) {
   return (big && tiles256 >= 256) ? 5 : v4;
 }
 
+void check_site(const Tensor& site) {
+  TORCH_CHECK(site.is_cuda() && site.scalar_type() == at::kInt && site.numel() >= 4 && site.is_contiguous(),
+              "fp8: a scale site is a contiguous int32 GPU tensor of 4 words");
+}
+
 Tensor empty_nhwc(int64_t N, int64_t C, int64_t H, int64_t W, const Tensor& like) {
   return at::empty({N, C, H, W}, like.options().memory_format(at::MemoryFormat::ChannelsLast));
 }
@@ -140,7 +146,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                              int64_t Csplit, const optional<Tensor>& xb1,
                              const optional<Tensor>& xb2, int64_t act_bwd, int64_t Cvalid,
                              bool want_stats, const optional<Tensor>& qs_x1,
-                             const optional<Tensor>& qs_x2, const optional<Tensor>& qs_w) {
+                             const optional<Tensor>& qs_x2, const optional<Tensor>& qs_w,
+                             const optional<Tensor>& y_qsite, int64_t y_qfmt) {
   check_act(x1, "conv_fwd x1", true);
   // fp8 operands: x e4m3 (activations) or e5m2 (gradients), weight image e4m3, each with
   // an fp8 scale site (csrc/fp8.hip); outputs stay bf16
@@ -221,6 +228,9 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   a.qs_x1 = fp8 ? qs_x1->data_ptr<int>() : nullptr;
   a.qs_x2 = (fp8 && x2) ? qs_x2->data_ptr<int>() : nullptr;
   a.qs_w = fp8 ? qs_w->data_ptr<int>() : nullptr;
+  a.q_out = nullptr;
+  a.q_site = nullptr;
+  a.q_fmt = 0;
 
   hipStream_t st = cur_stream(x1);
   // ---- tiny-Cout "col" path: dense GEMM over the input pixels (N = taps x Cvalid) + col2im
@@ -336,6 +346,16 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       a.stats_nchunks = (int)nch;
     }
   }
+  // fp8 shadow of y (the next conv's operand) from the epilogue: plain single-output GEMMs
+  Tensor yq;
+  if (y_qsite && splits == 1 && Csplit == Cout && !act_bwd) {
+    check_site(*y_qsite);
+    yq = at::empty_like(y1, y1.options().dtype(y_qfmt == 0 ? at::kFloat8_e4m3fn : at::kFloat8_e5m2),
+                        at::MemoryFormat::ChannelsLast);
+    a.q_out = yq.data_ptr();
+    a.q_site = y_qsite->data_ptr<int>();
+    a.q_fmt = (int)y_qfmt;
+  }
   int rc = -2;
   if (glds_ok) rc = p2p_conv_fwd_glds(&a, (int)mode, variant, st);
   if (rc == -2 && a.stats) {  // glds refused after all: no fused statistics
@@ -358,6 +378,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   std::vector<Tensor> out{y1};
   if (y2.defined()) out.push_back(y2);
   if (stats.defined()) out.push_back(stats);
+  if (yq.defined()) out.push_back(yq);   // always last (fp8 dtype)
   return out;
 }
 
@@ -457,9 +478,19 @@ Tensor weight_prep(const Tensor& w, int64_t swap, int64_t Xp, int64_t Yp,
 
 // all weight images of a network in one launch per WP_MAX tensors
 // both images of each weight (T <= 16) in one launch: returns [out0_0, out1_0, out0_1, ...]
-std::vector<Tensor> weight_prep_pairs(at::TensorList ws, at::IntArrayRef xa, at::IntArrayRef xb) {
+// sites (optional): e4m3 images instead of bf16, scaled by the current-scaling site
+// sites[site_idx[i]] (int32 [n][4], amax in word 0 -- csrc/fp8.hip)
+std::vector<Tensor> weight_prep_pairs(at::TensorList ws, at::IntArrayRef xa, at::IntArrayRef xb,
+                                      const optional<Tensor>& sites, at::OptionalIntArrayRef site_idx) {
   const size_t n = ws.size();
   TORCH_CHECK(xa.size() == n && xb.size() == n, "weight_prep_pairs: list sizes");
+  const bool f8 = sites.has_value();
+  if (f8)
+    TORCH_CHECK(site_idx.has_value() && site_idx->size() == n && sites->scalar_type() == at::kInt &&
+                    sites->dim() == 2 && sites->size(1) == 4 && sites->is_contiguous(),
+                "weight_prep_pairs: fp8 sites");
+  const auto odt = f8 ? at::kFloat8_e4m3fn : at::kBFloat16;
+  std::vector<int*> S;
   std::vector<Tensor> outs;
   outs.reserve(2 * n);
   std::vector<const float*> W;
@@ -468,9 +499,10 @@ std::vector<Tensor> weight_prep_pairs(at::TensorList ws, at::IntArrayRef xa, at:
   auto flush = [&]() {
     if (W.empty()) return;
     check_rc(p2p_weight_prep_pairs((int)W.size(), W.data(), O0.data(), O1.data(), A.data(), B.data(),
-                                   T.data(), XA.data(), XB.data(), cur_stream(ws[0])),
+                                   T.data(), XA.data(), XB.data(), f8 ? S.data() : nullptr,
+                                   cur_stream(ws[0])),
              "weight_prep_pairs");
-    W.clear(); O0.clear(); O1.clear(); A.clear(); B.clear(); T.clear(); XA.clear(); XB.clear();
+    W.clear(); O0.clear(); O1.clear(); A.clear(); B.clear(); T.clear(); XA.clear(); XB.clear(); S.clear();
   };
   for (size_t i = 0; i < n; ++i) {
     const Tensor& w = ws[i];
@@ -479,8 +511,13 @@ std::vector<Tensor> weight_prep_pairs(at::TensorList ws, at::IntArrayRef xa, at:
     const int64_t a = w.size(0), b = w.size(1), kh = w.size(2), kw = w.size(3);
     TORCH_CHECK(kh * kw <= 16 && xa[i] >= a && xb[i] >= b && xa[i] % 2 == 0 && xb[i] % 2 == 0,
                 "weight_prep_pairs: T <= 16, even padded sizes");
-    Tensor o0 = at::empty({xa[i], kh, kw, xb[i]}, w.options().dtype(at::kBFloat16));
-    Tensor o1 = at::empty({xb[i], kh, kw, xa[i]}, w.options().dtype(at::kBFloat16));
+    Tensor o0 = at::empty({xa[i], kh, kw, xb[i]}, w.options().dtype(odt));
+    Tensor o1 = at::empty({xb[i], kh, kw, xa[i]}, w.options().dtype(odt));
+    if (f8) {
+      const int64_t si = (*site_idx)[i];
+      TORCH_CHECK(si >= 0 && si < sites->size(0), "weight_prep_pairs: site index");
+      S.push_back(sites->data_ptr<int>() + 4 * si);
+    }
     outs.push_back(o0);
     outs.push_back(o1);
     W.push_back(w.data_ptr<float>());
@@ -542,8 +579,20 @@ std::vector<Tensor> norm_fwd(const Tensor& x, double eps, const optional<Tensor>
                              const optional<Tensor>& beta, const optional<Tensor>& prelu_w,
                              int64_t act, const optional<Tensor>& run_mean,
                              const optional<Tensor>& run_var, double momentum, bool batch,
-                             const optional<Tensor>& partials) {
+                             const optional<Tensor>& partials, const optional<Tensor>& qsite,
+                             const optional<Tensor>& q_out, int64_t qfmt) {
   check_act(x, "norm_fwd x");
+  // optional fp8 shadow of y written by the apply pass (q_out: same shape, fp8, NHWC)
+  void* qp = nullptr;
+  int* qs = nullptr;
+  if (q_out) {
+    TORCH_CHECK(qsite && q_out->numel() == x.numel() && q_out->element_size() == 1 &&
+                    q_out->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "norm_fwd: fp8 shadow output");
+    check_site(*qsite);
+    qp = q_out->data_ptr();
+    qs = qsite->data_ptr<int>();
+  }
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
   TORCH_CHECK(C <= 2048, "norm_fwd: C > 2048 unsupported");
   const int gN = batch ? 1 : (int)N;
@@ -564,7 +613,7 @@ std::vector<Tensor> norm_fwd(const Tensor& x, double eps, const optional<Tensor>
                                    mean.data_ptr<float>(), rstd.data_ptr<float>(),
                                    run_mean ? run_mean->data_ptr<float>() : nullptr,
                                    run_var ? run_var->data_ptr<float>() : nullptr, (float)momentum,
-                                   y.data_ptr(), cur_stream(x)),
+                                   y.data_ptr(), qp, qs, (int)qfmt, cur_stream(x)),
              "norm_fwd(partials)");
     return {y, mean, rstd};
   }
@@ -577,7 +626,7 @@ std::vector<Tensor> norm_fwd(const Tensor& x, double eps, const optional<Tensor>
                         mean.data_ptr<float>(), rstd.data_ptr<float>(),
                         run_mean ? run_mean->data_ptr<float>() : nullptr,
                         run_var ? run_var->data_ptr<float>() : nullptr, (float)momentum,
-                        ws.data_ptr<float>(), y.data_ptr(), cur_stream(x)),
+                        ws.data_ptr<float>(), y.data_ptr(), qp, qs, (int)qfmt, cur_stream(x)),
            "norm_fwd");
   return {y, mean, rstd};
 }
@@ -603,9 +652,20 @@ Tensor norm_apply(const Tensor& x, const Tensor& mean, const Tensor& rstd,
 Tensor norm_bwd(const Tensor& x, const Tensor& dy, const Tensor& mean, const Tensor& rstd,
                 const optional<Tensor>& gamma, const optional<Tensor>& beta, int64_t act,
                 const optional<Tensor>& dgamma, const optional<Tensor>& dbeta, bool need_dx,
-                bool batch, const optional<Tensor>& dsum) {
+                bool batch, const optional<Tensor>& dsum, const optional<Tensor>& qsite,
+                const optional<Tensor>& q_out, int64_t qfmt) {
   check_act(x, "norm_bwd x");
   check_act(dy, "norm_bwd dy");
+  void* qp = nullptr;
+  int* qs = nullptr;
+  if (q_out && need_dx) {
+    TORCH_CHECK(qsite && q_out->numel() == x.numel() && q_out->element_size() == 1 &&
+                    q_out->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "norm_bwd: fp8 shadow output");
+    check_site(*qsite);
+    qp = q_out->data_ptr();
+    qs = qsite->data_ptr<int>();
+  }
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
   const int gN = batch ? 1 : (int)N;
   const int gHW = batch ? (int)(N * HW) : (int)HW;
@@ -619,7 +679,8 @@ Tensor norm_bwd(const Tensor& x, const Tensor& dy, const Tensor& mean, const Ten
                         dgamma ? dgamma->data_ptr<float>() : nullptr,
                         dbeta ? dbeta->data_ptr<float>() : nullptr, ws.data_ptr<float>(),
                         need_dx ? dx.data_ptr() : nullptr,
-                        (need_dx && dsum) ? dsum->data_ptr<float>() : nullptr, cur_stream(x)),
+                        (need_dx && dsum) ? dsum->data_ptr<float>() : nullptr, qp, qs, (int)qfmt,
+                        cur_stream(x)),
            "norm_bwd");
   return dx;
 }
@@ -822,10 +883,6 @@ Tensor slice_channels(const Tensor& x, int64_t c0, int64_t C) {
 
 // out[c] (+)= scale * sum over all pixels of x[..., c]   (bias gradient)
 // ------------------------------------------------------------------ fp8 (csrc/fp8.hip)
-void check_site(const Tensor& site) {
-  TORCH_CHECK(site.is_cuda() && site.scalar_type() == at::kInt && site.numel() >= 4 && site.is_contiguous(),
-              "fp8: a scale site is a contiguous int32 GPU tensor of 4 words");
-}
 
 Tensor fp8_quant(const Tensor& x, Tensor site, int64_t fmt, int64_t use_cur) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16, "fp8_quant: bf16 input");
@@ -849,6 +906,32 @@ void fp8_amax(const Tensor& x, Tensor site, int64_t slot) {
   check_rc(p2p_fp8_amax(x.data_ptr(), x.scalar_type() == at::kFloat, x.numel(), site.data_ptr<int>(), (int)slot,
                         cur_stream(x)),
            "fp8_amax");
+}
+
+// amax of every fp32 tensor x[i] -> sites[idx[i]][0] (pre-zeroed by the caller)
+void fp8_amax_multi(at::TensorList xs, Tensor sites, at::IntArrayRef idx) {
+  TORCH_CHECK(xs.size() == idx.size(), "fp8_amax_multi: list sizes");
+  TORCH_CHECK(sites.is_cuda() && sites.scalar_type() == at::kInt && sites.is_contiguous() && sites.dim() == 2 &&
+                  sites.size(1) == 4,
+              "fp8_amax_multi: int32 [n][4] pool");
+  constexpr int MAXT = 48;
+  size_t i0 = 0;
+  while (i0 < xs.size()) {
+    const size_t cnt = std::min<size_t>(MAXT, xs.size() - i0);
+    std::vector<const float*> xp(cnt);
+    std::vector<long> n(cnt);
+    std::vector<int*> sp(cnt);
+    for (size_t i = 0; i < cnt; ++i) {
+      const Tensor& t = xs[i0 + i];
+      TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), "fp8_amax_multi: fp32 input");
+      TORCH_CHECK(idx[i0 + i] >= 0 && idx[i0 + i] < sites.size(0), "fp8_amax_multi: site index");
+      xp[i] = t.data_ptr<float>();
+      n[i] = t.numel();
+      sp[i] = sites.data_ptr<int>() + 4 * idx[i0 + i];
+    }
+    check_rc(p2p_fp8_amax_multi((int)cnt, xp.data(), n.data(), sp.data(), cur_stream(sites)), "fp8_amax_multi");
+    i0 += cnt;
+  }
 }
 
 void fp8_roll(Tensor sites) {
@@ -967,10 +1050,11 @@ TORCH_LIBRARY(p2p, m) {
   m.def("conv_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, int mode, int KH, int KW, int stride, "
         "int pad, int reflect, int up, int act_in, int OH, int OW, int Cout, int act_out, int Csplit, "
         "Tensor? xb1, Tensor? xb2, int act_bwd, int Cvalid=0, bool want_stats=False, Tensor? qs_x1=None, "
-        "Tensor? qs_x2=None, Tensor? qs_w=None) -> Tensor[]");
+        "Tensor? qs_x2=None, Tensor? qs_w=None, Tensor(a!)? y_qsite=None, int y_qfmt=0) -> Tensor[]");
   m.def("fp8_quant(Tensor x, Tensor(a!) site, int fmt, int use_cur=0) -> Tensor");
   m.def("fp8_amax(Tensor x, Tensor(a!) site, int slot) -> ()");
   m.def("fp8_roll(Tensor(a!) sites) -> ()");
+  m.def("fp8_amax_multi(Tensor[] x, Tensor(a!) sites, int[] idx) -> ()");
   m.def("fp8_dequant(Tensor q, Tensor site) -> Tensor");
   m.def("conv_wgrad(Tensor p1, Tensor? p2, int p_act, Tensor q1, Tensor? q2, int q_act, int KH, int KW, "
         "int stride, int pad, int reflect, int up, Tensor(a!) dw, float scale, int accumulate, "
@@ -986,14 +1070,16 @@ TORCH_LIBRARY(p2p, m) {
   m.def("l2norm(Tensor x, Tensor? gy, float eps) -> Tensor");
   m.def("pixel_shuffle(Tensor x, int r, int dir) -> Tensor");
   m.def("pad_fold(Tensor dxp, int H, int W, int pad, int up, int reflect, Tensor? xb, int act) -> Tensor");
-  m.def("weight_prep_pairs(Tensor[] w, int[] xa, int[] xb) -> Tensor[]");
+  m.def("weight_prep_pairs(Tensor[] w, int[] xa, int[] xb, Tensor(a!)? sites=None, int[]? site_idx=None) -> Tensor[]");
   m.def("weight_prep_multi(Tensor[] w, int[] swap, int[] xp, int[] yp) -> Tensor[]");
   m.def("norm_fwd(Tensor x, float eps, Tensor? gamma, Tensor? beta, Tensor? prelu_w, int act, "
-        "Tensor(a!)? run_mean, Tensor(b!)? run_var, float momentum, bool batch, Tensor? partials=None) -> Tensor[]");
+        "Tensor(a!)? run_mean, Tensor(b!)? run_var, float momentum, bool batch, Tensor? partials=None, "
+        "Tensor(c!)? qsite=None, Tensor(d!)? q_out=None, int qfmt=0) -> Tensor[]");
   m.def("norm_apply(Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? prelu_w, "
         "int act, bool batch) -> Tensor");
   m.def("norm_bwd(Tensor x, Tensor dy, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, int act, "
-        "Tensor(a!)? dgamma, Tensor(b!)? dbeta, bool need_dx, bool batch, Tensor(c!)? dsum) -> Tensor");
+        "Tensor(a!)? dgamma, Tensor(b!)? dbeta, bool need_dx, bool batch, Tensor(c!)? dsum, "
+        "Tensor(d!)? qsite=None, Tensor(e!)? q_out=None, int qfmt=0) -> Tensor");
   m.def("act(Tensor a, Tensor? b, int act, int mode) -> Tensor");
   m.def("dropout(Tensor x, float p, Tensor seed, int salt) -> Tensor");
   m.def("pad_channels(Tensor a, Tensor? b, int Co) -> Tensor");
@@ -1011,6 +1097,7 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("fp8_quant", fp8_quant);
   m.impl("fp8_amax", fp8_amax);
   m.impl("fp8_roll", fp8_roll);
+  m.impl("fp8_amax_multi", fp8_amax_multi);
   m.impl("fp8_dequant", fp8_dequant);
   m.impl("conv_wgrad", conv_wgrad);
   m.impl("weight_prep", weight_prep);

@@ -43,6 +43,11 @@ struct ConvFwdArgs {
   const int* qs_x1;
   const int* qs_x2;
   const int* qs_w;
+  // optional fp8 shadow of the (bf16) output, written by the epilogue in the same pass:
+  // q_out [N*OH*OW][Cout] bytes, q_site its scale site, q_fmt 0 = e4m3 / 1 = e5m2
+  void* q_out;
+  int* q_site;
+  int q_fmt;
 };
 
 // Weight gradient: C[R][Kq] = sum_m P[m][R] * im2col(Q)[m][Kq], written to per-split
@@ -80,6 +85,7 @@ int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t stream);
 int p2p_fp8_quant(const void* x, long n, int* site, int use_cur, int fmt, void* q, hipStream_t st);
 int p2p_fp8_amax(const void* x, int is_f32, long n, int* site, int slot, hipStream_t st);
 int p2p_fp8_roll(int* sites, int nsites, hipStream_t st);
+int p2p_fp8_amax_multi(int count, const float* const* x, const long* n, int* const* site, hipStream_t st);
 int p2p_fp8_dequant(const void* q, long n, const int* site, int fmt, void* y, hipStream_t st);
 int p2p_conv_wgrad_tile_rows(int R);
 int p2p_conv_wgrad_tile(const p2p::ConvWgradArgs* a, int* tile_r, int* tile_q);

@@ -2,8 +2,8 @@
 // staged; conv_fwd_glds.hip: global_load_lds multi-stage): tile geometry of the two GEMM
 // modes, the LDS swizzle of the [rows][64] bf16 operand tiles, and the fused epilogue.
 #pragma once
-#include "common.h"
 #include "conv.h"
+#include "fp8_dev.h"
 
 namespace p2p {
 
@@ -138,6 +138,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
   }
 
   constexpr int CPR = BN / 8;  // 8-channel chunks per row
+  const Fp8Shadow qsh{static_cast<uint8_t*>(a.q_out), a.q_site, a.q_fmt};
+  const float qsc = qsh.q ? fp8_shadow_scale(qsh) : 0.f;
+  float qmax = 0.f;
   for (int c = tid; c < BM * CPR; c += NT) {
     const int row = c / CPR, cc = c - row * CPR;
     const int m = m0 + row;
@@ -172,7 +175,18 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
     }
     bf16* y = static_cast<bf16*>(first ? a.y1 : a.y2);
     *reinterpret_cast<u32x4*>(y + pix * ld + cof) = v;
+    if (qsh.q) {  // host: only with Csplit == Cout, no act_bwd
+      const bf16x8 vb = __builtin_bit_cast(bf16x8, v);
+      float r[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        r[q] = (float)vb[q];
+        qmax = fmaxf(qmax, fabsf(r[q]));
+      }
+      *reinterpret_cast<uint2*>(qsh.q + pix * ld + cof) = fp8_pack8(r, qsc, qsh.fmt);
+    }
   }
+  if (qsh.q) fp8_amax_commit(qmax, qsh.site);
 }
 
 }  // namespace p2p

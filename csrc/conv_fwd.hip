@@ -619,14 +619,30 @@ namespace p2p {
 constexpr int WPP_MAX = 24;
 struct WPairList {
   const float* w[WPP_MAX];
-  bf16* out0[WPP_MAX];
-  bf16* out1[WPP_MAX];
+  void* out0[WPP_MAX];
+  void* out1[WPP_MAX];
+  int* site[WPP_MAX];  // F8: per-tensor scale site (amax in [0], e8m0 published to [2])
   int A[WPP_MAX], B[WPP_MAX], T[WPP_MAX], Xa[WPP_MAX], Xb[WPP_MAX];
 };
 
+// element pair (lo at the lower address) -> bf16x2 (4 B) or e4m3x2 (2 B) store
+template <bool F8>
+__device__ __forceinline__ void store_pair(void* base, long idx, bf16 lo, bf16 hi, float qsc) {
+  if constexpr (F8) {
+    const float fm = 448.f;
+    const float a = fminf(fmaxf((float)lo * qsc, -fm), fm), b = fminf(fmaxf((float)hi * qsc, -fm), fm);
+    const int pk = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    *reinterpret_cast<uint16_t*>(static_cast<uint8_t*>(base) + idx) = (uint16_t)(pk & 0xffff);
+  } else {
+    const uint32_t l = __builtin_bit_cast(uint16_t, lo), h = __builtin_bit_cast(uint16_t, hi);
+    *reinterpret_cast<uint32_t*>(static_cast<bf16*>(base) + idx) = l | (h << 16);
+  }
+}
+
 // TT = 16: the 4x4-kernel fast path (all index math shifts, float4 source loads);
-// TT = 0: any T <= 16 with runtime division.
-template <int TT>
+// TT = 0: any T <= 16 with runtime division.  F8: e4m3 images with the current-scaling
+// power-of-two scale of the tensor's site (fp8 conv path, csrc/fp8.hip).
+template <int TT, bool F8>
 __global__ void __launch_bounds__(256) weight_prep_pair_kernel(WPairList L) {
   constexpr int TA = 32, TB = 32, TMAX = 16, TS = TMAX + 2;  // +2: breaks the 32-B row stride
   __shared__ bf16 tile[TA][TB][TS];
@@ -638,6 +654,12 @@ __global__ void __launch_bounds__(256) weight_prep_pair_kernel(WPairList L) {
   if (!TT && L.T[k] == 16) return;
   const int ta = (Xa + TA - 1) / TA, tb = (Xb + TB - 1) / TB;
   const int tid = threadIdx.x;
+  float qsc = 0.f;
+  if constexpr (F8) {
+    const int e = fp8_exp(__int_as_float(L.site[k][0]), 0);
+    if (blockIdx.x == 0 && tid == 0) L.site[k][2] = 127 - e;
+    qsc = ldexpf(1.f, e);
+  }
   for (int tile_id = blockIdx.x; tile_id < ta * tb; tile_id += gridDim.x) {
     const int a0 = (tile_id / tb) * TA, b0 = (tile_id % tb) * TB;
     if constexpr (TT == 16) {
@@ -680,11 +702,7 @@ __global__ void __launch_bounds__(256) weight_prep_pair_kernel(WPairList L) {
         bl = (r - t * (TB / 2)) * 2;
       }
       const int a = a0 + al, b = b0 + bl;
-      if (a < Xa && b < Xb) {
-        const uint32_t lo = __builtin_bit_cast(uint16_t, tile[al][bl][t]);
-        const uint32_t hi = __builtin_bit_cast(uint16_t, tile[al][bl + 1][t]);
-        *reinterpret_cast<uint32_t*>(L.out0[k] + ((long)a * T + t) * Xb + b) = lo | (hi << 16);
-      }
+      if (a < Xa && b < Xb) store_pair<F8>(L.out0[k], ((long)a * T + t) * Xb + b, tile[al][bl][t], tile[al][bl + 1][t], qsc);
     }
     // out1[b][t][a]: bf16 pairs along a
     for (int idx = tid; idx < n0; idx += 256) {
@@ -700,11 +718,7 @@ __global__ void __launch_bounds__(256) weight_prep_pair_kernel(WPairList L) {
         al = (r - t * (TA / 2)) * 2;
       }
       const int a = a0 + al, b = b0 + bl;
-      if (b < Xb && a < Xa) {
-        const uint32_t lo = __builtin_bit_cast(uint16_t, tile[al][bl][t]);
-        const uint32_t hi = __builtin_bit_cast(uint16_t, tile[al + 1][bl][t]);
-        *reinterpret_cast<uint32_t*>(L.out1[k] + ((long)b * T + t) * Xa + a) = lo | (hi << 16);
-      }
+      if (b < Xb && a < Xa) store_pair<F8>(L.out1[k], ((long)b * T + t) * Xa + a, tile[al][bl][t], tile[al + 1][bl][t], qsc);
     }
     __syncthreads();
   }
@@ -713,17 +727,19 @@ __global__ void __launch_bounds__(256) weight_prep_pair_kernel(WPairList L) {
 
 extern "C" int p2p_weight_prep_pairs(int count, const float* const* w, void* const* out0, void* const* out1,
                                      const int* A, const int* B, const int* T, const int* Xa, const int* Xb,
-                                     hipStream_t st) {
+                                     int* const* site, hipStream_t st) {
   using namespace p2p;
   if (count <= 0) return 0;
   if (count > WPP_MAX) return -1;
   WPairList L;
   int maxt = 1;
+  const bool f8 = site != nullptr;
   for (int i = 0; i < count; ++i) {
     if (T[i] > 16 || (Xa[i] & 1) || (Xb[i] & 1)) return -1;
     L.w[i] = w[i];
-    L.out0[i] = static_cast<bf16*>(out0[i]);
-    L.out1[i] = static_cast<bf16*>(out1[i]);
+    L.out0[i] = out0[i];
+    L.out1[i] = out1[i];
+    L.site[i] = f8 ? site[i] : nullptr;
     L.A[i] = A[i];
     L.B[i] = B[i];
     L.T[i] = T[i];
@@ -735,8 +751,13 @@ extern "C" int p2p_weight_prep_pairs(int count, const float* const* w, void* con
   bool any16 = false, other = false;
   for (int i = 0; i < count; ++i) (T[i] == 16 ? any16 : other) = true;
   const dim3 grid((unsigned)(maxt < 2048 ? maxt : 2048), count);
-  if (any16) hipLaunchKernelGGL(weight_prep_pair_kernel<16>, grid, dim3(256), 0, st, L);
-  if (other) hipLaunchKernelGGL(weight_prep_pair_kernel<0>, grid, dim3(256), 0, st, L);
+  if (f8) {
+    if (any16) hipLaunchKernelGGL((weight_prep_pair_kernel<16, true>), grid, dim3(256), 0, st, L);
+    if (other) hipLaunchKernelGGL((weight_prep_pair_kernel<0, true>), grid, dim3(256), 0, st, L);
+  } else {
+    if (any16) hipLaunchKernelGGL((weight_prep_pair_kernel<16, false>), grid, dim3(256), 0, st, L);
+    if (other) hipLaunchKernelGGL((weight_prep_pair_kernel<0, false>), grid, dim3(256), 0, st, L);
+  }
   return (int)hipGetLastError();
 }
 

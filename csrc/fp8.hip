@@ -15,32 +15,9 @@
 // record amax_cur; p2p_fp8_roll (once per step, one launch for the whole pool) shifts the
 // window.  Current scaling (weights): p2p_fp8_amax writes amax_ref of this very tensor first.
 // Everything stays on the device (graph-capturable, no host sync).
-#include "common.h"
+#include "fp8_dev.h"
 
 namespace p2p {
-
-__device__ __forceinline__ float fp8_max(int fmt) { return fmt == 0 ? 448.f : 57344.f; }
-
-// k such that amax * 2^k <= fmax (largest such power of two); 0 when amax is 0 / not finite
-__device__ __forceinline__ int fp8_exp(float amax, int fmt) {
-  if (!(amax > 0.f) || !(amax < 3.0e38f)) return 0;
-  int e;
-  (void)frexpf(fp8_max(fmt) / amax, &e);  // fmax/amax = m * 2^e, m in [0.5, 1)
-  int k = e - 1;
-  return k < -120 ? -120 : (k > 120 ? 120 : k);
-}
-
-__device__ __forceinline__ uint32_t cvt4(float a, float b, float c, float d, int fmt) {
-  int lo, hi;
-  if (fmt == 0) {
-    lo = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-    hi = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, lo, true);
-  } else {
-    lo = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
-    hi = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, lo, true);
-  }
-  return (uint32_t)hi;
-}
 
 __device__ __forceinline__ float block_max(float v, float* red) {
 #pragma unroll
@@ -84,15 +61,50 @@ __global__ void __launch_bounds__(256) fp8_quant_kernel(const bf16* __restrict__
   }
 }
 
-// amax of |x| -> site[slot] (site[slot] pre-zeroed by the caller); bf16 or fp32 input
+// amax of |x| -> site[slot] (site[slot] pre-zeroed by the caller); bf16 or fp32 input,
+// 16-B vector loads + scalar tail
 template <typename T>
 __global__ void __launch_bounds__(256) fp8_amax_kernel(const T* __restrict__ x, long n, int* site, int slot) {
   __shared__ float red[4];
+  constexpr int V = 16 / sizeof(T);
   float amax = 0.f;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    amax = fmaxf(amax, fabsf((float)x[i]));
+  const long nv = n / V;
+  const long tid0 = (long)blockIdx.x * blockDim.x + threadIdx.x, stride = (long)gridDim.x * blockDim.x;
+  for (long i = tid0; i < nv; i += stride) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(x + i * V);
+    const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+    for (int j = 0; j < V; ++j) amax = fmaxf(amax, fabsf((float)e[j]));
+  }
+  for (long i = nv * V + tid0; i < n; i += stride) amax = fmaxf(amax, fabsf((float)x[i]));
   amax = block_max(amax, red);
-  if (threadIdx.x == 0) atomicMax(site + slot, __float_as_int(amax));
+  if (threadIdx.x == 0 && amax > 0.f) atomicMax(site + slot, __float_as_int(amax));
+}
+
+// multi-tensor amax of fp32 tensors (the weight masters: one launch per step for every
+// fp8 weight site), blockIdx.y = tensor; site[0] pre-zeroed
+constexpr int AMAX_MULTI = 48;
+struct AmaxList {
+  const float* x[AMAX_MULTI];
+  long n[AMAX_MULTI];
+  int* site[AMAX_MULTI];
+};
+
+__global__ void __launch_bounds__(256) fp8_amax_multi_kernel(AmaxList L) {
+  __shared__ float red[4];
+  const int t = blockIdx.y;
+  const float* __restrict__ x = L.x[t];
+  const long n = L.n[t];
+  float amax = 0.f;
+  const long nv = n / 4;
+  const long tid0 = (long)blockIdx.x * blockDim.x + threadIdx.x, stride = (long)gridDim.x * blockDim.x;
+  for (long i = tid0; i < nv; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    amax = fmaxf(fmaxf(amax, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));
+  }
+  for (long i = nv * 4 + tid0; i < n; i += stride) amax = fmaxf(amax, fabsf(x[i]));
+  amax = block_max(amax, red);
+  if (threadIdx.x == 0 && amax > 0.f) atomicMax(L.site[t], __float_as_int(amax));
 }
 
 __global__ void fp8_roll_kernel(int* sites, int nsites) {
@@ -154,6 +166,25 @@ int p2p_fp8_amax(const void* x, int is_f32, long n, int* site, int slot, hipStre
     hipLaunchKernelGGL(p2p::fp8_amax_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)x, n, site, slot);
   else
     hipLaunchKernelGGL(p2p::fp8_amax_kernel<p2p::bf16>, dim3(g), dim3(256), 0, st, (const p2p::bf16*)x, n, site, slot);
+  return (int)hipGetLastError();
+}
+
+int p2p_fp8_amax_multi(int count, const float* const* x, const long* n, int* const* site, hipStream_t st) {
+  using namespace p2p;
+  if (count <= 0) return 0;
+  if (count > AMAX_MULTI) return -1;
+  AmaxList L;
+  long mx = 1;
+  for (int i = 0; i < count; ++i) {
+    if (((uintptr_t)x[i]) & 15) return -1;
+    L.x[i] = x[i];
+    L.n[i] = n[i];
+    L.site[i] = site[i];
+    mx = n[i] > mx ? n[i] : mx;
+  }
+  long g = (mx / 4 + 256 * 8 - 1) / (256 * 8);
+  g = g < 1 ? 1 : (g > 256 ? 256 : g);
+  hipLaunchKernelGGL(fp8_amax_multi_kernel, dim3((unsigned)g, count), dim3(256), 0, st, L);
   return (int)hipGetLastError();
 }
 

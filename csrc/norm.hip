@@ -16,7 +16,7 @@
 //   1. norm_bwd_partial : block partial sums of dy and dy*xhat (recomputed from x)
 //   2. norm_bwd_finalize: per (n,c) coefficients; per-channel dgamma/dbeta (summed over n)
 //   3. norm_bwd_apply   : dx = A*dy + B + Cc*xhat
-#include "common.h"
+#include "fp8_dev.h"
 
 namespace p2p {
 
@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict_
                                                          const float* __restrict__ gamma,
                                                          const float* __restrict__ beta,
                                                          const float* __restrict__ prelu_w,
-                                                         int act, bf16* __restrict__ y) {
+                                                         int act, bf16* __restrict__ y, Fp8Shadow sh) {
   const int n = blockIdx.y, cb = blockIdx.x;
   const int CP = g.C >> 3;
   const int RP = 256 / CP;
@@ -168,28 +168,39 @@ __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict_
   if (tr >= RP) return;
   const int p0 = cb * g.chunk;
   const int p1 = min(g.HW, p0 + g.chunk);
-  float sc[8], sh[8];
+  float sc[8], sf[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = cg * 8 + j;
     const float r = rstd[(long)n * g.C + c];
     const float gm = gamma ? gamma[c] : 1.f;
     sc[j] = r * gm;
-    sh[j] = (gamma ? beta[c] : 0.f) - mean[(long)n * g.C + c] * r * gm;
+    sf[j] = (gamma ? beta[c] : 0.f) - mean[(long)n * g.C + c] * r * gm;
   }
   const float pw = prelu_w ? prelu_w[0] : 0.f;
   const long base = (long)n * g.HW * g.C + cg * 8;
-  auto one = [&](u32x4 v) -> u32x4 {
+  // optional fp8 shadow of y (the next conv's operand) written in the same pass
+  const float qsc = sh.q ? fp8_shadow_scale(sh) : 0.f;
+  float qmax = 0.f;
+  auto one = [&](u32x4 v, long off) {
     float f[8];
     unpack8(v, f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float t = f[j] * sc[j] + sh[j];
+      float t = f[j] * sc[j] + sf[j];
       if (prelu_w) t = t > 0.f ? t : pw * t;
       else t = act_fwd(t, act);
       f[j] = t;
     }
-    return pack8(f);
+    const u32x4 o = pack8(f);
+    *reinterpret_cast<u32x4*>(y + off) = o;
+    if (sh.q) {
+      float r[8];
+      unpack8(o, r);   // quantise the stored bf16 value: shadow == fp8(y) exactly
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qmax = fmaxf(qmax, fabsf(r[j]));
+      *reinterpret_cast<uint2*>(sh.q + off) = fp8_pack8(r, qsc, sh.fmt);
+    }
   };
   int p = p0 + tr;
   for (; p + 3 * RP < p1; p += 4 * RP) {
@@ -197,10 +208,10 @@ __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict_
 #pragma unroll
     for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const u32x4*>(x + base + (long)(p + u * RP) * g.C);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) *reinterpret_cast<u32x4*>(y + base + (long)(p + u * RP) * g.C) = one(v[u]);
+    for (int u = 0; u < 4; ++u) one(v[u], base + (long)(p + u * RP) * g.C);
   }
-  for (; p < p1; p += RP)
-    *reinterpret_cast<u32x4*>(y + base + (long)p * g.C) = one(*reinterpret_cast<const u32x4*>(x + base + (long)p * g.C));
+  for (; p < p1; p += RP) one(*reinterpret_cast<const u32x4*>(x + base + (long)p * g.C), base + (long)p * g.C);
+  if (sh.q) fp8_amax_commit(qmax, sh.site);
 }
 
 // ---------------------------------------------------------------- backward
@@ -361,7 +372,8 @@ __global__ void __launch_bounds__(256) norm_param_grad_kernel(const float* __res
 __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ dy, NormGeom g,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
-    const float* __restrict__ beta, int act, const float* __restrict__ coef, bf16* __restrict__ dx) {
+    const float* __restrict__ beta, int act, const float* __restrict__ coef, bf16* __restrict__ dx,
+    Fp8Shadow sh) {
   const int n = blockIdx.y, cb = blockIdx.x;
   const int CP = g.C >> 3;
   const int RP = 256 / CP;
@@ -384,7 +396,10 @@ __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
     c0[j] = coef[NC + ci];
   }
   const long base = (long)n * g.HW * g.C + cg * 8;
-  auto one = [&](u32x4 vx, u32x4 vd) -> u32x4 {
+  // optional fp8 (e5m2) shadow of dx: the producing conv's dgrad operand
+  const float qsc = sh.q ? fp8_shadow_scale(sh) : 0.f;
+  float qmax = 0.f;
+  auto one = [&](u32x4 vx, u32x4 vd, long off) {
     float fx[8], fd[8];
     unpack8(vx, fx);
     unpack8(vd, fd);
@@ -394,7 +409,15 @@ __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
       const float d = act ? fd[j] * act_gate(xh * ga[j] + be[j], act) : fd[j];
       fd[j] = ca[j] * d + c0[j] + cx[j] * xh;
     }
-    return pack8(fd);
+    const u32x4 o = pack8(fd);
+    *reinterpret_cast<u32x4*>(dx + off) = o;
+    if (sh.q) {
+      float r[8];
+      unpack8(o, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qmax = fmaxf(qmax, fabsf(r[j]));
+      *reinterpret_cast<uint2*>(sh.q + off) = fp8_pack8(r, qsc, sh.fmt);
+    }
   };
   int p = p0 + tr;
   for (; p + 3 * RP < p1; p += 4 * RP) {
@@ -405,13 +428,12 @@ __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
       vd[u] = *reinterpret_cast<const u32x4*>(dy + base + (long)(p + u * RP) * g.C);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      *reinterpret_cast<u32x4*>(dx + base + (long)(p + u * RP) * g.C) = one(vx[u], vd[u]);
+    for (int u = 0; u < 4; ++u) one(vx[u], vd[u], base + (long)(p + u * RP) * g.C);
   }
   for (; p < p1; p += RP)
-    *reinterpret_cast<u32x4*>(dx + base + (long)p * g.C) =
-        one(*reinterpret_cast<const u32x4*>(x + base + (long)p * g.C),
-            *reinterpret_cast<const u32x4*>(dy + base + (long)p * g.C));
+    one(*reinterpret_cast<const u32x4*>(x + base + (long)p * g.C),
+        *reinterpret_cast<const u32x4*>(dy + base + (long)p * g.C), base + (long)p * g.C);
+  if (sh.q) fp8_amax_commit(qmax, sh.site);
 }
 
 static inline NormGeom make_geom(int N, int HW, int C) {
@@ -445,7 +467,7 @@ long p2p_norm_ws_floats(int N, int HW, int C) {
 int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* gamma,
                  const float* beta, const float* prelu_w, int act, float* mean, float* rstd,
                  float* run_mean, float* run_var, float momentum, float* ws, void* y,
-                 hipStream_t st) {
+                 void* q, int* qsite, int qfmt, hipStream_t st) {
   using namespace p2p;
   NormGeom g = make_geom(N, HW, C);
   hipLaunchKernelGGL(norm_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
@@ -455,7 +477,7 @@ int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* ga
   if (y)
     hipLaunchKernelGGL(norm_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
                        static_cast<const bf16*>(x), g, mean, rstd, gamma, beta, prelu_w, act,
-                       static_cast<bf16*>(y));
+                       static_cast<bf16*>(y), Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
   return (int)hipGetLastError();
 }
 
@@ -465,7 +487,7 @@ int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* ga
 int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, const float* partials,
                           float eps, const float* gamma, const float* beta, const float* prelu_w,
                           int act, float* mean, float* rstd, float* run_mean, float* run_var,
-                          float momentum, void* y, hipStream_t st) {
+                          float momentum, void* y, void* q, int* qsite, int qfmt, hipStream_t st) {
   using namespace p2p;
   if (nchunks <= 0 || HW % nchunks) return -1;
   NormGeom pg;
@@ -478,7 +500,8 @@ int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, cons
                      mean, rstd, run_mean, run_var, momentum);
   NormGeom g = make_geom(N, HW, C);
   hipLaunchKernelGGL(norm_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st, static_cast<const bf16*>(x), g,
-                     mean, rstd, gamma, beta, prelu_w, act, static_cast<bf16*>(y));
+                     mean, rstd, gamma, beta, prelu_w, act, static_cast<bf16*>(y),
+                     Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
   return (int)hipGetLastError();
 }
 
@@ -490,7 +513,7 @@ int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const
   NormGeom g = make_geom(N, HW, C);
   hipLaunchKernelGGL(norm_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
                      static_cast<const bf16*>(x), g, mean, rstd, gamma, beta, prelu_w, act,
-                     static_cast<bf16*>(y));
+                     static_cast<bf16*>(y), Fp8Shadow{nullptr, nullptr, 0});
   return (int)hipGetLastError();
 }
 
@@ -498,7 +521,8 @@ int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const
 // column sums of dx (bias gradient of the producing conv), which are exactly zero.
 int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const float* mean,
                  const float* rstd, const float* gamma, const float* beta, int act, float* dgamma,
-                 float* dbeta, float* ws, void* dx, float* dsum, hipStream_t st) {
+                 float* dbeta, float* ws, void* dx, float* dsum, void* q, int* qsite, int qfmt,
+                 hipStream_t st) {
   using namespace p2p;
   NormGeom g = make_geom(N, HW, C);
   float* coef = ws + 2L * N * g.nchunks * C;
@@ -516,7 +540,8 @@ int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const floa
     hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, ws, g,
                        rstd, gamma, coef);
     hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st, xb, db, g, mean,
-                       rstd, gamma, beta, act, coef, static_cast<bf16*>(dx));
+                       rstd, gamma, beta, act, coef, static_cast<bf16*>(dx),
+                       Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
     if (dsum) (void)hipMemsetAsync(dsum, 0, sizeof(float) * C, st);
   }
   return (int)hipGetLastError();

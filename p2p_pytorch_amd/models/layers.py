@@ -98,7 +98,7 @@ class InstanceNorm2d(nn.Module):
             self.register_parameter("bias", None)
 
     def forward(self, x):
-        return ops.instance_norm(x, self.eps, self.act, self.weight, self.bias)
+        return ops.instance_norm(x, self.eps, self.act, self.weight, self.bias, qkey=id(self))
 
 
 class BatchNorm2d(nn.BatchNorm2d):
@@ -114,7 +114,8 @@ class BatchNorm2d(nn.BatchNorm2d):
             self.num_batches_tracked.add_(1)
         return ops.batch_norm(x, self.running_mean if self.track_running_stats else None,
                               self.running_var if self.track_running_stats else None,
-                              self.weight, self.bias, training, self.momentum, self.eps, self.act)
+                              self.weight, self.bias, training, self.momentum, self.eps, self.act,
+                              qkey=id(self))
 
 
 class Act(nn.Module):

@@ -43,17 +43,18 @@ def conv_transpose2d(x, weight, bias=None, stride=2, padding=1, act_in=None, act
     return ref.conv_transpose2d(x, weight, bias, stride, padding, act_in, act_out)
 
 
-def instance_norm(x, eps=1e-5, act=None, weight=None, bias=None):
+def instance_norm(x, eps=1e-5, act=None, weight=None, bias=None, qkey=None):
+    """``qkey`` (HIP path, fp8 precision): stable key of the module's fp8 shadow sites."""
     if _native.use_native(x):
-        return _hip().instance_norm(x, eps, act, weight, bias)
+        return _hip().instance_norm(x, eps, act, weight, bias, qkey)
     return ref.instance_norm(x, eps, act, weight, bias)
 
 
 def batch_norm(x, running_mean, running_var, weight, bias, training, momentum=0.1, eps=1e-5,
-               act=None):
+               act=None, qkey=None):
     if _native.use_native(x):
         return _hip().batch_norm(x, running_mean, running_var, weight, bias, training, momentum,
-                                 eps, act)
+                                 eps, act, qkey=qkey)
     return ref.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps, act)
 
 

@@ -74,8 +74,12 @@ class _Pool:
 
 
 _pools: dict = {}
+_wpools: dict = {}   # current-scaling weight sites (never rolled; word 0 recomputed per step)
 # per-step cache of quantised activations: (ptr, shape, version, site) -> (x, q)
 _qcache: dict = {}
+# fp8 "shadows" written by the producer of a bf16 tensor in the same pass (norm apply /
+# norm backward / conv epilogue): (ptr, shape, version) -> (x, q, site)
+_shadows: dict = {}
 
 
 def _pool(device) -> _Pool:
@@ -91,10 +95,53 @@ def site_tensor(device, key) -> torch.Tensor:
     return p.sites[p.site(key)]
 
 
+def wpool(device) -> _Pool:
+    p = _wpools.get(device)
+    if p is None:
+        p = _Pool(device)
+        _wpools[device] = p
+    return p
+
+
+def producer_site(device, key):
+    """(site, fresh) for a producer-side fused shadow.  A fresh site has no amax history
+    yet: the caller produces no fused shadow this time and calls ``bootstrap_shadow``."""
+    p = _pool(device)
+    i = p.site(key)
+    fresh = i in p.fresh
+    return p.sites[i], fresh
+
+
+def stash_shadow(x: torch.Tensor, q: torch.Tensor, site: torch.Tensor) -> None:
+    _shadows[(x.data_ptr(), tuple(x.shape), x._version)] = (x, q, site)
+
+
+def bootstrap_shadow(x: torch.Tensor, key, fmt: int) -> None:
+    """First step of a producer site: measure the tensor, quantise it standalone, stash it."""
+    P = _native.ops()
+    p = _pool(x.device)
+    i = p.site(key)
+    p.fresh.discard(i)
+    site = p.sites[i]
+    site[0].zero_()
+    P.fp8_amax(x, site, 0)
+    stash_shadow(x, P.fp8_quant(x, site, fmt, 0), site)
+
+
+def _shadow_dtype(fmt):
+    return torch.float8_e4m3fn if fmt == E4M3 else torch.float8_e5m2
+
+
+def shadow_buffer(like: torch.Tensor, fmt: int) -> torch.Tensor:
+    return torch.empty(like.shape, dtype=_shadow_dtype(fmt), device=like.device,
+                       memory_format=torch.channels_last)
+
+
 def begin_step() -> None:
     """Shift every delayed-scaling window (one launch per device) and drop the per-step
     quantisation cache."""
     _qcache.clear()
+    _shadows.clear()
     P = _native.ops()
     for p in _pools.values():
         if p.index:
@@ -104,6 +151,9 @@ def begin_step() -> None:
 def quant(x: torch.Tensor, key, fmt: int) -> tuple[torch.Tensor, torch.Tensor]:
     """Delayed-scaled fp8 copy of the bf16 NHWC tensor ``x`` (site ``key``); returns (q, site).
     The same tensor quantised twice for the same site in one step is reused."""
+    sh = _shadows.get((x.data_ptr(), tuple(x.shape), x._version))
+    if sh is not None and sh[1].dtype == _shadow_dtype(fmt):
+        return sh[1], sh[2]
     P = _native.ops()
     pool = _pool(x.device)
     i = pool.site(key)
@@ -132,6 +182,27 @@ def quant_weight(img: torch.Tensor, key) -> tuple[torch.Tensor, torch.Tensor]:
     site[0].zero_()
     P.fp8_amax(img, site, 0)
     return P.fp8_quant(img, site, E4M3, 0), site
+
+
+def prepare_weight_pairs(ws, xa, xb):
+    """e4m3 GEMM images (both layouts) of fp32 masters ``ws`` with current scaling: one
+    fill (zero the amax words), one multi-tensor amax launch, one image launch per 24
+    tensors.  Returns [(img0, img1, site)]."""
+    if not ws:
+        return []
+    P = _native.ops()
+    wp = wpool(ws[0].device)
+    idx = [wp.site(id(w)) for w in ws]
+    wp.sites[: len(wp.index), 0].zero_()
+    P.fp8_amax_multi(list(ws), wp.sites, idx)
+    imgs = P.weight_prep_pairs(list(ws), list(xa), list(xb), wp.sites, idx)
+    return [(imgs[2 * j], imgs[2 * j + 1], wp.sites[i]) for j, i in enumerate(idx)]
+
+
+def pair_ok(A: int, B: int) -> bool:
+    """Both GEMM images of a weight [A][B][k][k] feed fp8 convs (fwd and dgrad): the
+    channel granularity and N-tile limits of ``conv_ok`` hold for both orientations."""
+    return A % 32 == 0 and B % 32 == 0 and A > 32 and B > 32
 
 
 def conv_ok(C1: int, C2: int, Cout: int, act_in: int) -> bool:

@@ -137,22 +137,36 @@ def _weight_image_fp8(w: torch.Tensor, swap: int, xp: int, yp: int):
 
 
 def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout, act_out,
-               Csplit, xb1, xb2, act_bwd, Cvalid, want, weight=None, swap=0, xp=0, yp=0, role="x"):
+               Csplit, xb1, xb2, act_bwd, Cvalid, want, weight=None, swap=0, xp=0, yp=0, role="x",
+               y_qkey=None):
     """conv_fwd on bf16 operands, or -- fp8 precision and a geometry the fp8 kernel takes --
     on fp8 ones: x (role 'x': activations, e4m3; 'gy': gradients, e5m2) quantised with
-    delayed scaling, the weight image with current scaling."""
+    delayed scaling (or taken from the producer's fused shadow), the weight image with
+    current scaling.  ``y_qkey``: also emit an e4m3 shadow of the output from the epilogue
+    (the output feeds other fp8 convs directly) -- appended last to the returned list.
+    ``wimg`` may be None (built on demand for the bf16 path)."""
     C1 = x1.shape[1]
     C2 = 0 if x2 is None else x2.shape[1]
     if weight is not None and _f8.enabled() and _f8.conv_ok(C1, C2, Cout, act_in):
         fmt = _f8.E5M2 if role == "gy" else _f8.E4M3
         w8, sw = _weight_image_fp8(weight, swap, xp, yp)
+        yq = ()
+        if y_qkey is not None:
+            ysite, fresh = _f8.producer_site(x1.device, y_qkey)
+            yq = (None, 0) if fresh else (ysite, _f8.E4M3)
         k = id(weight)
         a1, s1 = _f8.quant(x1, (k, role, 1), fmt)
         a2, s2 = _f8.quant(x2, (k, role, 2), fmt) if x2 is not None else (None, None)
         return P().conv_fwd(a1, a2, w8, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout,
-                            act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, s1, s2, sw)
+                            act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, s1, s2, sw, *yq)
+    if wimg is None:
+        wimg = _weight_image(weight, swap, xp, yp)
+    yq = ()
+    if y_qkey is not None and _f8.enabled():
+        ysite, fresh = _f8.producer_site(x1.device, y_qkey)
+        yq = (None, None, None, None, 0) if fresh else (None, None, None, ysite, _f8.E4M3)
     return P().conv_fwd(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout,
-                        act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want)
+                        act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, *yq)
 
 
 def prepare_weights(*modules):
@@ -188,6 +202,18 @@ def prepare_weights(*modules):
                 yp.append(y_)
                 keys.append((w, (s_, x_, y_, None)))
     entries = []
+    if pw and _f8.enabled():
+        # fp8 precision: e4m3 images (current scaling) for the layers the fp8 convs take,
+        # bf16 images for the image-facing rest
+        sel = [i for i in range(len(pw)) if _f8.pair_ok(pkeys[i].shape[0], pkeys[i].shape[1])]
+        for j, (i0, i1, site) in zip(sel, _f8.prepare_weight_pairs(
+                [pw[i] for i in sel], [pa[i] for i in sel], [pb[i] for i in sel])):
+            w = pkeys[j]
+            entries.append((w, (0, pa[j], pb[j], "fp8"), (i0, site)))
+            entries.append((w, (1, pb[j], pa[j], "fp8"), (i1, site)))
+        rest = [i for i in range(len(pw)) if i not in set(sel)]
+        pw, pa, pb, pkeys = ([pw[i] for i in rest], [pa[i] for i in rest], [pb[i] for i in rest],
+                             [pkeys[i] for i in rest])
     if pw:
         imgs = P().weight_prep_pairs(pw, pa, pb)
         for i, w in enumerate(pkeys):
@@ -282,13 +308,24 @@ class ConvFn(torch.autograd.Function):
             OW = (W * cfg.up + 2 * p - KW) // s + 1
             mode, swap = 0, 0
         Coutp = _pad8(Cout)
-        wimg = _weight_image(weight, swap, Coutp, Cp)
         want = bool(cfg.stats) and Coutp == Cout
-        outs = _conv_call(q1, q2, wimg, _bias_padded(bias, Coutp), mode, KH, KW, s, p,
+        # fp8: an output that feeds other convs directly (relu / lrelu epilogue, no norm)
+        # gets its e4m3 shadow from the epilogue
+        y_qkey = None
+        if (_f8.enabled() and not cfg.stats and Coutp == Cout and Cout % 32 == 0
+                and cfg.act_out in ("relu", "lrelu")):
+            y_qkey = (id(weight), "y")
+        outs = _conv_call(q1, q2, None, _bias_padded(bias, Coutp), mode, KH, KW, s, p,
                           int(cfg.reflect), cfg.up, _act_code(cfg.act_in), OH, OW, Coutp,
                           _act_code(cfg.act_out), Coutp, None, None, 0, Cout, want,
-                          weight, swap, Coutp, Cp)
+                          weight, swap, Coutp, Cp, y_qkey=y_qkey)
         y = outs[0]
+        if y_qkey is not None:
+            if outs[-1].element_size() == 1:
+                _f8.stash_shadow(y, outs[-1], _f8.producer_site(y.device, y_qkey)[0])
+                outs = outs[:-1]
+            elif _f8.producer_site(y.device, y_qkey)[1]:
+                _f8.bootstrap_shadow(y, y_qkey, _f8.E4M3)
         if want and len(outs) == 2:
             _stash_stats(y, outs[1])
         if Coutp != Cout:
@@ -326,20 +363,17 @@ class ConvFn(torch.autograd.Function):
                 if q2 is not None:
                     raise NotImplementedError("virtual concat with reflect/upsample gather")
                 Hp, Wp = H * cfg.up + 2 * p, W * cfg.up + 2 * p
-                wimg = _weight_image(weight, 1, Cp, Coutp)
-                dxp = _conv_call(gyp, None, wimg, None, 1, KH, KW, s, 0, 0, 1, 0, Hp, Wp, Cp,
+                dxp = _conv_call(gyp, None, None, None, 1, KH, KW, s, 0, 0, 1, 0, Hp, Wp, Cp,
                                  0, Cp, None, None, 0, C1, False, weight, 1, Cp, Coutp, "gy")[0]
                 outs = [P().pad_fold(dxp, H, W, p, cfg.up, int(cfg.reflect),
                                      q1 if act_in else None, act_in)]
             elif cfg.transposed:
-                wimg = _weight_image(weight, 0, Cp, Coutp)
-                outs = _conv_call(gyp, None, wimg, None, 0, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
+                outs = _conv_call(gyp, None, None, None, 0, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
                                   split, q1 if act_in else None,
                                   q2 if (act_in and q2 is not None) else None, act_in, C1 + C2,
                                   False, weight, 0, Cp, Coutp, "gy")
             else:
-                wimg = _weight_image(weight, 1, Cp, Coutp)
-                outs = _conv_call(gyp, None, wimg, None, 1, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
+                outs = _conv_call(gyp, None, None, None, 1, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
                                   split, q1 if act_in else None,
                                   q2 if (act_in and q2 is not None) else None, act_in, C1 + C2,
                                   False, weight, 1, Cp, Coutp, "gy")
@@ -414,15 +448,30 @@ def conv_transpose2d(x, weight, bias=None, stride=2, padding=1, act_in=None, act
 class NormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, prelu_w, run_mean, run_var, eps, momentum, act, batch,
-                training):
+                training, qkey=None):
         x = to_nhwc_bf16(x)
         g = gamma.detach().float().contiguous() if gamma is not None else None
         b = beta.detach().float().contiguous() if beta is not None else None
         pw = prelu_w.detach().float().contiguous() if prelu_w is not None else None
+        # fp8: the normalised output is the next conv's operand -> e4m3 shadow from the apply
+        # pass; the input gradient (backward) the producing conv's dgrad operand -> e5m2
+        qkey = qkey if (qkey is not None and _f8.enabled() and training
+                        and x.shape[1] % 32 == 0) else None
+        ctx.qkey = qkey
         if training:
+            qargs, qy, ysite, fresh = (), None, None, False
+            if qkey is not None:
+                ysite, fresh = _f8.producer_site(x.device, (qkey, "y"))
+                if not fresh:
+                    qy = _f8.shadow_buffer(x, _f8.E4M3)
+                    qargs = (ysite, qy, _f8.E4M3)
             y, mean, rstd = P().norm_fwd(x, eps, g, b, pw, _act_code(act),
                                          run_mean if batch else None, run_var if batch else None,
-                                         momentum, batch, _take_stats(x))
+                                         momentum, batch, _take_stats(x), *qargs)
+            if qy is not None:
+                _f8.stash_shadow(y, qy, ysite)
+            elif fresh:
+                _f8.bootstrap_shadow(y, (qkey, "y"), _f8.E4M3)
         else:
             mean = run_mean.float().view(1, -1)
             rstd = torch.rsqrt(run_var.float() + eps).view(1, -1)
@@ -472,12 +521,22 @@ class NormFn(torch.autograd.Function):
                 xh = (x.float() - mean.view(1, -1, 1, 1)) * rstd.view(1, -1, 1, 1)
                 dg = (gy.float() * xh).sum((0, 2, 3))
                 db = gy.float().sum((0, 2, 3))
-            return dx, dg, db, gpw, None, None, None, None, None, None, None
+            return dx, dg, db, gpw, None, None, None, None, None, None, None, None
         dsum = torch.empty(x.shape[1], device=x.device, dtype=torch.float32) if need_x else None
-        dx = P().norm_bwd(x, gy, mean, rstd, g, b, fused_act, dg, db, need_x, batch, dsum)
+        qargs, qd, dsite, fresh = (), None, None, False
+        if ctx.qkey is not None and need_x:
+            dsite, fresh = _f8.producer_site(x.device, (ctx.qkey, "dx"))
+            if not fresh:
+                qd = _f8.shadow_buffer(x, _f8.E5M2)
+                qargs = (dsite, qd, _f8.E5M2)
+        dx = P().norm_bwd(x, gy, mean, rstd, g, b, fused_act, dg, db, need_x, batch, dsum, *qargs)
         if need_x:
             _stash_colsum(dx, dsum)
-        return (dx if need_x else None), dg, db, gpw, None, None, None, None, None, None, None
+            if qd is not None:
+                _f8.stash_shadow(dx, qd, dsite)
+            elif fresh:
+                _f8.bootstrap_shadow(dx, (ctx.qkey, "dx"), _f8.E5M2)
+        return (dx if need_x else None), dg, db, gpw, None, None, None, None, None, None, None, None
 
 
 def _norm_recompute(x, mean, rstd, gamma, beta, batch):
@@ -522,11 +581,12 @@ class _SliceCFn(torch.autograd.Function):
         return P().pad_channels(to_nhwc_bf16(g), None, ctx.cp), None
 
 
-def _norm_any_c(x, gamma, beta, prelu_w, run_mean, run_var, eps, momentum, act, batch, training):
+def _norm_any_c(x, gamma, beta, prelu_w, run_mean, run_var, eps, momentum, act, batch, training,
+                qkey=None):
     C = x.shape[1]
     if C % 8 == 0:
         return NormFn.apply(x, gamma, beta, prelu_w, run_mean, run_var, eps, momentum, act, batch,
-                            training)
+                            training, qkey)
     # odd channel counts (family-R tail BN(3)): pad to 8 with identity channels, slice back
     cp = _pad8(C)
     pad = cp - C
@@ -546,16 +606,17 @@ def _norm_any_c(x, gamma, beta, prelu_w, run_mean, run_var, eps, momentum, act, 
     return _SliceCFn.apply(y8, C)
 
 
-def instance_norm(x, eps=1e-5, act=None, weight=None, bias=None):
-    return _norm_any_c(x, weight, bias, None, None, None, eps, 0.0, act, False, True)
+def instance_norm(x, eps=1e-5, act=None, weight=None, bias=None, qkey=None):
+    """``qkey``: stable per-module key of the fp8 shadow scale sites (fp8 precision only)."""
+    return _norm_any_c(x, weight, bias, None, None, None, eps, 0.0, act, False, True, qkey)
 
 
 def batch_norm(x, running_mean, running_var, weight, bias, training, momentum=0.1, eps=1e-5,
-               act=None, prelu_weight=None):
+               act=None, prelu_weight=None, qkey=None):
     if not training and running_mean is None:
         training = True
     return _norm_any_c(x, weight, bias, prelu_weight, running_mean, running_var, eps, momentum,
-                       act, True, training)
+                       act, True, training, qkey)
 
 
 # ============================================================== elementwise

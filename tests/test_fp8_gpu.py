@@ -204,3 +204,43 @@ def test_unet_step_fp8_close_to_bf16():
         assert math.isfinite(b), (k, b)
         assert abs(a - b) <= 0.05 * abs(a) + 0.02, (k, a, b)
     assert all(math.isfinite(v) for d in res["fp8"] for v in d.values())
+
+
+def _expect_fp8(y, site, fmt):
+    k = 127 - int(site[2].item())
+    tdt, fmax = (torch.float8_e4m3fn, 448.0) if fmt == 0 else (torch.float8_e5m2, 57344.0)
+    return (y.float() * 2.0 ** k).clamp(-fmax, fmax).to(tdt).view(torch.uint8)
+
+
+@pytest.mark.parametrize("producer", ["norm", "conv_epilogue"])
+def test_fused_shadows_equal_standalone_quantisation(producer):
+    """Producer-fused fp8 shadows (norm apply / norm backward / conv epilogue) hold exactly
+    fp8(value * 2^k) of the bf16 tensor they shadow, k from the site's delayed amax."""
+    xl = rand_img(2, 64, 16, 16, seed=4).requires_grad_(True)
+    g = torch.Generator(device=DEV).manual_seed(6)
+    w = (torch.randn(64, 64, 3, 3, device=DEV, generator=g) * 0.05).requires_grad_(True)
+    key = 777001
+    for it in range(2):          # step 0 bootstraps the sites, step 1 uses the fused path
+        hip.begin_step()
+        # a non-leaf input: the gradient the norm backward returns reaches its hook as is
+        # (a leaf's AccumulateGrad would clone it)
+        x = xl * 1.0
+        grads = []
+        x.register_hook(grads.append)
+        if producer == "norm":
+            y = ops.instance_norm(x, act="lrelu", qkey=key)
+        else:
+            y = ops.conv2d(x, w, None, 1, 1, act_out="lrelu")
+        ent = f8._shadows.get((y.data_ptr(), tuple(y.shape), y._version))
+        assert ent is not None, "no shadow stashed"
+        q, site = ent[1], ent[2]
+        torch.cuda.synchronize()
+        assert torch.equal(q.view(torch.uint8), _expect_fp8(y, site, 0)), f"fwd shadow, step {it}"
+        if producer == "norm":
+            gy = rand_img(*y.shape, scale=1e-3, seed=7)
+            y.backward(gy)
+            dx = grads[0]
+            ent = f8._shadows.get((dx.data_ptr(), tuple(dx.shape), dx._version))
+            assert ent is not None, "no dx shadow"
+            torch.cuda.synchronize()
+            assert torch.equal(ent[1].view(torch.uint8), _expect_fp8(dx, ent[2], 1)), f"dx shadow, step {it}"

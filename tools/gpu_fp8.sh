@@ -10,3 +10,7 @@ for prec in ${PRECS:-fp8 bf16}; do
   timeout -k 10 400 python bench.py --batch ${B:-128} --steps 10 --warmup 3 --precision $prec >> gpurun_out/fp8bench.jsonl 2>> gpurun_out/fp8bench.err || exit $?
   tail -1 gpurun_out/fp8bench.jsonl | cut -c1-260
 done
+if [ -n "$PROF" ]; then
+  B=64 BENCH_ARGS="--precision fp8" bash tools/gpu_prof_native.sh || exit $?
+  head -40 gpurun_out/native_prof_b64/summary.txt
+fi
