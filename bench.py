@@ -72,7 +72,7 @@ def main():
     world, rank, local_rank = pdist.init_from_env()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch with torchrun for N>1")
-    dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    dev = pdist.local_device(local_rank) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
         torch.backends.cudnn.benchmark = True

@@ -23,14 +23,24 @@ def init_from_env(timeout_s: float = 600.0):
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         use_gpu = torch.cuda.is_available()
-        backend = "nccl" if use_gpu else "gloo"
+        # P2P_DIST_BACKEND=gloo: rehearsal of the multi-rank path on fewer GPUs than ranks
+        # (ranks share a device, gloo stages through the host).  Production: RCCL.
+        backend = os.environ.get("P2P_DIST_BACKEND", "nccl" if use_gpu else "gloo")
         kw = {}
         if use_gpu:
-            torch.cuda.set_device(local_rank)
-            kw["device_id"] = torch.device("cuda", local_rank)
+            torch.cuda.set_device(local_device(local_rank))
+            if backend == "nccl":
+                kw["device_id"] = local_device(local_rank)
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return world, rank, local_rank
+
+
+def local_device(local_rank: int) -> torch.device:
+    """The GPU of a local rank: one per rank; ranks wrap around when there are fewer GPUs
+    than ranks (only meaningful with the gloo rehearsal backend)."""
+    n = torch.cuda.device_count()
+    return torch.device("cuda", local_rank % n if n else 0)
 
 
 def is_dist() -> bool:

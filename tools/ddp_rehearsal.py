@@ -1,0 +1,122 @@
+#!/usr/bin/env python
+"""Multi-rank rehearsal of the data-parallel training path on ONE GPU.
+
+Launched by ``torch.distributed.run --nproc-per-node N`` with ``P2P_DIST_BACKEND=gloo``:
+all ranks share cuda:0 (``pdist.local_device`` wraps), gloo stages the collectives through
+the host.  What it checks on the real HIP kernels:
+
+  * rank-specific init is overwritten by the rank-0 broadcast;
+  * a full ``Pix2PixStep`` with per-network ``GradReducer`` s (small buckets -> several in
+    flight, hooks firing during backward) leaves every rank with bitwise identical G and D
+    parameters after Adam;
+  * the reduced G gradient equals the single-process gradient of the global batch.
+
+Exit status 0 = pass; rank 0 prints one JSON line.  (The production path is RCCL over xGMI
+with one GPU per rank; the driver's 8-GPU bench exercises that.)
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def build(seed, dev):
+    from p2p_pytorch_amd.models import define_D, define_G
+    torch.manual_seed(seed)
+    # unet_4 at 128x128: every instance norm sees >= 16x16 pixels.  (Deeper U-Nets normalise
+    # 2x2 maps, whose bf16 sensitivity makes ANY two batch compositions differ by ~10-20%:
+    # tools/debug/batch_consistency.py)
+    G = define_G(netG="unet_4", ngf=32, gpu_id=dev, verbose=False, use_dropout=False)
+    D = define_D(6, 32, norm="instance", netD="basic", gpu_id=dev, verbose=False)
+    return G, D
+
+
+def data(world, dev, per=2, size=128):
+    g = torch.Generator(device=dev).manual_seed(123)
+    A = torch.rand(per * world, 3, size, size, device=dev, generator=g) * 2 - 1
+    B = torch.rand(per * world, 3, size, size, device=dev, generator=g) * 2 - 1
+    cl = torch.channels_last
+    return A.to(torch.bfloat16).contiguous(memory_format=cl), B.to(torch.bfloat16).contiguous(memory_format=cl)
+
+
+def g_grads(G, D, a, b):
+    from p2p_pytorch_amd.models import GANLoss
+    from p2p_pytorch_amd.ops import l1
+    crit = GANLoss(gan_mode="vanilla")
+    fake = G(a)
+    loss = crit(D((a, fake)), True) + 100 * l1(fake, b)
+    loss.backward()
+    return loss
+
+
+def main():
+    import p2p_pytorch_amd as p2p
+    from p2p_pytorch_amd.engine.pix2pix import Pix2PixStep, set_requires_grad
+    from p2p_pytorch_amd.ops import hip
+    from p2p_pytorch_amd.parallel import GradReducer
+    from p2p_pytorch_amd.parallel import dist as pdist
+    p2p.set_backend("native")
+    world, rank, local_rank = pdist.init_from_env()
+    dev = pdist.local_device(local_rank)
+    torch.cuda.set_device(dev)
+    per = 2
+    A, B = data(world, dev, per)
+    a, b = A[per * rank:per * (rank + 1)], B[per * rank:per * (rank + 1)]
+
+    # ---- reduced G gradient == single-process gradient of the global batch
+    G, D = build(100 + rank, dev)
+    pdist.broadcast_module(G)
+    pdist.broadcast_module(D)
+    red = GradReducer(G, bucket_mb=0.5)
+    set_requires_grad(D, False)
+    hip.begin_step()
+    red.zero_grad()
+    g_grads(G, D, a, b)
+    red.finish()
+    got = {n: p.grad.detach().float().clone() for n, p in G.named_parameters()}
+    worst = 0.0
+    errs = []
+    if rank == 0:
+        G1, D1 = build(100, dev)
+        set_requires_grad(D1, False)
+        hip.begin_step()
+        g_grads(G1, D1, A, B)
+        for n, p in G1.named_parameters():
+            ref = p.grad.float()
+            scale = ref.abs().max().item()
+            if scale < 1e-8 and got[n].abs().max().item() < 1e-8:
+                continue        # exactly-zero grads (biases of norm-fed convs)
+            err = ((got[n] - ref).abs().max() / max(scale, 1e-12)).item()
+            errs.append((err, n, scale))
+            worst = max(worst, err)
+        errs.sort(reverse=True)
+    # ---- full training steps with both reducers: parameters stay identical across ranks
+    G, D = build(200 + rank, dev)
+    pdist.broadcast_module(G)
+    pdist.broadcast_module(D)
+    step = Pix2PixStep(G, D, reducer_g=GradReducer(G, bucket_mb=0.5), reducer_d=GradReducer(D, bucket_mb=0.5))
+    for _ in range(2):
+        losses = step.step(a, b)
+    torch.cuda.synchronize()
+    flat = torch.cat([p.detach().reshape(-1) for p in list(G.parameters()) + list(D.parameters())])
+    gathered = [torch.zeros_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    same = all(torch.equal(gathered[0], t) for t in gathered)
+    finite = all(torch.isfinite(v).all().item() for v in losses.values())
+    ok = same and finite and worst < 3e-2
+    if rank == 0:
+        print(json.dumps({"world": world, "backend": dist.get_backend(), "grad_rel_err_vs_global_batch": worst,
+                          "worst_params": errs[:4],
+                          "params_identical": same, "losses_finite": finite, "ok": ok}), flush=True)
+    pdist.destroy()
+    sys.exit(0 if ok else 1)
+
+
+if __name__ == "__main__":
+    main()

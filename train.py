@@ -109,7 +109,7 @@ def main(argv=None):
     use_cuda = (opt.cuda or world > 1 or opt.backend == "native") and torch.cuda.is_available()
     if opt.cuda and not torch.cuda.is_available():
         raise Exception("No GPU found, please run without --cuda")
-    device = torch.device("cuda", local_rank) if use_cuda else torch.device("cpu")
+    device = pdist.local_device(local_rank) if use_cuda else torch.device("cpu")
     if use_cuda:
         torch.cuda.set_device(device)
     p2p.set_backend(opt.backend or "native")
