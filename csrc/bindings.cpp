@@ -325,7 +325,10 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   }
   Tensor ws;
   if (splits > 1) {
-    ws = at::zeros({N * OH * OW, Cout}, obf.options().dtype(at::kFloat));
+    // P2P_DETERMINISTIC=1: per-split slabs reduced in order instead of fp32 atomics
+    const char* dv = std::getenv("P2P_DETERMINISTIC");
+    a.det = (dv && dv[0] == '1') ? 1 : 0;
+    ws = at::zeros({a.det ? splits : 1, N * OH * OW, Cout}, obf.options().dtype(at::kFloat));
     a.ws = ws.data_ptr<float>();
     a.splits = splits;
   }

@@ -30,6 +30,8 @@ struct ConvFwdArgs {
   int act_bwd;
   float* ws;       // split-K fp32 accumulator [N*OH*OW][Cout] (pre-zeroed) when splits > 1
   int splits;
+  int det;         // deterministic split-K: per-split slabs ws[split][N*OH*OW][Cout] (plain
+                   // stores), summed in split order by the finalize -- bitwise repeatable
   const void* zero;  // >= 16 zero bytes in global memory (global_load_lds padding source)
   // Normalisation statistics fused into the epilogue (null = off): every BM-row tile (all
   // rows inside one image and one parity class -- host-checked) writes the per-channel

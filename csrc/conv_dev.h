@@ -69,6 +69,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
 
   // ---- split-K: fp32 atomics straight from the accumulators (tiny-M layers only)
   if (a.splits > 1) {
+    float* wsb = a.det ? a.ws + (long)(blockIdx.z % a.splits) * a.N * a.OH * a.OW * a.Cout : a.ws;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -79,7 +80,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = rowb + r;
-          if (m < g.Mc) atomicAdd(a.ws + out_pix(m) * a.Cout + col, acc[i][j][r]);
+          if (m < g.Mc) {
+            if (a.det) wsb[out_pix(m) * a.Cout + col] = acc[i][j][r];
+            else atomicAdd(a.ws + out_pix(m) * a.Cout + col, acc[i][j][r]);
+          }
         }
       }
     return;

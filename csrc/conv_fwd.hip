@@ -266,8 +266,15 @@ __global__ void __launch_bounds__(256) conv_finalize_kernel(ConvFwdArgs a, long 
   for (long c = blockIdx.x * 256L + threadIdx.x; c < nchunks; c += (long)gridDim.x * 256) {
     const long pix = c / (a.Cout / 8);
     const int co = (int)(c - pix * (a.Cout / 8)) * 8;
-    const f32x4 v0 = *reinterpret_cast<const f32x4*>(a.ws + pix * a.Cout + co);
-    const f32x4 v1 = *reinterpret_cast<const f32x4*>(a.ws + pix * a.Cout + co + 4);
+    f32x4 v0 = *reinterpret_cast<const f32x4*>(a.ws + pix * a.Cout + co);
+    f32x4 v1 = *reinterpret_cast<const f32x4*>(a.ws + pix * a.Cout + co + 4);
+    if (a.det) {  // per-split slabs, summed in split order
+      for (int s = 1; s < a.splits; ++s) {
+        const float* w = a.ws + (long)s * P * a.Cout + pix * a.Cout + co;
+        v0 += *reinterpret_cast<const f32x4*>(w);
+        v1 += *reinterpret_cast<const f32x4*>(w + 4);
+      }
+    }
     float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
     if (a.bias) {
 #pragma unroll

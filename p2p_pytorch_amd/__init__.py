@@ -4,8 +4,10 @@ optimizer hot path, RCCL-over-xGMI data parallelism, and reference-compatible
 ``train.py`` / ``test.py`` / ``networks.py`` entrypoints.
 """
 from . import _native
-from ._native import get_backend, set_backend
+from ._native import get_backend, is_deterministic, set_backend, set_deterministic
+from .ops.fp8 import get_precision, set_precision
 
 __version__ = "0.1.0"
 
-__all__ = ["_native", "get_backend", "set_backend", "__version__"]
+__all__ = ["_native", "get_backend", "set_backend", "set_deterministic", "is_deterministic",
+           "get_precision", "set_precision", "__version__"]

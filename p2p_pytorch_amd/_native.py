@@ -42,6 +42,17 @@ def get_backend() -> str:
     return _backend
 
 
+def set_deterministic(flag: bool = True) -> None:
+    """Bitwise-repeatable HIP kernels: the conv split-K reduction switches from fp32 atomics
+    to per-split slabs summed in a fixed order (every other reduction in the extension --
+    wgrad slabs, norm / loss / column-sum partials -- is already order-fixed)."""
+    os.environ["P2P_DETERMINISTIC"] = "1" if flag else "0"
+
+
+def is_deterministic() -> bool:
+    return os.environ.get("P2P_DETERMINISTIC", "0") == "1"
+
+
 def load() -> bool:
     """Load the extension once; returns True when ``torch.ops.p2p`` is available."""
     global _loaded, _load_error

@@ -660,6 +660,17 @@ def new_salt() -> int:
     return next(_salt) & 0x7FFFFFFF
 
 
+def reset_rng(seed: int | None = None) -> None:
+    """Restart the dropout stream: device seeds re-derived from ``seed`` (default: torch's
+    initial seed) and the per-call salt counter rewound -- two runs from the same seed
+    draw identical masks (determinism tests, resume)."""
+    global _salt
+    _seeds.clear()
+    _salt = itertools.count(1)
+    if seed is not None:
+        torch.manual_seed(seed)
+
+
 def dropout(x, p, salt=None):
     return DropoutFn.apply(x, float(p), new_salt() if salt is None else int(salt))
 

@@ -72,6 +72,10 @@ def build_parser():
     p.add_argument("--steps_per_epoch", type=int, default=100, help="synthetic steps per epoch")
     p.add_argument("--device_cache", action="store_true",
                    help="decode the training set once into GPU memory (uint8) and batch there")
+    p.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
+                   help="(native) conv GEMM operand precision: bf16, or fp8 (e4m3 fwd / e5m2 dgrad)")
+    p.add_argument("--deterministic", action="store_true",
+                   help="(native) bitwise-repeatable kernels (ordered split-K reduction)")
     p.add_argument("--graph", action="store_true", help="capture the training step in a hipGraph")
     p.add_argument("--bucket_mb", type=float, default=64.0, help="gradient all-reduce bucket size")
     p.add_argument("--train_c", action="store_true",
@@ -113,6 +117,9 @@ def main(argv=None):
     if use_cuda:
         torch.cuda.set_device(device)
     p2p.set_backend(opt.backend or "native")
+    p2p.set_precision(opt.precision)
+    if opt.deterministic:
+        p2p.set_deterministic(True)
     if rank == 0:
         print(opt)
     torch.manual_seed(opt.seed)
