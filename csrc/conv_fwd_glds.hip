@@ -327,20 +327,21 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
     const bf16* A = As + stage * BM * BK;
     const bf16* B = Bs + stage * BN * BK;
     // fragments of both 32-deep halves are read up front (double-buffered registers) so
-    // the second half's LDS latency hides behind the first half's MFMAs
+    // the second half's LDS latency hides behind the first half's MFMAs; per half the B
+    // fragments come first (every MFMA row needs all of them)
     bf16x8 af[2][TM], bfr[2][TN];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int chunk = kk * 4 + (lane >> 4);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * TM * 16 + i * 16 + (lane & 15);
-        af[kk][i] = *reinterpret_cast<const bf16x8*>(A + swz(row, chunk));
-      }
-#pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * TN * 16 + j * 16 + (lane & 15);
         bfr[kk][j] = *reinterpret_cast<const bf16x8*>(B + swz(row, chunk));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * TM * 16 + i * 16 + (lane & 15);
+        af[kk][i] = *reinterpret_cast<const bf16x8*>(A + swz(row, chunk));
       }
     }
 #pragma unroll

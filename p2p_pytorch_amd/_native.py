@@ -19,7 +19,8 @@ import threading
 import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_C")
-LIB_PATH = os.path.join(_LIB_DIR, "libp2p_hip.so")
+# P2P_LIB: an alternative build of the extension (kernel A/B experiments, tools/build_ext.py --out)
+LIB_PATH = os.environ.get("P2P_LIB") or os.path.join(_LIB_DIR, "libp2p_hip.so")
 
 _lock = threading.Lock()
 _loaded = False

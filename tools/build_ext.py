@@ -69,12 +69,19 @@ def _compile(src, flags, hh, force, verbose):
     return obj, True
 
 
-def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
+def build(jobs: int = 8, force: bool = False, verbose: bool = False, defines=(), out: str | None = None) -> str:
+    """defines: extra -D macros (kernel experiments); out: alternative .so path (objects
+    go to their own build dir), loaded with P2P_LIB=<path>."""
+    global BUILD, OUT
+    if out:
+        tag = hashlib.sha256(" ".join(defines).encode()).hexdigest()[:8]
+        BUILD = os.path.join(ROOT, "build", "hip_" + tag)
+        OUT = os.path.abspath(out)
     os.makedirs(BUILD, exist_ok=True)
-    os.makedirs(OUT_DIR, exist_ok=True)
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
     inc, lib, abi = _torch_paths()
     hh = _headers_hash()
-    common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}", "-Wno-unused-result"]
+    common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}", "-Wno-unused-result"] + [f"-D{d}" for d in defines]
     hip_flags = common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
     cpp_flags = common + [f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__=1",
                           "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=p2p_hip",
@@ -111,8 +118,10 @@ def main():
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--define", action="append", default=[], help="extra -D macro (repeatable)")
+    ap.add_argument("--out", default=None, help="alternative output .so (load with P2P_LIB)")
     a = ap.parse_args()
-    print(build(a.jobs, a.force, a.verbose))
+    print(build(a.jobs, a.force, a.verbose, a.define, a.out))
 
 
 if __name__ == "__main__":
