@@ -40,6 +40,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batch", type=int, default=128, help="images per GPU (the eager baseline was measured at 128)")
     p.add_argument("--size", type=int, default=256)
+    p.add_argument("--family", default="pix2pix", choices=["pix2pix", "ref"],
+                   help="pix2pix: the headline U-Net + PatchGAN step (BASELINE.json); ref: the reference "
+                        "repo's own compression GAN step (C + ExpandNet G + 3-scale SN PatchGAN + VGG19 loss, "
+                        "train.py:291-414), measured for parity, not the headline")
     p.add_argument("--netG", default="unet_256")
     p.add_argument("--netD", default="basic")
     p.add_argument("--impl", default=os.environ.get("P2P_BACKEND", "native"), choices=["native", "torch"])
@@ -78,8 +82,16 @@ def main():
         torch.backends.cudnn.benchmark = True
     torch.manual_seed(123 + rank)
 
-    netG = define_G(netG=args.netG, gpu_id=dev, verbose=False)
-    netD = define_D(6, 64, norm="instance", netD=args.netD, gpu_id=dev, verbose=False)
+    ref = args.family == "ref"
+    if ref:
+        from p2p_pytorch_amd.models import define_C
+        netG = define_G(netG="expand", gpu_id=dev, verbose=False)
+        netD = define_D(6, 64, gpu_id=dev, netD="multiscale", verbose=False)
+        netC = define_C(gpu_id=dev, verbose=False)
+        pdist.broadcast_module(netC)
+    else:
+        netG = define_G(netG=args.netG, gpu_id=dev, verbose=False)
+        netD = define_D(6, 64, norm="instance", netD=args.netD, gpu_id=dev, verbose=False)
     pdist.broadcast_module(netG)
     pdist.broadcast_module(netD)
 
@@ -99,9 +111,13 @@ def main():
         act_dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
         mf = torch.channels_last
         autocast = None
-    trainer = Pix2PixStep(netG, netD, lr=2e-4, beta1=0.5, gan_mode=args.gan_mode,
-                          lambda_L1=args.lamb, reducer_g=reducer_g, reducer_d=reducer_d,
-                          autocast_dtype=autocast)
+    if ref:
+        from p2p_pytorch_amd.engine.compress_gan import CompressGANStep
+        trainer = CompressGANStep(netG, netD, netC, reducer_g=reducer_g, reducer_d=reducer_d)
+    else:
+        trainer = Pix2PixStep(netG, netD, lr=2e-4, beta1=0.5, gan_mode=args.gan_mode,
+                              lambda_L1=args.lamb, reducer_g=reducer_g, reducer_d=reducer_d,
+                              autocast_dtype=autocast)
 
     B, S = args.batch, args.size
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
@@ -139,8 +155,11 @@ def main():
 
     img_s = world * B * args.steps / dt_max
     base = EAGER_BASELINE_IMG_S_PER_GPU
+    model = (f"pix2pix {args.netG} + PatchGAN {args.netD} (70x70)" if not ref else
+             "reference compression GAN: CompressionNetwork + ExpandNetwork + 3-scale SN PatchGAN + VGG19 loss")
     out = {
-        "metric": f"train images/sec (whole node), {S}x{S} pix2pix U-Net+PatchGAN",
+        "metric": (f"train images/sec (whole node), {S}x{S} pix2pix U-Net+PatchGAN" if not ref else
+                   f"train images/sec (whole node), {S}x{S} reference compression GAN"),
         "value": round(img_s, 2),
         "unit": "images/sec",
         "n_gpus": world,
@@ -149,10 +168,10 @@ def main():
         "ms_per_step": round(1000.0 * dt_max / args.steps, 3),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(img_s / (base * world), 3) if base else None,
+        "vs_baseline": round(img_s / (base * world), 3) if (base and not ref) else None,
         "dtype": "fp8+bf16" if args.precision == "fp8" else "bf16",
         "data": "synthetic (random paired images, random-init weights)",
-        "config": {"model": f"pix2pix {args.netG} + PatchGAN {args.netD} (70x70)",
+        "config": {"model": model,
                    "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
                    "image_size": S, "parallelism": f"dp{world}", "impl": args.impl,
                    "gan_mode": args.gan_mode, "lambda_L1": args.lamb,
