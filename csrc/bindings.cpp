@@ -20,6 +20,9 @@
 #include "conv.h"
 
 extern "C" {
+long p2p_sn_ws_floats(int h, int wd);
+int p2p_sn_power_iter(const float* W, int h, int wd, float* u, float* v, float* sigma, float* ws,
+                      hipStream_t st);
 long p2p_norm_ws_floats(int N, int HW, int C);
 int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, const float* partials,
                           float eps, const float* gamma, const float* beta, const float* prelu_w,
@@ -885,6 +888,23 @@ Tensor slice_channels(const Tensor& x, int64_t c0, int64_t C) {
 }
 
 // out[c] (+)= scale * sum over all pixels of x[..., c]   (bias gradient)
+// ------------------------------------------------------------------ spectral norm (csrc/sn.hip)
+// one power iteration on W [h][wd] (fp32): v <- l2n(W^T u), u <- l2n(W v) in place; returns
+// sigma = u . (W v) as a 0-dim fp32 tensor
+Tensor sn_power_iter(const Tensor& w, Tensor u, Tensor v) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.dim() == 2,
+              "sn_power_iter: fp32 contiguous [h][wd] weight");
+  const int64_t h = w.size(0), wd = w.size(1);
+  TORCH_CHECK(u.scalar_type() == at::kFloat && u.is_contiguous() && u.numel() == h, "sn_power_iter: u");
+  TORCH_CHECK(v.scalar_type() == at::kFloat && v.is_contiguous() && v.numel() == wd, "sn_power_iter: v");
+  Tensor ws = at::empty({p2p_sn_ws_floats((int)h, (int)wd)}, w.options());
+  Tensor sigma = at::empty({}, w.options());
+  check_rc(p2p_sn_power_iter(w.data_ptr<float>(), (int)h, (int)wd, u.data_ptr<float>(), v.data_ptr<float>(),
+                             sigma.data_ptr<float>(), ws.data_ptr<float>(), cur_stream(w)),
+           "sn_power_iter");
+  return sigma;
+}
+
 // ------------------------------------------------------------------ fp8 (csrc/fp8.hip)
 
 Tensor fp8_quant(const Tensor& x, Tensor site, int64_t fmt, int64_t use_cur) {
@@ -1055,6 +1075,7 @@ TORCH_LIBRARY(p2p, m) {
         "Tensor? xb1, Tensor? xb2, int act_bwd, int Cvalid=0, bool want_stats=False, Tensor? qs_x1=None, "
         "Tensor? qs_x2=None, Tensor? qs_w=None, Tensor(a!)? y_qsite=None, int y_qfmt=0) -> Tensor[]");
   m.def("fp8_quant(Tensor x, Tensor(a!) site, int fmt, int use_cur=0) -> Tensor");
+  m.def("sn_power_iter(Tensor w, Tensor(a!) u, Tensor(b!) v) -> Tensor");
   m.def("fp8_amax(Tensor x, Tensor(a!) site, int slot) -> ()");
   m.def("fp8_roll(Tensor(a!) sites) -> ()");
   m.def("fp8_amax_multi(Tensor[] x, Tensor(a!) sites, int[] idx) -> ()");
@@ -1098,6 +1119,7 @@ TORCH_LIBRARY(p2p, m) {
 TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("conv_fwd", conv_fwd);
   m.impl("fp8_quant", fp8_quant);
+  m.impl("sn_power_iter", sn_power_iter);
   m.impl("fp8_amax", fp8_amax);
   m.impl("fp8_roll", fp8_roll);
   m.impl("fp8_amax_multi", fp8_amax_multi);

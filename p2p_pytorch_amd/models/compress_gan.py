@@ -22,8 +22,13 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .. import ops
+from .. import _native, ops
 from .layers import BatchNorm2d, Conv2d
+
+
+def ops_hip():
+    from ..ops import hip   # imported lazily: it touches torch.ops.p2p
+    return hip
 
 
 class PReLU(nn.PReLU):
@@ -195,6 +200,10 @@ class SpectralNorm(nn.Module):
         # raising an in-place-modification error.
         # fp32 always (also under an autocast region: sigma is a norm, and u / v are state)
         with torch.autocast(device_type=w.device.type, enabled=False):
+            if w.is_cuda and _native.use_native(w):
+                # HIP power iteration (csrc/sn.hip): 4 short launches, u / v in place
+                sigma = ops_hip().spectral_sigma(w2, u, v, self.power_iterations)
+                return w / sigma
             for _ in range(self.power_iterations):
                 v.data = l2normalize(torch.mv(w2.detach().t(), u.data))
                 u.data = l2normalize(torch.mv(w2.detach(), v.data))

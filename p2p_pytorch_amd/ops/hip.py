@@ -444,6 +444,34 @@ def conv_transpose2d(x, weight, bias=None, stride=2, padding=1, act_in=None, act
     return ConvFn.apply(x1, x2, weight, bias, cfg)
 
 
+# ============================================================== spectral norm
+class SigmaFn(torch.autograd.Function):
+    """sigma of the spectral-norm power iteration (csrc/sn.hip), u / v updated in place.
+
+    Backward: d sigma / d W = u v^T.  u and v are held by reference, not saved: like the
+    reference's ``.data`` swaps (networks.py:543-546), a backward through an earlier forward
+    of the step sees the newest u / v."""
+
+    @staticmethod
+    def forward(ctx, w2, u, v, iters):
+        w = w2.detach()
+        w = w if (w.dtype == torch.float32 and w.is_contiguous()) else w.float().contiguous()
+        sigma = None
+        for _ in range(max(1, int(iters))):
+            sigma = P().sn_power_iter(w, u.data, v.data)
+        ctx.uv = (u, v)
+        return sigma
+
+    @staticmethod
+    def backward(ctx, g):
+        u, v = ctx.uv
+        return g * torch.outer(u.detach(), v.detach()), None, None, None
+
+
+def spectral_sigma(w2, u, v, iters=1):
+    return SigmaFn.apply(w2, u, v, iters)
+
+
 # ============================================================== normalisation
 class NormFn(torch.autograd.Function):
     @staticmethod

@@ -560,3 +560,28 @@ def test_conv_epilogue_norm_stats(kind, N, C, H, Cout, norm):
         outs.append(z.float())
         assert not hip._stats_stash
     assert rel_err(outs[1], outs[0]) < 1e-2
+
+
+@pytest.mark.parametrize("h,wd", [(128, 1024), (512, 4096), (3, 70)])
+def test_spectral_norm_power_iteration(h, wd):
+    """csrc/sn.hip vs the reference's power iteration (networks.py:537-549) in fp32."""
+    from p2p_pytorch_amd.ops import hip
+    g = torch.Generator(device=DEV).manual_seed(9)
+    W = (torch.randn(h, wd, device=DEV, generator=g) * 0.05).requires_grad_(True)
+    u0 = torch.randn(h, device=DEV, generator=g)
+    v0 = torch.randn(wd, device=DEV, generator=g)
+    u0, v0 = u0 / (u0.norm() + 1e-12), v0 / (v0.norm() + 1e-12)
+    u, v = u0.clone(), v0.clone()
+    sig = hip.spectral_sigma(W, u, v, 1)
+    (sig * 3.0).backward()
+    # oracle
+    vr = W.detach().t().mv(u0)
+    vr = vr / (vr.norm() + 1e-12)
+    ur = W.detach().mv(vr)
+    ur = ur / (ur.norm() + 1e-12)
+    sr = torch.dot(ur, W.detach().mv(vr))
+    torch.cuda.synchronize()
+    assert torch.allclose(v, vr, rtol=1e-4, atol=1e-6)
+    assert torch.allclose(u, ur, rtol=1e-4, atol=1e-6)
+    assert abs(sig.item() - sr.item()) <= 1e-5 * abs(sr.item())
+    assert torch.allclose(W.grad, 3.0 * torch.outer(ur, vr), rtol=1e-4, atol=1e-7)
