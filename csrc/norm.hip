@@ -118,6 +118,23 @@ __global__ void __launch_bounds__(256) norm_partial_kernel(const bf16* __restric
   }
 }
 
+// Chunk-partial reductions (finalize passes): one block per (32-channel tile, group n);
+// thread (j, c) = (tid / 32, tid % 32) merges chunks j, j+8, j+16, ... of channel c0 + c in
+// order, then the 8 partial results merge through LDS in a fixed tree -- deterministic, and
+// parallel over chunks (BN has ~1-2k chunks per channel: a thread-per-channel serial merge
+// cost 300 us per call on the family-R step).
+constexpr int FIN_CT = 32, FIN_J = 8;
+
+// Chan's merge of (cnt, mean, M2) partials
+__device__ __forceinline__ void chan_merge(float& cA, float& mA, float& qA, float cB, float mB, float qB) {
+  const float tot = cA + cB;
+  if (tot <= 0.f) return;
+  const float d = mB - mA;
+  mA += d * (cB / tot);
+  qA += qB + d * d * (cA * cB / tot);
+  cA = tot;
+}
+
 // stats: [N][C] mean, [N][C] rstd (fp32).  bn: running stats update (N == 1).
 __global__ void __launch_bounds__(256) norm_finalize_kernel(const float* __restrict__ ws, NormGeom g,
                                                             float eps, float* __restrict__ mean_out,
@@ -125,29 +142,75 @@ __global__ void __launch_bounds__(256) norm_finalize_kernel(const float* __restr
                                                             float* __restrict__ run_mean,
                                                             float* __restrict__ run_var,
                                                             float momentum) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= g.N * g.C) return;
-  const int n = i / g.C, c = i % g.C;
-  const float* mb = ws + (long)n * g.nchunks * g.C + c;
-  const float* m2 = mb + (long)g.N * g.nchunks * g.C;
+  __shared__ float sc[FIN_J][FIN_CT], sm[FIN_J][FIN_CT], sq[FIN_J][FIN_CT];
+  const int n = blockIdx.y;
+  const int cl = threadIdx.x % FIN_CT, j = threadIdx.x / FIN_CT;
+  const int c = blockIdx.x * FIN_CT + cl;
   float cntA = 0.f, meanA = 0.f, M2A = 0.f;
-  for (int b = 0; b < g.nchunks; ++b) {
-    const float cntB = (float)min(g.chunk, g.HW - b * g.chunk);
-    const float meanB = mb[(long)b * g.C], M2B = m2[(long)b * g.C];
-    const float tot = cntA + cntB;
-    const float d = meanB - meanA;
-    meanA += d * (cntB / tot);
-    M2A += M2B + d * d * (cntA * cntB / tot);
-    cntA = tot;
+  if (c < g.C) {
+    const float* mb = ws + (long)n * g.nchunks * g.C + c;
+    const float* m2 = mb + (long)g.N * g.nchunks * g.C;
+    for (int b = j; b < g.nchunks; b += FIN_J)
+      chan_merge(cntA, meanA, M2A, (float)min(g.chunk, g.HW - b * g.chunk), mb[(long)b * g.C], m2[(long)b * g.C]);
   }
-  const float var = M2A / cntA;
-  mean_out[i] = meanA;
-  rstd_out[i] = rsqrtf(var + eps);
-  if (run_mean) {
-    const float unb = cntA > 1.f ? M2A / (cntA - 1.f) : var;
-    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * meanA;
-    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+  sc[j][cl] = cntA;
+  sm[j][cl] = meanA;
+  sq[j][cl] = M2A;
+  __syncthreads();
+  for (int w = FIN_J / 2; w > 0; w >>= 1) {
+    if (j < w) {
+      float cA = sc[j][cl], mA = sm[j][cl], qA = sq[j][cl];
+      chan_merge(cA, mA, qA, sc[j + w][cl], sm[j + w][cl], sq[j + w][cl]);
+      sc[j][cl] = cA;
+      sm[j][cl] = mA;
+      sq[j][cl] = qA;
+    }
+    __syncthreads();
   }
+  if (j == 0 && c < g.C) {
+    cntA = sc[0][cl];
+    meanA = sm[0][cl];
+    M2A = sq[0][cl];
+    const int i = n * g.C + c;
+    const float var = M2A / cntA;
+    mean_out[i] = meanA;
+    rstd_out[i] = rsqrtf(var + eps);
+    if (run_mean) {
+      const float unb = cntA > 1.f ? M2A / (cntA - 1.f) : var;
+      run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * meanA;
+      run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+    }
+  }
+}
+
+// sums of the two [N][nchunks][C] partial planes over chunks (and, ngroups > 1, over the
+// groups n0 .. n0+ngroups-1): block-parallel, fixed order
+__device__ __forceinline__ void chunk_sums(const float* __restrict__ ws, const NormGeom& g, int n0, int ngroups,
+                                           int c, int j, float& sa, float& sb, float (*ra)[FIN_CT],
+                                           float (*rb)[FIN_CT], int cl) {
+  sa = 0.f;
+  sb = 0.f;
+  if (c < g.C)
+    for (int n = n0; n < n0 + ngroups; ++n) {
+      const float* a = ws + (long)n * g.nchunks * g.C + c;
+      const float* b = a + (long)g.N * g.nchunks * g.C;
+      for (int k = j; k < g.nchunks; k += FIN_J) {
+        sa += a[(long)k * g.C];
+        sb += b[(long)k * g.C];
+      }
+    }
+  ra[j][cl] = sa;
+  rb[j][cl] = sb;
+  __syncthreads();
+  for (int w = FIN_J / 2; w > 0; w >>= 1) {
+    if (j < w) {
+      ra[j][cl] += ra[j + w][cl];
+      rb[j][cl] += rb[j + w][cl];
+    }
+    __syncthreads();
+  }
+  sa = ra[0][cl];
+  sb = rb[0][cl];
 }
 
 // y = act((x - mean) * rstd * gamma + beta); mean/rstd indexed [n][c] (BN: n == 0 always).
@@ -328,16 +391,14 @@ __global__ void __launch_bounds__(256) norm_bwd_finalize_kernel(const float* __r
                                                                 const float* __restrict__ rstd,
                                                                 const float* __restrict__ gamma,
                                                                 float* __restrict__ coef) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= g.N * g.C) return;
-  const int n = i / g.C, c = i % g.C;
-  const float* a = ws + (long)n * g.nchunks * g.C + c;
-  const float* b = a + (long)g.N * g.nchunks * g.C;
-  float sdy = 0.f, sdx = 0.f;
-  for (int k = 0; k < g.nchunks; ++k) {
-    sdy += a[(long)k * g.C];
-    sdx += b[(long)k * g.C];
-  }
+  __shared__ float ra[FIN_J][FIN_CT], rb[FIN_J][FIN_CT];
+  const int n = blockIdx.y;
+  const int cl = threadIdx.x % FIN_CT, j = threadIdx.x / FIN_CT;
+  const int c = blockIdx.x * FIN_CT + cl;
+  float sdy, sdx;
+  chunk_sums(ws, g, n, 1, c, j, sdy, sdx, ra, rb, cl);
+  if (j != 0 || c >= g.C) return;
+  const int i = n * g.C + c;
   const float r = rstd[i];
   const float inv = 1.f / (float)g.HW;
   const float ga = gamma ? gamma[c] : 1.f;
@@ -351,17 +412,12 @@ __global__ void __launch_bounds__(256) norm_bwd_finalize_kernel(const float* __r
 __global__ void __launch_bounds__(256) norm_param_grad_kernel(const float* __restrict__ ws, NormGeom g,
                                                               float* __restrict__ dgamma,
                                                               float* __restrict__ dbeta) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= g.C) return;
-  float sdy = 0.f, sdx = 0.f;
-  for (int n = 0; n < g.N; ++n) {
-    const float* a = ws + (long)n * g.nchunks * g.C + c;
-    const float* b = a + (long)g.N * g.nchunks * g.C;
-    for (int k = 0; k < g.nchunks; ++k) {
-      sdy += a[(long)k * g.C];
-      sdx += b[(long)k * g.C];
-    }
-  }
+  __shared__ float ra[FIN_J][FIN_CT], rb[FIN_J][FIN_CT];
+  const int cl = threadIdx.x % FIN_CT, j = threadIdx.x / FIN_CT;
+  const int c = blockIdx.x * FIN_CT + cl;
+  float sdy, sdx;
+  chunk_sums(ws, g, 0, g.N, c, j, sdy, sdx, ra, rb, cl);
+  if (j != 0 || c >= g.C) return;
   dgamma[c] += sdx;
   dbeta[c] += sdy;
 }
@@ -472,7 +528,7 @@ int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* ga
   NormGeom g = make_geom(N, HW, C);
   hipLaunchKernelGGL(norm_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
                      static_cast<const bf16*>(x), g, ws);
-  hipLaunchKernelGGL(norm_finalize_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, ws, g, eps,
+  hipLaunchKernelGGL(norm_finalize_kernel, dim3((C + FIN_CT - 1) / FIN_CT, N), dim3(256), 0, st, ws, g, eps,
                      mean, rstd, run_mean, run_var, momentum);
   if (y)
     hipLaunchKernelGGL(norm_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
@@ -496,8 +552,8 @@ int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, cons
   pg.C = C;
   pg.chunk = HW / nchunks;
   pg.nchunks = nchunks;
-  hipLaunchKernelGGL(norm_finalize_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, partials, pg, eps,
-                     mean, rstd, run_mean, run_var, momentum);
+  hipLaunchKernelGGL(norm_finalize_kernel, dim3((C + FIN_CT - 1) / FIN_CT, N), dim3(256), 0, st, partials, pg,
+                     eps, mean, rstd, run_mean, run_var, momentum);
   NormGeom g = make_geom(N, HW, C);
   hipLaunchKernelGGL(norm_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st, static_cast<const bf16*>(x), g,
                      mean, rstd, gamma, beta, prelu_w, act, static_cast<bf16*>(y),
@@ -531,13 +587,13 @@ int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const floa
   if (dgamma) {
     hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st, xb, db, g, mean,
                        rstd, gamma, beta, act, 0, ws);
-    hipLaunchKernelGGL(norm_param_grad_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, g,
+    hipLaunchKernelGGL(norm_param_grad_kernel, dim3((C + FIN_CT - 1) / FIN_CT), dim3(256), 0, st, ws, g,
                        dgamma, dbeta);
   }
   if (dx) {
     hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st, xb, db, g, mean,
                        rstd, gamma, beta, act, 1, ws);
-    hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, ws, g,
+    hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((C + FIN_CT - 1) / FIN_CT, N), dim3(256), 0, st, ws, g,
                        rstd, gamma, coef);
     hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st, xb, db, g, mean,
                        rstd, gamma, beta, act, coef, static_cast<bf16*>(dx),
