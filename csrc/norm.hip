@@ -118,12 +118,13 @@ __global__ void __launch_bounds__(256) norm_partial_kernel(const bf16* __restric
   }
 }
 
-// Chunk-partial reductions (finalize passes): one block per (32-channel tile, group n);
-// thread (j, c) = (tid / 32, tid % 32) merges chunks j, j+8, j+16, ... of channel c0 + c in
-// order, then the 8 partial results merge through LDS in a fixed tree -- deterministic, and
+// Chunk-partial reductions (finalize passes): one block per (CT-channel tile, group n);
+// thread (j, c) = (tid / CT, tid % CT) merges chunks j, j+J, j+2J, ... of channel c0 + c in
+// order, then the J partial results merge through LDS in a fixed tree -- deterministic, and
 // parallel over chunks (BN has ~1-2k chunks per channel: a thread-per-channel serial merge
 // cost 300 us per call on the family-R step).
-constexpr int FIN_CT = 32, FIN_J = 8;
+// CT channels x J chunk-lanes per block: (32, 8) for instance norm (few chunks per group),
+// (8, 32) when a group has hundreds of chunks (batch norm over N*H*W pixels)
 
 // Chan's merge of (cnt, mean, M2) partials
 __device__ __forceinline__ void chan_merge(float& cA, float& mA, float& qA, float cB, float mB, float qB) {
@@ -136,6 +137,7 @@ __device__ __forceinline__ void chan_merge(float& cA, float& mA, float& qA, floa
 }
 
 // stats: [N][C] mean, [N][C] rstd (fp32).  bn: running stats update (N == 1).
+template <int FIN_CT, int FIN_J>
 __global__ void __launch_bounds__(256) norm_finalize_kernel(const float* __restrict__ ws, NormGeom g,
                                                             float eps, float* __restrict__ mean_out,
                                                             float* __restrict__ rstd_out,
@@ -185,6 +187,7 @@ __global__ void __launch_bounds__(256) norm_finalize_kernel(const float* __restr
 
 // sums of the two [N][nchunks][C] partial planes over chunks (and, ngroups > 1, over the
 // groups n0 .. n0+ngroups-1): block-parallel, fixed order
+template <int FIN_CT, int FIN_J>
 __device__ __forceinline__ void chunk_sums(const float* __restrict__ ws, const NormGeom& g, int n0, int ngroups,
                                            int c, int j, float& sa, float& sb, float (*ra)[FIN_CT],
                                            float (*rb)[FIN_CT], int cl) {
@@ -386,6 +389,7 @@ __global__ void __launch_bounds__(256) norm_bwd_partial_kernel(
 }
 
 // coef: [N][C] A, [N][C] B, [N][C] Cc  with dx = A*dy_eff + B + Cc*xhat
+template <int FIN_CT, int FIN_J>
 __global__ void __launch_bounds__(256) norm_bwd_finalize_kernel(const float* __restrict__ ws,
                                                                 NormGeom g,
                                                                 const float* __restrict__ rstd,
@@ -396,7 +400,7 @@ __global__ void __launch_bounds__(256) norm_bwd_finalize_kernel(const float* __r
   const int cl = threadIdx.x % FIN_CT, j = threadIdx.x / FIN_CT;
   const int c = blockIdx.x * FIN_CT + cl;
   float sdy, sdx;
-  chunk_sums(ws, g, n, 1, c, j, sdy, sdx, ra, rb, cl);
+  chunk_sums<FIN_CT, FIN_J>(ws, g, n, 1, c, j, sdy, sdx, ra, rb, cl);
   if (j != 0 || c >= g.C) return;
   const int i = n * g.C + c;
   const float r = rstd[i];
@@ -409,6 +413,7 @@ __global__ void __launch_bounds__(256) norm_bwd_finalize_kernel(const float* __r
 }
 
 // d(gamma) = sum(dy_eff * xhat), d(beta) = sum(dy_eff) over every group of the channel
+template <int FIN_CT, int FIN_J>
 __global__ void __launch_bounds__(256) norm_param_grad_kernel(const float* __restrict__ ws, NormGeom g,
                                                               float* __restrict__ dgamma,
                                                               float* __restrict__ dbeta) {
@@ -416,7 +421,7 @@ __global__ void __launch_bounds__(256) norm_param_grad_kernel(const float* __res
   const int cl = threadIdx.x % FIN_CT, j = threadIdx.x / FIN_CT;
   const int c = blockIdx.x * FIN_CT + cl;
   float sdy, sdx;
-  chunk_sums(ws, g, 0, g.N, c, j, sdy, sdx, ra, rb, cl);
+  chunk_sums<FIN_CT, FIN_J>(ws, g, 0, g.N, c, j, sdy, sdx, ra, rb, cl);
   if (j != 0 || c >= g.C) return;
   dgamma[c] += sdx;
   dbeta[c] += sdy;
@@ -492,6 +497,9 @@ __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
   if (sh.q) fp8_amax_commit(qmax, sh.site);
 }
 
+// finalize-pass launches: many chunks per group -> 8 channels x 32 chunk-lanes per block
+static inline bool fin_wide(const NormGeom& g) { return g.nchunks >= 64; }
+
 static inline NormGeom make_geom(int N, int HW, int C) {
   NormGeom g;
   g.N = N;
@@ -528,8 +536,12 @@ int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* ga
   NormGeom g = make_geom(N, HW, C);
   hipLaunchKernelGGL(norm_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
                      static_cast<const bf16*>(x), g, ws);
-  hipLaunchKernelGGL(norm_finalize_kernel, dim3((C + FIN_CT - 1) / FIN_CT, N), dim3(256), 0, st, ws, g, eps,
-                     mean, rstd, run_mean, run_var, momentum);
+  if (fin_wide(g))
+    hipLaunchKernelGGL((norm_finalize_kernel<8, 32>), dim3((C + 7) / 8, N), dim3(256), 0, st, ws, g, eps, mean,
+                       rstd, run_mean, run_var, momentum);
+  else
+    hipLaunchKernelGGL((norm_finalize_kernel<32, 8>), dim3((C + 31) / 32, N), dim3(256), 0, st, ws, g, eps, mean,
+                       rstd, run_mean, run_var, momentum);
   if (y)
     hipLaunchKernelGGL(norm_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
                        static_cast<const bf16*>(x), g, mean, rstd, gamma, beta, prelu_w, act,
@@ -552,8 +564,12 @@ int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, cons
   pg.C = C;
   pg.chunk = HW / nchunks;
   pg.nchunks = nchunks;
-  hipLaunchKernelGGL(norm_finalize_kernel, dim3((C + FIN_CT - 1) / FIN_CT, N), dim3(256), 0, st, partials, pg,
-                     eps, mean, rstd, run_mean, run_var, momentum);
+  if (fin_wide(pg))
+    hipLaunchKernelGGL((norm_finalize_kernel<8, 32>), dim3((C + 7) / 8, N), dim3(256), 0, st, partials, pg, eps,
+                       mean, rstd, run_mean, run_var, momentum);
+  else
+    hipLaunchKernelGGL((norm_finalize_kernel<32, 8>), dim3((C + 31) / 32, N), dim3(256), 0, st, partials, pg, eps,
+                       mean, rstd, run_mean, run_var, momentum);
   NormGeom g = make_geom(N, HW, C);
   hipLaunchKernelGGL(norm_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st, static_cast<const bf16*>(x), g,
                      mean, rstd, gamma, beta, prelu_w, act, static_cast<bf16*>(y),
@@ -587,14 +603,20 @@ int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const floa
   if (dgamma) {
     hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st, xb, db, g, mean,
                        rstd, gamma, beta, act, 0, ws);
-    hipLaunchKernelGGL(norm_param_grad_kernel, dim3((C + FIN_CT - 1) / FIN_CT), dim3(256), 0, st, ws, g,
-                       dgamma, dbeta);
+    if (fin_wide(g) || N > 8)
+      hipLaunchKernelGGL((norm_param_grad_kernel<8, 32>), dim3((C + 7) / 8), dim3(256), 0, st, ws, g, dgamma, dbeta);
+    else
+      hipLaunchKernelGGL((norm_param_grad_kernel<32, 8>), dim3((C + 31) / 32), dim3(256), 0, st, ws, g, dgamma, dbeta);
   }
   if (dx) {
     hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st, xb, db, g, mean,
                        rstd, gamma, beta, act, 1, ws);
-    hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((C + FIN_CT - 1) / FIN_CT, N), dim3(256), 0, st, ws, g,
-                       rstd, gamma, coef);
+    if (fin_wide(g))
+      hipLaunchKernelGGL((norm_bwd_finalize_kernel<8, 32>), dim3((C + 7) / 8, N), dim3(256), 0, st, ws, g, rstd,
+                         gamma, coef);
+    else
+      hipLaunchKernelGGL((norm_bwd_finalize_kernel<32, 8>), dim3((C + 31) / 32, N), dim3(256), 0, st, ws, g, rstd,
+                         gamma, coef);
     hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st, xb, db, g, mean,
                        rstd, gamma, beta, act, coef, static_cast<bf16*>(dx),
                        Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
