@@ -38,7 +38,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=128, help="images per GPU (the eager baseline was measured at 128)")
+    p.add_argument("--batch", type=int, default=256,
+                   help="images per GPU (sized for HBM; the eager baseline's best measured batch was 128)")
     p.add_argument("--size", type=int, default=256)
     p.add_argument("--family", default="pix2pix", choices=["pix2pix", "ref"],
                    help="pix2pix: the headline U-Net + PatchGAN step (BASELINE.json); ref: the reference "
@@ -137,8 +138,13 @@ def main():
         from p2p_pytorch_amd.engine.graph import CapturedStep
         # capture runs its own warmup steps on a side stream, then records one step
         step = CapturedStep(trainer.step, real_A, real_B, warmup=2)
-    for _ in range(args.warmup):
+    t_w = time.perf_counter()
+    for i in range(args.warmup):
         losses = step(real_A, real_B)
+        if rank == 0:   # heartbeat on stderr (eager cudnn.benchmark warmups can take minutes)
+            sync()
+            print(f"[bench] warmup {i + 1}/{args.warmup} {time.perf_counter() - t_w:.1f}s",
+                  file=sys.stderr, flush=True)
     sync()
     pdist.barrier()
     sync()
