@@ -694,7 +694,6 @@ Tensor norm_bwd(const Tensor& x, const Tensor& dy, const Tensor& mean, const Ten
 // ------------------------------------------------------------------ elementwise
 Tensor act(const Tensor& a, const optional<Tensor>& b, int64_t act, int64_t mode) {
   TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16, "act: bf16 GPU tensor");
-  TORCH_CHECK(a.numel() % 8 == 0, "act: numel % 8");
   const auto mf = a.is_contiguous(at::MemoryFormat::ChannelsLast) && a.dim() == 4
                       ? at::MemoryFormat::ChannelsLast
                       : at::MemoryFormat::Contiguous;

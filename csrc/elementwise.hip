@@ -34,7 +34,18 @@ static inline unsigned egrid(long work) {
 // dx = dy * act'(x)   (relu / lrelu, from the input)    mode 1
 // dx = dy * act'(y)   (tanh / sigmoid / relu, from the output)  mode 2
 __global__ void __launch_bounds__(256) act_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b,
-                                                  long n8, int act, int mode, bf16* __restrict__ out) {
+                                                  long n, int act, int mode, bf16* __restrict__ out) {
+  const long n8 = n / 8;
+  // scalar tail (numel % 8: e.g. a 1-channel PatchGAN logit map of odd size)
+  if (blockIdx.x == 0 && threadIdx.x < (n & 7)) {
+    const long i = n8 * 8 + threadIdx.x;
+    const float fa = (float)a[i];
+    float r;
+    if (mode == 0) r = act_fwd(fa, act);
+    else if (mode == 1) r = fa * act_grad_from_input((float)b[i], act);
+    else r = fa * act_grad_from_output((float)b[i], act);
+    out[i] = (bf16)r;
+  }
   for (long e = blockIdx.x * 256L + threadIdx.x; e < n8; e += (long)gridDim.x * 256) {
     float fa[8], fb[8];
     unpack8e(*reinterpret_cast<const u32x4*>(a + e * 8), fa);
@@ -316,8 +327,8 @@ extern "C" {
 
 int p2p_act(const void* a, const void* b, long n, int act, int mode, void* out, hipStream_t st) {
   using namespace p2p;
-  hipLaunchKernelGGL(act_kernel, dim3(egrid(n / 8)), dim3(256), 0, st, static_cast<const bf16*>(a),
-                     static_cast<const bf16*>(b), n / 8, act, mode, static_cast<bf16*>(out));
+  hipLaunchKernelGGL(act_kernel, dim3(egrid(n / 8 > 0 ? n / 8 : 1)), dim3(256), 0, st, static_cast<const bf16*>(a),
+                     static_cast<const bf16*>(b), n, act, mode, static_cast<bf16*>(out));
   return (int)hipGetLastError();
 }
 
