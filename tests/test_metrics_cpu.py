@@ -47,3 +47,19 @@ def test_ssim_identity_and_corrected_mode():
     y = (x + 0.1).clamp(-1, 1)
     s = ssim(y, x, ref_compat=False)
     assert 0.0 < s.min() <= 1.0
+
+
+def test_reference_instance_norm_channels_last_n1():
+    """The CPU oracle must not inherit PyTorch's channels_last N==1 instance_norm backward
+    bug: its gradient equals the NCHW-contiguous one."""
+    import torch
+    from p2p_pytorch_amd.ops import reference as ref
+    torch.manual_seed(0)
+    x = torch.randn(1, 8, 4, 4) * 2 + 1
+    gy = torch.randn(1, 8, 4, 4)
+    grads = []
+    for cl in (False, True):
+        xx = (x.contiguous(memory_format=torch.channels_last) if cl else x.clone()).requires_grad_(True)
+        ref.instance_norm(xx).backward(gy)
+        grads.append(xx.grad)
+    assert torch.allclose(grads[0], grads[1], atol=1e-5)
