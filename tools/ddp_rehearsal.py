@@ -9,7 +9,7 @@ the host.  What it checks on the real HIP kernels:
   * a full ``Pix2PixStep`` with per-network ``GradReducer`` s (small buckets -> several in
     flight, hooks firing during backward) leaves every rank with bitwise identical G and D
     parameters after Adam;
-  * the reduced G gradient equals the single-process gradient of the global batch.
+  * the reduced G gradient equals the mean of the per-shard single-process gradients.
 
 Exit status 0 = pass; rank 0 prints one JSON line.  (The production path is RCCL over xGMI
 with one GPU per rank; the driver's 8-GPU bench exercises that.)
@@ -62,6 +62,7 @@ def main():
     from p2p_pytorch_amd.parallel import GradReducer
     from p2p_pytorch_amd.parallel import dist as pdist
     p2p.set_backend("native")
+    p2p.set_deterministic(True)     # ordered split-K: the same shard gives the same bits
     world, rank, local_rank = pdist.init_from_env()
     dev = pdist.local_device(local_rank)
     torch.cuda.set_device(dev)
@@ -83,16 +84,24 @@ def main():
     worst = 0.0
     errs = []
     if rank == 0:
-        G1, D1 = build(100, dev)
-        set_requires_grad(D1, False)
-        hip.begin_step()
-        g_grads(G1, D1, A, B)
-        for n, p in G1.named_parameters():
-            ref = p.grad.float()
-            scale = ref.abs().max().item()
+        # reference: the per-shard gradients computed single-process (same batch size as each
+        # rank, so the same kernels and tile splits), averaged.  (Comparing against ONE
+        # global-batch backward instead mixes in batch-size-dependent reduction orders,
+        # which the bf16 U-Net amplifies chaotically -- tools/debug/batch_consistency.py.)
+        ref = None
+        for r in range(world):
+            G1, D1 = build(100, dev)
+            set_requires_grad(D1, False)
+            hip.begin_step()
+            g_grads(G1, D1, A[per * r:per * (r + 1)], B[per * r:per * (r + 1)])
+            gr = {n: p.grad.detach().float().clone() for n, p in G1.named_parameters()}
+            ref = gr if ref is None else {n: ref[n] + gr[n] for n in ref}
+        for n in ref:
+            rg = ref[n] / world
+            scale = rg.abs().max().item()
             if scale < 1e-8 and got[n].abs().max().item() < 1e-8:
                 continue        # exactly-zero grads (biases of norm-fed convs)
-            err = ((got[n] - ref).abs().max() / max(scale, 1e-12)).item()
+            err = ((got[n] - rg).abs().max() / max(scale, 1e-12)).item()
             errs.append((err, n, scale))
             worst = max(worst, err)
         errs.sort(reverse=True)
@@ -109,9 +118,9 @@ def main():
     dist.all_gather(gathered, flat)
     same = all(torch.equal(gathered[0], t) for t in gathered)
     finite = all(torch.isfinite(v).all().item() for v in losses.values())
-    ok = same and finite and worst < 3e-2
+    ok = same and finite and worst < 1e-4
     if rank == 0:
-        print(json.dumps({"world": world, "backend": dist.get_backend(), "grad_rel_err_vs_global_batch": worst,
+        print(json.dumps({"world": world, "backend": dist.get_backend(), "grad_rel_err_vs_shard_mean": worst,
                           "worst_params": errs[:4],
                           "params_identical": same, "losses_finite": finite, "ok": ok}), flush=True)
     pdist.destroy()
