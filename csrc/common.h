@@ -60,7 +60,7 @@ __device__ __forceinline__ u32x4 act8(u32x4 v, int act) {
   return __builtin_bit_cast(u32x4, b);
 }
 
-__device__ __forceinline__ int reflect_idx(int i, int n) {
+__host__ __device__ __forceinline__ int reflect_idx(int i, int n) {
   // PyTorch ReflectionPad semantics (pad < n)
   i = i < 0 ? -i : i;
   return i >= n ? 2 * (n - 1) - i : i;
@@ -69,7 +69,7 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
 // Bijective XCD-aware remap of a linear workgroup id: blocks b and b+8 share an XCD
 // (MI355X dispatches round-robin over 8 XCDs); give each XCD a contiguous range of
 // logical tiles so tiles that share operand panels hit the same L2.
-__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+__host__ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   if (nwg < 16) return b;
   int q = nwg / 8, r = nwg % 8;
   int xcd = b % 8, loc = b / 8;
@@ -118,8 +118,10 @@ __host__ __device__ __forceinline__ FastDiv make_fastdiv(uint32_t d) {
   return f;
 }
 
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-  return (__umulhi(n, f.mul) + n) >> f.shift;
+// (the 64-bit product's high word is v_mul_hi_u32 on the device; plain C++ on the host, so
+// tests/native/host_checks.cpp runs this exact function under ASan/UBSan)
+__host__ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return ((uint32_t)(((uint64_t)n * f.mul) >> 32) + n) >> f.shift;
 }
 
 __device__ __forceinline__ float warp_sum(float v) {
