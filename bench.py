@@ -17,6 +17,7 @@ per-rank time of exactly K timed steps bracketed by barrier + device synchronize
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -45,6 +46,9 @@ def parse():
                    help="pix2pix: the headline U-Net + PatchGAN step (BASELINE.json); ref: the reference "
                         "repo's own compression GAN step (C + ExpandNet G + 3-scale SN PatchGAN + VGG19 loss, "
                         "train.py:291-414), measured for parity, not the headline")
+    p.add_argument("--mode", default="train", choices=["train", "infer"],
+                   help="train: one full GAN step (the headline); infer: generator forward only "
+                        "(test.py's path, eval mode, no grad) -- generated images/sec")
     p.add_argument("--netG", default="unet_256")
     p.add_argument("--netD", default="basic")
     p.add_argument("--impl", default=os.environ.get("P2P_BACKEND", "native"), choices=["native", "torch"])
@@ -131,13 +135,28 @@ def main():
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
-    step = trainer.step
+    step_fn = trainer.step
+    if args.mode == "infer":
+        gen_net = netG
+        gen_net.eval()
+        ctx = (torch.autocast(device_type="cuda", dtype=autocast) if autocast is not None
+               else contextlib.nullcontext())
+
+        def step_fn(a, b):    # noqa: ARG001 - same signature as the training step
+            if a.is_cuda and args.impl == "native":
+                from p2p_pytorch_amd.ops import hip
+                hip.begin_step()
+                hip.prepare_weights(gen_net)
+            with torch.no_grad(), ctx:
+                out = gen_net(netC(a) if ref else a)
+            return {"out_mean": out.float().mean()}
+    step = step_fn
     use_graph = (args.impl == "native" and dev.type == "cuda" and not args.no_graph
                  and (world == 1 or args.graph))
     if use_graph:
         from p2p_pytorch_amd.engine.graph import CapturedStep
         # capture runs its own warmup steps on a side stream, then records one step
-        step = CapturedStep(trainer.step, real_A, real_B, warmup=2)
+        step = CapturedStep(step_fn, real_A, real_B, warmup=2)
     t_w = time.perf_counter()
     for i in range(args.warmup):
         losses = step(real_A, real_B)
@@ -163,9 +182,10 @@ def main():
     base = EAGER_BASELINE_IMG_S_PER_GPU
     model = (f"pix2pix {args.netG} + PatchGAN {args.netD} (70x70)" if not ref else
              "reference compression GAN: CompressionNetwork + ExpandNetwork + 3-scale SN PatchGAN + VGG19 loss")
+    kind = "train" if args.mode == "train" else "inference (generator forward)"
     out = {
-        "metric": (f"train images/sec (whole node), {S}x{S} pix2pix U-Net+PatchGAN" if not ref else
-                   f"train images/sec (whole node), {S}x{S} reference compression GAN"),
+        "metric": (f"{kind} images/sec (whole node), {S}x{S} pix2pix U-Net+PatchGAN" if not ref else
+                   f"{kind} images/sec (whole node), {S}x{S} reference compression GAN"),
         "value": round(img_s, 2),
         "unit": "images/sec",
         "n_gpus": world,
@@ -174,7 +194,7 @@ def main():
         "ms_per_step": round(1000.0 * dt_max / args.steps, 3),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(img_s / (base * world), 3) if (base and not ref) else None,
+        "vs_baseline": round(img_s / (base * world), 3) if (base and not ref and args.mode == "train") else None,
         "dtype": "fp8+bf16" if args.precision == "fp8" else "bf16",
         "data": "synthetic (random paired images, random-init weights)",
         "config": {"model": model,
