@@ -6,8 +6,10 @@ forward-coupled hooks mis-fire on that pattern; here every network has its own r
 and the trainer says explicitly when a backward is complete (``finish``).
 
 Mechanism
-  * Parameters are packed, in reverse registration order (~ the order backward produces
-    their grads), into flat fp32 buckets of ``bucket_mb``.  Each ``p.grad`` is a *view*
+  * Parameters are packed into flat fp32 buckets of ``bucket_mb`` -- first in reverse
+    registration order, then (after the first backward) in the order their grads actually
+    became ready, with the last-ready bucket capped at ``tail_mb`` (its all-reduce is the
+    one backward cannot hide).  Each ``p.grad`` is a *view*
     into its bucket, so autograd accumulates straight into communication memory --
     no gather/scatter copies.
   * ``register_post_accumulate_grad_hook`` counts ready params; the moment a bucket is
@@ -40,29 +42,53 @@ class _Bucket:
 
 class GradReducer:
     def __init__(self, module: torch.nn.Module, bucket_mb: float = 64.0, process_group=None,
-                 comm_dtype: torch.dtype | None = None):
+                 comm_dtype: torch.dtype | None = None, tail_mb: float = 8.0, rebucket: bool = True):
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.backend = dist.get_backend(process_group) if dist.is_initialized() else None
         params = [p for p in module.parameters() if p.requires_grad]
         self.params = params
+        self.cap = int(bucket_mb * 1024 * 1024)
+        self.tail_cap = min(self.cap, int(tail_mb * 1024 * 1024))
+        self._build(list(reversed(params)))
+        # the first backward records the order grads actually become ready; the next
+        # zero_grad() re-buckets in that order (DDP's bucket rebuild), so every bucket fills
+        # contiguously in time and the last-ready one -- the all-reduce nothing can hide --
+        # is capped at tail_mb
+        self._ready_order: list | None = [] if rebucket else None
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params]
+        self.comm_dtype = comm_dtype
+        self.active = True
+
+    def _build(self, order):
         self.buckets: list[_Bucket] = []
         self._param_bucket = {}
         self._offset = {}
-        cap = int(bucket_mb * 1024 * 1024)
-        cur, cur_bytes = [], 0
-        for p in reversed(params):
+        groups, cur, cur_bytes = [], [], 0
+        # pack from the END of the ready order so the last-ready bucket gets the small cap
+        for p in reversed(order):
             nbytes = p.numel() * p.element_size()
+            cap = self.tail_cap if not groups else self.cap
             if cur and (cur_bytes + nbytes > cap or p.dtype != cur[0].dtype):
-                self._add_bucket(cur)
+                groups.append(cur)
                 cur, cur_bytes = [], 0
             cur.append(p)
             cur_bytes += nbytes
         if cur:
-            self._add_bucket(cur)
-        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params]
-        self.comm_dtype = comm_dtype
-        self.active = True
+            groups.append(cur)
+        for g in reversed(groups):
+            self._add_bucket(list(reversed(g)))
+
+    def _rebucket(self):
+        order = self._ready_order
+        self._ready_order = None
+        seen = set(id(p) for p in order)
+        order = order + [p for p in reversed(self.params) if id(p) not in seen]
+        old = {id(p): p.grad for p in self.params}
+        self._build(order)
+        for p in self.params:   # carry current grads over into the new flat buckets
+            if old[id(p)] is not None:
+                p.grad.copy_(old[id(p)])
 
     def _add_bucket(self, params):
         b = _Bucket(params, params[0].device, params[0].dtype, len(self.buckets))
@@ -79,6 +105,8 @@ class GradReducer:
     def _on_grad(self, p):
         if not self.active:
             return
+        if self._ready_order is not None:
+            self._ready_order.append(p)
         b = self._param_bucket[p]
         # autograd may have replaced the view (e.g. after set_to_none): copy back in.
         lo = b.flat.data_ptr()
@@ -127,6 +155,8 @@ class GradReducer:
         return t
 
     def zero_grad(self):
+        if self._ready_order:
+            self._rebucket()
         for b in self.buckets:
             b.flat.zero_()
             for p in b.params:  # keep grads as bucket views

@@ -73,6 +73,21 @@ def _worker(rank, world, port, q):
         loss.backward()
         red.finish()
         grads = {n: p.grad.detach().numpy().copy() for n, p in G.named_parameters()}
+        # second backward of the same batch: zero_grad() now re-buckets in the recorded
+        # grad-ready order (last-ready bucket capped) -- the reduced grads must not change
+        nb0 = [len(b.params) for b in red.buckets]
+        red.zero_grad()
+        assert red._ready_order is None, "rebucket did not run"
+        fake = G(a)
+        loss = crit(D(torch.cat((a, fake), 1)), True) + 100 * l1(fake, b)
+        loss.backward()
+        red.finish()
+        for n, p in G.named_parameters():
+            lo = red._param_bucket[p].flat.data_ptr()
+            assert lo <= p.grad.data_ptr() < lo + red._param_bucket[p].flat.numel() * 4, n
+            # (a different bucket layout changes the ring's per-element summation order)
+            assert torch.allclose(p.grad, torch.from_numpy(grads[n]), rtol=1e-5, atol=1e-7), \
+                ("rebucketed grad", n, nb0)
         opt = torch.optim.Adam(G.parameters(), lr=1e-3)
         opt.step()
         flat = torch.cat([p.detach().reshape(-1) for p in G.parameters()])
