@@ -49,6 +49,9 @@ int p2p_prelu_bwd(const void* x, const void* dy, long n, const float* w, void* d
 int p2p_tv_fwd(const void* x, int N, int H, int W, int C, float* ws, float* out, hipStream_t st);
 int p2p_tv_bwd(const void* x, int N, int H, int W, int C, const float* gout, void* dx, hipStream_t st);
 int p2p_quantize(const void* x, long n, int bits, void* y, hipStream_t st);
+int p2p_metrics_ws(int C, int H, int W);
+int p2p_image_metrics(const void* a, const void* b, int dtype, const long* strides, int N, int C, int H, int W,
+                      int shift, double data_range, double* ws, hipStream_t st);
 int p2p_avgpool3s2(const void* x, int N, int H, int W, int C, int OH, int OW, void* y, int bwd, hipStream_t st);
 int p2p_maxpool2(const void* x, const void* gy, int N, int H, int W, int C, void* out, hipStream_t st);
 int p2p_l2norm(const void* x, const void* gy, long P, int C, float eps, void* out, hipStream_t st);
@@ -759,6 +762,29 @@ Tensor tv_fwd(const Tensor& x) {
   return out;
 }
 
+// per-image (PSNR, SSIM) of two [N, C, H, W] image batches (any strides, fp32 or bf16):
+// returns float64 [N, 2]
+Tensor image_metrics(const Tensor& a, const Tensor& b, bool shift, double data_range) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.dim() == 4 && a.sizes() == b.sizes(),
+              "image_metrics: two 4-D CUDA tensors of one shape");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() &&
+                  (a.scalar_type() == at::kFloat || a.scalar_type() == at::kBFloat16),
+              "image_metrics: fp32 or bf16 inputs of one dtype");
+  const int N = (int)a.size(0), C = (int)a.size(1), H = (int)a.size(2), W = (int)a.size(3);
+  TORCH_CHECK(H >= 7 && W >= 7, "image_metrics: images of at least 7x7 (SSIM window)");
+  const long st[8] = {(long)a.stride(0), (long)a.stride(1), (long)a.stride(2), (long)a.stride(3),
+                      (long)b.stride(0), (long)b.stride(1), (long)b.stride(2), (long)b.stride(3)};
+  Tensor ws = at::empty({N, p2p_metrics_ws(C, H, W), 2}, a.options().dtype(at::kDouble));
+  check_rc(p2p_image_metrics(a.data_ptr(), b.data_ptr(), a.scalar_type() == at::kBFloat16 ? 1 : 0, st, N, C, H,
+                             W, shift ? 1 : 0, data_range, ws.data_ptr<double>(), cur_stream(a)),
+           "image_metrics");
+  Tensor sums = ws.sum(1);  // fixed-order reduction of the per-tile partials
+  Tensor mse = sums.select(1, 1) / ((double)C * H * W);
+  Tensor psnr = (255.0 * 255.0 / mse).log10() * 10.0;
+  Tensor ssim = sums.select(1, 0) / ((double)C * (H - 6) * (W - 6));
+  return at::stack({psnr, ssim}, 1);
+}
+
 Tensor tv_bwd(const Tensor& x, const Tensor& gout) {
   check_nhwc(x, "tv_bwd");
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
@@ -1088,6 +1114,7 @@ TORCH_LIBRARY(p2p, m) {
   m.def("tv_fwd(Tensor x) -> Tensor");
   m.def("tv_bwd(Tensor x, Tensor gout) -> Tensor");
   m.def("quantize(Tensor x, int bits) -> Tensor");
+  m.def("image_metrics(Tensor a, Tensor b, bool shift, float data_range) -> Tensor");
   m.def("avgpool3s2(Tensor x, int bwd, int H, int W) -> Tensor");
   m.def("maxpool2(Tensor x, Tensor? gy) -> Tensor");
   m.def("l2norm(Tensor x, Tensor? gy, float eps) -> Tensor");
@@ -1139,6 +1166,7 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("tv_fwd", tv_fwd);
   m.impl("tv_bwd", tv_bwd);
   m.impl("quantize", quantize);
+  m.impl("image_metrics", image_metrics);
   m.impl("avgpool3s2", avgpool3s2);
   m.impl("maxpool2", maxpool2);
   m.impl("l2norm", l2norm);

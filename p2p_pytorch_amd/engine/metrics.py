@@ -13,11 +13,17 @@ Reference-compatible semantics (``ref_compat=True``, the default):
     valid (un-padded) window positions and channels, and -- because the arrays are float
     with no ``data_range`` -- skimage's float dtype range 2.0 (C1 = (0.01 * 2)^2).
 ``ref_compat=False`` evaluates the [-1, 1] images mapped to [0, 1] and uses data_range 255.
+
+On the GPU with the native backend both metrics come from ONE HIP kernel
+(``csrc/metrics.hip``: exact integer 7x7 window moments, double SSIM ratio, fixed-order
+reduction); the tensor code below is the CPU path and the test oracle.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
+
+from .. import _native
 
 
 def to_uint8_levels(x: torch.Tensor, ref_compat: bool = True) -> torch.Tensor:
@@ -28,8 +34,33 @@ def to_uint8_levels(x: torch.Tensor, ref_compat: bool = True) -> torch.Tensor:
     return torch.floor((x * 255.0).clamp(0.0, 255.0))
 
 
+def _native_ok(a: torch.Tensor, b: torch.Tensor, win: int) -> bool:
+    return (win == 7 and _native.use_native(a) and a.shape == b.shape and a.dim() == 4
+            and a.dtype == b.dtype and a.dtype in (torch.float32, torch.bfloat16)
+            and a.shape[2] >= 7 and a.shape[3] >= 7)
+
+
+def image_metrics(pred: torch.Tensor, ground: torch.Tensor, ref_compat: bool = True,
+                  data_range: float | None = None):
+    """(psnr [N], ssim [N]) in one pass -- the eval loop's call (train.py:477-478)."""
+    if data_range is None:
+        data_range = 2.0 if ref_compat else 255.0
+    if _native_ok(pred, ground, 7):
+        out = _native.ops().image_metrics(pred.detach(), ground.detach(), not ref_compat,
+                                          float(data_range))
+        return out[:, 0].float(), out[:, 1].float()
+    return (_psnr_torch(ground, pred, ref_compat),
+            _ssim_torch(pred, ground, ref_compat, 7, data_range))
+
+
 def psnr(ground: torch.Tensor, pred: torch.Tensor, ref_compat: bool = True) -> torch.Tensor:
     """Per-image PSNR [N] in dB (inf where identical)."""
+    if _native_ok(pred, ground, 7):
+        return image_metrics(pred, ground, ref_compat)[0]
+    return _psnr_torch(ground, pred, ref_compat)
+
+
+def _psnr_torch(ground: torch.Tensor, pred: torch.Tensor, ref_compat: bool = True) -> torch.Tensor:
     g = to_uint8_levels(ground, ref_compat)
     p = to_uint8_levels(pred, ref_compat)
     mse = ((g - p) ** 2).flatten(1).mean(1)
@@ -39,6 +70,13 @@ def psnr(ground: torch.Tensor, pred: torch.Tensor, ref_compat: bool = True) -> t
 def ssim(pred: torch.Tensor, ground: torch.Tensor, ref_compat: bool = True, win: int = 7,
          data_range: float | None = None) -> torch.Tensor:
     """Per-image SSIM [N] (skimage structural_similarity, uniform window)."""
+    if _native_ok(pred, ground, win):
+        return image_metrics(pred, ground, ref_compat, data_range)[1]
+    return _ssim_torch(pred, ground, ref_compat, win, data_range)
+
+
+def _ssim_torch(pred: torch.Tensor, ground: torch.Tensor, ref_compat: bool = True, win: int = 7,
+                data_range: float | None = None) -> torch.Tensor:
     x = to_uint8_levels(pred, ref_compat).double()
     y = to_uint8_levels(ground, ref_compat).double()
     if data_range is None:

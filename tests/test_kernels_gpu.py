@@ -585,3 +585,28 @@ def test_spectral_norm_power_iteration(h, wd):
     assert torch.allclose(u, ur, rtol=1e-4, atol=1e-6)
     assert abs(sig.item() - sr.item()) <= 1e-5 * abs(sr.item())
     assert torch.allclose(W.grad, 3.0 * torch.outer(ur, vr), rtol=1e-4, atol=1e-7)
+
+
+@pytest.mark.parametrize("dtype,cl,ref_compat,hw", [
+    (torch.bfloat16, True, True, (37, 70)),
+    (torch.float32, False, True, (256, 256)),
+    (torch.float32, True, False, (7, 129)),
+])
+def test_image_metrics_kernel(dtype, cl, ref_compat, hw):
+    """csrc/metrics.hip (one pass PSNR + SSIM) vs the float64 tensor oracle on the CPU."""
+    from p2p_pytorch_amd.engine import metrics
+    H, W = hw
+    g = torch.Generator(device=DEV).manual_seed(11)
+    a = torch.rand(3, 3, H, W, device=DEV, generator=g) * 2.2 - 1.1
+    b = (a + 0.1 * torch.randn(3, 3, H, W, device=DEV, generator=g)).clamp(-1, 1)
+    b[2] = a[2]                                  # identical image: PSNR inf, SSIM 1
+    a, b = a.to(dtype), b.to(dtype)
+    if cl:
+        a = a.contiguous(memory_format=torch.channels_last)
+    p, s = metrics.image_metrics(b, a, ref_compat)
+    rp = metrics._psnr_torch(a.cpu(), b.cpu(), ref_compat)
+    rs = metrics._ssim_torch(b.cpu(), a.cpu(), ref_compat)
+    assert torch.isinf(p[2]) and torch.isinf(rp[2])
+    assert torch.allclose(p[:2].cpu(), rp[:2], rtol=0, atol=1e-4), (p, rp)
+    assert torch.allclose(s.cpu().double(), rs.double(), rtol=0, atol=1e-6), (s, rs)
+    assert abs(s[2].item() - 1.0) < 1e-12

@@ -73,6 +73,7 @@ def main():
         M = B * OH * OH if kind == "conv" else B * H * H
         macs = (B * OH * OH * cout * cin * k * k) if kind == "conv" else (B * H * H * cin * cout * k * k)
         flops = 2.0 * macs
+        y_first = None
         for var in variants:
             os.environ["P2P_CONV_VARIANT"] = var
             row = {"layer": name, "variant": var}
@@ -89,6 +90,14 @@ def main():
 
                 if op == "fwd":
                     fn = fwd
+                    # every variant's output against the first variant's (same bf16 inputs)
+                    with torch.no_grad():
+                        yv = fwd().float()
+                    if y_first is None:
+                        y_first = yv
+                    else:
+                        row["fwd_rel_err_vs_first"] = float(
+                            ((yv - y_first).abs().max() / y_first.abs().max().clamp_min(1e-6)).item())
                 else:
                     y = fwd()
                     gy = torch.randn_like(y)

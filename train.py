@@ -104,7 +104,7 @@ def main(argv=None):
                                       get_training_set)
     from p2p_pytorch_amd.engine.checkpoint import (checkpoint_path, latest_checkpoint,
                                                    load_checkpoint, save_checkpoint)
-    from p2p_pytorch_amd.engine.metrics import psnr, ssim
+    from p2p_pytorch_amd.engine.metrics import image_metrics
     from p2p_pytorch_amd.models import (define_C, define_D, define_G, get_scheduler,
                                         update_learning_rate)
     from p2p_pytorch_amd.parallel import dist as pdist
@@ -287,8 +287,9 @@ def main(argv=None):
                         pred = net_g(ops.quantize(net_c(tgt), opt.bits))
                     else:
                         pred = net_g(inp)
-                    ps.append(psnr(tgt, pred).clamp(max=60.0))
-                    ss.append(ssim(pred, tgt))
+                    p_i, s_i = image_metrics(pred, tgt)   # one HIP kernel on the GPU
+                    ps.append(p_i.clamp(max=60.0))
+                    ss.append(s_i)
             if ps:
                 pt, st = torch.cat(ps), torch.cat(ss)
                 stats = torch.stack([pt.sum(), st.sum(), torch.tensor(float(len(pt)), device=pt.device),
