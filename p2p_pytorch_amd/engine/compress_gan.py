@@ -70,6 +70,10 @@ class CompressGANStep:
         self.reducer_g, self.reducer_d = reducer_g, reducer_d
         self.nan_guard = nan_guard
         self.skipped = None
+        self.timer = None     # optional utils.PhaseTimer: per-phase HIP-event ms
+
+    def _phase(self, name):
+        return self.timer.phase(name) if self.timer is not None else trace_range(name)
 
     def _opt_step(self, opt, reducer, *losses):
         if not self.nan_guard:
@@ -120,13 +124,13 @@ class CompressGANStep:
         tv = calc_tv_Loss(fake_b)
         loss_g = loss_g_gan + loss_feat + content + tv * self.lambda_tv
         # ---- updates: G first (its backward also reaches D; those grads are dropped)
-        with trace_range("G_bwd_opt"):
+        with self._phase("G_bwd_opt"):
             self._zero(self.opt_g, self.reducer_g)
             loss_g.backward()
             if self.reducer_g is not None:
                 self.reducer_g.finish()
             self._opt_step(self.opt_g, self.reducer_g, loss_g)
-        with trace_range("D_bwd_opt"):
+        with self._phase("D_bwd_opt"):
             self._zero(self.opt_d, self.reducer_d)
             loss_d.backward()
             if self.reducer_d is not None:

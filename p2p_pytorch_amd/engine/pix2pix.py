@@ -52,6 +52,10 @@ class Pix2PixStep:
         # host sync; agreed across ranks with one 4-byte MAX all-reduce) and is counted
         self.nan_guard = nan_guard
         self.skipped = None
+        self.timer = None     # optional utils.PhaseTimer: per-phase HIP-event ms
+
+    def _phase(self, name):
+        return self.timer.phase(name) if self.timer is not None else trace_range(name)
 
     def _guarded_step(self, opt, reducer, *losses):
         if not self.nan_guard:
@@ -85,9 +89,9 @@ class Pix2PixStep:
             hip.begin_step()      # weight images re-cast once per step (graph-safe)
             hip.advance_rng()     # new dropout masks
             hip.prepare_weights(netG, netD)   # all bf16 weight images, one launch each
-        with self._ctx(real_A.device), trace_range("G_fwd"):
+        with self._ctx(real_A.device), self._phase("G_fwd"):
             fake_B = netG(real_A)
-        with self._ctx(real_A.device), trace_range("D_fwd"):
+        with self._ctx(real_A.device), self._phase("D_fwd"):
             # ---- D
             set_requires_grad(netD, True)
             fuse = self.fuse_d_batch
@@ -106,7 +110,7 @@ class Pix2PixStep:
                 pred_real = netD(self._d_input(real_A, real_B))
                 loss_D_real = self.criterionGAN(pred_real, True)
             loss_D = (loss_D_fake + loss_D_real) * 0.5
-        with trace_range("D_bwd_opt"):
+        with self._phase("D_bwd_opt"):
             self._zero(self.opt_D, self.reducer_d)
             loss_D.backward()
             if self.reducer_d is not None:
@@ -117,12 +121,12 @@ class Pix2PixStep:
             hip.prepare_weights(netD)         # D moved: fresh images for the G phase
         # ---- G
         set_requires_grad(netD, False)
-        with self._ctx(real_A.device), trace_range("G_loss_fwd"):
+        with self._ctx(real_A.device), self._phase("G_loss_fwd"):
             pred_fake = netD(self._d_input(real_A, fake_B))
             loss_G_GAN = self.criterionGAN(pred_fake, True)
             loss_G_L1 = l1(fake_B, real_B) * self.lambda_L1
             loss_G = loss_G_GAN + loss_G_L1
-        with trace_range("G_bwd_opt"):
+        with self._phase("G_bwd_opt"):
             self._zero(self.opt_G, self.reducer_g)
             loss_G.backward()
             if self.reducer_g is not None:

@@ -18,6 +18,10 @@ Mechanism
   * ``finish()`` enqueues any incomplete bucket (params that got no grad contribute
     zeros), makes the compute stream wait on every collective (no host sync) and scales
     by 1/world.
+  * ``enable_timing()`` (logging only): collectives are issued from a side stream
+    bracketed by HIP events, and ``comm_stats()`` reports the last backward's collective
+    busy time, the part of it left exposed after backward's last kernel, and the overlap
+    fraction -- the JSONL "comm ms / overlap %" of SURVEY.md section 5.5.
   * Bucket size: xGMI is point-to-point (7 links x ~153 GB/s per GPU); RCCL's ring /
     direct algorithms are per-link bound, so few large buckets (tens of MB) amortise the
     per-collective latency while still leaving >= 2-4 buckets per network to overlap.
@@ -29,7 +33,7 @@ import torch.distributed as dist
 
 
 class _Bucket:
-    __slots__ = ("params", "flat", "pending", "work", "index")
+    __slots__ = ("params", "flat", "pending", "work", "index", "events")
 
     def __init__(self, params, device, dtype, index):
         self.params = params
@@ -38,6 +42,19 @@ class _Bucket:
         self.pending = len(params)
         self.work = None
         self.index = index
+        self.events = None
+
+
+class _StreamJoin:
+    """Work handle of a timed collective: waiting = ordering the current stream after the
+    side stream that issued it."""
+    __slots__ = ("stream",)
+
+    def __init__(self, stream):
+        self.stream = stream
+
+    def wait(self):
+        torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
 
 
 class GradReducer:
@@ -59,6 +76,9 @@ class GradReducer:
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params]
         self.comm_dtype = comm_dtype
         self.active = True
+        self._timing = False
+        self._comm_stream = None
+        self._last = None        # (bucket events, end-of-backward event) of the last finish()
 
     def _build(self, order):
         self.buckets: list[_Bucket] = []
@@ -129,15 +149,39 @@ class GradReducer:
         if self.world == 1:
             b.work = True
             return
-        b.work = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        if not self._timing or torch.cuda.is_current_stream_capturing() or not b.flat.is_cuda:
+            b.work = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            return
+        # timed: issue from a side stream so the events bracket the collective itself
+        cur = torch.cuda.current_stream(b.flat.device)
+        if self._comm_stream is None:
+            self._comm_stream = torch.cuda.Stream(device=b.flat.device)
+        cs = self._comm_stream
+        cs.wait_stream(cur)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(cs):
+            e0.record(cs)
+            work = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            work.wait()                     # cs waits for RCCL's stream (no host sync)
+            e1.record(cs)
+        b.flat.record_stream(cs)
+        b.events = (e0, e1)
+        b.work = _StreamJoin(cs)
 
     # ------------------------------------------------------------------ API
     def finish(self):
         """Complete the reduction of this backward: launch stragglers, wait (stream-ordered),
         average, and reset bookkeeping for the next backward."""
+        end_bwd = None
+        if self._timing and self.world > 1 and self.buckets and self.buckets[0].flat.is_cuda \
+                and not torch.cuda.is_current_stream_capturing():
+            end_bwd = torch.cuda.Event(enable_timing=True)
+            end_bwd.record()
         for b in self.buckets:
             if b.work is None:
                 self._launch(b)
+        if end_bwd is not None:
+            self._last = ([b.events for b in self.buckets if b.events is not None], end_bwd)
         inv = 1.0 / self.world
         for b in self.buckets:
             if b.work is not True and b.work is not None:
@@ -145,7 +189,38 @@ class GradReducer:
             if self.world > 1:
                 b.flat.mul_(inv)
             b.work = None
+            b.events = None
             b.pending = len(b.params)
+
+    def enable_timing(self, on: bool = True):
+        self._timing = bool(on)
+        return self
+
+    def comm_stats(self) -> dict:
+        """Collective timing of the last timed backward (host-synchronises on its events):
+        ``comm_ms`` = busy time of the bucket all-reduces (union of their intervals),
+        ``exposed_ms`` = how long they ran past the end of backward's compute,
+        ``overlap`` = 1 - exposed / comm."""
+        if not self._last or not self._last[0]:
+            return {}
+        evs, end_bwd = self._last
+        evs[-1][1].synchronize()
+        end_bwd.synchronize()
+        ref = evs[0][0]
+        spans = sorted((ref.elapsed_time(e0), ref.elapsed_time(e1)) for e0, e1 in evs)
+        busy, cur_s, cur_e = 0.0, None, None
+        for s0, s1 in spans:
+            if cur_e is None or s0 > cur_e:
+                if cur_e is not None:
+                    busy += cur_e - cur_s
+                cur_s, cur_e = s0, s1
+            else:
+                cur_e = max(cur_e, s1)
+        busy += cur_e - cur_s
+        t_end = ref.elapsed_time(end_bwd)
+        exposed = max(0.0, max(s1 for _, s1 in spans) - t_end)
+        return {"comm_ms": busy, "exposed_ms": exposed,
+                "overlap": 1.0 - exposed / busy if busy > 0 else 1.0, "buckets": len(spans)}
 
     def all_reduce_max_(self, t: torch.Tensor):
         """In-place MAX over ranks of a small device tensor (e.g. the NaN-guard flag), so

@@ -36,8 +36,14 @@ def test_train_resume_test_pix2pix_gpu(workdir, extra):
     import p2p_pytorch_amd as p2p
     try:
         base = ["--dataset", "toy", "--name", "g", "--netG", "unet_256", "--netD", "basic", "--cuda",
-                "--batch_size", "2", "--lamb", "100", "--threads", "0", "--epochsave", "1", "--device_cache"] + extra
+                "--batch_size", "2", "--lamb", "100", "--threads", "0", "--epochsave", "1", "--device_cache",
+                "--log_json", "m.jsonl"] + extra
         train.main(base + ["--nepoch", "1"])
+        import json
+        recs = [json.loads(l) for l in open(workdir / "m.jsonl")]
+        assert recs and all(r["img_s"] > 0 for r in recs)
+        if "--graph" not in extra:   # per-phase HIP-event ms in the JSONL stream
+            assert set(recs[-1]["phase_ms"]) >= {"G_fwd", "D_fwd", "D_bwd_opt", "G_bwd_opt"}
         ck = workdir / "checkpoint/toy/net_g_epoch_1.pth"
         assert ck.exists()
         st = torch.load(ck, weights_only=True)

@@ -109,20 +109,29 @@ def main():
     G, D = build(200 + rank, dev)
     pdist.broadcast_module(G)
     pdist.broadcast_module(D)
-    step = Pix2PixStep(G, D, reducer_g=GradReducer(G, bucket_mb=0.5), reducer_d=GradReducer(D, bucket_mb=0.5))
+    # (timed reducers + phase timer: the JSONL comm / overlap path of train.py --log_json)
+    from p2p_pytorch_amd.utils import PhaseTimer
+    rg_, rd_ = GradReducer(G, bucket_mb=0.5).enable_timing(), GradReducer(D, bucket_mb=0.5).enable_timing()
+    step = Pix2PixStep(G, D, reducer_g=rg_, reducer_d=rd_)
+    step.timer = PhaseTimer()
     for _ in range(2):
         losses = step.step(a, b)
     torch.cuda.synchronize()
+    comm = {"G": rg_.comm_stats(), "D": rd_.comm_stats()}
+    phases = step.timer.report()
+    timed = all(c.get("comm_ms", 0) > 0 and c.get("buckets", 0) > 1 for c in comm.values()) and \
+        set(phases) >= {"G_fwd", "D_fwd", "D_bwd_opt", "G_bwd_opt"}
     flat = torch.cat([p.detach().reshape(-1) for p in list(G.parameters()) + list(D.parameters())])
     gathered = [torch.zeros_like(flat) for _ in range(world)]
     dist.all_gather(gathered, flat)
     same = all(torch.equal(gathered[0], t) for t in gathered)
     finite = all(torch.isfinite(v).all().item() for v in losses.values())
-    ok = same and finite and worst < 1e-4
+    ok = same and finite and worst < 1e-4 and timed
     if rank == 0:
         print(json.dumps({"world": world, "backend": dist.get_backend(), "grad_rel_err_vs_shard_mean": worst,
                           "worst_params": errs[:4],
-                          "params_identical": same, "losses_finite": finite, "ok": ok}), flush=True)
+                          "params_identical": same, "losses_finite": finite, "comm": comm,
+                          "phase_ms": phases, "ok": ok}), flush=True)
     pdist.destroy()
     sys.exit(0 if ok else 1)
 

@@ -87,6 +87,9 @@ def build_parser():
     p.add_argument("--resume", action="store_true", help="resume from the newest checkpoint")
     p.add_argument("--log_every", type=int, default=50)
     p.add_argument("--log_json", default=None, help="append JSONL metrics here (rank 0)")
+    p.add_argument("--phase_times", type=int, default=None,
+                   help="per-phase HIP-event ms and RCCL comm / overlap stats in the JSONL stream "
+                        "(default: on with --log_json and no --graph)")
     p.add_argument("--no_eval", action="store_true")
     p.add_argument("--no_nan_guard", action="store_true",
                    help="apply updates even when a loss is NaN/Inf (default: skip on device)")
@@ -219,6 +222,13 @@ def main(argv=None):
     step_fn = trainer.step
     num_epoch = opt.nepoch + 1
     jlog = JsonlLogger(opt.log_json, rank)
+    timing = (opt.phase_times if opt.phase_times is not None else bool(opt.log_json and not opt.graph))
+    if timing and use_cuda:
+        from p2p_pytorch_amd.utils import PhaseTimer
+        trainer.timer = PhaseTimer()
+        for r in (reducer_g, reducer_d):
+            if r is not None:
+                r.enable_timing()
     wd_s = opt.watchdog_s if opt.watchdog_s is not None else (1800.0 if world > 1 else 0.0)
     watchdog = StepWatchdog(wd_s).start()
     for epoch in range(start_epoch, num_epoch):
@@ -252,6 +262,13 @@ def main(argv=None):
                 keys = sorted(sums)
                 vals = torch.stack([torch.as_tensor(sums[k], device=device).float() for k in keys])
                 pdist.all_reduce_mean_([vals])
+                extra = {}   # every rank drains its timers; rank 0 logs
+                if getattr(trainer, "timer", None) is not None:
+                    extra["phase_ms"] = {k: v / count for k, v in trainer.timer.report().items()}
+                    for tag, r in (("G", reducer_g), ("D", reducer_d)):
+                        st = r.comm_stats() if r is not None else {}
+                        if st:
+                            extra[f"comm_{tag}"] = st
                 if rank == 0:
                     means = {k: float(v) / count for k, v in zip(keys, vals.tolist())}
                     dt = time.perf_counter() - t0
@@ -262,7 +279,7 @@ def main(argv=None):
                     skipped = getattr(trainer, "skipped", None)
                     jlog.log(epoch=epoch, iter=iteration, img_s=ips,
                              skipped_updates=float(skipped) if skipped is not None else 0.0,
-                             **means)
+                             **means, **extra)
         update_learning_rate(sched_g, opt_g, verbose=rank == 0)
         update_learning_rate(sched_d, opt_d, verbose=rank == 0)
         for o in (opt_g, opt_d):
