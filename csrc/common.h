@@ -26,24 +26,23 @@ __device__ __forceinline__ float act_fwd(float v, int act) {
   }
 }
 
-// derivative of act expressed through the activation's INPUT x (relu / lrelu)
+// derivative of act expressed through the activation's INPUT x (relu / lrelu).  Branch-free
+// in the per-element part: the negative-side slope depends only on the (wave-uniform) code,
+// so it is computed once per unrolled block, and each element costs one compare + select
+// instead of a scalar branch.
+__device__ __forceinline__ float neg_slope(int act) {
+  return act == ACT_RELU ? 0.f : (act == ACT_LRELU ? LRELU_SLOPE : 1.f);
+}
 __device__ __forceinline__ float act_grad_from_input(float x, int act) {
-  switch (act) {
-    case ACT_RELU: return x > 0.f ? 1.f : 0.f;
-    case ACT_LRELU: return x > 0.f ? 1.f : LRELU_SLOPE;
-    default: return 1.f;
-  }
+  return x > 0.f ? 1.f : neg_slope(act);
 }
 
-// derivative of act expressed through the activation's OUTPUT y (tanh / sigmoid / relu)
+// derivative of act expressed through the activation's OUTPUT y (tanh / sigmoid / relu),
+// branch-free (selects only)
 __device__ __forceinline__ float act_grad_from_output(float y, int act) {
-  switch (act) {
-    case ACT_RELU: return y > 0.f ? 1.f : 0.f;
-    case ACT_LRELU: return y > 0.f ? 1.f : LRELU_SLOPE;
-    case ACT_TANH: return 1.f - y * y;
-    case ACT_SIGMOID: return y * (1.f - y);
-    default: return 1.f;
-  }
+  const float pw = y > 0.f ? 1.f : neg_slope(act);
+  const float t = act == ACT_TANH ? 1.f - y * y : y * (1.f - y);
+  return act >= ACT_TANH ? t : pw;
 }
 
 __device__ __forceinline__ u32x4 zero_u32x4() { return u32x4{0u, 0u, 0u, 0u}; }

@@ -92,18 +92,30 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
   // ---- epilogue: bias + act in registers, bf16 tile staged in LDS, 16-B stores
   bf16* Cs = reinterpret_cast<bf16*>(smem);
   constexpr int LDC = BN + 8;
+  // the activation is dispatched ONCE per tile (compile-time body per code), not by a
+  // wave-uniform branch per accumulator element
+  auto stage_tile = [&](auto act_tag) {
+    constexpr int ACT = decltype(act_tag)::value;
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int coll = wn * TN * 16 + j * 16 + (lane & 15);
-    const int col = n0 + coll;
-    const float bj = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
+    for (int j = 0; j < TN; ++j) {
+      const int coll = wn * TN * 16 + j * 16 + (lane & 15);
+      const int col = n0 + coll;
+      const float bj = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int rowb = wm * TM * 16 + i * 16 + (lane >> 4) * 4;
+      for (int i = 0; i < TM; ++i) {
+        const int rowb = wm * TM * 16 + i * 16 + (lane >> 4) * 4;
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Cs[(rowb + r) * LDC + coll] = (bf16)act_fwd(acc[i][j][r] + bj, a.act_out);
+        for (int r = 0; r < 4; ++r)
+          Cs[(rowb + r) * LDC + coll] = (bf16)act_fwd(acc[i][j][r] + bj, ACT);
+      }
     }
+  };
+  switch (a.act_out) {
+    case ACT_RELU: stage_tile(std::integral_constant<int, ACT_RELU>{}); break;
+    case ACT_LRELU: stage_tile(std::integral_constant<int, ACT_LRELU>{}); break;
+    case ACT_TANH: stage_tile(std::integral_constant<int, ACT_TANH>{}); break;
+    case ACT_SIGMOID: stage_tile(std::integral_constant<int, ACT_SIGMOID>{}); break;
+    default: stage_tile(std::integral_constant<int, ACT_NONE>{}); break;
   }
   __syncthreads();
 

@@ -411,7 +411,8 @@ namespace p2p {
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-template <int MODE, int CVP>
+// ACT >= 0: the output activation as a compile-time code (no per-element switch); -1: runtime
+template <int MODE, int CVP, int ACT>
 __global__ void __launch_bounds__(256) col2im_kernel(const bf16* __restrict__ col, int ldc, int N, int H,
                                                      int W, int OH, int OW, int KH, int KW, int s, int p,
                                                      int Cv, int Coutp, const float* __restrict__ bias,
@@ -483,7 +484,7 @@ __global__ void __launch_bounds__(256) col2im_kernel(const bf16* __restrict__ co
           float v = 0.f;
 #pragma unroll
           for (int k = 0; k < CVP; ++k)
-            if (k == co && co < Cv) v = act_fwd(acc[k] + (bias ? bias[co] : 0.f), act_out);
+            if (k == co && co < Cv) v = act_fwd(acc[k] + (bias ? bias[co] : 0.f), ACT >= 0 ? ACT : act_out);
           if (act_bwd) v *= act_grad_from_input(h ? bf_hi(xw[q]) : bf_lo(xw[q]), act_bwd);
           v2[h] = v;
         }
@@ -509,9 +510,15 @@ extern "C" int p2p_col2im(int mode, const void* col, int ldc, int N, int H, int 
   p2p::bf16* o = static_cast<p2p::bf16*>(y);
   const int cvp = Cv <= 2 ? Cv : (Cv <= 4 ? 4 : (Cv <= 8 ? 8 : 16));
   if (Cv > 16 || Cv < 1 || ldc % cvp) return -1;
-#define P2P_COL2IM(M, V)                                                                              \
-  hipLaunchKernelGGL((p2p::col2im_kernel<M, V>), dim3((unsigned)blocks), dim3(256), 0, st, c, ldc, N, H, W, \
+#define P2P_COL2IM_A(M, V, A)                                                                            \
+  hipLaunchKernelGGL((p2p::col2im_kernel<M, V, A>), dim3((unsigned)blocks), dim3(256), 0, st, c, ldc, N, H, W, \
                      OH, OW, KH, KW, s, p, Cv, Coutp, bias, act_out, x, act_bwd, o)
+#define P2P_COL2IM(M, V)                                           \
+  do {                                                             \
+    if (act_out == p2p::ACT_NONE) P2P_COL2IM_A(M, V, p2p::ACT_NONE); \
+    else if (act_out == p2p::ACT_TANH) P2P_COL2IM_A(M, V, p2p::ACT_TANH); \
+    else P2P_COL2IM_A(M, V, -1);                                   \
+  } while (0)
   if (mode == 0) {
     if (cvp == 1) P2P_COL2IM(0, 1);
     else if (cvp == 2) P2P_COL2IM(0, 2);
@@ -526,6 +533,7 @@ extern "C" int p2p_col2im(int mode, const void* col, int ldc, int N, int H, int 
     else P2P_COL2IM(1, 16);
   }
 #undef P2P_COL2IM
+#undef P2P_COL2IM_A
   return (int)hipGetLastError();
 }
 

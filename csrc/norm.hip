@@ -216,16 +216,34 @@ __device__ __forceinline__ void chunk_sums(const float* __restrict__ ws, const N
   sb = rb[0][cl];
 }
 
+// The activation is a template parameter of the element-wise kernels: a runtime code,
+// even a wave-uniform one, costs a compare + branch per element (measured on the conv
+// epilogue: 6 % of the whole training step).  ACT_PRELU_T: the shared-slope PReLU.
+constexpr int ACT_PRELU_T = 5;
+
+template <typename F>
+static void with_act(int act, F&& f) {
+  switch (act) {
+    case ACT_RELU: f(std::integral_constant<int, ACT_RELU>{}); break;
+    case ACT_LRELU: f(std::integral_constant<int, ACT_LRELU>{}); break;
+    case ACT_TANH: f(std::integral_constant<int, ACT_TANH>{}); break;
+    case ACT_SIGMOID: f(std::integral_constant<int, ACT_SIGMOID>{}); break;
+    case ACT_PRELU_T: f(std::integral_constant<int, ACT_PRELU_T>{}); break;
+    default: f(std::integral_constant<int, ACT_NONE>{}); break;
+  }
+}
+
 // y = act((x - mean) * rstd * gamma + beta); mean/rstd indexed [n][c] (BN: n == 0 always).
 // grid (chunks, N): each thread owns one 8-channel chunk (its 8 scale/shift pairs live in
 // registers) and strides over the block's pixels.
+template <int ACT>
 __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict__ x, NormGeom g,
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ rstd,
                                                          const float* __restrict__ gamma,
                                                          const float* __restrict__ beta,
                                                          const float* __restrict__ prelu_w,
-                                                         int act, bf16* __restrict__ y, Fp8Shadow sh) {
+                                                         bf16* __restrict__ y, Fp8Shadow sh) {
   const int n = blockIdx.y, cb = blockIdx.x;
   const int CP = g.C >> 3;
   const int RP = 256 / CP;
@@ -254,8 +272,8 @@ __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict_
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float t = f[j] * sc[j] + sf[j];
-      if (prelu_w) t = t > 0.f ? t : pw * t;
-      else t = act_fwd(t, act);
+      if constexpr (ACT == ACT_PRELU_T) t = t > 0.f ? t : pw * t;
+      else t = act_fwd(t, ACT);
       f[j] = t;
     }
     const u32x4 o = pack8(f);
@@ -327,10 +345,11 @@ __device__ __forceinline__ void block_rows_reduce(const float* s1, const float* 
 
 // ws: [N][nchunks][C] sum(dy_eff * gs), [N][nchunks][C] sum(dy_eff * gs * xhat);
 // gs = gamma (dx pass) or 1 (dgamma / dbeta pass: scale_gamma = 0)
+template <int ACT>
 __global__ void __launch_bounds__(256) norm_bwd_partial_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ dy, NormGeom g,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
-    const float* __restrict__ beta, int act, int scale_gamma, float* __restrict__ ws) {
+    const float* __restrict__ beta, int scale_gamma, float* __restrict__ ws) {
   const int n = blockIdx.y, cb = blockIdx.x;
   const int CP = g.C >> 3;
   const int RP = 256 / CP;
@@ -357,7 +376,7 @@ __global__ void __launch_bounds__(256) norm_bwd_partial_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float xh = (fx[j] - mu[j]) * rs[j];
-        const float d = fd[j] * act_gate(xh * ga[j] + be[j], act) * gs[j];
+        const float d = fd[j] * act_gate(xh * ga[j] + be[j], ACT) * gs[j];
         s1[j] += d;
         s2[j] += d * xh;
       }
@@ -430,10 +449,11 @@ __global__ void __launch_bounds__(256) norm_param_grad_kernel(const float* __res
 // dx = A*dy_eff + B + Cc*xhat.  (The column sums of dx -- the bias gradient of the conv
 // that produced x -- are exactly zero for a normalised group: sum_p dx = Cc * sum_p xhat = 0,
 // so the host returns that exact zero instead of re-reading dx.)
+template <int ACT>
 __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ dy, NormGeom g,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
-    const float* __restrict__ beta, int act, const float* __restrict__ coef, bf16* __restrict__ dx,
+    const float* __restrict__ beta, const float* __restrict__ coef, bf16* __restrict__ dx,
     Fp8Shadow sh) {
   const int n = blockIdx.y, cb = blockIdx.x;
   const int CP = g.C >> 3;
@@ -467,7 +487,7 @@ __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float xh = (fx[j] - mu[j]) * rs[j];
-      const float d = act ? fd[j] * act_gate(xh * ga[j] + be[j], act) : fd[j];
+      const float d = ACT ? fd[j] * act_gate(xh * ga[j] + be[j], ACT) : fd[j];
       fd[j] = ca[j] * d + c0[j] + cx[j] * xh;
     }
     const u32x4 o = pack8(fd);
@@ -543,9 +563,11 @@ int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* ga
     hipLaunchKernelGGL((norm_finalize_kernel<32, 8>), dim3((C + 31) / 32, N), dim3(256), 0, st, ws, g, eps, mean,
                        rstd, run_mean, run_var, momentum);
   if (y)
-    hipLaunchKernelGGL(norm_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
-                       static_cast<const bf16*>(x), g, mean, rstd, gamma, beta, prelu_w, act,
-                       static_cast<bf16*>(y), Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
+    with_act(prelu_w ? ACT_PRELU_T : act, [&](auto t) {
+      hipLaunchKernelGGL((norm_apply_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st,
+                         static_cast<const bf16*>(x), g, mean, rstd, gamma, beta, prelu_w, static_cast<bf16*>(y),
+                         Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
+    });
   return (int)hipGetLastError();
 }
 
@@ -571,9 +593,11 @@ int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, cons
     hipLaunchKernelGGL((norm_finalize_kernel<32, 8>), dim3((C + 31) / 32, N), dim3(256), 0, st, partials, pg, eps,
                        mean, rstd, run_mean, run_var, momentum);
   NormGeom g = make_geom(N, HW, C);
-  hipLaunchKernelGGL(norm_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st, static_cast<const bf16*>(x), g,
-                     mean, rstd, gamma, beta, prelu_w, act, static_cast<bf16*>(y),
-                     Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
+  with_act(prelu_w ? ACT_PRELU_T : act, [&](auto t) {
+    hipLaunchKernelGGL((norm_apply_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st,
+                       static_cast<const bf16*>(x), g, mean, rstd, gamma, beta, prelu_w, static_cast<bf16*>(y),
+                       Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
+  });
   return (int)hipGetLastError();
 }
 
@@ -583,9 +607,11 @@ int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const
                    hipStream_t st) {
   using namespace p2p;
   NormGeom g = make_geom(N, HW, C);
-  hipLaunchKernelGGL(norm_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
-                     static_cast<const bf16*>(x), g, mean, rstd, gamma, beta, prelu_w, act,
-                     static_cast<bf16*>(y), Fp8Shadow{nullptr, nullptr, 0});
+  with_act(prelu_w ? ACT_PRELU_T : act, [&](auto t) {
+    hipLaunchKernelGGL((norm_apply_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st,
+                       static_cast<const bf16*>(x), g, mean, rstd, gamma, beta, prelu_w, static_cast<bf16*>(y),
+                       Fp8Shadow{nullptr, nullptr, 0});
+  });
   return (int)hipGetLastError();
 }
 
@@ -601,25 +627,31 @@ int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const floa
   const bf16* xb = static_cast<const bf16*>(x);
   const bf16* db = static_cast<const bf16*>(dy);
   if (dgamma) {
-    hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st, xb, db, g, mean,
-                       rstd, gamma, beta, act, 0, ws);
+    with_act(act, [&](auto t) {
+      hipLaunchKernelGGL((norm_bwd_partial_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st, xb,
+                         db, g, mean, rstd, gamma, beta, 0, ws);
+    });
     if (fin_wide(g) || N > 8)
       hipLaunchKernelGGL((norm_param_grad_kernel<8, 32>), dim3((C + 7) / 8), dim3(256), 0, st, ws, g, dgamma, dbeta);
     else
       hipLaunchKernelGGL((norm_param_grad_kernel<32, 8>), dim3((C + 31) / 32), dim3(256), 0, st, ws, g, dgamma, dbeta);
   }
   if (dx) {
-    hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st, xb, db, g, mean,
-                       rstd, gamma, beta, act, 1, ws);
+    with_act(act, [&](auto t) {
+      hipLaunchKernelGGL((norm_bwd_partial_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st, xb,
+                         db, g, mean, rstd, gamma, beta, 1, ws);
+    });
     if (fin_wide(g))
       hipLaunchKernelGGL((norm_bwd_finalize_kernel<8, 32>), dim3((C + 7) / 8, N), dim3(256), 0, st, ws, g, rstd,
                          gamma, coef);
     else
       hipLaunchKernelGGL((norm_bwd_finalize_kernel<32, 8>), dim3((C + 31) / 32, N), dim3(256), 0, st, ws, g, rstd,
                          gamma, coef);
-    hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(g.nchunks, N), dim3(256), 0, st, xb, db, g, mean,
-                       rstd, gamma, beta, act, coef, static_cast<bf16*>(dx),
-                       Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
+    with_act(act, [&](auto t) {
+      hipLaunchKernelGGL((norm_bwd_apply_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st, xb, db,
+                         g, mean, rstd, gamma, beta, coef, static_cast<bf16*>(dx),
+                         Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
+    });
     if (dsum) (void)hipMemsetAsync(dsum, 0, sizeof(float) * C, st);
   }
   return (int)hipGetLastError();
