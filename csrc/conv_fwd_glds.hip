@@ -59,8 +59,12 @@ __device__ __forceinline__ u32x4 relu_fp8x16(u32x4 v) {
 // the bf16 one ([rows][128 B], 16-B chunks, same swizzle), so per K tile the staging, LDS
 // traffic and MFMA cycles are unchanged while the tile carries twice the MACs.  Dequant:
 // per-source power-of-two scales as the MFMA's E8M0 scale operands (csrc/fp8.hip).
-template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU, int F8>
+// PK8 (non-FASTK, MODE 0, bf16): the packed 8-channel image inputs (C1 == 8, no second
+// source, KW | 8) -- one 16-B chunk is exactly one tap, so a row's chunk keeps its tap offset
+// (ty0 + kt * 8 / KW, tx) from tile to tile and the loader needs no per-tile divisions.
+template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU, int F8, bool PK8 = false>
 __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs a) {
+  static_assert(!PK8 || (!FASTK && MODE == 0 && F8 == 0), "PK8: packed bf16 image convs");
   using T = typename std::conditional<F8 != 0, uint8_t, bf16>::type;
   constexpr int EPC = 16 / (int)sizeof(T);  // elements per 16-B chunk
   constexpr int BKE = 8 * EPC;              // K elements per tile (128 B per row)
@@ -154,6 +158,16 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
     b_base[i] = w + (long)(b_ok[i] ? co : 0) * wrow + b_off[i];
   }
 
+  int pk_ty[PK8 ? AROWS : 1], pk_tx[PK8 ? AROWS : 1];
+  const int pk_dty = PK8 ? 8 / g.Ti : 0;   // tap rows advanced per 8-tap K tile
+  if constexpr (PK8) {
+#pragma unroll
+    for (int i = 0; i < AROWS; ++i) {
+      const int c = r_c[i] / EPC;            // this row's chunk == tap within the tile
+      pk_ty[i] = c / g.Ti;
+      pk_tx[i] = c - pk_ty[i] * g.Ti;
+    }
+  }
   auto issue = [&](int kt, int stage) {
     const int k0 = kt * BKE;
     T* Ast = As + stage * BM * BKE;
@@ -205,6 +219,27 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
 #pragma unroll
       for (int i = 0; i < BROWS; ++i) {
         const T* gp = b_ok[i] ? b_base[i] + woff : zero;
+        glds16(gp, Bst + (wid * 8 + RPP * i) * BKE);
+      }
+    } else if constexpr (PK8) {
+      const int ntaps = g.Kc >> 3;
+#pragma unroll
+      for (int i = 0; i < AROWS; ++i) {
+        const int tap = kt * 8 + r_c[i] / EPC;
+        const int t_y = pk_ty[i] + kt * pk_dty, t_x = pk_tx[i];
+        int uy = r_y[i] + t_y, ux = r_x[i] + t_x;
+        if (a.reflect && r_y[i] > -(1 << 27)) {
+          uy = reflect_idx(uy, Hu);
+          ux = reflect_idx(ux, Wu);
+        }
+        const bool inb = (unsigned)uy < (unsigned)Hu && (unsigned)ux < (unsigned)Wu && tap < ntaps;
+        const long off = (long)(r_img[i] + (uy >> ush) * a.W + (ux >> ush)) * 8;
+        glds16(inb ? x1 + off : zero, Ast + (wid * 8 + RPP * i) * BKE);
+      }
+#pragma unroll
+      for (int i = 0; i < BROWS; ++i) {
+        const int k = k0 + b_off[i];
+        const T* gp = (b_ok[i] && k < g.Kc) ? b_base[i] - b_off[i] + k : zero;
         glds16(gp, Bst + (wid * 8 + RPP * i) * BKE);
       }
     } else {
@@ -364,7 +399,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
   conv_epilogue<BM, BN, WM, WN, MODE, NT>(a, g, acc, m0, n0, smem, fd_hwq, fd_wq);
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU, int F8>
+template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU, int F8, bool PK8 = false>
 static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int pipe = STAGES * (BM + BN) * BK * 2;
   constexpr int epi = BM * (BN + 8) * 2 + 2 * (WM * WN * 64) * 4;  // + stats scratch
@@ -372,7 +407,7 @@ static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU, F8>),
+        reinterpret_cast<const void*>(&conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU, F8, PK8>),
         hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
@@ -391,12 +426,12 @@ static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   const long mtiles = (mmax + BM - 1) / BM;
   const long ntiles = (a.Cout + BN - 1) / BN;
   dim3 grid((unsigned)(mtiles * ntiles), 1, (unsigned)(classes * a.splits));
-  hipLaunchKernelGGL((conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU, F8>), grid, dim3(WM * WN * 64), smem,
+  hipLaunchKernelGGL((conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU, F8, PK8>), grid, dim3(WM * WN * 64), smem,
                      st, a);
   return (int)hipGetLastError();
 }
 
-template <int MODE, bool FASTK, bool RELU, int F8>
+template <int MODE, bool FASTK, bool RELU, int F8, bool PK8 = false>
 static int dispatch_glds2(const ConvFwdArgs& a, int variant, hipStream_t st) {
   if constexpr (F8 != 0) {
     // fp8: the bf16 winners only (256x256 / 256x128 for wide layers, 128x64 below)
@@ -411,6 +446,11 @@ static int dispatch_glds2(const ConvFwdArgs& a, int variant, hipStream_t st) {
   // variant: 2 = 2-stage 128-row tile, 3 = 3-stage 128-row tile, 4 = 3-stage 256x128 8 waves,
   // 5 = 2-stage 256x256 (8 waves of 128x64: half the LDS fragment traffic per MFMA of 4),
   // 6 = 2-stage 256x64 on 4 waves of 64x64 (N <= 64 layers)
+  if constexpr (PK8) {   // image layers: K = taps x 8 is short -> the 2-block-per-CU 128-row tiles
+    if (a.Cout > 64) return launch_glds<128, 128, 2, 2, MODE, 2, FASTK, RELU, F8, true>(a, st);
+    if (a.Cout > 32) return launch_glds<128, 64, 2, 2, MODE, 2, FASTK, RELU, F8, true>(a, st);
+    return -2;
+  }
   if (a.Cout > 128 && variant == 5) return launch_glds<256, 256, 2, 4, MODE, 2, FASTK, RELU, F8>(a, st);
   if (a.Cout > 64) {
     if (variant == 5) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU, F8>(a, st);
@@ -436,6 +476,10 @@ static int dispatch_glds(const ConvFwdArgs& a, int variant, hipStream_t st) {
     else
       return fastk ? dispatch_glds2<MODE, true, true, F8>(a, variant, st)
                    : dispatch_glds2<MODE, false, true, F8>(a, variant, st);
+  }
+  if constexpr (MODE == 0 && F8 == 0) {
+    if (!fastk && a.C1 == 8 && a.C2 == 0 && a.KW <= 8 && 8 % a.KW == 0 && variant != 1)
+      return dispatch_glds2<MODE, false, false, F8, true>(a, variant, st);
   }
   return fastk ? dispatch_glds2<MODE, true, false, F8>(a, variant, st)
                : dispatch_glds2<MODE, false, false, F8>(a, variant, st);
