@@ -153,7 +153,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                              const optional<Tensor>& xb2, int64_t act_bwd, int64_t Cvalid,
                              bool want_stats, const optional<Tensor>& qs_x1,
                              const optional<Tensor>& qs_x2, const optional<Tensor>& qs_w,
-                             const optional<Tensor>& y_qsite, int64_t y_qfmt) {
+                             const optional<Tensor>& y_qsite, int64_t y_qfmt,
+                             const optional<Tensor>& res) {
   check_act(x1, "conv_fwd x1", true);
   // fp8 operands: x e4m3 (activations) or e5m2 (gradients), weight image e4m3, each with
   // an fp8 scale site (csrc/fp8.hip); outputs stay bf16
@@ -225,6 +226,14 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   a.xb1 = act_bwd ? xb1->data_ptr() : nullptr;
   a.xb2 = (act_bwd && Csplit < Cout) ? xb2->data_ptr() : nullptr;
   a.act_bwd = (int)act_bwd;
+  a.res1 = nullptr;
+  if (res) {
+    check_act(*res, "conv_fwd res");
+    TORCH_CHECK(Csplit == Cout && res->size(0) == N && res->size(1) == Cout && res->size(2) == OH &&
+                    res->size(3) == OW,
+                "conv_fwd: res must match the (unsplit) output");
+    a.res1 = res->data_ptr();
+  }
   a.ws = nullptr;
   a.splits = 1;
   a.zero = zero_page(x1);
@@ -244,6 +253,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   if (Cout <= 16 && Cv <= 16 && Csplit == Cout && !reflect && up == 1 && C1 % 64 == 0 &&
       C2 % 64 == 0) {
     TORCH_CHECK(!fp8, "conv_fwd: fp8 is not supported on the tiny-Cout col path");
+    TORCH_CHECK(!res, "conv_fwd: no residual on the tiny-Cout col path");
     // col[i][t*Cvp + co]: each tap's outputs padded to Cvp (4 / 8 / 16) so col2im reads
     // one aligned vector per tap
     const int64_t T = KH * KW;
@@ -1098,7 +1108,7 @@ TORCH_LIBRARY(p2p, m) {
   m.def("conv_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, int mode, int KH, int KW, int stride, "
         "int pad, int reflect, int up, int act_in, int OH, int OW, int Cout, int act_out, int Csplit, "
         "Tensor? xb1, Tensor? xb2, int act_bwd, int Cvalid=0, bool want_stats=False, Tensor? qs_x1=None, "
-        "Tensor? qs_x2=None, Tensor? qs_w=None, Tensor(a!)? y_qsite=None, int y_qfmt=0) -> Tensor[]");
+        "Tensor? qs_x2=None, Tensor? qs_w=None, Tensor(a!)? y_qsite=None, int y_qfmt=0, Tensor? res=None) -> Tensor[]");
   m.def("fp8_quant(Tensor x, Tensor(a!) site, int fmt, int use_cur=0) -> Tensor");
   m.def("sn_power_iter(Tensor w, Tensor(a!) u, Tensor(b!) v) -> Tensor");
   m.def("fp8_amax(Tensor x, Tensor(a!) site, int slot) -> ()");

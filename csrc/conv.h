@@ -28,6 +28,8 @@ struct ConvFwdArgs {
   const void* xb1; // dgrad epilogue: multiply by act'(xb) (same channel split as y)
   const void* xb2;
   int act_bwd;
+  const void* res1; // dgrad epilogue: + res1 (bf16, y1's layout) after the act' gate -- the
+                    // other consumer's gradient of a tensor read twice (U-Net skips)
   float* ws;       // split-K fp32 accumulator [N*OH*OW][Cout] (pre-zeroed) when splits > 1
   int splits;
   int det;         // deterministic split-K: per-split slabs ws[split][N*OH*OW][Cout] (plain

@@ -189,6 +189,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
         v = __builtin_bit_cast(u32x4, vb);
       }
     }
+    if (a.res1 && first) {   // host: res1 only with Csplit == Cout
+      bf16x8 vb = __builtin_bit_cast(bf16x8, v);
+      const bf16x8 rb = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(a.res1) + pix * ld + cof);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) vb[q] = (bf16)((float)vb[q] + (float)rb[q]);
+      v = __builtin_bit_cast(u32x4, vb);
+    }
     bf16* y = static_cast<bf16*>(first ? a.y1 : a.y2);
     *reinterpret_cast<u32x4*>(y + pix * ld + cof) = v;
     if (qsh.q) {  // host: only with Csplit == Cout, no act_bwd

@@ -293,6 +293,11 @@ __global__ void __launch_bounds__(256) conv_finalize_kernel(ConvFwdArgs a, long 
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] *= act_grad_from_input((float)xv[j], a.act_bwd);
     }
+    if (a.res1 && first) {
+      const bf16x8 rv = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(a.res1) + pix * ld + cof);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (float)(bf16)v[j] + (float)rv[j];
+    }
     bf16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];

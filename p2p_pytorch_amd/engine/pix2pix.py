@@ -129,6 +129,9 @@ class Pix2PixStep:
         with self._phase("G_bwd_opt"):
             self._zero(self.opt_G, self.reducer_g)
             loss_G.backward()
+            if real_A.is_cuda and _native.get_backend() == "native":
+                from ..ops import hip
+                hip.assert_no_deferred()      # every parked U-Net skip gradient consumed
             if self.reducer_g is not None:
                 self.reducer_g.finish()
             self._guarded_step(self.opt_G, self.reducer_g, loss_G)

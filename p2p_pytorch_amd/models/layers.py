@@ -5,6 +5,8 @@ fuse the neighbouring pad / upsample / concat / activation into the conv itself.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -26,12 +28,13 @@ class Conv2d(nn.Conv2d):
         self.norm_stats = False   # set by link_norm(): a norm consumes the output
         self.grad_gate = None     # set by link_gate(): apply the producer's act' in dgrad
         self.out_gated = False    # set by link_gate(): consumers apply act_out' for us
+        self.skip_grad = None     # set by link_skip(): "take" a parked skip gradient in dgrad
 
     def forward(self, x):  # noqa: D401
         return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.pad_mode,
                           self.upsample, self.act_in, self.act_out,
                           stats=self.norm_stats and self.training, grad_gate=self.grad_gate,
-                          out_gated=self.out_gated)
+                          out_gated=self.out_gated, skip_grad=self.skip_grad)
 
 
 class ConvTranspose2d(nn.ConvTranspose2d):
@@ -47,12 +50,14 @@ class ConvTranspose2d(nn.ConvTranspose2d):
         self.norm_stats = False
         self.grad_gate = None
         self.out_gated = False
+        self.skip_grad = None
 
     def forward(self, x):
         return ops.conv_transpose2d(x, self.weight, self.bias, self.stride[0], self.padding[0],
                                     self.act_in, self.act_out,
                                     stats=self.norm_stats and self.training,
-                                    grad_gate=self.grad_gate, out_gated=self.out_gated)
+                                    grad_gate=self.grad_gate, out_gated=self.out_gated,
+                                    skip_grad=self.skip_grad)
 
 
 def link_norm(conv, norm):
@@ -60,6 +65,18 @@ def link_norm(conv, norm):
     emits the per-tile (mean, M2) partials and the norm skips its own statistics pass."""
     if isinstance(norm, (InstanceNorm2d, BatchNorm2d)) and hasattr(conv, "norm_stats"):
         conv.norm_stats = True
+
+
+def link_skip(first, second):
+    """``first`` (whose backward runs first: the decoder ConvT reading a U-Net skip as the
+    x1 half of its virtual concat) parks its skip gradient; ``second`` (the next encoder
+    conv, reading the same tensor as its only input) adds it in its dgrad epilogue -- one
+    gradient write per skip instead of two writes plus autograd's accumulate kernel."""
+    if os.environ.get("P2P_SKIP_GRAD_FUSE", "1") == "0":   # A/B knob
+        return
+    if hasattr(first, "skip_grad") and hasattr(second, "skip_grad"):
+        first.skip_grad = "defer"
+        second.skip_grad = "take"
 
 
 def link_gate(producer, consumers):

@@ -28,7 +28,7 @@ from __future__ import annotations
 
 import torch.nn as nn
 
-from .layers import Conv2d, ConvTranspose2d, Dropout, link_gate, link_norm, norm_layer
+from .layers import Conv2d, ConvTranspose2d, Dropout, link_gate, link_norm, link_skip, norm_layer
 
 
 class UnetGenerator(nn.Module):
@@ -70,6 +70,9 @@ class UnetGenerator(nn.Module):
         # outermost encoder output feeds downs[1] and (skip) ups[0]; innermost feeds ups[n-1]
         link_gate(self.downs[0], [self.downs[1], self.ups[0]])
         link_gate(self.downs[n - 1], [self.ups[n - 1]])
+        # skip i is read by ups[i] (backward first) and downs[i + 1]: one gradient write
+        for i in range(n - 1):
+            link_skip(self.ups[i], self.downs[i + 1])
 
     def forward(self, x):
         n = self.num_downs

@@ -25,21 +25,22 @@ def _hip():
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, pad_mode="zeros", upsample=1,
-           act_in=None, act_out=None, stats=False, grad_gate=None, out_gated=False):
+           act_in=None, act_out=None, stats=False, grad_gate=None, out_gated=False, skip_grad=None):
     """HIP-path fusion hints (ignored by the oracle): ``stats`` -- the output feeds a norm,
     emit its statistics; ``grad_gate`` / ``out_gated`` -- move the producer's activation
-    derivative into this conv's dgrad epilogue (see ``hip._ConvCfg``)."""
+    derivative into this conv's dgrad epilogue; ``skip_grad`` -- one gradient write for a
+    tensor read by two convs (see ``hip._ConvCfg``)."""
     if _native.use_native(_first(x)):
         return _hip().conv2d(x, weight, bias, stride, padding, pad_mode, upsample, act_in, act_out,
-                             stats, grad_gate, out_gated)
+                             stats, grad_gate, out_gated, skip_grad)
     return ref.conv2d(x, weight, bias, stride, padding, pad_mode, upsample, act_in, act_out)
 
 
 def conv_transpose2d(x, weight, bias=None, stride=2, padding=1, act_in=None, act_out=None,
-                     stats=False, grad_gate=None, out_gated=False):
+                     stats=False, grad_gate=None, out_gated=False, skip_grad=None):
     if _native.use_native(_first(x)):
         return _hip().conv_transpose2d(x, weight, bias, stride, padding, act_in, act_out, stats,
-                                       grad_gate, out_gated)
+                                       grad_gate, out_gated, skip_grad)
     return ref.conv_transpose2d(x, weight, bias, stride, padding, act_in, act_out)
 
 

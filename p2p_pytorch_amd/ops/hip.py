@@ -138,13 +138,14 @@ def _weight_image_fp8(w: torch.Tensor, swap: int, xp: int, yp: int):
 
 def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout, act_out,
                Csplit, xb1, xb2, act_bwd, Cvalid, want, weight=None, swap=0, xp=0, yp=0, role="x",
-               y_qkey=None):
+               y_qkey=None, res=None):
     """conv_fwd on bf16 operands, or -- fp8 precision and a geometry the fp8 kernel takes --
     on fp8 ones: x (role 'x': activations, e4m3; 'gy': gradients, e5m2) quantised with
     delayed scaling (or taken from the producer's fused shadow), the weight image with
     current scaling.  ``y_qkey``: also emit an e4m3 shadow of the output from the epilogue
     (the output feeds other fp8 convs directly) -- appended last to the returned list.
-    ``wimg`` may be None (built on demand for the bf16 path)."""
+    ``wimg`` may be None (built on demand for the bf16 path).  ``res``: bf16 tensor added to
+    the (unsplit) output in the epilogue, after the act' gate."""
     C1 = x1.shape[1]
     C2 = 0 if x2 is None else x2.shape[1]
     if weight is not None and _f8.enabled() and _f8.conv_ok(C1, C2, Cout, act_in):
@@ -158,7 +159,7 @@ def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, 
         a1, s1 = _f8.quant(x1, (k, role, 1), fmt)
         a2, s2 = _f8.quant(x2, (k, role, 2), fmt) if x2 is not None else (None, None)
         return P().conv_fwd(a1, a2, w8, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout,
-                            act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, s1, s2, sw, *yq)
+                            act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, s1, s2, sw, *yq, res=res)
     if wimg is None:
         wimg = _weight_image(weight, swap, xp, yp)
     yq = ()
@@ -166,7 +167,7 @@ def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, 
         ysite, fresh = _f8.producer_site(x1.device, y_qkey)
         yq = (None, None, None, None, 0) if fresh else (None, None, None, ysite, _f8.E4M3)
     return P().conv_fwd(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout,
-                        act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, *yq)
+                        act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, *yq, res=res)
 
 
 def prepare_weights(*modules):
@@ -259,12 +260,20 @@ class _ConvCfg:
     """``grad_gate``: activation derivative (from the input value) applied to the input
     gradient in the dgrad epilogue -- the producer of this conv's input stored
     ``act(x)`` and set ``out_gated`` so it skips its own gate pass (valid only when every
-    consumer of that output gates; the models wire both ends)."""
+    consumer of that output gates; the models wire both ends).
+
+    ``skip_grad``: a tensor read by two convs (a U-Net skip: the decoder ConvT, whose backward
+    runs first, and the next encoder conv) gets ONE gradient write instead of two plus an
+    autograd add -- "defer": this conv's x1 gradient is parked in ``_DEFERRED`` (keyed by the
+    tensor's storage) and not returned; "take": this conv's dgrad epilogue adds the parked
+    gradient of its x1.  ``assert_no_deferred()`` checks after backward that every parked
+    gradient was consumed."""
     __slots__ = ("transposed", "KH", "KW", "stride", "pad", "reflect", "up", "act_in", "act_out",
-                 "stats", "grad_gate", "out_gated")
+                 "stats", "grad_gate", "out_gated", "skip_grad")
 
     def __init__(self, transposed, KH, KW, stride, pad, reflect, up, act_in, act_out, stats=False,
-                 grad_gate=None, out_gated=False):
+                 grad_gate=None, out_gated=False, skip_grad=None):
+        self.skip_grad = skip_grad
         self.stats = stats
         self.grad_gate = grad_gate
         self.out_gated = out_gated
@@ -289,6 +298,18 @@ def _prep_inputs(x1, x2):
         return x1, x2, C1, C2, C1 + C2, False
     cp = _pad8(C1 + C2)
     return P().pad_channels(x1, x2, cp), None, C1, C2, cp, True
+
+
+_DEFERRED: dict = {}   # storage ptr -> parked input gradient (``_ConvCfg.skip_grad``)
+
+
+def assert_no_deferred():
+    """Every gradient parked by a skip_grad="defer" conv must have been consumed by its
+    "take" partner during the same backward; a leftover would be a lost gradient."""
+    if _DEFERRED:
+        n = len(_DEFERRED)
+        _DEFERRED.clear()
+        raise RuntimeError(f"skip_grad: {n} deferred gradient(s) were never consumed")
 
 
 class ConvFn(torch.autograd.Function):
@@ -373,10 +394,16 @@ class ConvFn(torch.autograd.Function):
                                   q2 if (act_in and q2 is not None) else None, act_in, C1 + C2,
                                   False, weight, 0, Cp, Coutp, "gy")
             else:
+                res = None
+                if cfg.skip_grad == "take" and q2 is None and not packed and need_x1:
+                    res = _DEFERRED.pop(q1.data_ptr(), None)
+                    if res is not None and (res.shape != (q1.shape[0], Cp, H, W) or Cp != C1):
+                        _DEFERRED[q1.data_ptr()] = res   # not fusable: added below instead
+                        res = None
                 outs = _conv_call(gyp, None, None, None, 1, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
                                   split, q1 if act_in else None,
                                   q2 if (act_in and q2 is not None) else None, act_in, C1 + C2,
-                                  False, weight, 1, Cp, Coutp, "gy")
+                                  False, weight, 1, Cp, Coutp, "gy", res=res)
             if q2 is not None:
                 gx1, gx2 = outs[0], outs[1]
             elif packed:
@@ -389,6 +416,16 @@ class ConvFn(torch.autograd.Function):
                 gx1 = None
             if not need_x2:
                 gx2 = None
+            if cfg.skip_grad == "take" and gx1 is not None and q2 is None:
+                parked = _DEFERRED.pop(q1.data_ptr(), None)
+                if parked is not None:
+                    gx1 = gx1 + parked
+            if cfg.skip_grad == "defer" and gx1 is not None:
+                key = q1.data_ptr()
+                if key in _DEFERRED:
+                    raise RuntimeError("skip_grad: a deferred gradient of this tensor is pending")
+                _DEFERRED[key] = gx1
+                gx1 = None
         if need_w:
             gw = torch.empty_like(weight, dtype=torch.float32, memory_format=torch.contiguous_format)
             act_in = _act_code(cfg.act_in)
@@ -425,22 +462,22 @@ def _pair(v):
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, pad_mode="zeros", upsample=1,
-           act_in=None, act_out=None, stats=False, grad_gate=None, out_gated=False):
+           act_in=None, act_out=None, stats=False, grad_gate=None, out_gated=False, skip_grad=None):
     s, s2 = _pair(stride)
     p, p2 = _pair(padding)
     if s != s2 or p != p2:
         raise NotImplementedError("anisotropic stride/padding")
     x1, x2 = _split_input(x)
     cfg = _ConvCfg(False, weight.shape[2], weight.shape[3], s, p, pad_mode == "reflect" and p > 0,
-                   int(upsample or 1), act_in, act_out, stats, grad_gate, out_gated)
+                   int(upsample or 1), act_in, act_out, stats, grad_gate, out_gated, skip_grad)
     return ConvFn.apply(x1, x2, weight, bias, cfg)
 
 
 def conv_transpose2d(x, weight, bias=None, stride=2, padding=1, act_in=None, act_out=None,
-                     stats=False, grad_gate=None, out_gated=False):
+                     stats=False, grad_gate=None, out_gated=False, skip_grad=None):
     x1, x2 = _split_input(x)
     cfg = _ConvCfg(True, weight.shape[2], weight.shape[3], int(stride), int(padding), False, 1,
-                   act_in, act_out, stats, grad_gate, out_gated)
+                   act_in, act_out, stats, grad_gate, out_gated, skip_grad)
     return ConvFn.apply(x1, x2, weight, bias, cfg)
 
 

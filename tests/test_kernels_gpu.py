@@ -407,6 +407,47 @@ def test_unet_patchgan_step_matches_oracle():
     assert not worse, worse
 
 
+def test_unet_skip_grad_fusion_matches_unfused():
+    """U-Net skip gradients: ONE write (decoder ConvT parks it, the encoder conv's dgrad
+    epilogue adds it) must equal autograd's two writes + accumulate, and leave nothing
+    parked."""
+    from p2p_pytorch_amd.models import define_G
+    from p2p_pytorch_amd.ops import hip
+    torch.manual_seed(0)
+    G = define_G(netG="unet_128", gpu_id=DEV, verbose=False, use_dropout=False)
+    A = bf(torch.rand(2, 3, 128, 128, device=DEV) * 2 - 1)
+    gy = bf(torch.rand(2, 3, 128, 128, device=DEV) - 0.5)
+    convs = [m for m in G.modules() if hasattr(m, "skip_grad")]
+    assert sum(m.skip_grad == "defer" for m in convs) == G.num_downs - 1
+    assert sum(m.skip_grad == "take" for m in convs) == G.num_downs - 1
+
+    def run(fused, backend="native"):
+        saved = [m.skip_grad for m in convs]
+        if not fused:
+            for m in convs:
+                m.skip_grad = None
+        _native.set_backend(backend)
+        try:
+            G.zero_grad(set_to_none=True)
+            a, g = (A, gy) if backend == "native" else (A.float(), gy.float())
+            G(a).backward(g)
+            hip.assert_no_deferred()
+        finally:
+            _native.set_backend("native")
+            for m, v in zip(convs, saved):
+                m.skip_grad = v
+        return {n: p.grad.detach().float().clone() for n, p in G.named_parameters()}
+
+    g32 = run(False, "torch")
+    g0 = run(False)
+    g1 = run(True)
+    # same math up to bf16 rounding order; judged against the fp32 oracle the fused path
+    # must be no less accurate than the unfused one (a deep U-Net amplifies rounding)
+    worse = [(n, rel_err(g1[n], g32[n]), rel_err(g0[n], g32[n])) for n in g0
+             if rel_err(g1[n], g32[n]) > 1.5 * rel_err(g0[n], g32[n]) + 0.02]
+    assert not worse, worse
+
+
 # ---------------------------------------------------------------- family-R fringe ops
 def _grad_pair(fn_h, fn_r, x, gy_seed=21):
     """HIP op on the GPU vs the same op in fp32 on the CPU (the oracle must not depend on
