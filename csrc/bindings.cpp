@@ -911,6 +911,30 @@ Tensor pad_channels(const Tensor& a, const optional<Tensor>& b, int64_t Co) {
   return out;
 }
 
+// pad_channels_into: the same into a caller-provided NHWC view (a batch slice of a bigger
+// packed tensor: the two halves of the fused D batch are packed straight into one buffer)
+void pad_channels_into(const Tensor& a, const optional<Tensor>& b, const Tensor& out) {
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && a.dim() == 4, "pad_channels_into: a");
+  check_act(out, "pad_channels_into out");
+  Tensor ac = a.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor bc;
+  int64_t Cb = 0;
+  if (b) {
+    bc = b->contiguous(at::MemoryFormat::ChannelsLast);
+    TORCH_CHECK(bc.size(0) == a.size(0) && bc.size(2) == a.size(2) && bc.size(3) == a.size(3),
+                "pad_channels_into: b shape");
+    Cb = bc.size(1);
+  }
+  const int64_t Co = out.size(1);
+  TORCH_CHECK(out.size(0) == a.size(0) && out.size(2) == a.size(2) && out.size(3) == a.size(3) &&
+                  ac.size(1) + Cb <= Co && Co % 8 == 0,
+              "pad_channels_into: out shape");
+  check_rc(p2p_pad_channels(ac.data_ptr(), (int)ac.size(1), bc.defined() ? bc.data_ptr() : nullptr,
+                            (int)Cb, a.size(0) * a.size(2) * a.size(3), (int)Co, out.data_ptr(),
+                            cur_stream(a)),
+           "pad_channels_into");
+}
+
 Tensor slice_channels(const Tensor& x, int64_t c0, int64_t C) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4, "slice_channels: x");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "slice_channels: NHWC input");
@@ -1143,6 +1167,7 @@ TORCH_LIBRARY(p2p, m) {
   m.def("act(Tensor a, Tensor? b, int act, int mode) -> Tensor");
   m.def("dropout(Tensor x, float p, Tensor seed, int salt) -> Tensor");
   m.def("pad_channels(Tensor a, Tensor? b, int Co) -> Tensor");
+  m.def("pad_channels_into(Tensor a, Tensor? b, Tensor(a!) out) -> ()");
   m.def("slice_channels(Tensor x, int c0, int C) -> Tensor");
   m.def("colsum(Tensor x, Tensor(a!) out, float scale, bool accumulate) -> ()");
   m.def("loss_fwd(Tensor a, Tensor? b, int kind, float t, float scale) -> Tensor");
@@ -1170,6 +1195,7 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("act", act);
   m.impl("dropout", dropout);
   m.impl("pad_channels", pad_channels);
+  m.impl("pad_channels_into", pad_channels_into);
   m.impl("pad_fold", pad_fold);
   m.impl("prelu_fwd", prelu_fwd);
   m.impl("prelu_bwd", prelu_bwd);

@@ -100,8 +100,15 @@ class Pix2PixStep:
                     netD, MultiscaleDiscriminator)
             if fuse:
                 B = real_A.shape[0]
-                pred = netD(self._d_input(torch.cat((real_A, real_A), 0),
-                                          torch.cat((fake_B.detach(), real_B), 0)))
+                if (real_A.is_cuda and _native.get_backend() == "native"
+                        and (real_A.shape[1] + real_B.shape[1]) % 8):
+                    # packed pad-8 image input, both halves written in place (no cat)
+                    from ..ops import hip
+                    d_in = hip.pack_pairs([(real_A, fake_B.detach()), (real_A, real_B)])
+                else:
+                    d_in = self._d_input(torch.cat((real_A, real_A), 0),
+                                         torch.cat((fake_B.detach(), real_B), 0))
+                pred = netD(d_in)
                 loss_D_fake = self.criterionGAN(pred[:B], False)
                 loss_D_real = self.criterionGAN(pred[B:], True)
             else:

@@ -284,8 +284,33 @@ class _ConvCfg:
         self.act_in, self.act_out = act_in, act_out
 
 
+def pack_pairs(pairs):
+    """Channel-concat + zero-pad each ``(a, b)`` pair into one batch-stacked packed NHWC
+    tensor (a pad-8 image conv input) with one kernel per pair and no ``torch.cat``
+    (the fused 2B discriminator batch).  The result carries its logical channel split
+    (``_p2p_packed``), so a conv reading it takes the packed path with the right weight
+    layout; it is a constant (no gradient flows back to the pairs)."""
+    a0, b0 = pairs[0]
+    C1, C2 = a0.shape[1], b0.shape[1]
+    N = sum(a.shape[0] for a, _ in pairs)
+    out = torch.empty(N, _pad8(C1 + C2), a0.shape[2], a0.shape[3], device=a0.device,
+                      dtype=torch.bfloat16, memory_format=CL)
+    n0 = 0
+    for a, b in pairs:
+        if a.shape[1] != C1 or b.shape[1] != C2:
+            raise ValueError("pack_pairs: every pair needs the same channel split")
+        n = a.shape[0]
+        P().pad_channels_into(to_nhwc_bf16(a.detach()), to_nhwc_bf16(b.detach()), out[n0:n0 + n])
+        n0 += n
+    out._p2p_packed = (C1, C2)
+    return out
+
+
 def _prep_inputs(x1, x2):
     """Return (q1, q2, C1, C2, Cp, packed): kernel inputs with 8-aligned channel counts."""
+    pk = getattr(x1, "_p2p_packed", None)
+    if pk is not None and x2 is None:   # pre-packed by pack_pairs()
+        return x1, None, pk[0], pk[1], x1.shape[1], True
     x1 = to_nhwc_bf16(x1)
     C1 = x1.shape[1]
     if x2 is None:
