@@ -55,6 +55,10 @@ def parse():
     p.add_argument("--lamb", type=float, default=100.0)
     p.add_argument("--gan_mode", default="vanilla")
     p.add_argument("--bucket_mb", type=float, default=64.0)
+    p.add_argument("--comm_dtype", default="fp32", choices=["fp32", "bf16"],
+                   help="gradient all-reduce wire dtype (bf16: pre-scaled, half the xGMI bytes)")
+    p.add_argument("--force_comm", action="store_true",
+                   help="attach the reducers and issue the RCCL collectives even on one GPU")
     p.add_argument("--no_graph", action="store_true", help="(native) disable hipGraph capture")
     p.add_argument("--graph", action="store_true",
                    help="(native) force hipGraph capture also for N>1 (default: N == 1 only)")
@@ -101,10 +105,15 @@ def main():
     pdist.broadcast_module(netD)
 
     reducer_g = reducer_d = None
-    if world > 1:
+    if world > 1 or args.force_comm:
         from p2p_pytorch_amd.parallel import GradReducer
-        reducer_g = GradReducer(netG, bucket_mb=args.bucket_mb)
-        reducer_d = GradReducer(netD, bucket_mb=args.bucket_mb)
+        if world == 1:
+            pdist.init_single(dev)
+        cdt = torch.bfloat16 if args.comm_dtype == "bf16" else None
+        reducer_g = GradReducer(netG, bucket_mb=args.bucket_mb, comm_dtype=cdt,
+                                force_comm=args.force_comm)
+        reducer_d = GradReducer(netD, bucket_mb=args.bucket_mb, comm_dtype=cdt,
+                                force_comm=args.force_comm)
 
     if args.impl == "torch":
         act_dtype = torch.float32
@@ -179,7 +188,11 @@ def main():
     finite = all(v == v and abs(v) != float("inf") for v in loss_vals.values())
 
     img_s = world * B * args.steps / dt_max
-    base = EAGER_BASELINE_IMG_S_PER_GPU
+    # the measured eager baseline is for the headline config only (256x256 pix2pix U-Net-256
+    # + 70x70 PatchGAN training); other sizes / families / modes have no baseline
+    headline = (not ref and args.mode == "train" and S == 256 and args.netG == "unet_256"
+                and args.netD == "basic")
+    base = EAGER_BASELINE_IMG_S_PER_GPU if headline else None
     model = (f"pix2pix {args.netG} + PatchGAN {args.netD} (70x70)" if not ref else
              "reference compression GAN: CompressionNetwork + ExpandNetwork + 3-scale SN PatchGAN + VGG19 loss")
     kind = "train" if args.mode == "train" else "inference (generator forward)"
@@ -194,7 +207,7 @@ def main():
         "ms_per_step": round(1000.0 * dt_max / args.steps, 3),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(img_s / (base * world), 3) if (base and not ref and args.mode == "train") else None,
+        "vs_baseline": round(img_s / (base * world), 3) if base else None,
         "dtype": "fp8+bf16" if args.precision == "fp8" else "bf16",
         "data": "synthetic (random paired images, random-init weights)",
         "config": {"model": model,
@@ -204,6 +217,10 @@ def main():
                    "hipgraph": bool(use_graph),
                    "conv_precision": ("fp8 e4m3 fwd / e5m2 dgrad, bf16 wgrad + first/last layers"
                                       if args.precision == "fp8" else "bf16")},
+        "max_mem_gib": (round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)
+                        if dev.type == "cuda" else None),
+        "comm": ({"dtype": args.comm_dtype, "bucket_mb": args.bucket_mb}
+                 if reducer_g is not None else None),
         "losses_finite": finite,
         "losses": loss_vals,
     }

@@ -30,7 +30,8 @@ def _cpu_state(module):
 
 
 def save_checkpoint(path, epoch, net_g, net_c=None, net_d=None, opt_g=None, opt_d=None,
-                    sched_g=None, sched_d=None, losslogger=None, extra=None, rank=0):
+                    sched_g=None, sched_d=None, losslogger=None, extra=None, rank=0,
+                    opt_c=None, sched_c=None):
     """Write the reference dict (+ full-resume keys) atomically; no-op on ranks != 0."""
     if rank != 0:
         return None
@@ -47,6 +48,10 @@ def save_checkpoint(path, epoch, net_g, net_c=None, net_d=None, opt_g=None, opt_
         state["scheduler_g"] = sched_g.state_dict()
     if sched_d is not None:
         state["scheduler_d"] = sched_d.state_dict()
+    if opt_c is not None:
+        state["optimizer_c"] = opt_c.state_dict()
+    if sched_c is not None:
+        state["scheduler_c"] = sched_c.state_dict()
     state["losslogger"] = list(losslogger or [])
     state["rng_cpu"] = torch.get_rng_state()
     if torch.cuda.is_available():
@@ -67,8 +72,14 @@ def _move_optimizer_state(opt, device):
                 st[k] = v.to(device)
 
 
+def has_scheduler_state(path) -> bool:
+    """True when ``path`` carries scheduler state (a file written here, not by the reference)."""
+    return "scheduler_g" in torch.load(path, map_location="cpu", weights_only=True, mmap=True)
+
+
 def load_checkpoint(path, net_g=None, net_c=None, net_d=None, opt_g=None, opt_d=None,
-                    sched_g=None, sched_d=None, device=None, strict=True):
+                    sched_g=None, sched_d=None, device=None, strict=True, opt_c=None,
+                    sched_c=None):
     """Restore whatever the file holds; returns (start_epoch, losslogger).
 
     A reference-written file (epoch + G + C only) restores the networks and the epoch;
@@ -80,12 +91,12 @@ def load_checkpoint(path, net_g=None, net_c=None, net_d=None, opt_g=None, opt_d=
         net_c.load_state_dict(state["state_dict_c"], strict=strict)
     if net_d is not None and "state_dict_d" in state:
         net_d.load_state_dict(state["state_dict_d"], strict=strict)
-    for opt, key in ((opt_g, "optimizer_g"), (opt_d, "optimizer_d")):
+    for opt, key in ((opt_g, "optimizer_g"), (opt_d, "optimizer_d"), (opt_c, "optimizer_c")):
         if opt is not None and key in state:
             opt.load_state_dict(state[key])
             if device is not None:
                 _move_optimizer_state(opt, device)
-    for sch, key in ((sched_g, "scheduler_g"), (sched_d, "scheduler_d")):
+    for sch, key in ((sched_g, "scheduler_g"), (sched_d, "scheduler_d"), (sched_c, "scheduler_c")):
         if sch is not None and key in state:
             sch.load_state_dict(state[key])
     if "rng_cpu" in state:

@@ -15,12 +15,23 @@ Reference semantics kept by default: optimizer_c is built
 D's parameters (A1) and round() has no gradient (A2), so the C phase changes no
 parameter -- its loss is computed and logged, its backward is skipped because it is
 provably a no-op (``c_phase_backward=True`` runs it anyway for cost parity).
-``train_c=True`` fixes both quirks: a straight-through quantiser and an Adam over C.
+``train_c=True`` fixes both quirks: a straight-through quantiser and an Adam over C
+(``opt_c``, always built so train.py can schedule and checkpoint it like the reference's
+``optimizer_c`` / ``net_c_scheduler``, train.py:243-246, :441-443).
+
+D's gradients from the G loss are discarded by the reference (``optimizer_d.zero_grad()``
+before ``loss_d.backward()``, train.py:384-389), so the third D forward (the one the G loss
+sees) runs with D frozen: the G backward computes only D's input gradients, and no D
+gradient -- hence no D all-reduce under data parallelism -- exists for that backward.
+Discarded backwards that still reach a reduced network (the C-phase backward into G) run
+under ``reducer.paused()``.
 
 All three D passes go through the fused ops (virtual concat of (a, b) on the native
 path; spectral-norm 1/sigma on the weight image).  Losses stay on the device.
 """
 from __future__ import annotations
+
+import contextlib
 
 import torch
 
@@ -41,17 +52,16 @@ class _STEQuantize(torch.autograd.Function):
         return g, None
 
 
-def set_requires_grad(nets, flag):
-    for n in nets:
-        for p in n.parameters():
-            p.requires_grad_(flag)
+def set_requires_grad(params, flag):
+    for p in params:
+        p.requires_grad_(flag)
 
 
 class CompressGANStep:
     def __init__(self, net_g, net_d, net_c, lr=2e-4, beta1=0.5, bits=3, lambda_feat=10.0,
                  lambda_vgg=10.0, lambda_tv=1.0, n_layers_d=3, num_d=3, image_pool=None,
                  train_c=False, c_phase_backward=False, vgg=None, reducer_g=None,
-                 reducer_d=None, nan_guard=True):
+                 reducer_d=None, reducer_c=None, nan_guard=True):
         self.net_g, self.net_d, self.net_c = net_g, net_d, net_c
         self.criterionGAN = GANLoss()                      # LSGAN, reference default
         self.criterionVGG = vgg if vgg is not None else VGGLoss()
@@ -63,14 +73,26 @@ class CompressGANStep:
         self.d_weights = 1.0 / num_d
         self.opt_g = make_adam(net_g.parameters(), lr=lr, betas=(beta1, 0.999))
         self.opt_d = make_adam(net_d.parameters(), lr=lr, betas=(beta1, 0.999))
+        # D's trainable parameters (SN's weight_u / weight_v are Parameters that never train)
+        self._d_trainable = [p for p in net_d.parameters() if p.requires_grad]
         self.train_c = train_c
-        self.opt_c = make_adam(net_c.parameters(), lr=lr, betas=(beta1, 0.999)) if train_c else None
+        self.opt_c = make_adam(net_c.parameters(), lr=lr, betas=(beta1, 0.999))
         self.c_phase_backward = c_phase_backward
         self.image_pool = image_pool
-        self.reducer_g, self.reducer_d = reducer_g, reducer_d
+        self.reducer_g, self.reducer_d, self.reducer_c = reducer_g, reducer_d, reducer_c
         self.nan_guard = nan_guard
-        self.skipped = None
+        self.skipped = torch.zeros((), device=dev) if nan_guard else None
         self.timer = None     # optional utils.PhaseTimer: per-phase HIP-event ms
+
+    def optimizers(self):
+        return [self.opt_g, self.opt_d, self.opt_c]
+
+    def state_tensors(self):
+        """Tensors one step mutates (CapturedStep snapshots them around its warmup)."""
+        from .graph import trainer_state_tensors
+        extra = [self.skipped] if self.skipped is not None else []
+        return trainer_state_tensors([self.net_g, self.net_d, self.net_c], self.optimizers(),
+                                     extra)
 
     def _phase(self, name):
         return self.timer.phase(name) if self.timer is not None else trace_range(name)
@@ -104,6 +126,7 @@ class CompressGANStep:
         compressed = self._quant(C(real_b))
         fake_b = G(compressed.detach())
         # ---- D losses (reference computes all losses before any update)
+        set_requires_grad(self._d_trainable, True)
         fake_in = self._d_in(real_a, fake_b.detach())
         if self.image_pool is not None and self.image_pool.pool_size > 0:
             fake_in = self.image_pool.query(torch.cat((real_a, fake_b.detach()), 1))
@@ -112,8 +135,12 @@ class CompressGANStep:
         pred_real = D(self._d_in(real_a, real_b.detach()))
         loss_d_real = self.criterionGAN(pred_real, True)
         loss_d = (loss_d_fake + loss_d_real) * 0.5
-        # ---- G losses
+        # ---- G losses: D frozen (its G-loss gradients are discarded by the reference)
+        set_requires_grad(self._d_trainable, False)
         pred_fake_g = D(self._d_in(real_a, fake_b))
+        # back on before any backward: autograd's AccumulateGrad skips a leaf that no longer
+        # requires grad, which would silently drop the D-loss gradients
+        set_requires_grad(self._d_trainable, True)
         loss_g_gan = self.criterionGAN(pred_fake_g, True)
         loss_feat = 0.0
         for i in range(len(pred_fake_g)):
@@ -142,13 +169,18 @@ class CompressGANStep:
             fake_ac = G(compressed)     # also advances G's BN running stats, as the reference
             loss_c = ops.mse(fake_ac, real_b) + self.criterionVGG(compressed, real_b) * \
                 self.lambda_vgg
+        paused_g = (self.reducer_g.paused() if self.reducer_g is not None
+                    else contextlib.nullcontext())
         if self.train_c:
-            self.opt_c.zero_grad(set_to_none=True)
-            self.opt_g.zero_grad(set_to_none=True)
-            loss_c.backward()
-            self.opt_c.step()
+            self._zero(self.opt_c, self.reducer_c)
+            with paused_g:      # the G grads of this backward are discarded (zeroed next step)
+                loss_c.backward()
+            if self.reducer_c is not None:
+                self.reducer_c.finish()
+            self._opt_step(self.opt_c, self.reducer_c, loss_c)
         elif self.c_phase_backward:
-            loss_c.backward()   # reference: grads land on G (zeroed next step) -- no effect
+            with paused_g:      # reference: grads land on G (zeroed next step) -- no effect
+                loss_c.backward()
         return {"D": loss_d.detach(), "G_GAN": loss_g_gan.detach(),
                 "C": loss_c.detach(), "G_GAN_Feat": torch.as_tensor(loss_feat).detach(),
                 "VGG": content.detach(), "TV": tv.detach(), "G": loss_g.detach()}

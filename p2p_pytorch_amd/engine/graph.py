@@ -6,22 +6,89 @@ is captured ONCE into a HIP graph (``torch.cuda.CUDAGraph`` is hipGraph on ROCm)
 replayed: zero Python / launch overhead, identical kernels and numerics.
 
 Requirements the native path already meets (see ops/hip.py, engine/optim.py):
-  * no host synchronisation inside the step (losses stay on the device);
+  * no host synchronisation inside the step (losses stay on the device; the data-parallel
+    reducer's collectives are stream-ordered, so RCCL all-reduces are captured too);
   * per-step state that must change between replays lives in device memory: the Adam
     step counter and learning rate (FusedAdam), the dropout seed (``hip.advance_rng``);
   * bf16 weight images are re-cast inside the captured region (``hip.begin_step``).
+
+Warmup: capture needs a few real steps first (allocator pools, the reducer's ready-order
+re-bucketing, fp8 scale bootstraps).  When the trainer exposes ``state_tensors()`` every
+tensor a step mutates (parameters, buffers, optimizer moments and counters, RNG seeds,
+guard counters) is snapshotted before the warmup and restored before the capture, so
+replay k is exactly eager step k from the same initial state -- the warmup trains nothing
+(tests/test_graph_gpu.py pins this bitwise in deterministic mode).
 New input batches are copied into the static input buffers before each replay.
-Multi-GPU runs use the eager path (RCCL collectives are launched from the reducer hooks).
 """
 from __future__ import annotations
 
 import torch
 
 
+def trainer_state_tensors(modules, optimizers, extra=()):
+    """Every tensor a training step mutates in place: parameters and buffers of
+    ``modules``, the optimizer state (moments, device step / lr counters) and ``extra``."""
+    out, seen = [], set()
+
+    def add(t):
+        if isinstance(t, torch.Tensor) and id(t) not in seen:
+            seen.add(id(t))
+            out.append(t)
+
+    for m in modules:
+        if m is None:
+            continue
+        for t in m.parameters():
+            add(t.data)
+        for t in m.buffers():
+            add(t)
+    for opt in optimizers:
+        if opt is None:
+            continue
+        for st in opt.state.values():
+            for v in st.values():
+                add(v)
+        for t in getattr(opt, "_step_t", []):
+            add(t)
+    for t in extra:
+        add(t)
+    return out
+
+
+class _Snapshot:
+    def __init__(self, trainer):
+        self.trainer = trainer
+        self.tensors = list(trainer.state_tensors())
+        self.saved = [t.detach().clone() for t in self.tensors]
+        # python-side optimizer step counts (reported by state_dict only)
+        self.py_steps = []
+        for opt in getattr(trainer, "optimizers", lambda: [])():
+            if opt is not None:
+                self.py_steps.append((opt, {k: dict(st).get("step") for k, st in opt.state.items()}))
+
+    def restore(self):
+        now = list(self.trainer.state_tensors())
+        if len(now) != len(self.tensors) or any(a is not b for a, b in zip(now, self.tensors)):
+            raise RuntimeError("CapturedStep: the trainer's state tensors changed identity "
+                               "during warmup; cannot restore the pre-warmup state")
+        with torch.no_grad():
+            for t, s in zip(self.tensors, self.saved):
+                t.copy_(s)
+        for opt, steps in self.py_steps:
+            for k, v in steps.items():
+                if v is not None and k in opt.state:
+                    opt.state[k]["step"] = v
+
+
 class CapturedStep:
-    def __init__(self, step_fn, *example_inputs, warmup: int = 2):
+    def __init__(self, step_fn, *example_inputs, warmup: int = 2, restore: bool = True):
         self.step_fn = step_fn
         self.static_inputs = [x.clone() for x in example_inputs]
+        trainer = getattr(step_fn, "__self__", None)
+        snap = None
+        if restore and trainer is not None and hasattr(trainer, "state_tensors"):
+            torch.cuda.synchronize()
+            snap = _Snapshot(trainer)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -29,6 +96,9 @@ class CapturedStep:
                 step_fn(*self.static_inputs)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        if snap is not None:
+            snap.restore()
+            torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.static_out = step_fn(*self.static_inputs)

@@ -27,6 +27,19 @@ class FusedAdam(torch.optim.Optimizer):
         dev = self.param_groups[0]["params"][0].device
         self._lr_t = [torch.tensor([float(g["lr"])], device=dev) for g in self.param_groups]
         self._step_t = [torch.zeros(1, device=dev) for _ in self.param_groups]
+        # moments allocated up front (not on first step): the state tensors exist before any
+        # warmup, so a graph capture can snapshot and restore them (engine/graph.py)
+        for g in self.param_groups:
+            for p in g["params"]:
+                self._init_state(p)
+
+    def _init_state(self, p):
+        st = self.state[p]
+        if not st:
+            st["step"] = 0
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+        return st
 
     def sync_lr(self):
         for g, t in zip(self.param_groups, self._lr_t):
@@ -47,11 +60,7 @@ class FusedAdam(torch.optim.Optimizer):
             for p in group["params"]:
                 if p.grad is None:
                     continue
-                st = self.state[p]
-                if not st:
-                    st["step"] = 0
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                st = self._init_state(p)
                 st["step"] += 1
                 params.append(p)
                 grads.append(p.grad.contiguous())

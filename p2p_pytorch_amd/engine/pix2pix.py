@@ -22,6 +22,7 @@ import torch
 
 from .. import _native
 from ..models.compress_gan import MultiscaleDiscriminator
+from ..models.layers import BatchNorm2d
 from ..models.losses import GANLoss
 from ..ops import l1
 from ..utils.tracing import trace_range
@@ -45,14 +46,31 @@ class Pix2PixStep:
         self.opt_D = make_adam(netD.parameters(), lr=lr, betas=(beta1, 0.999))
         self.reducer_g, self.reducer_d = reducer_g, reducer_d
         self.autocast_dtype = autocast_dtype
-        # D(fake.detach()) and D(real) as ONE 2B-batch forward/backward (D is per-sample:
-        # instance norm, no batch statistics), halving D launches and doubling GEMM M.
+        # D(fake.detach()) and D(real) as ONE 2B-batch forward/backward, halving D launches
+        # and doubling GEMM M -- only when D is per-sample: a BatchNorm would take its
+        # statistics over fake and real together (and update its running stats once)
+        self.d_per_sample = not any(isinstance(m, (BatchNorm2d, torch.nn.BatchNorm2d))
+                                    for m in netD.modules())
         self.fuse_d_batch = fuse_d_batch
         # NaN/Inf guard: a non-finite loss skips that network's update on the device (no
         # host sync; agreed across ranks with one 4-byte MAX all-reduce) and is counted
         self.nan_guard = nan_guard
-        self.skipped = None
+        dev = next(netG.parameters()).device
+        self.skipped = torch.zeros((), device=dev) if nan_guard else None
         self.timer = None     # optional utils.PhaseTimer: per-phase HIP-event ms
+
+    def optimizers(self):
+        return [self.opt_G, self.opt_D]
+
+    def state_tensors(self):
+        """Tensors one step mutates (CapturedStep snapshots them around its warmup)."""
+        from .graph import trainer_state_tensors
+        extra = [self.skipped] if self.skipped is not None else []
+        dev = next(self.netG.parameters()).device
+        if dev.type == "cuda" and _native.get_backend() == "native":
+            from ..ops import hip
+            extra.append(hip._seed(dev))
+        return trainer_state_tensors([self.netG, self.netD], self.optimizers(), extra)
 
     def _phase(self, name):
         return self.timer.phase(name) if self.timer is not None else trace_range(name)
@@ -96,8 +114,9 @@ class Pix2PixStep:
             set_requires_grad(netD, True)
             fuse = self.fuse_d_batch
             if fuse is None:
-                fuse = real_A.is_cuda and _native.get_backend() == "native" and not isinstance(
-                    netD, MultiscaleDiscriminator)
+                fuse = (real_A.is_cuda and _native.get_backend() == "native"
+                        and not isinstance(netD, MultiscaleDiscriminator))
+            fuse = fuse and self.d_per_sample
             if fuse:
                 B = real_A.shape[0]
                 if (real_A.is_cuda and _native.get_backend() == "native"

@@ -145,12 +145,20 @@ class Act(nn.Module):
 
 
 class Dropout(nn.Module):
-    def __init__(self, p=0.5):
+    _next_salt = 1
+
+    def __init__(self, p=0.5, salt=None):
         super().__init__()
         self.p = p
+        # fixed per module: masks vary per step through the device seed only (models pass
+        # their own salts so two instances of a network draw identical masks)
+        if salt is None:
+            salt = Dropout._next_salt
+            Dropout._next_salt += 1
+        self.salt = int(salt)
 
     def forward(self, x):
-        return ops.dropout(x, self.p, self.training)
+        return ops.dropout(x, self.p, self.training, self.salt)
 
 
 def norm_layer(kind: str, channels: int, act=None):

@@ -64,7 +64,8 @@ class UnetGenerator(nn.Module):
                                             act_out="tanh" if i == 0 else None))
             self.up_norms.append(norm_layer(norm, cout, act="relu") if i > 0 else nn.Identity())
         self.dropouts = nn.ModuleList(
-            [Dropout(0.5) if i in self.drop_levels else nn.Identity() for i in range(n)])
+            [Dropout(0.5, salt=1000 + i) if i in self.drop_levels else nn.Identity()
+             for i in range(n)])
         for c, m in list(zip(self.downs, self.down_norms)) + list(zip(self.ups, self.up_norms)):
             link_norm(c, m)
         # outermost encoder output feeds downs[1] and (skip) ups[0]; innermost feeds ups[n-1]

@@ -73,11 +73,13 @@ def act(x, name):
     return ref.apply_act(x, name)
 
 
-def dropout(x, p, training):
+def dropout(x, p, training, salt=None):
+    """``salt``: per-module constant mixed with the device seed (advanced once per step), so
+    a captured graph draws the same masks as the eager step it replays."""
     if not training or p == 0.0:
         return x
     if _native.use_native(x):
-        return _hip().dropout(x, p)
+        return _hip().dropout(x, p, salt)
     return ref.dropout(x, p, training)
 
 

@@ -48,6 +48,7 @@ def begin_step():
     _gen[0] += 1
     _colsum_stash.clear()
     _stats_stash.clear()
+    _DEFERRED.clear()   # a backward that raised part-way must not leak parked skip gradients
     if _f8._pools:
         _f8.begin_step()
 

@@ -1,23 +1,39 @@
 """Bucketed gradient all-reduce overlapped with backward (RCCL over xGMI).
 
 Why not ``DistributedDataParallel``: one pix2pix step runs D three times and G once,
-with two optimizers and D frozen in the G phase.  DDP's
-forward-coupled hooks mis-fire on that pattern; here every network has its own reducer
-and the trainer says explicitly when a backward is complete (``finish``).
+with two optimizers and D frozen in the G phase; the
+reference-family step even back-propagates the G loss through D and then throws those D
+gradients away (/root/reference/train.py:384-389).  DDP's forward-coupled hooks mis-fire
+on that pattern; here every network has its own reducer and the trainer says explicitly
+when a backward starts (``zero_grad``), when one must not be reduced (``paused``) and when
+one is complete (``finish``).
 
 Mechanism
   * Parameters are packed into flat fp32 buckets of ``bucket_mb`` -- first in reverse
     registration order, then (after the first backward) in the order their grads actually
     became ready, with the last-ready bucket capped at ``tail_mb`` (its all-reduce is the
-    one backward cannot hide).  Each ``p.grad`` is a *view*
-    into its bucket, so autograd accumulates straight into communication memory --
-    no gather/scatter copies.
+    one backward cannot hide).  Rank 0's recorded order is broadcast, so every rank builds
+    the same layout even when autograd's ready order differs between ranks.  Each
+    ``p.grad`` is a *view* into its bucket, so autograd accumulates straight into
+    communication memory -- no gather/scatter copies.
   * ``register_post_accumulate_grad_hook`` counts ready params; the moment a bucket is
     complete its ``all_reduce`` is enqueued (async).  RCCL runs it on its own HIP stream,
     ordered after the producing kernels by an event, so it overlaps the rest of backward.
+  * Per-backward state (pending counts, in-flight work) is reset by ``zero_grad`` -- which
+    first joins any collective still in flight, so zeroing never races a reduction -- and by
+    ``finish``.  A gradient that arrives for a bucket already sent raises instead of being
+    silently half-reduced.
+  * ``paused()``: a backward whose gradients will be discarded (the reference's D grads
+    from the G loss, the C-phase backward) launches no collective.
+  * ``comm_dtype=torch.bfloat16``: the bucket is pre-scaled by 1/world into a bf16 comm
+    buffer (exact for power-of-two worlds), all-reduced in bf16 (half the xGMI bytes) and
+    widened back into the fp32 grads by ``finish``.
   * ``finish()`` enqueues any incomplete bucket (params that got no grad contribute
     zeros), makes the compute stream wait on every collective (no host sync) and scales
-    by 1/world.
+    by 1/world.  Nothing in ``_on_grad`` / ``finish`` synchronises the host, so a step with
+    reducers can be captured into one hipGraph (RCCL collectives are graph-capturable).
+  * ``force_comm=True`` issues the collectives even at world size 1 (exercises the RCCL
+    and capture path on a single GPU).
   * ``enable_timing()`` (logging only): collectives are issued from a side stream
     bracketed by HIP events, and ``comm_stats()`` reports the last backward's collective
     busy time, the part of it left exposed after backward's last kernel, and the overlap
@@ -28,17 +44,21 @@ Mechanism
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.distributed as dist
 
 
 class _Bucket:
-    __slots__ = ("params", "flat", "pending", "work", "index", "events")
+    __slots__ = ("params", "flat", "cbuf", "pending", "work", "index", "events")
 
-    def __init__(self, params, device, dtype, index):
+    def __init__(self, params, device, dtype, index, comm_dtype):
         self.params = params
         n = sum(p.numel() for p in params)
         self.flat = torch.zeros(n, device=device, dtype=dtype)
+        self.cbuf = (torch.empty(n, device=device, dtype=comm_dtype)
+                     if comm_dtype is not None and comm_dtype != dtype else None)
         self.pending = len(params)
         self.work = None
         self.index = index
@@ -59,12 +79,15 @@ class _StreamJoin:
 
 class GradReducer:
     def __init__(self, module: torch.nn.Module, bucket_mb: float = 64.0, process_group=None,
-                 comm_dtype: torch.dtype | None = None, tail_mb: float = 8.0, rebucket: bool = True):
+                 comm_dtype: torch.dtype | None = None, tail_mb: float = 8.0, rebucket: bool = True,
+                 force_comm: bool = False):
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.backend = dist.get_backend(process_group) if dist.is_initialized() else None
+        self.comm = dist.is_initialized() and (self.world > 1 or force_comm)
         params = [p for p in module.parameters() if p.requires_grad]
         self.params = params
+        self.comm_dtype = comm_dtype if self.comm else None
         self.cap = int(bucket_mb * 1024 * 1024)
         self.tail_cap = min(self.cap, int(tail_mb * 1024 * 1024))
         self._build(list(reversed(params)))
@@ -74,7 +97,6 @@ class GradReducer:
         # is capped at tail_mb
         self._ready_order: list | None = [] if rebucket else None
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params]
-        self.comm_dtype = comm_dtype
         self.active = True
         self._timing = False
         self._comm_stream = None
@@ -99,11 +121,25 @@ class GradReducer:
         for g in reversed(groups):
             self._add_bucket(list(reversed(g)))
 
+    def _agreed_order(self, order):
+        """Rank 0's ready order, as parameter indices, on every rank."""
+        if not self.comm:
+            return order
+        index = {id(p): i for i, p in enumerate(self.params)}
+        dev = self.params[0].device
+        if self.backend == "nccl" and dev.type != "cuda":
+            dev = torch.device("cuda", torch.cuda.current_device())
+        t = torch.tensor([index[id(p)] for p in order], dtype=torch.int64, device=dev)
+        src = dist.get_global_rank(self.pg, 0) if self.pg is not None else 0
+        dist.broadcast(t, src, group=self.pg)
+        return [self.params[i] for i in t.tolist()]
+
     def _rebucket(self):
         order = self._ready_order
         self._ready_order = None
         seen = set(id(p) for p in order)
         order = order + [p for p in reversed(self.params) if id(p) not in seen]
+        order = self._agreed_order(order)
         old = {id(p): p.grad for p in self.params}
         self._build(order)
         for p in self.params:   # carry current grads over into the new flat buckets
@@ -111,7 +147,7 @@ class GradReducer:
                 p.grad.copy_(old[id(p)])
 
     def _add_bucket(self, params):
-        b = _Bucket(params, params[0].device, params[0].dtype, len(self.buckets))
+        b = _Bucket(params, params[0].device, params[0].dtype, len(self.buckets), self.comm_dtype)
         off = 0
         for p in params:
             n = p.numel()
@@ -125,9 +161,14 @@ class GradReducer:
     def _on_grad(self, p):
         if not self.active:
             return
+        b = self._param_bucket[p]
+        if b.work is not None:
+            raise RuntimeError(
+                "GradReducer: a gradient arrived for a bucket whose all-reduce was already "
+                "launched (a second backward without zero_grad()/finish(); wrap backwards whose "
+                "gradients are discarded in reducer.paused())")
         if self._ready_order is not None:
             self._ready_order.append(p)
-        b = self._param_bucket[p]
         # autograd may have replaced the view (e.g. after set_to_none): copy back in.
         lo = b.flat.data_ptr()
         if not (lo <= p.grad.data_ptr() < lo + b.flat.numel() * b.flat.element_size()):
@@ -146,34 +187,68 @@ class GradReducer:
     def _launch(self, b: _Bucket):
         if b.work is not None:
             return
-        if self.world == 1:
+        if not self.comm:
             b.work = True
             return
-        if not self._timing or torch.cuda.is_current_stream_capturing() or not b.flat.is_cuda:
-            b.work = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
-            return
-        # timed: issue from a side stream so the events bracket the collective itself
-        cur = torch.cuda.current_stream(b.flat.device)
-        if self._comm_stream is None:
-            self._comm_stream = torch.cuda.Stream(device=b.flat.device)
-        cs = self._comm_stream
-        cs.wait_stream(cur)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        with torch.cuda.stream(cs):
-            e0.record(cs)
-            work = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
-            work.wait()                     # cs waits for RCCL's stream (no host sync)
-            e1.record(cs)
-        b.flat.record_stream(cs)
-        b.events = (e0, e1)
-        b.work = _StreamJoin(cs)
+        timed = self._timing and not torch.cuda.is_current_stream_capturing() and b.flat.is_cuda
+        cur = torch.cuda.current_stream(b.flat.device) if b.flat.is_cuda else None
+        if timed:
+            if self._comm_stream is None:
+                self._comm_stream = torch.cuda.Stream(device=b.flat.device)
+            cs = self._comm_stream
+            cs.wait_stream(cur)
+            ctx = torch.cuda.stream(cs)
+        else:
+            ctx = contextlib.nullcontext()
+        with ctx:
+            buf = b.flat
+            if b.cbuf is not None:
+                # pre-scale into the narrow comm buffer: sum of world terms of x/world
+                torch.mul(b.flat, 1.0 / self.world, out=b.cbuf)
+                buf = b.cbuf
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(cs)
+                work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                work.wait()                     # cs waits for RCCL's stream (no host sync)
+                e1.record(cs)
+                b.flat.record_stream(cs)
+                if b.cbuf is not None:
+                    b.cbuf.record_stream(cs)
+                b.events = (e0, e1)
+                b.work = _StreamJoin(cs)
+            else:
+                b.work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+
+    def _reset(self):
+        for b in self.buckets:
+            b.work = None
+            b.events = None
+            b.pending = len(b.params)
+
+    def _join_inflight(self):
+        # collectives launched but never finished (e.g. a backward abandoned by an
+        # exception): order the current stream after them before anything reuses the buckets
+        for b in self.buckets:
+            if b.work is not None and b.work is not True:
+                b.work.wait()
 
     # ------------------------------------------------------------------ API
+    @contextlib.contextmanager
+    def paused(self):
+        """Backwards run inside launch no collective and leave the bookkeeping alone (their
+        gradients are discarded by the next ``zero_grad``)."""
+        prev, self.active = self.active, False
+        try:
+            yield self
+        finally:
+            self.active = prev
+
     def finish(self):
         """Complete the reduction of this backward: launch stragglers, wait (stream-ordered),
         average, and reset bookkeeping for the next backward."""
         end_bwd = None
-        if self._timing and self.world > 1 and self.buckets and self.buckets[0].flat.is_cuda \
+        if self._timing and self.comm and self.buckets and self.buckets[0].flat.is_cuda \
                 and not torch.cuda.is_current_stream_capturing():
             end_bwd = torch.cuda.Event(enable_timing=True)
             end_bwd.record()
@@ -186,11 +261,11 @@ class GradReducer:
         for b in self.buckets:
             if b.work is not True and b.work is not None:
                 b.work.wait()
-            if self.world > 1:
+            if b.cbuf is not None:
+                b.flat.copy_(b.cbuf)            # already averaged (pre-scaled)
+            elif self.world > 1:
                 b.flat.mul_(inv)
-            b.work = None
-            b.events = None
-            b.pending = len(b.params)
+        self._reset()
 
     def enable_timing(self, on: bool = True):
         self._timing = bool(on)
@@ -225,18 +300,24 @@ class GradReducer:
     def all_reduce_max_(self, t: torch.Tensor):
         """In-place MAX over ranks of a small device tensor (e.g. the NaN-guard flag), so
         every rank takes the same skip decision."""
-        if self.world > 1:
+        if self.comm and self.world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.pg)
         return t
 
     def zero_grad(self):
+        """Start a backward: join stale collectives, (re-bucket once), zero the buckets and
+        reset the per-backward bookkeeping."""
+        self._join_inflight()
         if self._ready_order:
             self._rebucket()
         for b in self.buckets:
             b.flat.zero_()
-            for p in b.params:  # keep grads as bucket views
-                if p.grad is None:
+            lo = b.flat.data_ptr()
+            hi = lo + b.flat.numel() * b.flat.element_size()
+            for p in b.params:  # keep grads as bucket views (set_to_none / foreign grads)
+                if p.grad is None or not (lo <= p.grad.data_ptr() < hi):
                     self._rebind(p, b, copy=False)
+        self._reset()
 
     def remove(self):
         for h in self._hooks:

@@ -36,6 +36,25 @@ def init_from_env(timeout_s: float = 600.0):
     return world, rank, local_rank
 
 
+def init_single(device=None, backend: str | None = None):
+    """A world-size-1 process group (RCCL on a GPU): lets the reducers issue real
+    collectives on one GPU (``GradReducer(force_comm=True)``) -- the RCCL + hipGraph
+    capture path exercised without a second device."""
+    if dist.is_initialized():
+        return
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:
+        import socket
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+        s.close()
+    use_gpu = device is not None and torch.device(device).type == "cuda"
+    backend = backend or ("nccl" if use_gpu else "gloo")
+    kw = {"device_id": torch.device(device)} if backend == "nccl" else {}
+    dist.init_process_group(backend=backend, rank=0, world_size=1, **kw)
+
+
 def local_device(local_rank: int) -> torch.device:
     """The GPU of a local rank: one per rank; ranks wrap around when there are fewer GPUs
     than ranks (only meaningful with the gloo rehearsal backend)."""

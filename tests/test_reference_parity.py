@@ -250,3 +250,23 @@ def test_compress_gan_step_matches_reference_loop(refnet):
         assert torch.allclose(t1.float(), t2.float(), atol=1e-5, rtol=1e-4), n1
     for (n1, t1), (n2, t2) in zip(rd.state_dict().items(), d.state_dict().items()):
         assert torch.allclose(t1, t2, atol=1e-5, rtol=1e-4), n1
+
+
+def test_networks_nlayer_discriminator_is_reference_class(refnet):
+    """``networks.NLayerDiscriminator`` takes the reference signature and builds the
+    spectral-norm PatchGAN with the reference's keys (networks.py:758-806)."""
+    import networks
+    torch.manual_seed(0)
+    ours = networks.NLayerDiscriminator(6, 64, 3, None, False, True)
+    ref = refnet.NLayerDiscriminator(6, 64, 3, None, False, True)
+    assert list(ours.state_dict()) == list(ref.state_dict())
+    for (k, a), (_, b) in zip(ours.state_dict().items(), ref.state_dict().items()):
+        assert a.shape == b.shape, k
+    ours.load_state_dict(ref.state_dict())
+    x = torch.rand(1, 6, 32, 32) * 2 - 1
+    with torch.no_grad():
+        yo, yr = ours(x), ref(x)
+    assert len(yo) == len(yr) == 5
+    for a, b in zip(yo, yr):
+        assert torch.allclose(a, b, atol=1e-5, rtol=1e-4)
+    assert networks.PatchGANDiscriminator is not networks.NLayerDiscriminator

@@ -29,6 +29,11 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
+# the reference train.py's importable helpers (train.py:33-126), same names and signatures
+from p2p_pytorch_amd.engine.ref_helpers import (  # noqa: E402,F401
+    calc_c_loss, calc_Gram_Loss, calc_tv_Loss, extract_features, gram, load_checkpoint, psnr,
+    ssim, tensor2img, tensor2np)
+
 
 def build_parser():
     p = argparse.ArgumentParser(description="pix2pix-pytorch-implementation")
@@ -97,6 +102,8 @@ def build_parser():
                    help="abort (exit 124) when no step finishes for this long; default 1800 s "
                         "for multi-GPU runs, off for one GPU")
     p.add_argument("--max_eval", type=int, default=0, help="limit eval images (0 = all)")
+    p.add_argument("--no_eval_images", dest="eval_images", action="store_false",
+                   help="do not write the reference's in/tar/pred/comp.png eval samples")
     return p
 
 
@@ -105,8 +112,10 @@ def main(argv=None):
     import p2p_pytorch_amd as p2p
     from p2p_pytorch_amd.data import (DevicePairCache, SyntheticPairs, get_test_set,
                                       get_training_set)
-    from p2p_pytorch_amd.engine.checkpoint import (checkpoint_path, latest_checkpoint,
-                                                   load_checkpoint, save_checkpoint)
+    from p2p_pytorch_amd.data.image_io import save_img
+    from p2p_pytorch_amd.engine.checkpoint import (checkpoint_path, has_scheduler_state,
+                                                   latest_checkpoint, save_checkpoint)
+    from p2p_pytorch_amd.engine.checkpoint import load_checkpoint as load_full_checkpoint
     from p2p_pytorch_amd.engine.metrics import image_metrics
     from p2p_pytorch_amd.models import (define_C, define_D, define_G, get_scheduler,
                                         update_learning_rate)
@@ -196,8 +205,9 @@ def main(argv=None):
                                   reducer_g=reducer_g, reducer_d=reducer_d,
                                   nan_guard=not opt.no_nan_guard)
         opt_g, opt_d = trainer.opt_g, trainer.opt_d
-    sched_g = get_scheduler(opt_g, opt)
-    sched_d = get_scheduler(opt_d, opt)
+    # the reference's third optimizer / scheduler pair (train.py:243-246, :441-443): over C
+    # when --train_c fixes quirk A1, and stepped + checkpointed like the other two
+    opt_c = getattr(trainer, "opt_c", None)
 
     # ---- resume
     start_epoch = opt.epoch_count
@@ -212,11 +222,21 @@ def main(argv=None):
                                   opt.epoch_count - 1)
         if not os.path.exists(ck_path):
             raise SystemExit(f"=> No checkpoint found at '{ck_path}'")
+    # a restored scheduler already counts the finished epochs (last_epoch): its lambda must
+    # not add epoch_count on top; a reference-written file (no scheduler state) starts a
+    # fresh scheduler whose lambda is offset by epoch_count, as in the reference
+    sched_opt = opt
+    if ck_path and has_scheduler_state(ck_path):
+        sched_opt = argparse.Namespace(**{**vars(opt), "epoch_count": 1})
+    sched_g = get_scheduler(opt_g, sched_opt)
+    sched_d = get_scheduler(opt_d, sched_opt)
+    sched_c = get_scheduler(opt_c, sched_opt) if opt_c is not None else None
     if ck_path:
         if rank == 0:
             print(f"=> Loading checkpoint '{ck_path}'")
-        start_epoch, losslogger = load_checkpoint(ck_path, net_g, net_c, net_d, opt_g, opt_d,
-                                                  sched_g, sched_d, device=device)
+        start_epoch, losslogger = load_full_checkpoint(
+            ck_path, net_g, net_c, net_d, opt_g, opt_d, sched_g, sched_d, device=device,
+            opt_c=opt_c, sched_c=sched_c)
 
     from p2p_pytorch_amd.utils import JsonlLogger, StepWatchdog
     step_fn = trainer.step
@@ -273,18 +293,29 @@ def main(argv=None):
                     means = {k: float(v) / count for k, v in zip(keys, vals.tolist())}
                     dt = time.perf_counter() - t0
                     ips = count * opt.batch_size * world / max(dt, 1e-9)
-                    print("itr: %d/%d [%3d/%3d] " % (iteration, n_it, epoch, num_epoch - 1) +
-                          " ".join(f"[{k}: {means[k]:.6f}]" for k in keys) +
-                          f" [{ips:.1f} img/s]", flush=True)
+                    head = "itr: %d/%d [%3d/%3d] " % (iteration, n_it, epoch, num_epoch - 1)
+                    if not pix2pix:
+                        # the reference's progress line (train.py:421-436); its "C" field is
+                        # the VGG content loss, DGC = D / G-GAN / C-phase losses
+                        print(head + "[DGC: %.6f/%.6f/%.6f] [GF: %.6f] [C: %.6f] [TV: %.6f] "
+                              "[Tot: %.6f]" % (means["D"], means["G_GAN"], means["C"],
+                                               means["G_GAN_Feat"], means["VGG"], means["TV"],
+                                               means["G"]) + f" [{ips:.1f} img/s]", flush=True)
+                    else:
+                        print(head + " ".join(f"[{k}: {means[k]:.6f}]" for k in keys) +
+                              f" [{ips:.1f} img/s]", flush=True)
                     skipped = getattr(trainer, "skipped", None)
                     jlog.log(epoch=epoch, iter=iteration, img_s=ips,
                              skipped_updates=float(skipped) if skipped is not None else 0.0,
                              **means, **extra)
         update_learning_rate(sched_g, opt_g, verbose=rank == 0)
         update_learning_rate(sched_d, opt_d, verbose=rank == 0)
-        for o in (opt_g, opt_d):
+        if sched_c is not None:
+            update_learning_rate(sched_c, opt_c, verbose=rank == 0)
+        for o in (opt_g, opt_d, opt_c):
             if hasattr(o, "sync_lr"):
                 o.sync_lr()
+        jlog.log(epoch=epoch, lr_g=opt_g.param_groups[0]["lr"], lr_d=opt_d.param_groups[0]["lr"])
 
         # ---- eval (train.py:450-502), no autograd
         if test_set is not None and not opt.no_eval:
@@ -294,16 +325,28 @@ def main(argv=None):
                 net_c.eval()
             ps, ss = [], []
             n_eval = len(test_set) if not opt.max_eval else min(opt.max_eval, len(test_set))
+            # one random test image's input / target / prediction / compressed view is dumped
+            # to in.png, tar.png, pred.png, comp.png (train.py:462, :469-473; the reference's
+            # inclusive randint bound can miss every image, quirk A14)
+            rande = random.randint(0, max(n_eval - 1, 0))
             with torch.no_grad():
                 for i in range(rank, n_eval, world):
                     inp, tgt = test_set[i]
                     inp = inp.unsqueeze(0).to(device, act_dtype).contiguous(memory_format=torch.channels_last)
                     tgt = tgt.unsqueeze(0).to(device, act_dtype).contiguous(memory_format=torch.channels_last)
+                    comp = None
                     if net_c is not None:
                         from p2p_pytorch_amd import ops
-                        pred = net_g(ops.quantize(net_c(tgt), opt.bits))
+                        comp = ops.quantize(net_c(tgt), opt.bits)
+                        pred = net_g(comp)
                     else:
                         pred = net_g(inp)
+                    if i == rande and opt.eval_images and rank == 0:
+                        save_img(inp[0].float().cpu(), "in.png")
+                        save_img(tgt[0].float().cpu(), "tar.png")
+                        save_img(pred[0].float().cpu(), "pred.png")
+                        if comp is not None:
+                            save_img(comp[0].float().cpu(), "comp.png")
                     p_i, s_i = image_metrics(pred, tgt)   # one HIP kernel on the GPU
                     ps.append(p_i.clamp(max=60.0))
                     ss.append(s_i)
@@ -330,7 +373,7 @@ def main(argv=None):
         if epoch % opt.epochsave == 0:
             path = checkpoint_path(opt.checkpoint_dir, opt.dataset or "synthetic", opt.name, epoch)
             save_checkpoint(path, epoch, net_g, net_c, net_d, opt_g, opt_d, sched_g, sched_d,
-                            losslogger, rank=rank)
+                            losslogger, rank=rank, opt_c=opt_c, sched_c=sched_c)
             pdist.barrier()
             if rank == 0:
                 print("Checkpoint saved to {}".format(path))
