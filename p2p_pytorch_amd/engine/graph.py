@@ -39,7 +39,7 @@ def trainer_state_tensors(modules, optimizers, extra=()):
         if m is None:
             continue
         for t in m.parameters():
-            add(t.data)
+            add(t)          # the Parameter itself (``.data`` is a fresh object per access)
         for t in m.buffers():
             add(t)
     for opt in optimizers:
