@@ -105,7 +105,7 @@ class Pix2PixStep:
         if real_A.is_cuda and _native.get_backend() == "native":
             from ..ops import hip
             hip.begin_step()      # weight images re-cast once per step (graph-safe)
-            hip.advance_rng()     # new dropout masks
+            hip.advance_rng(real_A.device)     # new dropout masks
             hip.prepare_weights(netG, netD)   # all bf16 weight images, one launch each
         with self._ctx(real_A.device), self._phase("G_fwd"):
             fake_B = netG(real_A)

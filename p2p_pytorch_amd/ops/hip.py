@@ -250,7 +250,11 @@ def _seed(device):
 
 
 def advance_rng(device=None):
-    """Advance the device-side dropout seed (captured into graphs as one tiny kernel)."""
+    """Advance the device-side dropout seed (captured into graphs as one tiny kernel).
+    With ``device`` the seed is created first if needed, so the first step already draws
+    from seed + 1 whether or not a warmup created the seed earlier (graph == eager)."""
+    if device is not None:
+        _seed(device)
     for d, s in _seeds.items():
         if device is None or d == device:
             s.add_(1)

@@ -7,9 +7,11 @@ running statistics (advanced by both G forwards) and the spectral-norm u / v vec
 (advanced by all three D forwards).  A second run with the default lr checks that the
 native update moves each parameter in the oracle's direction.
 
-Bounds (bf16 activations against fp32): losses 3 %, each gradient tensor 10 % of its own
-max-abs (absolute floor 1e-3 of the largest gradient in the network: BN-fed conv biases
-have an exactly-zero true gradient), running stats 3 %.
+Per-dtype bounds: the same step in stock PyTorch bf16 autocast on the GPU (the eager
+baseline) measures how far bf16 arithmetic alone moves each quantity from the fp32
+oracle; the native step may be at most 2x that far (+1 % of the quantity's scale) --
+losses, every gradient tensor (absolute floor 1e-3 of the network's largest gradient:
+BN-fed conv biases have an exactly-zero true gradient), running stats and u / v.
 """
 import copy
 
@@ -35,11 +37,12 @@ def _rel(a, b):
     return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-12)).item()
 
 
-def _run_pair(lr):
+def _run_pair(lr, eager_bf16=False):
     from p2p_pytorch_amd.engine.compress_gan import CompressGANStep
     p2p.set_backend("native")
     G, D, C, vgg = _nets()
     Gg, Dg, Cg, vggg = (copy.deepcopy(m).cuda() for m in (G, D, C, vgg))
+    Ge, De, Ce, vgge = (copy.deepcopy(m).cuda() for m in (G, D, C, vgg))
     g = torch.Generator().manual_seed(5)
     a = torch.rand(2, 3, 64, 64, generator=g) * 2 - 1
     b = torch.rand(2, 3, 64, 64, generator=g) * 2 - 1
@@ -51,37 +54,64 @@ def _run_pair(lr):
         return x.cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
 
     out_g = gpu.step(dev(a), dev(b))
+    out_e = None
+    if eager_bf16:            # stock PyTorch kernels, bf16 autocast: the dtype's own error
+        p2p.set_backend("torch")
+        try:
+            eager = CompressGANStep(Ge, De, Ce, lr=lr, vgg=vgge)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out_e = eager.step(a.cuda(), b.cuda())
+        finally:
+            p2p.set_backend("native")
     torch.cuda.synchronize()
-    return (G, D, C), (Gg, Dg, Cg), out_c, out_g
+    return (G, D, C), (Gg, Dg, Cg), (Ge, De, Ce), out_c, out_g, out_e
+
+
+def _record(tag, rows):
+    import json
+    import os
+    if os.path.isdir("gpurun_out"):
+        with open("gpurun_out/bounds.jsonl", "a") as f:
+            f.write(json.dumps({"test": tag, "rows": rows}) + "\n")
 
 
 def test_family_r_step_gpu_matches_cpu_oracle():
-    (G, D, _), (Gg, Dg, _), out_c, out_g = _run_pair(lr=0.0)
+    (G, D, _), (Gg, Dg, _), (Ge, De, _), out_c, out_g, out_e = _run_pair(0.0, eager_bf16=True)
+    rows, bad = [], []
     for k in out_c:
-        ref, got = float(out_c[k]), float(out_g[k])
-        assert abs(got - ref) <= 3e-2 * abs(ref) + 1e-4, (k, got, ref)
-    bad = []
-    for net, netg in ((G, Gg), (D, Dg)):
-        grads = [(n, p.grad, pg.grad) for (n, p), (_, pg) in
-                 zip(net.named_parameters(), netg.named_parameters()) if p.grad is not None]
+        ref, got, eb = float(out_c[k]), float(out_g[k]), float(out_e[k])
+        rows.append(("loss:" + k, abs(got - ref), abs(eb - ref), abs(ref)))
+        if abs(got - ref) > 2 * abs(eb - ref) + 1e-2 * abs(ref) + 1e-5:
+            bad.append(("loss", k, got, ref, eb))
+    for net, netg, nete in ((G, Gg, Ge), (D, Dg, De)):
+        grads = [(n, p.grad, pg.grad, pe.grad) for (n, p), (_, pg), (_, pe) in
+                 zip(net.named_parameters(), netg.named_parameters(), nete.named_parameters())
+                 if p.grad is not None]
         assert grads
-        gscale = max(gr.abs().max().item() for _, gr, _ in grads)
-        for n, gr, gg in grads:
+        gscale = max(gr.abs().max().item() for _, gr, _, _ in grads)
+        for n, gr, gg, ge in grads:
             assert gg is not None and torch.isfinite(gg).all(), n
             err = (gg.cpu().float() - gr.float()).abs().max().item()
-            if err > 0.10 * gr.abs().max().item() and err > 1e-3 * gscale:
-                bad.append((n, err, gr.abs().max().item()))
+            erre = (ge.cpu().float() - gr.float()).abs().max().item()
+            scale = gr.abs().max().item()
+            rows.append((n, err, erre, scale))
+            if err > 2 * erre + 1e-2 * scale and err > 1e-3 * gscale:
+                bad.append((n, err, erre, scale))
+    for net, netg, nete, it in ((G, Gg, Ge, "buffers"), (D, Dg, De, "uv")):
+        src = (lambda m: m.named_buffers()) if it == "buffers" else (lambda m: m.named_parameters())
+        for (n, t), (_, tg), (_, te) in zip(src(net), src(netg), src(nete)):
+            if not t.dtype.is_floating_point or (it == "uv" and not n.endswith(("_u", "_v"))):
+                continue
+            err, erre = _rel(tg.cpu(), t), _rel(te.cpu(), t)
+            rows.append((n, err, erre, 1.0))
+            if err > 2 * erre + 1e-2:
+                bad.append((n, err, erre))
+    _record("family_r_step_vs_oracle", rows)
     assert not bad, bad
-    for (n, t), (_, tg) in zip(G.named_buffers(), Gg.named_buffers()):
-        if t.dtype.is_floating_point:
-            assert _rel(tg.cpu(), t) < 3e-2, n
-    for (n, t), (_, tg) in zip(D.named_parameters(), Dg.named_parameters()):
-        if n.endswith("_u") or n.endswith("_v"):
-            assert _rel(tg.cpu(), t) < 3e-2, n
 
 
 def test_family_r_update_direction_matches_oracle():
-    nets, nets_g, _, _ = _run_pair(lr=2e-4)
+    nets, nets_g, _, _, _, _ = _run_pair(lr=2e-4)
     fresh = _nets()
     agree = total = 0
     for net0, net, netg in zip(fresh, nets, nets_g):

@@ -1,10 +1,6 @@
-set -o pipefail
-cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -v --timeout 120 --timeout-method thread -k "pack_pairs or skip_grad" > gpurun_out/pack_t.log 2>&1; rc=$?; tail -5 gpurun_out/pack_t.log; [ $rc -eq 0 ] || exit $rc
-for i in 1 2; do
-timeout -k 10 400 python bench.py --steps 20 --warmup 5 >> gpurun_out/pack_bench.jsonl 2>> gpurun_out/pack_bench.err || exit $?
-echo "$(tail -1 gpurun_out/pack_bench.jsonl | cut -c80-160)"
-done
-B=256 timeout -k 10 700 bash tools/gpu_prof_native.sh || exit $?
-head -45 gpurun_out/native_prof_b256/summary.txt | cut -c1-150
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && rm -f gpurun_out/bounds.jsonl
+timeout -k 10 300 python tools/diag_graph.py > gpurun_out/diag_graph.jsonl 2> gpurun_out/diag.err; echo diag rc=$?
+cat gpurun_out/diag_graph.jsonl
+DROP=0 timeout -k 10 300 python tools/diag_graph.py > gpurun_out/diag_graph_nodrop.jsonl 2>> gpurun_out/diag.err; echo diag2 rc=$?
+cat gpurun_out/diag_graph_nodrop.jsonl
+timeout -k 10 400 python -u -m pytest tests/test_family_r_gpu.py -q --timeout 300 --timeout-method thread > gpurun_out/famr.log 2>&1; echo famr rc=$?; tail -3 gpurun_out/famr.log
