@@ -74,6 +74,9 @@ int p2p_loss_fwd(const void* a, const void* b, int is_f32, long n, int kind, flo
 int p2p_loss_bwd(const void* a, const void* b, int is_f32, long n, int kind, float t, float scale,
                  const float* gout, void* ga, void* gb, hipStream_t st);
 int p2p_adam_max_tensors();
+int p2p_union_weight(const float* w, int CinT, int CoutT, int co_off, int nv, int Nrows, int Cpad,
+                     const float* bias, void* out, float* bias_out, hipStream_t st);
+int p2p_sum_partials(const float* ws, int nb, float scale, float* out, hipStream_t st);
 int p2p_adam(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
              const long* n, const float* lr, const float* step, const float* skip, float b1, float b2,
              float eps, float wd, hipStream_t st);
@@ -398,6 +401,105 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   if (y2.defined()) out.push_back(y2);
   if (stats.defined()) out.push_back(stats);
   if (yq.defined()) out.push_back(yq);   // always last (fp8 dtype)
+  return out;
+}
+
+// ------------------------------------------------------------------ packed-image layers
+// GEMM operand (bf16 [Nrows][9][Cpad]) + bias (fp32 [Nrows]) of the 3x3 union conv that
+// computes a 4x4 stride-2 pad-1 transposed conv onto a 3-channel image (csrc/image.hip)
+std::vector<Tensor> union_weight(const Tensor& w, int64_t co_off, int64_t nv, int64_t Nrows, int64_t Cpad,
+                                 const optional<Tensor>& bias) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.dim() == 4 &&
+                  w.size(2) == 4 && w.size(3) == 4,
+              "union_weight: fp32 contiguous [CinT][CoutT][4][4] weight");
+  TORCH_CHECK(nv >= 1 && nv <= 4 && Nrows >= 16 && Cpad >= w.size(0) && Cpad % 8 == 0 &&
+                  co_off + nv <= w.size(1),
+              "union_weight: geometry");
+  if (bias) TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= co_off + nv, "union_weight: bias");
+  Tensor img = at::empty({Nrows, 3, 3, Cpad}, w.options().dtype(at::kBFloat16));
+  Tensor bu = at::empty({Nrows}, w.options());
+  check_rc(p2p_union_weight(w.data_ptr<float>(), (int)w.size(0), (int)w.size(1), (int)co_off, (int)nv, (int)Nrows,
+                            (int)Cpad, bias ? bias->data_ptr<float>() : nullptr, img.data_ptr(),
+                            bu.data_ptr<float>(), cur_stream(w)),
+           "union_weight");
+  return {img, bu};
+}
+
+// The union GEMM over the [N][H][W] grid of x1 (| x2), writing the packed [N][2H][2W][8]
+// image ``out`` through the depth-to-space epilogue (conv.h ``d2s``): mode 1 = image forward
+// (returns the device scalar lam_scale * sum|fake - pk_a[3..5]|), mode 2 = head gradient.
+Tensor conv_d2s(const Tensor& x1, const optional<Tensor>& x2, const Tensor& w, const Tensor& bias, int64_t act_in,
+                int64_t act_out, int64_t mode, Tensor out, const Tensor& pk_a, const optional<Tensor>& pk_f,
+                double scale) {
+  check_act(x1, "conv_d2s x1");
+  check_act(pk_a, "conv_d2s pk_a");
+  check_act(out, "conv_d2s out");
+  const int64_t N = x1.size(0), H = x1.size(2), W = x1.size(3);
+  int64_t C2 = 0;
+  if (x2) {
+    check_act(*x2, "conv_d2s x2");
+    TORCH_CHECK(x2->size(0) == N && x2->size(2) == H && x2->size(3) == W, "conv_d2s: concat shape");
+    C2 = x2->size(1);
+  }
+  const int64_t C1 = x1.size(1), C = C1 + C2;
+  TORCH_CHECK(C1 % 64 == 0 && C2 % 64 == 0 && C1 <= 1024 && C2 <= 1024, "conv_d2s: channel groups of 64");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.numel() == 32 * 9 * C,
+              "conv_d2s: union weight [32][3][3][C]");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() == 32, "conv_d2s: union bias [32]");
+  TORCH_CHECK(mode == 1 || mode == 2, "conv_d2s: mode");
+  TORCH_CHECK(act_in == 0 || act_in == 1, "conv_d2s: input act none / relu");
+  for (const Tensor* t : {static_cast<const Tensor*>(&out), &pk_a}) {
+    TORCH_CHECK(t->size(0) == N && t->size(1) == 8 && t->size(2) == 2 * H && t->size(3) == 2 * W,
+                "conv_d2s: packed image tensors must be [N][8][2H][2W]");
+  }
+  if (mode == 2) {
+    TORCH_CHECK(pk_f.has_value(), "conv_d2s: head gradient needs pk_f");
+    check_act(*pk_f, "conv_d2s pk_f");
+    TORCH_CHECK(pk_f->sizes() == out.sizes(), "conv_d2s: pk_f shape");
+  }
+  p2p::ConvFwdArgs a{};
+  a.x1 = x1.data_ptr();
+  a.x2 = x2 ? x2->data_ptr() : nullptr;
+  a.C1 = (int)C1;
+  a.C2 = (int)C2;
+  a.C = (int)C;
+  a.N = (int)N;
+  a.H = (int)H;
+  a.W = (int)W;
+  a.up = 1;
+  a.KH = a.KW = 3;
+  a.stride = 1;
+  a.pad = 1;
+  a.act_in = (int)act_in;
+  a.OH = (int)H;
+  a.OW = (int)W;
+  a.Cout = 32;
+  a.Csplit = 32;
+  a.w = w.data_ptr();
+  a.bias = bias.data_ptr<float>();
+  a.act_out = (int)act_out;
+  a.y1 = out.data_ptr();
+  a.splits = 1;
+  a.zero = zero_page(x1);
+  a.d2s = (int)mode;
+  a.pk_a = pk_a.data_ptr();
+  a.pk_f = mode == 2 ? pk_f->data_ptr() : nullptr;
+  a.d2s_scale = (float)scale;
+  const int64_t blocks = (N * H * W + 255) / 256;
+  Tensor part, l1;
+  if (mode == 1) {
+    part = at::zeros({blocks}, x1.options().dtype(at::kFloat));
+    a.l1_part = part.data_ptr<float>();
+  }
+  hipStream_t st = cur_stream(x1);
+  const int rc = p2p_conv_fwd_glds(&a, 0, 7, st);
+  TORCH_CHECK(rc != -2, "conv_d2s: no union-GEMM kernel for this geometry");
+  check_rc(rc, "conv_d2s");
+  if (mode == 1) {
+    l1 = at::empty({}, x1.options().dtype(at::kFloat));
+    check_rc(p2p_sum_partials(a.l1_part, (int)blocks, (float)scale, l1.data_ptr<float>(), st), "conv_d2s l1");
+    return l1;
+  }
   return out;
 }
 
@@ -1143,6 +1245,9 @@ TORCH_LIBRARY(p2p, m) {
         "int stride, int pad, int reflect, int up, Tensor(a!) dw, float scale, int accumulate, "
         "int flip=0) -> ()");
   m.def("weight_prep(Tensor w, int swap, int Xp, int Yp, Tensor? scale) -> Tensor");
+  m.def("union_weight(Tensor w, int co_off, int nv, int Nrows, int Cpad, Tensor? bias) -> Tensor[]");
+  m.def("conv_d2s(Tensor x1, Tensor? x2, Tensor w, Tensor bias, int act_in, int act_out, int mode, "
+        "Tensor(a!) out, Tensor pk_a, Tensor? pk_f, float scale) -> Tensor");
   m.def("prelu_fwd(Tensor x, Tensor w) -> Tensor");
   m.def("prelu_bwd(Tensor x, Tensor gy, Tensor w, bool need_x) -> Tensor[]");
   m.def("tv_fwd(Tensor x) -> Tensor");
@@ -1187,6 +1292,8 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("fp8_dequant", fp8_dequant);
   m.impl("conv_wgrad", conv_wgrad);
   m.impl("weight_prep", weight_prep);
+  m.impl("union_weight", union_weight);
+  m.impl("conv_d2s", conv_d2s);
   m.impl("weight_prep_multi", weight_prep_multi);
   m.impl("weight_prep_pairs", weight_prep_pairs);
   m.impl("norm_fwd", norm_fwd);

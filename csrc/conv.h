@@ -52,6 +52,21 @@ struct ConvFwdArgs {
   void* q_out;
   int* q_site;
   int q_fmt;
+  // Depth-to-space packed-image epilogue (0 = off).  The stride-2 4x4 pad-1 transposed conv
+  // onto a small image is computed as a 3x3 pad-1 "union" conv over its input grid: GEMM
+  // column n = cls * 4 + j (cls = ry * 2 + rx the output parity class, j < 3 the image
+  // channel), so one GEMM row (grid position q) yields the 2x2 output pixels 2q + (ry, rx).
+  // y1 is then a packed [N][2*OH][2*OW][8] bf16 image (16 B per pixel).
+  //  1: image forward -- pixel = (pk_a[0..2], y[0..2], 0, 0): the pair (A | fake) written in
+  //     place; per-block sum of |y - pk_a[3..5]| into l1_part[block] (the L1 term)
+  //  2: head gradient -- pixel = ((g + d2s_scale * sign(f - b)) * (1 - f^2), 0...) with
+  //     g the GEMM value, f = pk_f[3 + j] (tanh output), b = pk_a[3 + j] (target): the
+  //     pre-tanh gradient of the generator's last layer, in slots 0..2
+  int d2s;
+  const void* pk_a;
+  const void* pk_f;
+  float d2s_scale;
+  float* l1_part;
 };
 
 // Weight gradient: C[R][Kq] = sum_m P[m][R] * im2col(Q)[m][Kq], written to per-split

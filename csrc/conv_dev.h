@@ -119,6 +119,56 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
   }
   __syncthreads();
 
+  if (a.d2s) {  // depth-to-space packed image (d1 forward / its head gradient)
+    const int Ho = 2 * a.OH, Wo = 2 * a.OW;
+    float l1 = 0.f;
+    for (int it = tid; it < BM * 4; it += NT) {
+      const int row = it >> 2, cls = it & 3;
+      const int m = m0 + row;
+      if (m >= g.Mc) continue;
+      const int n = (int)fdiv((uint32_t)m, fd_hwq);
+      const int r = m - n * HWq;
+      const int qy = (int)fdiv((uint32_t)r, fd_wq);
+      const int qx = r - qy * g.Wq;
+      const long P = ((long)n * Ho + 2 * qy + (cls >> 1)) * Wo + 2 * qx + (cls & 1);
+      const bf16* c = Cs + row * LDC + cls * 4;
+      const bf16x8 ab = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(a.pk_a) + P * 8);
+      bf16x8 o;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = (bf16)0.f;
+      if (a.d2s == 1) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          o[j] = ab[j];
+          o[3 + j] = c[j];
+          l1 += fabsf((float)c[j] - (float)ab[3 + j]);
+        }
+      } else {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(a.pk_f) + P * 8);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const float f = (float)af[3 + j], b = (float)ab[3 + j];
+          const float sg = (float)(f > b) - (float)(f < b);
+          o[j] = (bf16)(((float)c[j] + a.d2s_scale * sg) * (1.f - f * f));
+        }
+      }
+      *reinterpret_cast<bf16x8*>(static_cast<bf16*>(a.y1) + P * 8) = o;
+    }
+    if (a.d2s == 1 && a.l1_part) {
+      float* red = reinterpret_cast<float*>(smem + BM * LDC * 2);
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) l1 += __shfl_xor(l1, off);
+      if (lane == 0) red[wid] = l1;
+      __syncthreads();
+      if (tid == 0) {
+        float t = 0.f;
+        for (int w = 0; w < NT / 64; ++w) t += red[w];
+        a.l1_part[blockIdx.x] = t;
+      }
+    }
+    return;
+  }
+
   if (a.stats) {
     // per-column (mean, M2) of the tile's BM bf16 outputs, shifted by the tile's first row
     // (no E[x^2] - E[x]^2 cancellation); NT / BN threads per column, combined in LDS

@@ -452,6 +452,14 @@ static int dispatch_glds2(const ConvFwdArgs& a, int variant, hipStream_t st) {
     return -2;
   }
   if (a.Cout > 128 && variant == 5) return launch_glds<256, 256, 2, 4, MODE, 2, FASTK, RELU, F8>(a, st);
+  // 7 = 256x32 on 4 waves of 64x32: the skinny union GEMMs of the packed-image layers
+  // (d1 forward / c1 dgrad: 4 parity classes x 3 image channels, padded to 32 columns)
+  if (variant == 7) {
+    if constexpr (MODE == 0 && FASTK) {
+      if (a.Cout <= 32) return launch_glds<256, 32, 4, 1, MODE, 2, FASTK, RELU, F8>(a, st);
+    }
+    return -2;
+  }
   if (a.Cout > 64) {
     if (variant == 5) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU, F8>(a, st);
     if (variant == 2) return launch_glds<128, 128, 2, 2, MODE, 2, FASTK, RELU, F8>(a, st);

@@ -403,6 +403,13 @@ int p2p_loss_fwd(const void* a, const void* b, int is_f32, long n, int kind, flo
   return (int)hipGetLastError();
 }
 
+// out[0] = scale * sum(ws[0..nb)) in a fixed order (per-block partials -> scalar)
+int p2p_sum_partials(const float* ws, int nb, float scale, float* out, hipStream_t st) {
+  using namespace p2p;
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, ws, nb, scale, out);
+  return (int)hipGetLastError();
+}
+
 int p2p_loss_bwd(const void* a, const void* b, int is_f32, long n, int kind, float t, float scale,
                  const float* gout, void* ga, void* gb, hipStream_t st) {
   using namespace p2p;

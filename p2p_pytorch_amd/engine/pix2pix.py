@@ -38,7 +38,7 @@ def set_requires_grad(nets, flag: bool):
 class Pix2PixStep:
     def __init__(self, netG, netD, lr=2e-4, beta1=0.5, gan_mode="vanilla", lambda_L1=100.0,
                  reducer_g=None, reducer_d=None, autocast_dtype=None, fuse_d_batch=None,
-                 nan_guard=True):
+                 nan_guard=True, packed=None):
         self.netG, self.netD = netG, netD
         self.criterionGAN = GANLoss(gan_mode=gan_mode)
         self.lambda_L1 = float(lambda_L1)
@@ -52,6 +52,8 @@ class Pix2PixStep:
         self.d_per_sample = not any(isinstance(m, (BatchNorm2d, torch.nn.BatchNorm2d))
                                     for m in netD.modules())
         self.fuse_d_batch = fuse_d_batch
+        # packed-image path (native backend, U-Net + PatchGAN on 3 + 3 channels): None = auto
+        self.packed = packed
         # NaN/Inf guard: a non-finite loss skips that network's update on the device (no
         # host sync; agreed across ranks with one 4-byte MAX all-reduce) and is counted
         self.nan_guard = nan_guard
@@ -100,13 +102,80 @@ class Pix2PixStep:
             return (a, b)
         return torch.cat((a, b), 1)
 
+    def _packed_ok(self, real_A, real_B):
+        """The packed-image path (ops/hip.py image head): U-Net G and a 4x4 s2 p1 PatchGAN
+        on 3 + 3 channel images, the 2B D batch, vanilla / lsgan losses."""
+        from ..models.pix2pix import NLayerDiscriminator, PixelDiscriminator, UnetGenerator
+        if self.packed is False or self.fuse_d_batch is False or not self.d_per_sample:
+            return False
+        if not (isinstance(self.netG, UnetGenerator) and self.netG.packed_ok(real_A)):
+            return False
+        if not isinstance(self.netD, NLayerDiscriminator) or isinstance(self.netD, PixelDiscriminator):
+            return False
+        c0 = self.netD.convs[0]
+        return (real_A.shape[1] == 3 and real_B.shape[1] == 3 and c0.in_channels == 6
+                and tuple(c0.kernel_size) == (4, 4) and c0.stride[0] == 2 and c0.padding[0] == 1
+                and c0.weight.shape[0] % 64 == 0 and real_A.shape == real_B.shape)
+
     def step(self, real_A, real_B):
         netG, netD = self.netG, self.netD
-        if real_A.is_cuda and _native.get_backend() == "native":
+        native = real_A.is_cuda and _native.get_backend() == "native"
+        if native:
             from ..ops import hip
             hip.begin_step()      # weight images re-cast once per step (graph-safe)
             hip.advance_rng(real_A.device)     # new dropout masks
             hip.prepare_weights(netG, netD)   # all bf16 weight images, one launch each
+            if self._packed_ok(real_A, real_B):
+                return self._step_packed(real_A, real_B)
+        return self._step_unpacked(real_A, real_B)
+
+    def _step_packed(self, real_A, real_B):
+        """Same phases as ``_step_unpacked`` on the packed pair tensor dd = [(A | fake);
+        (A | B)] (2B x 8 channels, 16 B per pixel): G reads (A | B) and writes (A | fake) in
+        place with the L1 term; D's two halves are its fused D batch; the G-phase D backward
+        returns G's pre-tanh gradient with the L1 term fused (ops/hip.py image head)."""
+        from ..ops import hip
+        netG, netD = self.netG, self.netD
+        B, _, H, W = real_A.shape
+        dd = torch.empty(2 * B, 8, H, W, device=real_A.device, dtype=torch.bfloat16,
+                         memory_format=torch.channels_last)
+        hip.P().pad_channels_into(hip.to_nhwc_bf16(real_A), hip.to_nhwc_bf16(real_B),
+                                  dd.narrow(0, B, B))
+        dd._p2p_packed = (3, 3)
+        scale = self.lambda_L1 / float(B * 3 * H * W)
+        with self._phase("G_fwd"):
+            fake_pk, loss_G_L1 = netG.forward_packed(dd, scale)
+        with self._phase("D_fwd"):
+            set_requires_grad(netD, True)
+            pred = netD(dd)                   # [D(A | fake.detach()); D(A | B)], one 2B pass
+            loss_D_fake = self.criterionGAN(pred[:B], False)
+            loss_D_real = self.criterionGAN(pred[B:], True)
+            loss_D = (loss_D_fake + loss_D_real) * 0.5
+        with self._phase("D_bwd_opt"):
+            self._zero(self.opt_D, self.reducer_d)
+            loss_D.backward()
+            if self.reducer_d is not None:
+                self.reducer_d.finish()
+            self._guarded_step(self.opt_D, self.reducer_d, loss_D)
+        hip.prepare_weights(netD)             # D moved: fresh images for the G phase
+        set_requires_grad(netD, False)
+        with self._phase("G_loss_fwd"):
+            pred_fake = netD(fake_pk)
+            loss_G_GAN = self.criterionGAN(pred_fake, True)
+            # the L1 term's gradient is injected by the fused first-D-conv dgrad (weight 1)
+            loss_G = loss_G_GAN + loss_G_L1
+        with self._phase("G_bwd_opt"):
+            self._zero(self.opt_G, self.reducer_g)
+            loss_G.backward()
+            hip.assert_no_deferred()          # every parked U-Net skip gradient consumed
+            if self.reducer_g is not None:
+                self.reducer_g.finish()
+            self._guarded_step(self.opt_G, self.reducer_g, loss_G)
+        return {"D": loss_D.detach(), "G_GAN": loss_G_GAN.detach(), "G_L1": loss_G_L1.detach(),
+                "G": loss_G.detach()}
+
+    def _step_unpacked(self, real_A, real_B):
+        netG, netD = self.netG, self.netD
         with self._ctx(real_A.device), self._phase("G_fwd"):
             fake_B = netG(real_A)
         with self._ctx(real_A.device), self._phase("D_fwd"):

@@ -88,6 +88,44 @@ class UnetGenerator(nn.Module):
             u = self.dropouts[i](self.up_norms[i](u))
         return u
 
+    def packed_ok(self, x) -> bool:
+        """The packed-image path (ops/hip.py, image head) applies: 3 -> 3 channels, the
+        standard outermost 4x4 s2 p1 layers, channel groups of 64."""
+        from ..ops import hip
+        n = self.num_downs
+        return (n >= 2 and self.downs[0].in_channels == 3 and self.ups[0].out_channels == 3
+                and self.channels[0] % 64 == 0 and x.shape[-1] % 2 == 0 and x.shape[-2] % 2 == 0
+                and tuple(self.downs[0].kernel_size) == (4, 4) and self.downs[0].stride[0] == 2
+                and self.downs[0].padding[0] == 1 and hip.image_head_ok(
+                    self.ups[0], _Shape(self.channels[0]), _Shape(self.channels[0])))
+
+    def forward_packed(self, dd, scale):
+        """Training forward on the packed pair tensor ``dd`` = [(unset); (A | B)] (2N x 8
+        channels, see ops/hip.py image head): reads A from ``dd[N:]``, writes the generated
+        image into ``dd[:N]`` as (A | fake) and returns (that view, ``scale * sum|fake - B|``)."""
+        from ..ops import hip
+        n = self.num_downs
+        N = dd.shape[0] // 2
+        ab = dd.narrow(0, N, N)
+        ab._p2p_packed = (3, 3)          # e1's weight is zero on the B channels
+        skips = []
+        h = ab
+        for i in range(n):
+            h = self.down_norms[i](self.downs[i](h))
+            skips.append(h)
+        u = self.dropouts[n - 1](self.up_norms[n - 1](self.ups[n - 1](skips[n - 1])))
+        for i in range(n - 2, 0, -1):
+            u = self.ups[i]((skips[i], u))
+            u = self.dropouts[i](self.up_norms[i](u))
+        return hip.image_head(skips[0], u, self.ups[0], dd, scale)
+
+
+class _Shape:
+    """Channel-count stand-in for ``image_head_ok`` checks before any tensor exists."""
+
+    def __init__(self, c):
+        self.shape = (1, c)
+
 
 class NLayerDiscriminator(nn.Module):
     """PatchGAN.  With n_layers=3 and 4x4 kernels the receptive field is 70x70

@@ -345,6 +345,9 @@ def assert_no_deferred():
 class ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x1, x2, weight, bias, cfg: _ConvCfg):
+        # a packed (A | fake) image from ImageHeadFn: its input gradient is the fused head
+        # gradient (d2s mode 2) instead of a plain dgrad
+        ctx.head = getattr(x1, "_p2p_head", None) if x2 is None else None
         q1, q2, C1, C2, Cp, packed = _prep_inputs(x1, x2)
         N, _, H, W = q1.shape
         KH, KW, s, p = cfg.KH, cfg.KW, cfg.stride, cfg.pad
@@ -392,91 +395,203 @@ class ConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         q1, q2, weight, y = ctx.saved_tensors
-        cfg = ctx.cfg
-        C1, C2, Cp, packed, Cout, Coutp, H, W = ctx.geo
         need_x1 = ctx.needs_input_grad[0]
-        need_x2 = ctx.has_x2 and ctx.needs_input_grad[1]
-        need_w = ctx.needs_input_grad[2]
-        need_b = ctx.has_bias and ctx.needs_input_grad[3]
-        gy = to_nhwc_bf16(gy)
-        if cfg.act_out not in (None, "none") and not cfg.out_gated:
-            gy = P().act(gy, y, _act_code(cfg.act_out), 2)
-        gyp = gy if Coutp == Cout else P().pad_channels(gy, None, Coutp)
-        KH, KW, s, p = cfg.KH, cfg.KW, cfg.stride, cfg.pad
-        gx1 = gx2 = gw = gb = None
-        if need_x1 or need_x2:
-            # input-gradient gate: the input activation's derivative, or the producer's
-            act_in = _act_code(cfg.act_in) or _act_code(cfg.grad_gate)
-            split = C1 if (q2 is not None) else Cp
-            if cfg.reflect or cfg.up != 1:
-                # family-R ConvLayer / UpsampleConvLayer: dgrad onto the virtual padded,
-                # upsampled input (a plain pad-0 transposed conv), then fold it back
-                if q2 is not None:
-                    raise NotImplementedError("virtual concat with reflect/upsample gather")
-                Hp, Wp = H * cfg.up + 2 * p, W * cfg.up + 2 * p
-                dxp = _conv_call(gyp, None, None, None, 1, KH, KW, s, 0, 0, 1, 0, Hp, Wp, Cp,
-                                 0, Cp, None, None, 0, C1, False, weight, 1, Cp, Coutp, "gy")[0]
-                outs = [P().pad_fold(dxp, H, W, p, cfg.up, int(cfg.reflect),
-                                     q1 if act_in else None, act_in)]
-            elif cfg.transposed:
-                outs = _conv_call(gyp, None, None, None, 0, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
-                                  split, q1 if act_in else None,
-                                  q2 if (act_in and q2 is not None) else None, act_in, C1 + C2,
-                                  False, weight, 0, Cp, Coutp, "gy")
-            else:
-                res = None
-                if cfg.skip_grad == "take" and q2 is None and not packed and need_x1:
-                    res = _DEFERRED.pop(q1.data_ptr(), None)
-                    if res is not None and (res.shape != (q1.shape[0], Cp, H, W) or Cp != C1):
-                        _DEFERRED[q1.data_ptr()] = res   # not fusable: added below instead
-                        res = None
-                outs = _conv_call(gyp, None, None, None, 1, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
-                                  split, q1 if act_in else None,
-                                  q2 if (act_in and q2 is not None) else None, act_in, C1 + C2,
-                                  False, weight, 1, Cp, Coutp, "gy", res=res)
-            if q2 is not None:
-                gx1, gx2 = outs[0], outs[1]
-            elif packed:
-                g = outs[0]
-                gx1 = P().slice_channels(g, 0, C1) if need_x1 else None
-                gx2 = P().slice_channels(g, C1, C2) if need_x2 else None
-            else:
-                gx1 = outs[0]
-            if not need_x1:
-                gx1 = None
-            if not need_x2:
-                gx2 = None
-            if cfg.skip_grad == "take" and gx1 is not None and q2 is None:
-                parked = _DEFERRED.pop(q1.data_ptr(), None)
-                if parked is not None:
-                    gx1 = gx1 + parked
-            if cfg.skip_grad == "defer" and gx1 is not None:
-                key = q1.data_ptr()
-                if key in _DEFERRED:
-                    raise RuntimeError("skip_grad: a deferred gradient of this tensor is pending")
-                _DEFERRED[key] = gx1
-                gx1 = None
-        if need_w:
-            gw = torch.empty_like(weight, dtype=torch.float32, memory_format=torch.contiguous_format)
-            act_in = _act_code(cfg.act_in)
-            if cfg.transposed:
-                P().conv_wgrad(q1, q2, act_in, gyp, None, 0, KH, KW, s, p, 0, 1, gw, 1.0, 0)
-            elif (s == 1 and Coutp <= 16 and Cp >= 128 and KH == KW and not cfg.reflect
-                  and cfg.up == 1):
-                # tiny-Cout stride-1 conv (PatchGAN logits): the GEMM's R = Cout would waste
-                # the MFMA tile, so compute it in transposed-conv form -- rows = input
-                # channels, the dY gather with pad K-1-p, taps flipped by the reduce
-                P().conv_wgrad(q1, q2, act_in, gyp, None, 0, KH, KW, 1, KH - 1 - p, 0, 1, gw,
-                               1.0, 0, 1)
-            else:
-                P().conv_wgrad(gyp, None, 0, q1, q2, act_in, KH, KW, s, p, int(cfg.reflect),
-                               cfg.up, gw, 1.0, 0)
-        if need_b:
-            gb = _take_colsum(gy) if cfg.act_out in (None, "none") else None
-            if gb is None:
-                gb = torch.empty(Cout, device=gy.device, dtype=torch.float32)
-                P().colsum(gyp, gb, 1.0, False)
+        if ctx.head is not None and need_x1 and _head_dgrad_ok(ctx.cfg, weight, q1):
+            gx1 = _head_dgrad(ctx.head, q1, weight, to_nhwc_bf16(gy))
+            gw = None
+            if ctx.needs_input_grad[2] or (ctx.has_bias and ctx.needs_input_grad[3]):
+                _, _, gw, gb = _conv_backward(ctx.cfg, ctx.geo, q1, q2, weight, y, gy, False, False,
+                                              ctx.needs_input_grad[2],
+                                              ctx.has_bias and ctx.needs_input_grad[3])
+                return gx1, None, gw, gb, None
+            return gx1, None, None, None, None
+        gx1, gx2, gw, gb = _conv_backward(ctx.cfg, ctx.geo, q1, q2, weight, y, gy, need_x1,
+                                          ctx.has_x2 and ctx.needs_input_grad[1],
+                                          ctx.needs_input_grad[2],
+                                          ctx.has_bias and ctx.needs_input_grad[3])
         return gx1, gx2, gw, gb, None
+
+
+def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, need_b):
+    """Input / weight / bias gradients of one fused conv (ConvFn's backward, shared with the
+    image head): dgrad with the input-activation gate, concat split and skip-gradient
+    hand-off in its epilogue; wgrad; bias = column sums (or the norm's exact zero)."""
+    C1, C2, Cp, packed, Cout, Coutp, H, W = geo
+    gy = to_nhwc_bf16(gy)
+    if cfg.act_out not in (None, "none") and not cfg.out_gated:
+        gy = P().act(gy, y, _act_code(cfg.act_out), 2)
+    gyp = gy if (Coutp == Cout or gy.shape[1] == Coutp) else P().pad_channels(gy, None, Coutp)
+    KH, KW, s, p = cfg.KH, cfg.KW, cfg.stride, cfg.pad
+    gx1 = gx2 = gw = gb = None
+    if need_x1 or need_x2:
+        # input-gradient gate: the input activation's derivative, or the producer's
+        act_in = _act_code(cfg.act_in) or _act_code(cfg.grad_gate)
+        split = C1 if (q2 is not None) else Cp
+        if cfg.reflect or cfg.up != 1:
+            # family-R ConvLayer / UpsampleConvLayer: dgrad onto the virtual padded,
+            # upsampled input (a plain pad-0 transposed conv), then fold it back
+            if q2 is not None:
+                raise NotImplementedError("virtual concat with reflect/upsample gather")
+            Hp, Wp = H * cfg.up + 2 * p, W * cfg.up + 2 * p
+            dxp = _conv_call(gyp, None, None, None, 1, KH, KW, s, 0, 0, 1, 0, Hp, Wp, Cp,
+                             0, Cp, None, None, 0, C1, False, weight, 1, Cp, Coutp, "gy")[0]
+            outs = [P().pad_fold(dxp, H, W, p, cfg.up, int(cfg.reflect),
+                                 q1 if act_in else None, act_in)]
+        elif cfg.transposed:
+            outs = _conv_call(gyp, None, None, None, 0, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
+                              split, q1 if act_in else None,
+                              q2 if (act_in and q2 is not None) else None, act_in, C1 + C2,
+                              False, weight, 0, Cp, Coutp, "gy")
+        else:
+            res = None
+            if cfg.skip_grad == "take" and q2 is None and not packed and need_x1:
+                res = _DEFERRED.pop(q1.data_ptr(), None)
+                if res is not None and (res.shape != (q1.shape[0], Cp, H, W) or Cp != C1):
+                    _DEFERRED[q1.data_ptr()] = res   # not fusable: added below instead
+                    res = None
+            outs = _conv_call(gyp, None, None, None, 1, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
+                              split, q1 if act_in else None,
+                              q2 if (act_in and q2 is not None) else None, act_in, C1 + C2,
+                              False, weight, 1, Cp, Coutp, "gy", res=res)
+        if q2 is not None:
+            gx1, gx2 = outs[0], outs[1]
+        elif packed:
+            g = outs[0]
+            gx1 = P().slice_channels(g, 0, C1) if need_x1 else None
+            gx2 = P().slice_channels(g, C1, C2) if need_x2 else None
+        else:
+            gx1 = outs[0]
+        if not need_x1:
+            gx1 = None
+        if not need_x2:
+            gx2 = None
+        if cfg.skip_grad == "take" and gx1 is not None and q2 is None:
+            parked = _DEFERRED.pop(q1.data_ptr(), None)
+            if parked is not None:
+                gx1 = gx1 + parked
+        if cfg.skip_grad == "defer" and gx1 is not None:
+            key = q1.data_ptr()
+            if key in _DEFERRED:
+                raise RuntimeError("skip_grad: a deferred gradient of this tensor is pending")
+            _DEFERRED[key] = gx1
+            gx1 = None
+    if need_w:
+        gw = torch.empty_like(weight, dtype=torch.float32, memory_format=torch.contiguous_format)
+        act_in = _act_code(cfg.act_in)
+        if cfg.transposed:
+            P().conv_wgrad(q1, q2, act_in, gyp, None, 0, KH, KW, s, p, 0, 1, gw, 1.0, 0)
+        elif (s == 1 and Coutp <= 16 and Cp >= 128 and KH == KW and not cfg.reflect
+              and cfg.up == 1):
+            # tiny-Cout stride-1 conv (PatchGAN logits): the GEMM's R = Cout would waste
+            # the MFMA tile, so compute it in transposed-conv form -- rows = input
+            # channels, the dY gather with pad K-1-p, taps flipped by the reduce
+            P().conv_wgrad(q1, q2, act_in, gyp, None, 0, KH, KW, 1, KH - 1 - p, 0, 1, gw,
+                           1.0, 0, 1)
+        else:
+            P().conv_wgrad(gyp, None, 0, q1, q2, act_in, KH, KW, s, p, int(cfg.reflect),
+                           cfg.up, gw, 1.0, 0)
+    if need_b:
+        gb = _take_colsum(gy) if cfg.act_out in (None, "none") else None
+        if gb is None:
+            gb = torch.empty(Cout, device=gy.device, dtype=torch.float32)
+            P().colsum(gyp, gb, 1.0, False)
+    return gx1, gx2, gw, gb
+
+
+# ============================================================== packed image head
+# The pix2pix step's image-facing layers run on ONE packed [N][8][H][W] bf16 pair tensor
+# per batch half (16 B per pixel: A in channels 0..2, B or the generated image in 3..5,
+# zeros in 6..7) -- csrc/image.hip.  The generator's first conv reads (A | B) with zero
+# weights on the B channels; its last transposed conv writes (A | fake) in place through the
+# depth-to-space epilogue together with the L1 term; the discriminator reads the 2B stack
+# [(A | fake); (A | B)] directly; and its first conv's input gradient comes back as the
+# generator's pre-tanh gradient (L1 sign term and tanh' fused in), so no 3-channel tensor,
+# channel pad / slice, col2im, tanh' or L1 kernel remains.
+#
+# Contract: the L1 value returned by image_head enters the loss LINEARLY with weight 1 (the
+# trainer's ``loss_G = loss_G_GAN + loss_G_L1``); its gradient lambda * sign(fake - B) / n is
+# injected by the fused dgrad, not routed through autograd.
+
+
+def _head_dgrad_ok(cfg, weight, x):
+    return (not cfg.transposed and cfg.KH == 4 and cfg.KW == 4 and cfg.stride == 2
+            and cfg.pad == 1 and cfg.up == 1 and not cfg.reflect and cfg.act_in is None
+            and weight.shape[1] == 6 and weight.shape[0] % 64 == 0 and x.shape[1] == 8)
+
+
+def _head_dgrad(head, af, weight, gy):
+    """d(loss)/d(pre-tanh fake) in slots 0..2 of a packed tensor: the first D conv's input
+    gradient on the fake channels (3..5) as a 3x3 union GEMM, + the L1 sign term, x tanh'."""
+    ab, scale = head
+    img, _ = P().union_weight(weight.detach().float().contiguous(), 3, 3, 32, gy.shape[1], None)
+    zb = torch.zeros(32, device=gy.device, dtype=torch.float32)
+    dz = torch.empty_like(af, memory_format=CL)
+    P().conv_d2s(gy, None, img, zb, 0, 0, 2, dz, ab, af, float(scale))
+    dz._p2p_dz = True
+    return dz
+
+
+class ImageHeadFn(torch.autograd.Function):
+    """The generator's last layer, ``tanh(ConvT4x4s2p1(relu(cat(skip, u))) + b)``, written as
+    the fake half of the packed pair tensor ``dd[:N]`` (with A copied from ``dd[N:]``)."""
+
+    @staticmethod
+    def forward(ctx, skip, u, weight, bias, dd, scale, cfg):
+        skip, u = to_nhwc_bf16(skip), to_nhwc_bf16(u)
+        N = skip.shape[0]
+        ab = dd.narrow(0, N, N)
+        af = dd.narrow(0, 0, N)
+        img, bu = P().union_weight(weight.detach().float().contiguous(), 0, 3, 32,
+                                   skip.shape[1] + u.shape[1],
+                                   None if bias is None else bias.detach().float().contiguous())
+        l1 = P().conv_d2s(skip, u, img, bu, _act_code(cfg.act_in), _act_code("tanh"), 1, af, ab,
+                          None, float(scale))
+        ctx.cfg = cfg
+        ctx.scale = float(scale)
+        ctx.has_bias = bias is not None
+        ctx.geo = (skip.shape[1], u.shape[1], skip.shape[1] + u.shape[1], False, 3, 8,
+                   skip.shape[2], skip.shape[3])
+        ctx.save_for_backward(skip, u, weight, af, ab)
+        ctx.mark_non_differentiable(l1)
+        af._p2p_packed = (3, 3)
+        af._p2p_head = (ab, float(scale))
+        return af, l1
+
+    @staticmethod
+    def backward(ctx, gaf, _gl1):
+        skip, u, weight, af, ab = ctx.saved_tensors
+        if getattr(gaf, "_p2p_dz", False):
+            dz = gaf                       # fused by the consumer (_head_dgrad)
+        else:                              # any other consumer: the same math, unfused
+            f = af[:, 3:6].float()
+            g = gaf[:, 3:6].float() + ctx.scale * torch.sign(f - ab[:, 3:6].float())
+            dz = torch.zeros_like(af, memory_format=CL)
+            dz[:, 0:3] = (g * (1 - f * f)).to(torch.bfloat16)
+        cfg = _ConvCfg(True, 4, 4, 2, 1, False, 1, ctx.cfg.act_in, None,
+                       skip_grad=ctx.cfg.skip_grad)
+        gx1, gx2, gw, gb = _conv_backward(cfg, ctx.geo, skip, u, weight, None, dz,
+                                          ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                                          ctx.needs_input_grad[2],
+                                          ctx.has_bias and ctx.needs_input_grad[3])
+        if gb is not None:
+            gb = gb[:3].contiguous()
+        return gx1, gx2, gw, gb, None, None, None
+
+
+def image_head(skip, u, module, dd, scale):
+    """(A | fake) written into ``dd[:N]`` by ``module`` (the U-Net's outermost ConvTranspose2d,
+    4x4 s2 p1, input ReLU, tanh) plus ``scale * sum|fake - B|`` (the L1 term)."""
+    cfg = _ConvCfg(True, 4, 4, 2, 1, False, 1, module.act_in, "tanh",
+                   skip_grad=module.skip_grad)
+    return ImageHeadFn.apply(skip, u, module.weight, module.bias, dd, float(scale), cfg)
+
+
+def image_head_ok(module, skip, u) -> bool:
+    w = module.weight
+    return (w.shape[1] == 3 and tuple(w.shape[2:]) == (4, 4) and module.stride[0] == 2
+            and module.padding[0] == 1 and module.act_in == "relu" and module.act_out == "tanh"
+            and skip.shape[1] % 64 == 0 and u.shape[1] % 64 == 0
+            and skip.shape[1] + u.shape[1] == w.shape[0])
 
 
 def _split_input(x):

@@ -1,6 +1,12 @@
+#!/bin/bash
+# packed image path: numerics vs oracle, graph equivalence, then bench + kernel profile
+set -o pipefail
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && rm -f gpurun_out/bounds.jsonl
-timeout -k 10 300 python tools/diag_graph.py > gpurun_out/diag_graph.jsonl 2> gpurun_out/diag.err; echo diag rc=$?
-cat gpurun_out/diag_graph.jsonl
-DROP=0 timeout -k 10 300 python tools/diag_graph.py > gpurun_out/diag_graph_nodrop.jsonl 2>> gpurun_out/diag.err; echo diag2 rc=$?
-cat gpurun_out/diag_graph_nodrop.jsonl
-timeout -k 10 400 python -u -m pytest tests/test_family_r_gpu.py -q --timeout 300 --timeout-method thread > gpurun_out/famr.log 2>&1; echo famr rc=$?; tail -3 gpurun_out/famr.log
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_pix2pix_step_gpu.py tests/test_graph_gpu.py tests/test_determinism_gpu.py -q --timeout 300 --timeout-method thread > gpurun_out/kt.log 2>&1; rc=$?
+echo "tests rc=$rc: $(tail -1 gpurun_out/kt.log)"; grep -E "^FAILED|^E  " gpurun_out/kt.log | head -20
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_b256.jsonl 2> gpurun_out/bench.err || exit $?
+cut -c1-260 gpurun_out/bench_b256.jsonl
+B=256 bash tools/gpu_prof_native.sh || exit $?
+head -45 gpurun_out/native_prof_b256/summary.txt
