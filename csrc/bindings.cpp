@@ -443,9 +443,11 @@ Tensor conv_d2s(const Tensor& x1, const optional<Tensor>& x2, const Tensor& w, c
   }
   const int64_t C1 = x1.size(1), C = C1 + C2;
   TORCH_CHECK(C1 % 64 == 0 && C2 % 64 == 0 && C1 <= 1024 && C2 <= 1024, "conv_d2s: channel groups of 64");
-  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.numel() == 32 * 9 * C,
-              "conv_d2s: union weight [32][3][3][C]");
-  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() == 32, "conv_d2s: union bias [32]");
+  const int64_t nrows = w.numel() / (9 * C);
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.numel() == nrows * 9 * C &&
+                  (nrows == 16 || nrows == 32),
+              "conv_d2s: union weight [16|32][3][3][C]");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() == nrows, "conv_d2s: union bias");
   TORCH_CHECK(mode == 1 || mode == 2, "conv_d2s: mode");
   TORCH_CHECK(act_in == 0 || act_in == 1, "conv_d2s: input act none / relu");
   for (const Tensor* t : {static_cast<const Tensor*>(&out), &pk_a}) {
@@ -456,6 +458,48 @@ Tensor conv_d2s(const Tensor& x1, const optional<Tensor>& x2, const Tensor& w, c
     TORCH_CHECK(pk_f.has_value(), "conv_d2s: head gradient needs pk_f");
     check_act(*pk_f, "conv_d2s pk_f");
     TORCH_CHECK(pk_f->sizes() == out.sizes(), "conv_d2s: pk_f shape");
+  }
+  hipStream_t st = cur_stream(x1);
+  if (nrows == 16) {
+    // halo-tile kernel: persistent blocks (one per CU) over 16x16 tiles of the input grid
+    p2p::HaloArgs h{};
+    h.x1 = static_cast<const __bf16*>(x1.data_ptr());
+    h.x2 = x2 ? static_cast<const __bf16*>(x2->data_ptr()) : nullptr;
+    h.C1 = (int)C1;
+    h.C2 = (int)C2;
+    h.N = (int)N;
+    h.H = (int)H;
+    h.W = (int)W;
+    h.w = static_cast<const __bf16*>(w.data_ptr());
+    h.bias = bias.data_ptr<float>();
+    h.act_out = (int)act_out;
+    h.mode = (int)mode;
+    h.out = static_cast<__bf16*>(out.data_ptr());
+    h.pk_a = static_cast<const __bf16*>(pk_a.data_ptr());
+    h.pk_f = mode == 2 ? static_cast<const __bf16*>(pk_f->data_ptr()) : nullptr;
+    h.scale = (float)scale;
+    h.zero = static_cast<const __bf16*>(zero_page(x1));
+    h.tiles_x = (int)((W + 15) / 16);
+    h.tiles_y = (int)((H + 15) / 16);
+    h.ntiles = (int)N * h.tiles_x * h.tiles_y;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int blocks = std::max(1, std::min(h.ntiles, cus));
+    Tensor part;
+    if (mode == 1) {
+      part = at::zeros({blocks}, x1.options().dtype(at::kFloat));
+      h.l1_part = part.data_ptr<float>();
+    }
+    const int rc = p2p_halo_union(&h, act_in == 1 ? 1 : 0, blocks, st);
+    TORCH_CHECK(rc != -2, "conv_d2s: no halo kernel for C1 ", C1, " C2 ", C2);
+    check_rc(rc, "conv_d2s(halo)");
+    if (mode == 1) {
+      Tensor l1 = at::empty({}, x1.options().dtype(at::kFloat));
+      check_rc(p2p_sum_partials(h.l1_part, blocks, (float)scale, l1.data_ptr<float>(), st), "conv_d2s l1");
+      return l1;
+    }
+    return out;
   }
   p2p::ConvFwdArgs a{};
   a.x1 = x1.data_ptr();
@@ -491,7 +535,6 @@ Tensor conv_d2s(const Tensor& x1, const optional<Tensor>& x2, const Tensor& w, c
     part = at::zeros({blocks}, x1.options().dtype(at::kFloat));
     a.l1_part = part.data_ptr<float>();
   }
-  hipStream_t st = cur_stream(x1);
   const int rc = p2p_conv_fwd_glds(&a, 0, 7, st);
   TORCH_CHECK(rc != -2, "conv_d2s: no union-GEMM kernel for this geometry");
   check_rc(rc, "conv_d2s");

@@ -92,9 +92,30 @@ struct ConvWgradArgs {
   const void* zero;  // zero page for the global_load_lds variant
 };
 
+// Halo-tile union conv (csrc/halo_conv.hip): the conv_d2s GEMM with a resident 16-column
+// weight and 18x18 halo tiles of the input grid staged once per 64-channel chunk.
+struct HaloArgs {
+  const __bf16* x1;
+  const __bf16* x2;
+  int C1, C2;          // NHWC channel counts, multiples of 64 (C1 + C2 <= 128)
+  int N, H, W;         // input (q) grid
+  const __bf16* w;     // union image [16][9][C1 + C2]
+  const float* bias;   // [16]
+  int act_out;         // tanh (image forward) / none
+  int mode;            // d2s mode: 1 image forward, 2 head gradient
+  __bf16* out;         // packed [N][2H][2W][8]
+  const __bf16* pk_a;
+  const __bf16* pk_f;
+  float scale;
+  float* l1_part;      // [blocks] (mode 1)
+  const __bf16* zero;
+  int tiles_x, tiles_y, ntiles;
+};
+
 }  // namespace p2p
 
 extern "C" {
+int p2p_halo_union(const p2p::HaloArgs* a, int relu, int blocks, hipStream_t st);
 int p2p_conv_fwd(const p2p::ConvFwdArgs* a, int mode, int bm, int bn, hipStream_t stream);
 int p2p_conv_finalize(const p2p::ConvFwdArgs* a, hipStream_t stream);
 // global_load_lds pipelined variant (FAST layers, BN in {64, 128}); returns -2 if the

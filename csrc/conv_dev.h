@@ -44,6 +44,36 @@ __device__ __forceinline__ ClassGeom class_geom(const ConvFwdArgs& a, int cls) {
   return g;
 }
 
+// One packed output pixel P of the depth-to-space epilogue (conv.h ``d2s``) from its three
+// GEMM values c[0..2]: mode 1 writes (pk_a[0..2], c, 0, 0) and returns sum|c - pk_a[3..5]|;
+// mode 2 writes ((c + scale * sign(f - b)) * (1 - f^2), 0 ...) with f = pk_f[3..5], b = pk_a[3..5].
+__device__ __forceinline__ float d2s_pixel(int mode, long P, const bf16* c, const bf16* pk_a, const bf16* pk_f,
+                                           float scale, bf16* out) {
+  const bf16x8 ab = *reinterpret_cast<const bf16x8*>(pk_a + P * 8);
+  bf16x8 o;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o[q] = (bf16)0.f;
+  float l1 = 0.f;
+  if (mode == 1) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      o[j] = ab[j];
+      o[3 + j] = c[j];
+      l1 += fabsf((float)c[j] - (float)ab[3 + j]);
+    }
+  } else {
+    const bf16x8 af = *reinterpret_cast<const bf16x8*>(pk_f + P * 8);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float f = (float)af[3 + j], b = (float)ab[3 + j];
+      const float sg = (float)(f > b) - (float)(f < b);
+      o[j] = (bf16)(((float)c[j] + scale * sg) * (1.f - f * f));
+    }
+  }
+  *reinterpret_cast<bf16x8*>(out + P * 8) = o;
+  return l1;
+}
+
 // bias + output activation in registers, the bf16 tile staged through LDS, 16-B stores
 // with the optional act'(x) multiply (dgrad) and the concat channel split; split-K tiles
 // accumulate fp32 atomics instead.
@@ -131,28 +161,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
       const int qy = (int)fdiv((uint32_t)r, fd_wq);
       const int qx = r - qy * g.Wq;
       const long P = ((long)n * Ho + 2 * qy + (cls >> 1)) * Wo + 2 * qx + (cls & 1);
-      const bf16* c = Cs + row * LDC + cls * 4;
-      const bf16x8 ab = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(a.pk_a) + P * 8);
-      bf16x8 o;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) o[q] = (bf16)0.f;
-      if (a.d2s == 1) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          o[j] = ab[j];
-          o[3 + j] = c[j];
-          l1 += fabsf((float)c[j] - (float)ab[3 + j]);
-        }
-      } else {
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(a.pk_f) + P * 8);
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const float f = (float)af[3 + j], b = (float)ab[3 + j];
-          const float sg = (float)(f > b) - (float)(f < b);
-          o[j] = (bf16)(((float)c[j] + a.d2s_scale * sg) * (1.f - f * f));
-        }
-      }
-      *reinterpret_cast<bf16x8*>(static_cast<bf16*>(a.y1) + P * 8) = o;
+      l1 += d2s_pixel(a.d2s, P, Cs + row * LDC + cls * 4, static_cast<const bf16*>(a.pk_a),
+                      static_cast<const bf16*>(a.pk_f), a.d2s_scale, static_cast<bf16*>(a.y1));
     }
     if (a.d2s == 1 && a.l1_part) {
       float* red = reinterpret_cast<float*>(smem + BM * LDC * 2);

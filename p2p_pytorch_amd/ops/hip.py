@@ -513,6 +513,11 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
 # injected by the fused dgrad, not routed through autograd.
 
 
+# union GEMM columns: 16 = the halo-tile kernel (csrc/halo_conv.hip); 32 = the implicit-GEMM
+# 256x32 glds tile (conv_fwd_glds.hip variant 7), kept as the A/B reference path
+UNION_ROWS = 16
+
+
 def _head_dgrad_ok(cfg, weight, x):
     return (not cfg.transposed and cfg.KH == 4 and cfg.KW == 4 and cfg.stride == 2
             and cfg.pad == 1 and cfg.up == 1 and not cfg.reflect and cfg.act_in is None
@@ -523,8 +528,9 @@ def _head_dgrad(head, af, weight, gy):
     """d(loss)/d(pre-tanh fake) in slots 0..2 of a packed tensor: the first D conv's input
     gradient on the fake channels (3..5) as a 3x3 union GEMM, + the L1 sign term, x tanh'."""
     ab, scale = head
-    img, _ = P().union_weight(weight.detach().float().contiguous(), 3, 3, 32, gy.shape[1], None)
-    zb = torch.zeros(32, device=gy.device, dtype=torch.float32)
+    img, _ = P().union_weight(weight.detach().float().contiguous(), 3, 3, UNION_ROWS,
+                              gy.shape[1], None)
+    zb = torch.zeros(UNION_ROWS, device=gy.device, dtype=torch.float32)
     dz = torch.empty_like(af, memory_format=CL)
     P().conv_d2s(gy, None, img, zb, 0, 0, 2, dz, ab, af, float(scale))
     dz._p2p_dz = True
@@ -541,7 +547,7 @@ class ImageHeadFn(torch.autograd.Function):
         N = skip.shape[0]
         ab = dd.narrow(0, N, N)
         af = dd.narrow(0, 0, N)
-        img, bu = P().union_weight(weight.detach().float().contiguous(), 0, 3, 32,
+        img, bu = P().union_weight(weight.detach().float().contiguous(), 0, 3, UNION_ROWS,
                                    skip.shape[1] + u.shape[1],
                                    None if bias is None else bias.detach().float().contiguous())
         l1 = P().conv_d2s(skip, u, img, bu, _act_code(cfg.act_in), _act_code("tanh"), 1, af, ab,
