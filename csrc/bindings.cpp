@@ -282,8 +282,10 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     g.y1 = col.data_ptr();
     g.y2 = nullptr;
     int grc = -2;
-    if (Ncol > 32 && (act_in == 0 || act_in == 1))
-      grc = p2p_conv_fwd_glds(&g, 0, conv_variant(Ncol, C), st);
+    // Ncol <= 32 (the PatchGAN logits: 16 taps x 1 channel): the 256x32 glds tile streams
+    // the wide input once at full rate (the register-staged 256x16 kernel ran at ~1/3 of it)
+    if (act_in == 0 || act_in == 1)
+      grc = p2p_conv_fwd_glds(&g, 0, Ncol > 32 ? conv_variant(Ncol, C) : 7, st);
     if (grc == -2) {
       const int gbn = Ncol <= 16 ? 16 : (Ncol <= 32 ? 32 : (Ncol <= 64 ? 64 : 128));
       const int gbm = gbn <= 32 ? 256 : 128;
