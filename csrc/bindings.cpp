@@ -381,7 +381,39 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     a.q_fmt = (int)y_qfmt;
   }
   int rc = -2;
-  if (glds_ok) rc = p2p_conv_fwd_glds(&a, (int)mode, variant, st);
+  // packed 8-channel image convs (4x4 s2 p1): the halo-tile kernel (csrc/halo_pk8.hip)
+  if (mode == 0 && !fp8 && C1 == 8 && C2 == 0 && KH == 4 && KW == 4 && stride == 2 && pad == 1 && !reflect &&
+      up == 1 && act_in == 0 && splits == 1 && !a.stats && !a.q_out && !a.res1 && (Cout == 64 || Cout == 128) &&
+      std::getenv("P2P_NO_HALO") == nullptr) {
+    p2p::HaloPk8Args h{};
+    h.x = static_cast<const __bf16*>(x1.data_ptr());
+    h.Hi = (int)H;
+    h.Wi = (int)W;
+    h.Ho = (int)OH;
+    h.Wo = (int)OW;
+    h.w = static_cast<const __bf16*>(w.data_ptr());
+    h.bias = a.bias;
+    h.Cout = (int)Cout;
+    h.act_out = (int)act_out;
+    h.y1 = static_cast<__bf16*>(a.y1);
+    h.y2 = static_cast<__bf16*>(a.y2);
+    h.Csplit = (int)Csplit;
+    h.xb1 = static_cast<const __bf16*>(a.xb1);
+    h.xb2 = static_cast<const __bf16*>(a.xb2);
+    h.zero = static_cast<const __bf16*>(a.zero);
+    h.tiles_x = (int)((OW + 15) / 16);
+    h.tiles_y = (int)((OH + 15) / 16);
+    h.ntiles = (int)N * h.tiles_x * h.tiles_y;
+    const bool gate_ok = act_bwd == 0 || act_bwd == 1;
+    if (gate_ok && (act_bwd == 0 || Cout == 128) && OH == (H + 2 - 4) / 2 + 1 && OW == (W + 2 - 4) / 2 + 1) {
+      if (act_bwd == 0) h.xb1 = h.xb2 = nullptr;
+      int dev = 0, cus = 256;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      rc = p2p_halo_pk8(&h, std::max(1, std::min(h.ntiles, cus)), st);
+    }
+  }
+  if (rc == -2 && glds_ok) rc = p2p_conv_fwd_glds(&a, (int)mode, variant, st);
   if (rc == -2 && a.stats) {  // glds refused after all: no fused statistics
     a.stats = nullptr;
     stats = Tensor();

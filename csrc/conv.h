@@ -112,9 +112,27 @@ struct HaloArgs {
   int tiles_x, tiles_y, ntiles;
 };
 
+// Halo-tile packed-image conv (csrc/halo_pk8.hip): 4x4 s2 p1 over [N][Hi][Wi][8] bf16,
+// Cout 64 (bias + act) or 128 (optionally the ReLU gate of a dgrad, split output).
+struct HaloPk8Args {
+  const __bf16* x;
+  int Hi, Wi, Ho, Wo;
+  const __bf16* w;     // [Cout][16][8] weight image
+  const float* bias;   // [Cout] or null
+  int Cout, act_out;
+  __bf16* y1;          // channels [0, Csplit), ld Csplit
+  __bf16* y2;          // channels [Csplit, Cout), ld Cout - Csplit
+  int Csplit;
+  const __bf16* xb1;   // ReLU-gate inputs (same split), null = no gate
+  const __bf16* xb2;
+  const __bf16* zero;
+  int tiles_x, tiles_y, ntiles;
+};
+
 }  // namespace p2p
 
 extern "C" {
+int p2p_halo_pk8(const p2p::HaloPk8Args* a, int blocks, hipStream_t st);
 int p2p_halo_union(const p2p::HaloArgs* a, int relu, int blocks, hipStream_t st);
 int p2p_conv_fwd(const p2p::ConvFwdArgs* a, int mode, int bm, int bn, hipStream_t stream);
 int p2p_conv_finalize(const p2p::ConvFwdArgs* a, hipStream_t stream);
