@@ -191,8 +191,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     TORCH_CHECK(xb1.has_value(), "conv_fwd: act_bwd needs xb1");
     check_act(*xb1, "xb1");
     TORCH_CHECK(xb1->size(1) == Csplit && xb1->size(2) == OH && xb1->size(3) == OW, "xb1 shape");
-    if (Csplit < Cout) {
-      TORCH_CHECK(xb2.has_value(), "conv_fwd: act_bwd needs xb2");
+    if (Csplit < Cout && xb2.has_value()) {   // no xb2: the second half is not gated
       check_act(*xb2, "xb2");
       TORCH_CHECK(xb2->size(1) == Cout - Csplit, "xb2 shape");
     }
@@ -227,7 +226,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   a.y2 = y2.defined() ? y2.data_ptr() : nullptr;
   a.Csplit = (int)Csplit;
   a.xb1 = act_bwd ? xb1->data_ptr() : nullptr;
-  a.xb2 = (act_bwd && Csplit < Cout) ? xb2->data_ptr() : nullptr;
+  a.xb2 = (act_bwd && Csplit < Cout && xb2) ? xb2->data_ptr() : nullptr;
   a.act_bwd = (int)act_bwd;
   a.res1 = nullptr;
   if (res) {
@@ -410,7 +409,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       int dev = 0, cus = 256;
       (void)hipGetDevice(&dev);
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      rc = p2p_halo_pk8(&h, std::max(1, std::min(h.ntiles, cus)), st);
+      const int per_cu = Cout == 128 ? 1 : 2;   // halo_pk8.hip launch bounds
+      rc = p2p_halo_pk8(&h, std::max(1, std::min(h.ntiles, per_cu * cus)), st);
     }
   }
   if (rc == -2 && glds_ok) rc = p2p_conv_fwd_glds(&a, (int)mode, variant, st);

@@ -227,8 +227,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
     const bool first = co < a.Csplit;
     const int ld = first ? a.Csplit : a.Cout - a.Csplit;
     const int cof = first ? co : co - a.Csplit;
-    if (a.act_bwd) {
-      const bf16* xb = static_cast<const bf16*>(first ? a.xb1 : a.xb2);
+    const bf16* xb = static_cast<const bf16*>(first ? a.xb1 : a.xb2);
+    if (a.act_bwd && xb) {   // a null half is gated by its producer's backward instead
       const u32x4 xv = *reinterpret_cast<const u32x4*>(xb + pix * ld + cof);
       if (a.act_bwd == ACT_RELU) {
         // zero the gradient where x <= 0 (bf16 sign / zero test on the int pipe)

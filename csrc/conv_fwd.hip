@@ -287,8 +287,8 @@ __global__ void __launch_bounds__(256) conv_finalize_kernel(ConvFwdArgs a, long 
     const bool first = co < a.Csplit;
     const int ld = first ? a.Csplit : a.Cout - a.Csplit;
     const int cof = first ? co : co - a.Csplit;
-    if (a.act_bwd) {
-      const bf16* xb = static_cast<const bf16*>(first ? a.xb1 : a.xb2);
+    const bf16* xb = static_cast<const bf16*>(first ? a.xb1 : a.xb2);
+    if (a.act_bwd && xb) {
       bf16x8 xv = *reinterpret_cast<const bf16x8*>(xb + pix * ld + cof);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] *= act_grad_from_input((float)xv[j], a.act_bwd);

@@ -157,13 +157,45 @@ __global__ void __launch_bounds__(256) halo_union_kernel(HaloArgs a) {
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      // depth-to-space stores: 4 output pixels per thread, their packed-image operands
+      // loaded before any is used (one HBM round trip per tile, not four)
       const int Ho = 2 * a.H, Wo = 2 * a.W;
-      for (int item = tid; item < 256 * 4; item += 256) {
-        const int row = item >> 2, cls = item & 3;
+      long P[4];
+      bool ok[4];
+      bf16x8 ab[4], af[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int item = tid + q * 256, row = item >> 2, cls = item & 3;
         const int qy = qy0 + (row >> 4), qx = qx0 + (row & 15);
-        if (qy >= a.H || qx >= a.W) continue;
-        const long P = ((long)n * Ho + 2 * qy + (cls >> 1)) * Wo + 2 * qx + (cls & 1);
-        l1 += d2s_pixel(a.mode, P, Cs + row * LDC + cls * 4, a.pk_a, a.pk_f, a.scale, a.out);
+        ok[q] = qy < a.H && qx < a.W;
+        P[q] = ((long)n * Ho + 2 * (ok[q] ? qy : 0) + (cls >> 1)) * Wo + 2 * (ok[q] ? qx : 0) + (cls & 1);
+        ab[q] = *reinterpret_cast<const bf16x8*>(a.pk_a + P[q] * 8);
+        if (a.mode == 2) af[q] = *reinterpret_cast<const bf16x8*>(a.pk_f + P[q] * 8);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int item = tid + q * 256, row = item >> 2, cls = item & 3;
+        if (!ok[q]) continue;
+        const bf16* c = Cs + row * LDC + cls * 4;
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (bf16)0.f;
+        if (a.mode == 1) {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            o[j] = ab[q][j];
+            o[3 + j] = c[j];
+            l1 += fabsf((float)c[j] - (float)ab[q][3 + j]);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const float f = (float)af[q][3 + j], b = (float)ab[q][3 + j];
+            const float sg = (float)(f > b) - (float)(f < b);
+            o[j] = (bf16)(((float)c[j] + a.scale * sg) * (1.f - f * f));
+          }
+        }
+        *reinterpret_cast<bf16x8*>(a.out + P[q] * 8) = o;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();   // staging read before the stage is re-filled

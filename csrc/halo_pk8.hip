@@ -41,14 +41,17 @@ __device__ __forceinline__ int unit_of(int hy, int hx) { return (hy * 2 + (hx & 
 
 }  // namespace
 
+// TN = 8 (128 channels) keeps 128 accumulators + 8 B fragments live: one block per CU
+// (512-register budget, no spill); TN = 4 runs two blocks per CU
 template <int TN, int ACT, bool GATE>
-__global__ void __launch_bounds__(256) halo_pk8_kernel(HaloPk8Args a) {
+__global__ void __launch_bounds__(256, TN >= 8 ? 1 : 2) halo_pk8_kernel(HaloPk8Args a) {
   constexpr int NC = TN * 16;              // output channels of the block (== Cout)
-  constexpr int LDC = 64 + 8;              // staging row: 64 channels at a time
+  constexpr int PC = 32;                   // channels per epilogue piece
+  constexpr int LDC = PC + 8;              // staging row (80 B: 16-B aligned, spread banks)
+  static_assert(256 * LDC * 2 <= SUNITS * 16, "epilogue piece fits in one halo stage");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* As = reinterpret_cast<bf16*>(smem);                               // 2 x SUNITS units
   bf16* Bs = As + 2 * SUNITS * 8;                                         // NC x 16 units
-  bf16* Cs = Bs + NC * 16 * 8;                                            // 256 x LDC
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int my_tiles = (a.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
   if (my_tiles <= 0) return;
@@ -103,7 +106,7 @@ __global__ void __launch_bounds__(256) halo_pk8_kernel(HaloPk8Args a) {
     }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    const bf16* A = As + stage * SUNITS * 8;
+    bf16* A = As + stage * SUNITS * 8;
     f32x4 acc[4][TN];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -126,13 +129,17 @@ __global__ void __launch_bounds__(256) halo_pk8_kernel(HaloPk8Args a) {
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
       }
     }
-    // ---- epilogue: 64 channels at a time through the staging tile, 16-B stores
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();     // every wave done with this stage: it hosts the staging tile
+    // ---- epilogue, 32 channels at a time: bias + act staged as bf16 in this stage's LDS,
+    // then 16-B stores (the ReLU-gate inputs of a piece are loaded before any is used)
     int n, oy0, ox0;
     origin(k, n, oy0, ox0);
+    bf16* Cs = A;
 #pragma unroll
-    for (int half = 0; half < NC / 64; ++half) {
+    for (int piece = 0; piece < NC / PC; ++piece) {
 #pragma unroll
-      for (int j = half * 4; j < half * 4 + 4; ++j) {
+      for (int j = piece * 2; j < piece * 2 + 2; ++j) {
         const int col = j * 16 + px;
         const float bj = a.bias ? a.bias[col] : 0.f;
 #pragma unroll
@@ -140,34 +147,47 @@ __global__ void __launch_bounds__(256) halo_pk8_kernel(HaloPk8Args a) {
           const int rowb = wid * 64 + i * 16 + kq * 4;
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            Cs[(rowb + r) * LDC + (col - half * 64)] = (bf16)act_fwd(acc[i][j][r] + bj, ACT);
+            Cs[(rowb + r) * LDC + (col - piece * PC)] = (bf16)act_fwd(acc[i][j][r] + bj, ACT);
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      const int co0 = piece * PC;
+      const bool first = co0 < a.Csplit;          // a piece never straddles the split (host)
+      const int ld = first ? a.Csplit : NC - a.Csplit;
+      const int cof0 = first ? co0 : co0 - a.Csplit;
+      bf16* yb = first ? a.y1 : a.y2;
+      const bf16* xb = first ? a.xb1 : a.xb2;
+      long pix[4];
+      bool ok[4];
+      u32x4 xv[4];
 #pragma unroll
-      for (int it = tid; it < 256 * 8; it += 256) {   // 256 pixels x 8 chunks of 8 channels
-        const int row = it >> 3, cc = it & 7;
+      for (int q = 0; q < 4; ++q) {               // 256 pixels x 4 chunks of 8 channels
+        const int it = tid + q * 256, row = it >> 2;
         const int oy = oy0 + (row >> 4), ox = ox0 + (row & 15);
-        if (oy >= a.Ho || ox >= a.Wo) continue;
-        const long pix = ((long)n * a.Ho + oy) * a.Wo + ox;
-        u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * LDC + cc * 8);
-        const int co = half * 64 + cc * 8;
-        const bool first = co < a.Csplit;
-        const int ld = first ? a.Csplit : NC - a.Csplit;
-        const int cof = first ? co : co - a.Csplit;
-        if constexpr (GATE) {   // ReLU' of the layer's input (dgrad of a ReLU-input conv)
-          const u32x4 xv = *reinterpret_cast<const u32x4*>((first ? a.xb1 : a.xb2) + pix * ld + cof);
+        ok[q] = oy < a.Ho && ox < a.Wo;
+        pix[q] = ((long)n * a.Ho + (ok[q] ? oy : 0)) * a.Wo + (ok[q] ? ox : 0);
+        if constexpr (GATE) {
+          xv[q] = xb ? *reinterpret_cast<const u32x4*>(xb + pix[q] * ld + cof0 + (it & 3) * 8)
+                     : u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};
+        }
+      }
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint32_t xw = xv[q];
+      for (int q = 0; q < 4; ++q) {
+        const int it = tid + q * 256, row = it >> 2, cc = it & 3;
+        if (!ok[q]) continue;
+        u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * LDC + cc * 8);
+        if constexpr (GATE) {   // ReLU' of the layer's input (dgrad of a ReLU-input conv)
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const uint32_t xw = xv[q][w];
             uint32_t keep = 0;
             if ((int16_t)(xw & 0xffffu) > 0) keep |= 0xffffu;
             if ((int16_t)(xw >> 16) > 0) keep |= 0xffff0000u;
-            v[q] &= keep;
+            v[w] &= keep;
           }
         }
-        *reinterpret_cast<u32x4*>((first ? a.y1 : a.y2) + pix * ld + cof) = v;
+        *reinterpret_cast<u32x4*>(yb + pix[q] * ld + cof0 + cc * 8) = v;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -177,7 +197,7 @@ __global__ void __launch_bounds__(256) halo_pk8_kernel(HaloPk8Args a) {
 
 template <int TN, int ACT, bool GATE>
 static int launch_pk8(const HaloPk8Args& a, int blocks, hipStream_t st) {
-  constexpr int smem = (2 * SUNITS + TN * 16 * 16) * 16 + 256 * (64 + 8) * 2;
+  constexpr int smem = (2 * SUNITS + TN * 16 * 16) * 16;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo_pk8_kernel<TN, ACT, GATE>),
@@ -193,15 +213,17 @@ static int launch_pk8(const HaloPk8Args& a, int blocks, hipStream_t st) {
 // -2: geometry / epilogue not covered (the caller uses the implicit GEMM)
 extern "C" int p2p_halo_pk8(const p2p::HaloPk8Args* a, int blocks, hipStream_t st) {
   using namespace p2p;
-  const bool gate = a->xb1 != nullptr;
+  const bool gate = a->xb1 != nullptr || a->xb2 != nullptr;
+  if (a->Csplit % 32) return -2;   // epilogue pieces never straddle the split
   if (a->Cout == 64 && !gate) {
     if (a->act_out == ACT_LRELU) return launch_pk8<4, ACT_LRELU, false>(*a, blocks, st);
     if (a->act_out == ACT_NONE) return launch_pk8<4, ACT_NONE, false>(*a, blocks, st);
     if (a->act_out == ACT_RELU) return launch_pk8<4, ACT_RELU, false>(*a, blocks, st);
     return -2;
   }
+  if (a->Csplit % 32) return -2;   // epilogue pieces never straddle the split
   if (a->Cout == 128 && a->act_out == ACT_NONE) {
-    if (gate) return (a->xb2 || a->Csplit == 128) ? launch_pk8<8, ACT_NONE, true>(*a, blocks, st) : -2;
+    if (gate) return launch_pk8<8, ACT_NONE, true>(*a, blocks, st);
     return launch_pk8<8, ACT_NONE, false>(*a, blocks, st);
   }
   return -2;

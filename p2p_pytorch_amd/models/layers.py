@@ -51,13 +51,14 @@ class ConvTranspose2d(nn.ConvTranspose2d):
         self.grad_gate = None
         self.out_gated = False
         self.skip_grad = None
+        self.gate_x2 = True       # False: the concat's second half arrives already ReLU'd
 
     def forward(self, x):
         return ops.conv_transpose2d(x, self.weight, self.bias, self.stride[0], self.padding[0],
                                     self.act_in, self.act_out,
                                     stats=self.norm_stats and self.training,
                                     grad_gate=self.grad_gate, out_gated=self.out_gated,
-                                    skip_grad=self.skip_grad)
+                                    skip_grad=self.skip_grad, gate_x2=self.gate_x2)
 
 
 def link_norm(conv, norm):

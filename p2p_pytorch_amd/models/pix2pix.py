@@ -74,6 +74,10 @@ class UnetGenerator(nn.Module):
         # skip i is read by ups[i] (backward first) and downs[i + 1]: one gradient write
         for i in range(n - 1):
             link_skip(self.ups[i], self.downs[i + 1])
+            # the up half u = [dropout](ReLU(norm(.))) is ReLU'd by its producer, whose
+            # backward applies the same gate [norm > 0]: the ConvT's input ReLU' on u is
+            # redundant, so its dgrad epilogue gates (and re-reads) the skip half only
+            self.ups[i].gate_x2 = False
 
     def forward(self, x):
         n = self.num_downs

@@ -37,10 +37,12 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, pad_mode="zeros", upsample
 
 
 def conv_transpose2d(x, weight, bias=None, stride=2, padding=1, act_in=None, act_out=None,
-                     stats=False, grad_gate=None, out_gated=False, skip_grad=None):
+                     stats=False, grad_gate=None, out_gated=False, skip_grad=None, gate_x2=True):
+    """``gate_x2=False`` (HIP path): the second half of a virtual-concat input is already
+    ReLU'd by its producer, whose backward applies the same gate -- skip re-reading it."""
     if _native.use_native(_first(x)):
         return _hip().conv_transpose2d(x, weight, bias, stride, padding, act_in, act_out, stats,
-                                       grad_gate, out_gated, skip_grad)
+                                       grad_gate, out_gated, skip_grad, gate_x2)
     return ref.conv_transpose2d(x, weight, bias, stride, padding, act_in, act_out)
 
 

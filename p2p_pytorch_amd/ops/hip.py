@@ -274,11 +274,12 @@ class _ConvCfg:
     gradient of its x1.  ``assert_no_deferred()`` checks after backward that every parked
     gradient was consumed."""
     __slots__ = ("transposed", "KH", "KW", "stride", "pad", "reflect", "up", "act_in", "act_out",
-                 "stats", "grad_gate", "out_gated", "skip_grad")
+                 "stats", "grad_gate", "out_gated", "skip_grad", "gate_x2")
 
     def __init__(self, transposed, KH, KW, stride, pad, reflect, up, act_in, act_out, stats=False,
-                 grad_gate=None, out_gated=False, skip_grad=None):
+                 grad_gate=None, out_gated=False, skip_grad=None, gate_x2=True):
         self.skip_grad = skip_grad
+        self.gate_x2 = gate_x2
         self.stats = stats
         self.grad_gate = grad_gate
         self.out_gated = out_gated
@@ -440,8 +441,8 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
         elif cfg.transposed:
             outs = _conv_call(gyp, None, None, None, 0, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
                               split, q1 if act_in else None,
-                              q2 if (act_in and q2 is not None) else None, act_in, C1 + C2,
-                              False, weight, 0, Cp, Coutp, "gy")
+                              q2 if (act_in and q2 is not None and cfg.gate_x2) else None,
+                              act_in, C1 + C2, False, weight, 0, Cp, Coutp, "gy")
         else:
             res = None
             if cfg.skip_grad == "take" and q2 is None and not packed and need_x1:
@@ -574,7 +575,7 @@ class ImageHeadFn(torch.autograd.Function):
             dz = torch.zeros_like(af, memory_format=CL)
             dz[:, 0:3] = (g * (1 - f * f)).to(torch.bfloat16)
         cfg = _ConvCfg(True, 4, 4, 2, 1, False, 1, ctx.cfg.act_in, None,
-                       skip_grad=ctx.cfg.skip_grad)
+                       skip_grad=ctx.cfg.skip_grad, gate_x2=ctx.cfg.gate_x2)
         gx1, gx2, gw, gb = _conv_backward(cfg, ctx.geo, skip, u, weight, None, dz,
                                           ctx.needs_input_grad[0], ctx.needs_input_grad[1],
                                           ctx.needs_input_grad[2],
@@ -588,7 +589,7 @@ def image_head(skip, u, module, dd, scale):
     """(A | fake) written into ``dd[:N]`` by ``module`` (the U-Net's outermost ConvTranspose2d,
     4x4 s2 p1, input ReLU, tanh) plus ``scale * sum|fake - B|`` (the L1 term)."""
     cfg = _ConvCfg(True, 4, 4, 2, 1, False, 1, module.act_in, "tanh",
-                   skip_grad=module.skip_grad)
+                   skip_grad=module.skip_grad, gate_x2=getattr(module, "gate_x2", True))
     return ImageHeadFn.apply(skip, u, module.weight, module.bias, dd, float(scale), cfg)
 
 
@@ -625,10 +626,10 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, pad_mode="zeros", upsample
 
 
 def conv_transpose2d(x, weight, bias=None, stride=2, padding=1, act_in=None, act_out=None,
-                     stats=False, grad_gate=None, out_gated=False, skip_grad=None):
+                     stats=False, grad_gate=None, out_gated=False, skip_grad=None, gate_x2=True):
     x1, x2 = _split_input(x)
     cfg = _ConvCfg(True, weight.shape[2], weight.shape[3], int(stride), int(padding), False, 1,
-                   act_in, act_out, stats, grad_gate, out_gated, skip_grad)
+                   act_in, act_out, stats, grad_gate, out_gated, skip_grad, gate_x2)
     return ConvFn.apply(x1, x2, weight, bias, cfg)
 
 
