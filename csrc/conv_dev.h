@@ -88,7 +88,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
   const int wm = wid / WN, wn = wid % WN;
   const int HWq = g.Hq * g.Wq;
   const int s = a.stride;
-  auto out_pix = [&](int m) -> long {
+  auto out_pix = [&](int m) __attribute__((always_inline)) -> long {
     if (MODE == 0) return m;
     const int n = (int)fdiv((uint32_t)m, fd_hwq);
     const int r = m - n * HWq;
@@ -97,8 +97,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
     return ((long)n * a.OH + qy * s + g.ry) * a.OW + qx * s + g.rx;
   };
 
-  // ---- split-K: fp32 atomics straight from the accumulators (tiny-M layers only)
-  if (a.splits > 1) {
+  // ---- split-K: fp32 atomics straight from the accumulators (tiny-M layers only).  Not
+  // compiled into the big tiles (the host never splits them): its out_pix division loop
+  // is not unrolled there, which made the compiler keep the accumulators in scratch.
+  if constexpr (BM * BN <= 256 * 128) if (a.splits > 1) {
     float* wsb = a.det ? a.ws + (long)(blockIdx.z % a.splits) * a.N * a.OH * a.OW * a.Cout : a.ws;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -124,7 +126,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
   constexpr int LDC = BN + 8;
   // the activation is dispatched ONCE per tile (compile-time body per code), not by a
   // wave-uniform branch per accumulator element
-  auto stage_tile = [&](auto act_tag) {
+  auto stage_tile = [&](auto act_tag) __attribute__((always_inline)) {
     constexpr int ACT = decltype(act_tag)::value;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {

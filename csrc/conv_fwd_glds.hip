@@ -302,98 +302,156 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: STAGES-1 tiles in flight
+#ifdef P2P_NO_LATE
+  constexpr bool LATE = false;
+#else
+  constexpr bool LATE = STAGES == 2 && F8 == 0;
+#endif
+  if constexpr (LATE) {
+    // 2-slot ring with prefetch distance 2: each K tile's fragments are read into registers
+    // up front (they already were), a second barrier then frees its slot, and tile kt + 2 is
+    // issued into it BEFORE the MFMAs -- two K tiles of MFMA time cover each load instead of
+    // one, with the same LDS (the 256x256 tile's vmcnt(0) per tile was exposed HBM latency)
+    issue(kt0, 0);
+    if (kt0 + 1 < kt1) issue(kt0 + 1, 1);
+    int stage = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      if (kt + 1 < kt1) wait_vmcnt<LOADS>();   // tile kt landed; kt + 1 may still fly
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16* A = As + stage * BM * BK;
+      const bf16* B = Bs + stage * BN * BK;
+      // first 32-deep half: read and multiply; second half: read, then free the slot (every
+      // wave's reads retired + barrier) and issue tile kt + 2 before its MFMAs -- only one
+      // half's fragments are live across the issue (register budget of the 256x256 tile)
 #pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (kt0 + s < kt1) issue(kt0 + s, s);
-
-  int stage = 0;
-  for (int kt = kt0; kt < kt1; ++kt) {
-    // retire tile kt (this wave's share), then the barrier makes every wave's share visible
-    if (kt + STAGES - 2 < kt1) wait_vmcnt<LOADS * (STAGES - 2)>();
-    else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (kt + STAGES - 1 < kt1) {
-      int ns = stage + STAGES - 1;
-      if (ns >= STAGES) ns -= STAGES;
-      issue(kt + STAGES - 1, ns);
-    }
-    if constexpr (F8 != 0) {
-      const T* A = As + stage * BM * BKE;
-      const T* B = Bs + stage * BN * BKE;
-      // this lane's 32-deep k block comes from one source tensor (host: C1 % 32 == 0):
-      // its E8M0 dequant exponent is the MFMA's scale_a
-      int sa = ex1;
-      if (C2 > 0) {
-        const int k = FASTK ? kt * BKE : kt * BKE + 32 * (lane >> 4);
-        const int tap = (int)fdiv((uint32_t)k, fd_c);
-        sa = (k - tap * C) < C1 ? ex1 : ex2;
-      }
-      // operand layout of the 16x16x128 f8 MFMA: lane group q = lane>>4 holds K [16q, 16q+16)
-      // in its low 16 bytes and K [64+16q, 64+16q+16) in its high 16 bytes (LDS chunks q and
-      // q+4), and its scale operand covers K block [32q, 32q+32) -- probes/mfma_fp8_scale.hip
-      const int c0 = lane >> 4;
-      i32x8 af[TM], bfr[TN];
+      for (int kk = 0; kk < 2; ++kk) {
+        const int chunk = kk * 4 + (lane >> 4);
+        bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * TM * 16 + i * 16 + (lane & 15);
-        u32x4 lo = *reinterpret_cast<const u32x4*>(A + 2 * swz(row, c0));
-        u32x4 hi = *reinterpret_cast<const u32x4*>(A + 2 * swz(row, c0 + 4));
-        if constexpr (RELU) {
-          lo = relu_fp8x16(lo);
-          hi = relu_fp8x16(hi);
+        for (int j = 0; j < TN; ++j) {
+          const int row = wn * TN * 16 + j * 16 + (lane & 15);
+          bfr[j] = *reinterpret_cast<const bf16x8*>(B + swz(row, chunk));
         }
-        af[i] = cat8(lo, hi);
-      }
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * TN * 16 + j * 16 + (lane & 15);
-        bfr[j] = cat8(*reinterpret_cast<const u32x4*>(B + 2 * swz(row, c0)),
-                      *reinterpret_cast<const u32x4*>(B + 2 * swz(row, c0 + 4)));
-      }
+        for (int i = 0; i < TM; ++i) {
+          const int row = wm * TM * 16 + i * 16 + (lane & 15);
+          af[i] = *reinterpret_cast<const bf16x8*>(A + swz(row, chunk));
+        }
+        if (kk == 1) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();         // every wave holds its fragments: slot free
+          __builtin_amdgcn_sched_barrier(0);
+          if (kt + 2 < kt1) issue(kt + 2, stage);
+        }
+        if constexpr (RELU) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], F8 - 1, 0, 0, sa,
-                                                                       0, ew);
-    } else {
-    const bf16* A = As + stage * BM * BK;
-    const bf16* B = Bs + stage * BN * BK;
-    // fragments of both 32-deep halves are read up front (double-buffered registers) so
-    // the second half's LDS latency hides behind the first half's MFMAs; per half the B
-    // fragments come first (every MFMA row needs all of them)
-    bf16x8 af[2][TM], bfr[2][TN];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + (lane >> 4);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * TN * 16 + j * 16 + (lane & 15);
-        bfr[kk][j] = *reinterpret_cast<const bf16x8*>(B + swz(row, chunk));
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * TM * 16 + i * 16 + (lane & 15);
-        af[kk][i] = *reinterpret_cast<const bf16x8*>(A + swz(row, chunk));
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      if constexpr (RELU) {
+          for (int i = 0; i < TM; ++i)
+            af[i] = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, af[i])));
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
-          af[kk][i] = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, af[kk][i])));
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+      stage ^= 1;
     }
+  } else {
+    // prologue: STAGES-1 tiles in flight
+  #pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s)
+      if (kt0 + s < kt1) issue(kt0 + s, s);
+
+    int stage = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      // retire tile kt (this wave's share), then the barrier makes every wave's share visible
+      if (kt + STAGES - 2 < kt1) wait_vmcnt<LOADS * (STAGES - 2)>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + STAGES - 1 < kt1) {
+        int ns = stage + STAGES - 1;
+        if (ns >= STAGES) ns -= STAGES;
+        issue(kt + STAGES - 1, ns);
+      }
+      if constexpr (F8 != 0) {
+        const T* A = As + stage * BM * BKE;
+        const T* B = Bs + stage * BN * BKE;
+        // this lane's 32-deep k block comes from one source tensor (host: C1 % 32 == 0):
+        // its E8M0 dequant exponent is the MFMA's scale_a
+        int sa = ex1;
+        if (C2 > 0) {
+          const int k = FASTK ? kt * BKE : kt * BKE + 32 * (lane >> 4);
+          const int tap = (int)fdiv((uint32_t)k, fd_c);
+          sa = (k - tap * C) < C1 ? ex1 : ex2;
+        }
+        // operand layout of the 16x16x128 f8 MFMA: lane group q = lane>>4 holds K [16q, 16q+16)
+        // in its low 16 bytes and K [64+16q, 64+16q+16) in its high 16 bytes (LDS chunks q and
+        // q+4), and its scale operand covers K block [32q, 32q+32) -- probes/mfma_fp8_scale.hip
+        const int c0 = lane >> 4;
+        i32x8 af[TM], bfr[TN];
+  #pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = wm * TM * 16 + i * 16 + (lane & 15);
+          u32x4 lo = *reinterpret_cast<const u32x4*>(A + 2 * swz(row, c0));
+          u32x4 hi = *reinterpret_cast<const u32x4*>(A + 2 * swz(row, c0 + 4));
+          if constexpr (RELU) {
+            lo = relu_fp8x16(lo);
+            hi = relu_fp8x16(hi);
+          }
+          af[i] = cat8(lo, hi);
+        }
+  #pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int row = wn * TN * 16 + j * 16 + (lane & 15);
+          bfr[j] = cat8(*reinterpret_cast<const u32x4*>(B + 2 * swz(row, c0)),
+                        *reinterpret_cast<const u32x4*>(B + 2 * swz(row, c0 + 4)));
+        }
+  #pragma unroll
+        for (int i = 0; i < TM; ++i)
+  #pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], F8 - 1, 0, 0, sa,
+                                                                         0, ew);
+      } else {
+      const bf16* A = As + stage * BM * BK;
+      const bf16* B = Bs + stage * BN * BK;
+      // fragments of both 32-deep halves are read up front (double-buffered registers) so
+      // the second half's LDS latency hides behind the first half's MFMAs; per half the B
+      // fragments come first (every MFMA row needs all of them)
+      bf16x8 af[2][TM], bfr[2][TN];
+  #pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int chunk = kk * 4 + (lane >> 4);
+  #pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int row = wn * TN * 16 + j * 16 + (lane & 15);
+          bfr[kk][j] = *reinterpret_cast<const bf16x8*>(B + swz(row, chunk));
+        }
+  #pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = wm * TM * 16 + i * 16 + (lane & 15);
+          af[kk][i] = *reinterpret_cast<const bf16x8*>(A + swz(row, chunk));
+        }
+      }
+  #pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if constexpr (RELU) {
+  #pragma unroll
+          for (int i = 0; i < TM; ++i)
+            af[kk][i] = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, af[kk][i])));
+        }
+  #pragma unroll
+        for (int i = 0; i < TM; ++i)
+  #pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+      }
+      }
+      stage = stage + 1 == STAGES ? 0 : stage + 1;
     }
-    stage = stage + 1 == STAGES ? 0 : stage + 1;
   }
   __syncthreads();  // every wave done with the ring before the epilogue reuses the LDS
   conv_epilogue<BM, BN, WM, WN, MODE, NT>(a, g, acc, m0, n0, smem, fd_hwq, fd_wq);
@@ -401,6 +459,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
 
 template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU, int F8, bool PK8 = false>
 static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
+  if (BM * BN > 256 * 128 && a.splits > 1) return -2;   // no split-K epilogue in big tiles
   constexpr int pipe = STAGES * (BM + BN) * BK * 2;
   constexpr int epi = BM * (BN + 8) * 2 + 2 * (WM * WN * 64) * 4;  // + stats scratch
   constexpr int smem = pipe > epi ? pipe : epi;
