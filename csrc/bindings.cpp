@@ -135,6 +135,11 @@ int conv_variant(int64_t Cout, int64_t kmax, int64_t tiles256 = 0) {
   if (v && v[0] == 'g' && v[1] >= '2' && v[1] <= '4') return v[1] - '0';
   if (v && v[0] == 'g' && v[1] == '5') return big ? 5 : v4;
   if (v && v[0] == 'g' && v[1] == '6') return (Cout <= 64 && kmax > 256) ? 6 : ((big && tiles256 >= 256) ? 5 : v4);
+  if (v && v[0] == 'g' && v[1] == '8') {   // g8: 256x64 for N <= 64; g89: also 256x128 for N <= 128
+    if (Cout <= 64 && kmax > 256) return 8;
+    if (v[2] == '9' && Cout <= 128 && kmax > 256) return 9;
+  }
+  if (v && v[0] == 'g' && v[1] == '9' && Cout > 64 && Cout <= 128 && kmax > 256) return 9;
   return (big && tiles256 >= 256) ? 5 : v4;
 }
 
@@ -322,7 +327,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   int bm, bn;
   if (glds_ok) {
     bn = variant == 5 ? 256 : (Cout > 64 ? 128 : 64);
-    bm = (variant == 4 || variant == 5 || variant == 6) ? 256 : 128;
+    bm = (variant == 4 || variant == 5 || variant == 6 || variant == 8 || variant == 9) ? 256 : 128;
   } else if (Cout <= 16) {
     bn = 16;
     bm = mmax >= 4096 ? 256 : 64;

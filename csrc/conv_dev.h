@@ -100,7 +100,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
   // ---- split-K: fp32 atomics straight from the accumulators (tiny-M layers only).  Not
   // compiled into the big tiles (the host never splits them): its out_pix division loop
   // is not unrolled there, which made the compiler keep the accumulators in scratch.
-  if constexpr (BM * BN <= 256 * 128) if (a.splits > 1) {
+  if constexpr (TM * TN <= 16) if (a.splits > 1) {
     float* wsb = a.det ? a.ws + (long)(blockIdx.z % a.splits) * a.N * a.OH * a.OW * a.Cout : a.ws;
 #pragma unroll
     for (int i = 0; i < TM; ++i)

@@ -459,7 +459,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
 
 template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU, int F8, bool PK8 = false>
 static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
-  if (BM * BN > 256 * 128 && a.splits > 1) return -2;   // no split-K epilogue in big tiles
+  if ((BM / WM / 16) * (BN / WN / 16) > 16 && a.splits > 1) return -2;   // no split-K epilogue in big wave tiles
   constexpr int pipe = STAGES * (BM + BN) * BK * 2;
   constexpr int epi = BM * (BN + 8) * 2 + 2 * (WM * WN * 64) * 4;  // + stats scratch
   constexpr int smem = pipe > epi ? pipe : epi;
@@ -519,6 +519,11 @@ static int dispatch_glds2(const ConvFwdArgs& a, int variant, hipStream_t st) {
     }
     return -2;
   }
+  // 8 = 256x64 on 2 waves of 128x64, 9 = 256x128 on 4 waves of 128x64: the 256x256 tile's
+  // per-wave operand reuse (384 B of LDS fragments per MFMA) for N = 64 / 128 layers
+  if (variant == 8 && a.Cout <= 64) return launch_glds<256, 64, 2, 1, MODE, 2, FASTK, RELU, F8>(a, st);
+  if (variant == 9 && a.Cout > 64 && a.Cout <= 128)
+    return launch_glds<256, 128, 2, 2, MODE, 2, FASTK, RELU, F8>(a, st);
   if (a.Cout > 64) {
     if (variant == 5) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU, F8>(a, st);
     if (variant == 2) return launch_glds<128, 128, 2, 2, MODE, 2, FASTK, RELU, F8>(a, st);
