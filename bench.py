@@ -61,7 +61,7 @@ def parse():
                    help="attach the reducers and issue the RCCL collectives even on one GPU")
     p.add_argument("--no_graph", action="store_true", help="(native) disable hipGraph capture")
     p.add_argument("--graph", action="store_true",
-                   help="(native) force hipGraph capture also for N>1 (default: N == 1 only)")
+                   help="(native) hipGraph capture (the default for every N; kept for compatibility)")
     p.add_argument("--precision", default=os.environ.get("P2P_PRECISION", "bf16"), choices=["bf16", "fp8"],
                    help="(native) conv GEMM operands: bf16, or fp8 (e4m3 fwd / e5m2 dgrad, bf16 wgrad; "
                         "BASELINE config 5)")
@@ -160,12 +160,23 @@ def main():
                 out = gen_net(netC(a) if ref else a)
             return {"out_mean": out.float().mean()}
     step = step_fn
-    use_graph = (args.impl == "native" and dev.type == "cuda" and not args.no_graph
-                 and (world == 1 or args.graph))
+    # one hipGraph per rank, RCCL bucket all-reduces captured inside it (graph-safe reducer,
+    # tests/test_graph_gpu.py); ranks agree on graph vs eager so collectives always match
+    use_graph = args.impl == "native" and dev.type == "cuda" and not args.no_graph
     if use_graph:
         from p2p_pytorch_amd.engine.graph import CapturedStep
-        # capture runs its own warmup steps on a side stream, then records one step
-        step = CapturedStep(step_fn, real_A, real_B, warmup=2)
+        ok = 1.0
+        try:
+            # capture runs its own warmup steps on a side stream, then records one step
+            step = CapturedStep(step_fn, real_A, real_B, warmup=2)
+        except Exception as e:  # noqa: BLE001 - any capture failure: eager on every rank
+            print(f"[bench] rank {rank}: graph capture failed ({type(e).__name__}: {e}); eager",
+                  file=sys.stderr, flush=True)
+            ok = 0.0
+        if world > 1:
+            ok = pdist.min_scalar(ok, dev)
+        if ok < 1.0:
+            step, use_graph = step_fn, False
     t_w = time.perf_counter()
     for i in range(args.warmup):
         losses = step(real_A, real_B)

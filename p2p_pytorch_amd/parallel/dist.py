@@ -110,6 +110,14 @@ def max_scalar(x: float, device) -> float:
     return float(t.item())
 
 
+def min_scalar(x: float, device) -> float:
+    if not is_dist():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return float(t.item())
+
+
 def all_reduce_mean_(tensors):
     """In-place mean of a list of (device) scalars/tensors across ranks -- used for logged
     loss scalars and eval metrics every N steps (not every step)."""

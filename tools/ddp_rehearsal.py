@@ -9,7 +9,12 @@ the host.  What it checks on the real HIP kernels:
   * a full ``Pix2PixStep`` with per-network ``GradReducer`` s (small buckets -> several in
     flight, hooks firing during backward) leaves every rank with bitwise identical G and D
     parameters after Adam;
-  * the reduced G gradient equals the mean of the per-shard single-process gradients.
+  * the reduced G gradient equals the mean of the per-shard single-process gradients;
+  * the reference-family step (CompressGANStep: C + ExpandNetwork G + 3-scale SN PatchGAN
+    D + VGG19 loss) with reducers on G and D: every D bucket is all-reduced exactly once per
+    step (the G-loss backward, whose D gradients the reference discards, launches none), the
+    reduced D gradient equals the mean of the ranks' local ones, and G / D / C stay bitwise
+    identical across ranks over 3 steps (/root/reference/train.py:384-390).
 
 Exit status 0 = pass; rank 0 prints one JSON line.  (The production path is RCCL over xGMI
 with one GPU per rank; the driver's 8-GPU bench exercises that.)
@@ -53,6 +58,56 @@ def g_grads(G, D, a, b):
     loss = crit(D((a, fake)), True) + 100 * l1(fake, b)
     loss.backward()
     return loss
+
+
+def family_r_phase(world, rank, dev, steps=3):
+    """Reference-family step with reducers on the GPU kernels (see module docstring)."""
+    from p2p_pytorch_amd.engine.compress_gan import CompressGANStep
+    from p2p_pytorch_amd.models import VGGLoss, define_C, define_D, define_G
+    from p2p_pytorch_amd.parallel import GradReducer
+    from p2p_pytorch_amd.parallel import dist as pdist
+    torch.manual_seed(300 + rank)
+    G = define_G(gpu_id=dev, verbose=False)
+    D = define_D(6, 32, gpu_id=dev, verbose=False)
+    C = define_C(gpu_id=dev, verbose=False)
+    for m in (G, D, C):
+        pdist.broadcast_module(m)
+    torch.manual_seed(7)
+    vgg = VGGLoss().to(dev)
+    red_g, red_d = GradReducer(G, bucket_mb=1.0), GradReducer(D, bucket_mb=0.25)
+    launches, local = [], {}
+    orig = red_d._launch
+
+    def spy(b):
+        launches.append(b.index)
+        local[b.index] = b.flat.detach().clone()
+        orig(b)
+
+    red_d._launch = spy
+    step = CompressGANStep(G, D, C, vgg=vgg, reducer_g=red_g, reducer_d=red_d)
+    g = torch.Generator(device=dev).manual_seed(321)
+    cl = torch.channels_last
+    worst, once, same = 0.0, True, True
+    for _ in range(steps):
+        A = (torch.rand(world, 3, 64, 64, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+        B = (torch.rand(world, 3, 64, 64, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+        launches.clear()
+        local.clear()
+        step.step(A[rank:rank + 1].contiguous(memory_format=cl), B[rank:rank + 1].contiguous(memory_format=cl))
+        torch.cuda.synchronize()
+        once = once and sorted(launches) == list(range(len(red_d.buckets)))
+        for bk in red_d.buckets:
+            gl = [torch.zeros_like(local[bk.index]) for _ in range(world)]
+            dist.all_gather(gl, local[bk.index])
+            mean = torch.stack(gl).float().mean(0)
+            worst = max(worst, float((bk.flat.float() - mean).abs().max() / mean.abs().max().clamp_min(1e-12)))
+        for m in (G, D, C):
+            f = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+            gg = [torch.zeros_like(f) for _ in range(world)]
+            dist.all_gather(gg, f)
+            same = same and all(torch.equal(gg[0], t) for t in gg)
+    return {"d_buckets_once_per_step": once, "d_grad_rel_err_vs_rank_mean": worst,
+            "params_identical": same, "ok": bool(once and same and worst < 1e-5)}
 
 
 def main():
@@ -126,12 +181,13 @@ def main():
     dist.all_gather(gathered, flat)
     same = all(torch.equal(gathered[0], t) for t in gathered)
     finite = all(torch.isfinite(v).all().item() for v in losses.values())
-    ok = same and finite and worst < 1e-4 and timed
+    fam_r = family_r_phase(world, rank, dev)
+    ok = same and finite and worst < 1e-4 and timed and fam_r["ok"]
     if rank == 0:
         print(json.dumps({"world": world, "backend": dist.get_backend(), "grad_rel_err_vs_shard_mean": worst,
                           "worst_params": errs[:4],
                           "params_identical": same, "losses_finite": finite, "comm": comm,
-                          "phase_ms": phases, "ok": ok}), flush=True)
+                          "phase_ms": phases, "family_r": fam_r, "ok": ok}), flush=True)
     pdist.destroy()
     sys.exit(0 if ok else 1)
 

@@ -270,7 +270,7 @@ def main(argv=None):
         for iteration, batch in enumerate(batches, 1):
             real_a = batch[0].to(device, act_dtype).contiguous(memory_format=torch.channels_last)
             real_b = batch[1].to(device, act_dtype).contiguous(memory_format=torch.channels_last)
-            if opt.graph and use_cuda and world == 1 and step_fn is trainer.step:
+            if opt.graph and use_cuda and step_fn is trainer.step:
                 from p2p_pytorch_amd.engine.graph import CapturedStep
                 step_fn = CapturedStep(trainer.step, real_a, real_b)
             losses = step_fn(real_a, real_b)
