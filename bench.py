@@ -162,7 +162,12 @@ def main():
     step = step_fn
     # one hipGraph per rank, RCCL bucket all-reduces captured inside it (graph-safe reducer,
     # tests/test_graph_gpu.py); ranks agree on graph vs eager so collectives always match
-    use_graph = args.impl == "native" and dev.type == "cuda" and not args.no_graph
+    # (gloo -- the one-GPU multi-rank rehearsal backend -- stages through the host and
+    # cannot be captured; a failed capture leaves the process in capture mode, so only
+    # RCCL process groups are captured)
+    use_graph = (args.impl == "native" and dev.type == "cuda" and not args.no_graph
+                 and (world == 1 or (pdist.backend() == "nccl"
+                                     and os.environ.get("P2P_GRAPH_MULTI", "1") != "0")))
     if use_graph:
         from p2p_pytorch_amd.engine.graph import CapturedStep
         ok = 1.0

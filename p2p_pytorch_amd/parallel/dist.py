@@ -70,6 +70,10 @@ def world_size() -> int:
     return dist.get_world_size() if is_dist() else 1
 
 
+def backend() -> str | None:
+    return dist.get_backend() if (dist.is_available() and dist.is_initialized()) else None
+
+
 def rank() -> int:
     return dist.get_rank() if is_dist() else 0
 

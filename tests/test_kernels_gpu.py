@@ -413,7 +413,8 @@ def test_unet_patchgan_step_matches_oracle():
         assert torch.isfinite(gh[n]).all(), n
         eh, ee = rel_err(gh[n], g32[n]), rel_err(g16[n], g32[n])
         rows.append((n, eh, ee))
-        if eh > 1.5 * ee + 0.03:
+        # measured worst (eh - 1.5 ee) = -0.002 over the 24 tensors (gpurun_out/bounds.jsonl)
+        if eh > 1.5 * ee + 0.01:
             worse.append((n, eh, ee))
     _record("unet_patchgan_grads", rows)
     assert not worse, worse
@@ -633,7 +634,8 @@ def test_family_r_networks_match_oracle():
         assert torch.isfinite(gh[n]).all(), n
         eh, ee = rel_err(gh[n], g32[n]), rel_err(g16[n], g32[n])
         rows.append((n, eh, ee, (gh[n] - g32[n]).abs().max().item() / gscale))
-        if eh > 2.0 * ee + 0.1 and (gh[n] - g32[n]).abs().max().item() > 1e-3 * gscale:
+        # measured worst (eh - 1.5 ee) = -0.004 over the 97 tensors (gpurun_out/bounds.jsonl)
+        if eh > 1.5 * ee + 0.02 and (gh[n] - g32[n]).abs().max().item() > 1e-3 * gscale:
             worse.append((n, eh, ee))
     _record("family_r_grads", rows)
     assert not worse, worse
