@@ -36,9 +36,9 @@ int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const
                    const float* gamma, const float* beta, const float* prelu_w, int act, void* y,
                    hipStream_t st);
 int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const float* mean,
-                 const float* rstd, const float* gamma, const float* beta, int act, float* dgamma,
-                 float* dbeta, float* ws, void* dx, float* dsum, void* q, int* qsite, int qfmt,
-                 hipStream_t st);
+                 const float* rstd, const float* gamma, const float* beta, int act,
+                 const float* prelu_w, float* dprelu, float* dgamma, float* dbeta, float* ws, void* dx,
+                 float* dsum, void* q, int* qsite, int qfmt, hipStream_t st);
 int p2p_act(const void* a, const void* b, long n, int act, int mode, void* out, hipStream_t st);
 int p2p_dropout(const void* x, long n, float p, const int64_t* seed, unsigned salt, void* y,
                 hipStream_t st);
@@ -54,7 +54,8 @@ int p2p_image_metrics(const void* a, const void* b, int dtype, const long* strid
                       int shift, double data_range, double* ws, hipStream_t st);
 int p2p_avgpool3s2(const void* x, int N, int H, int W, int C, int OH, int OW, void* y, int bwd, hipStream_t st);
 int p2p_maxpool2(const void* x, const void* gy, int N, int H, int W, int C, void* out, hipStream_t st);
-int p2p_l2norm(const void* x, const void* gy, long P, int C, float eps, void* out, hipStream_t st);
+int p2p_l2norm(const void* x, const void* gy, long P, int C, float eps, const void* res, void* out,
+               hipStream_t st);
 int p2p_pixel_shuffle(const void* in, int N, int OH, int OW, int OC, int r, int dir, void* out,
                       hipStream_t st);
 int p2p_weight_prep_pairs(int count, const float* const* w, void* const* out0, void* const* out1,
@@ -416,6 +417,40 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
       const int per_cu = Cout == 128 ? 1 : 2;   // halo_pk8.hip launch bounds
       rc = p2p_halo_pk8(&h, std::max(1, std::min(h.ntiles, per_cu * cus)), st);
+    }
+  }
+  // stride-1 9x9 convs with 8-32 input channels and <= 32 outputs (family R's full-res
+  // layers): the halo-tile direct conv (csrc/halo_kxk.hip); MODE 1 stride 1 = flipped taps
+  if (rc == -2 && !fp8 && C2 == 0 && KH == 9 && KW == 9 && stride == 1 && (C1 == 8 || C1 == 16 || C1 == 32) &&
+      Cout <= 32 && Csplit == Cout && act_in == 0 && act_bwd == 0 && !a.res1 && !a.q_out && !a.stats &&
+      (mode == 0 || (up == 1 && !reflect && pad <= 8)) && std::getenv("P2P_NO_HALO") == nullptr) {
+    p2p::HaloKArgs h{};
+    h.x = static_cast<const __bf16*>(x1.data_ptr());
+    h.C = (int)C1;
+    h.N = (int)N;
+    h.H = (int)H;
+    h.W = (int)W;
+    h.up = (int)up;
+    h.pad = mode == 0 ? (int)pad : (int)(KH - 1 - pad);
+    h.reflect = (int)reflect;
+    h.flip = mode == 1 ? 1 : 0;
+    h.OH = (int)OH;
+    h.OW = (int)OW;
+    h.w = static_cast<const __bf16*>(w.data_ptr());
+    h.bias = a.bias;
+    h.Cout = (int)Cout;
+    h.act_out = (int)act_out;
+    h.y = static_cast<__bf16*>(a.y1);
+    h.zero = static_cast<const __bf16*>(a.zero);
+    h.tiles_x = (int)((OW + 15) / 16);
+    h.tiles_y = (int)((OH + 15) / 16);
+    h.ntiles = (int)N * h.tiles_x * h.tiles_y;
+    if (OH == H * up + 2 * h.pad - KH + 1 && OW == W * up + 2 * h.pad - KW + 1) {
+      int dev = 0, cus = 256;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      rc = p2p_halo_kxk(&h, 9, std::max(1, std::min(h.ntiles, cus)), st);
+      if (rc == 0) splits = 1;   // no split-K partials to finalize: the halo kernel wrote y
     }
   }
   if (rc == -2 && glds_ok) rc = p2p_conv_fwd_glds(&a, (int)mode, variant, st);
@@ -856,8 +891,15 @@ Tensor norm_bwd(const Tensor& x, const Tensor& dy, const Tensor& mean, const Ten
                 const optional<Tensor>& gamma, const optional<Tensor>& beta, int64_t act,
                 const optional<Tensor>& dgamma, const optional<Tensor>& dbeta, bool need_dx,
                 bool batch, const optional<Tensor>& dsum, const optional<Tensor>& qsite,
-                const optional<Tensor>& q_out, int64_t qfmt) {
+                const optional<Tensor>& q_out, int64_t qfmt, const optional<Tensor>& prelu_w,
+                const optional<Tensor>& dprelu) {
   check_act(x, "norm_bwd x");
+  if (prelu_w)
+    TORCH_CHECK(prelu_w->numel() == 1 && prelu_w->scalar_type() == at::kFloat && prelu_w->is_cuda(),
+                "norm_bwd: prelu_w must be a 1-element fp32 GPU tensor");
+  if (dprelu)
+    TORCH_CHECK(prelu_w && dprelu->numel() == 1 && dprelu->scalar_type() == at::kFloat,
+                "norm_bwd: dprelu needs prelu_w and a 1-element fp32 tensor");
   check_act(dy, "norm_bwd dy");
   void* qp = nullptr;
   int* qs = nullptr;
@@ -879,6 +921,8 @@ Tensor norm_bwd(const Tensor& x, const Tensor& dy, const Tensor& mean, const Ten
   check_rc(p2p_norm_bwd(x.data_ptr(), dy.data_ptr(), gN, gHW, (int)C, mean.data_ptr<float>(),
                         rstd.data_ptr<float>(), gamma ? gamma->data_ptr<float>() : nullptr,
                         beta ? beta->data_ptr<float>() : nullptr, (int)act,
+                        prelu_w ? prelu_w->data_ptr<float>() : nullptr,
+                        dprelu ? dprelu->data_ptr<float>() : nullptr,
                         dgamma ? dgamma->data_ptr<float>() : nullptr,
                         dbeta ? dbeta->data_ptr<float>() : nullptr, ws.data_ptr<float>(),
                         need_dx ? dx.data_ptr() : nullptr,
@@ -1025,13 +1069,17 @@ Tensor maxpool2(const Tensor& x, const optional<Tensor>& gy) {
   return out;
 }
 
-Tensor l2norm(const Tensor& x, const optional<Tensor>& gy, double eps) {
+Tensor l2norm(const Tensor& x, const optional<Tensor>& gy, double eps, const optional<Tensor>& res) {
   check_nhwc(x, "l2norm");
   if (gy) check_nhwc(*gy, "l2norm gy");
+  if (res) {
+    check_nhwc(*res, "l2norm res");
+    TORCH_CHECK(res->sizes() == x.sizes() && !gy, "l2norm: res must match x (forward only)");
+  }
   Tensor out = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   const int64_t C = x.size(1);
   check_rc(p2p_l2norm(x.data_ptr(), gy ? gy->data_ptr() : nullptr, x.numel() / C, (int)C, (float)eps,
-                      out.data_ptr(), cur_stream(x)),
+                      res ? res->data_ptr() : nullptr, out.data_ptr(), cur_stream(x)),
            "l2norm");
   return out;
 }
@@ -1338,7 +1386,7 @@ TORCH_LIBRARY(p2p, m) {
   m.def("image_metrics(Tensor a, Tensor b, bool shift, float data_range) -> Tensor");
   m.def("avgpool3s2(Tensor x, int bwd, int H, int W) -> Tensor");
   m.def("maxpool2(Tensor x, Tensor? gy) -> Tensor");
-  m.def("l2norm(Tensor x, Tensor? gy, float eps) -> Tensor");
+  m.def("l2norm(Tensor x, Tensor? gy, float eps, Tensor? res=None) -> Tensor");
   m.def("pixel_shuffle(Tensor x, int r, int dir) -> Tensor");
   m.def("pad_fold(Tensor dxp, int H, int W, int pad, int up, int reflect, Tensor? xb, int act) -> Tensor");
   m.def("weight_prep_pairs(Tensor[] w, int[] xa, int[] xb, Tensor(a!)? sites=None, int[]? site_idx=None) -> Tensor[]");
@@ -1350,7 +1398,8 @@ TORCH_LIBRARY(p2p, m) {
         "int act, bool batch) -> Tensor");
   m.def("norm_bwd(Tensor x, Tensor dy, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, int act, "
         "Tensor(a!)? dgamma, Tensor(b!)? dbeta, bool need_dx, bool batch, Tensor(c!)? dsum, "
-        "Tensor(d!)? qsite=None, Tensor(e!)? q_out=None, int qfmt=0) -> Tensor");
+        "Tensor(d!)? qsite=None, Tensor(e!)? q_out=None, int qfmt=0, Tensor? prelu_w=None, "
+        "Tensor(f!)? dprelu=None) -> Tensor");
   m.def("act(Tensor a, Tensor? b, int act, int mode) -> Tensor");
   m.def("dropout(Tensor x, float p, Tensor seed, int salt) -> Tensor");
   m.def("pad_channels(Tensor a, Tensor? b, int Co) -> Tensor");

@@ -129,9 +129,25 @@ struct HaloPk8Args {
   int tiles_x, tiles_y, ntiles;
 };
 
+// Halo-tile direct conv for stride-1 KxK convs with few channels (csrc/halo_kxk.hip): input
+// C in {8, 16, 32}, Cout <= 32 (multiple of 8), reflect / zero pad, nearest upsample, and
+// flip = 1 for a stride-1 transposed conv (taps reversed; the host passes pad = K - 1 - p).
+struct HaloKArgs {
+  const __bf16* x;     // NHWC [N][H][W][C]
+  int C, N, H, W, up, pad, reflect, flip;
+  int OH, OW;
+  const __bf16* w;     // [Cout][K*K][C] weight image
+  const float* bias;   // [Cout] or null
+  int Cout, act_out;
+  __bf16* y;           // NHWC [N][OH][OW][Cout]
+  const __bf16* zero;
+  int tiles_x, tiles_y, ntiles;
+};
+
 }  // namespace p2p
 
 extern "C" {
+int p2p_halo_kxk(const p2p::HaloKArgs* a, int KS, int blocks, hipStream_t st);
 int p2p_halo_pk8(const p2p::HaloPk8Args* a, int blocks, hipStream_t st);
 int p2p_halo_union(const p2p::HaloArgs* a, int relu, int blocks, hipStream_t st);
 int p2p_conv_fwd(const p2p::ConvFwdArgs* a, int mode, int bm, int bn, hipStream_t stream);

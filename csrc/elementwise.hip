@@ -42,6 +42,7 @@ __global__ void __launch_bounds__(256) act_kernel(const bf16* __restrict__ a, co
     const float fa = (float)a[i];
     float r;
     if (mode == 0) r = act_fwd(fa, act);
+    else if (mode == 3) r = act_fwd(fa + (float)b[i], act);
     else if (mode == 1) r = fa * act_grad_from_input((float)b[i], act);
     else r = fa * act_grad_from_output((float)b[i], act);
     out[i] = (bf16)r;
@@ -53,6 +54,7 @@ __global__ void __launch_bounds__(256) act_kernel(const bf16* __restrict__ a, co
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       if (mode == 0) fa[j] = act_fwd(fa[j], act);
+      else if (mode == 3) fa[j] = act_fwd(fa[j] + fb[j], act);   // fused residual add
       else if (mode == 1) fa[j] = fa[j] * act_grad_from_input(fb[j], act);
       else fa[j] = fa[j] * act_grad_from_output(fb[j], act);
     }
@@ -321,6 +323,107 @@ __global__ void __launch_bounds__(256) loss_grad_kernel(const void* __restrict__
   }
 }
 
+// Vectorised loss kernels: 16-B loads (8 bf16 / 4 fp32 per thread per pass), kind and dtype
+// as template parameters (the scalar kernels above remain for misaligned views).  Element
+// partition per block is fixed by n -> deterministic partial sums.
+template <int F32>
+struct LossVec {
+  static constexpr int V = F32 ? 4 : 8;
+  __device__ static void load(const void* p, long v, float* f) {
+    if constexpr (F32) {
+      const float4 q = reinterpret_cast<const float4*>(p)[v];
+      f[0] = q.x; f[1] = q.y; f[2] = q.z; f[3] = q.w;
+    } else {
+      unpack8e(reinterpret_cast<const u32x4*>(p)[v], f);
+    }
+  }
+  __device__ static void store(void* p, long v, const float* f) {
+    if constexpr (F32) reinterpret_cast<float4*>(p)[v] = make_float4(f[0], f[1], f[2], f[3]);
+    else reinterpret_cast<u32x4*>(p)[v] = pack8e(f);
+  }
+};
+
+template <int F32, int KIND, bool HAS_B>
+__global__ void __launch_bounds__(256) loss_partial_vec_kernel(const void* __restrict__ a,
+                                                               const void* __restrict__ b, long n,
+                                                               float t, float* __restrict__ ws) {
+  using L = LossVec<F32>;
+  constexpr int V = L::V;
+  const long nv = n / V;
+  float s = 0.f;
+  for (long v = blockIdx.x * 256L + threadIdx.x; v < nv; v += (long)gridDim.x * 256) {
+    float fa[V], fb[V];
+    L::load(a, v, fa);
+    if constexpr (HAS_B) L::load(b, v, fb);
+#pragma unroll
+    for (int j = 0; j < V; ++j) s += loss_elem(KIND, fa[j], HAS_B ? fb[j] : 0.f, t);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < n - nv * V) {
+    const long e = nv * V + threadIdx.x;
+    s += loss_elem(KIND, ldval(a, e, F32), HAS_B ? ldval(b, e, F32) : 0.f, t);
+  }
+  __shared__ float red[4];
+  s = warp_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) ws[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+template <int F32, int KIND, bool HAS_B>
+__global__ void __launch_bounds__(256) loss_grad_vec_kernel(const void* __restrict__ a,
+                                                            const void* __restrict__ b, long n, float t,
+                                                            float scale, const float* __restrict__ gout,
+                                                            void* __restrict__ ga, void* __restrict__ gb) {
+  using L = LossVec<F32>;
+  constexpr int V = L::V;
+  const float g = gout[0] * scale;
+  const long nv = n / V;
+  for (long v = blockIdx.x * 256L + threadIdx.x; v < nv; v += (long)gridDim.x * 256) {
+    float fa[V], fb[V];
+    L::load(a, v, fa);
+    if constexpr (HAS_B) L::load(b, v, fb);
+#pragma unroll
+    for (int j = 0; j < V; ++j) fa[j] = g * loss_grad(KIND, fa[j], HAS_B ? fb[j] : 0.f, t);
+    if (ga) L::store(ga, v, fa);
+    if (gb) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) fa[j] = -fa[j];
+      L::store(gb, v, fa);
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < n - nv * V) {
+    const long e = nv * V + threadIdx.x;
+    const float v = g * loss_grad(KIND, ldval(a, e, F32), HAS_B ? ldval(b, e, F32) : 0.f, t);
+    if (ga) {
+      if (F32) static_cast<float*>(ga)[e] = v;
+      else static_cast<bf16*>(ga)[e] = (bf16)v;
+    }
+    if (gb) {
+      if (F32) static_cast<float*>(gb)[e] = -v;
+      else static_cast<bf16*>(gb)[e] = (bf16)(-v);
+    }
+  }
+}
+
+template <typename F>
+static void with_loss(int is_f32, int kind, bool has_b, F&& f) {
+  auto k2 = [&](auto f32) {
+    switch (kind) {
+      case 0: f(f32, std::integral_constant<int, 0>{}, std::false_type{}); break;
+      case 1: f(f32, std::integral_constant<int, 1>{}, std::false_type{}); break;
+      case 2: f(f32, std::integral_constant<int, 2>{}, std::false_type{}); break;
+      case 3: f(f32, std::integral_constant<int, 3>{}, std::true_type{}); break;
+      case 4: f(f32, std::integral_constant<int, 4>{}, std::true_type{}); break;
+      default: f(f32, std::integral_constant<int, 5>{}, std::false_type{}); break;
+    }
+  };
+  (void)has_b;
+  if (is_f32) k2(std::integral_constant<int, 1>{});
+  else k2(std::integral_constant<int, 0>{});
+}
+
+static inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 }  // namespace p2p
 
 extern "C" {
@@ -398,7 +501,15 @@ int p2p_loss_fwd(const void* a, const void* b, int is_f32, long n, int kind, flo
                  float* ws, float* out, hipStream_t st) {
   using namespace p2p;
   const int nb = p2p_loss_blocks(n);
-  hipLaunchKernelGGL(loss_partial_kernel, dim3(nb), dim3(256), 0, st, a, b, is_f32, n, kind, t, ws);
+  const bool pair = kind == 3 || kind == 4;
+  if (al16(a) && (!pair || (b && al16(b)))) {
+    with_loss(is_f32, kind, pair, [&](auto f32, auto k, auto hb) {
+      hipLaunchKernelGGL((loss_partial_vec_kernel<decltype(f32)::value, decltype(k)::value, decltype(hb)::value>),
+                         dim3(nb), dim3(256), 0, st, a, b, n, t, ws);
+    });
+  } else {
+    hipLaunchKernelGGL(loss_partial_kernel, dim3(nb), dim3(256), 0, st, a, b, is_f32, n, kind, t, ws);
+  }
   hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, ws, nb, scale, out);
   return (int)hipGetLastError();
 }
@@ -413,8 +524,17 @@ int p2p_sum_partials(const float* ws, int nb, float scale, float* out, hipStream
 int p2p_loss_bwd(const void* a, const void* b, int is_f32, long n, int kind, float t, float scale,
                  const float* gout, void* ga, void* gb, hipStream_t st) {
   using namespace p2p;
-  hipLaunchKernelGGL(loss_grad_kernel, dim3(egrid(n)), dim3(256), 0, st, a, b, is_f32, n, kind, t, scale,
-                     gout, ga, gb);
+  const bool pair = kind == 3 || kind == 4;
+  if (al16(a) && (!pair || (b && al16(b))) && (!ga || al16(ga)) && (!gb || al16(gb))) {
+    const long nv = n / (is_f32 ? 4 : 8);
+    with_loss(is_f32, kind, pair, [&](auto f32, auto k, auto hb) {
+      hipLaunchKernelGGL((loss_grad_vec_kernel<decltype(f32)::value, decltype(k)::value, decltype(hb)::value>),
+                         dim3(egrid(nv > 0 ? nv : 1)), dim3(256), 0, st, a, b, n, t, scale, gout, ga, gb);
+    });
+  } else {
+    hipLaunchKernelGGL(loss_grad_kernel, dim3(egrid(n)), dim3(256), 0, st, a, b, is_f32, n, kind, t, scale,
+                       gout, ga, gb);
+  }
   return (int)hipGetLastError();
 }
 

@@ -216,11 +216,82 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16* __restrict
   }
 }
 
+// 8-channel vector variants (C % 8 == 0, even H and W -- every VGG pool): one thread per
+// (output pixel, 8-channel chunk) reads its 2x2 window once (4 x 16-B loads); the backward
+// writes all four input-gradient vectors from that one read of x and gy.  Same tie rule as
+// max2x2_arg (first maximum in window order wins; NaN propagates).
+__device__ __forceinline__ void max2x2_vec(const bf16* x, long base, long rowst, int C, float* m,
+                                           int* arg) {
+  float f[4][8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bf16x8 v = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(
+                                                     x + base + (k >> 1) * rowst + (k & 1) * C));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[k][j] = (float)v[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m[j] = f[0][j];
+    arg[j] = 0;
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+      if (f[k][j] > m[j] || f[k][j] != f[k][j]) {
+        m[j] = f[k][j];
+        arg[j] = k;
+      }
+  }
+}
+
+__global__ void __launch_bounds__(256) maxpool_fwd_vec_kernel(const bf16* __restrict__ x, int N, int H, int W,
+                                                              int C, bf16* __restrict__ y) {
+  const int OH = H / 2, OW = W / 2, CG = C / 8;
+  const long n = (long)N * OH * OW * CG;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int cg = (int)(e % CG);
+    const long p = e / CG;
+    const int ow = (int)(p % OW);
+    const long bh = p / OW;   // b * OH + oh
+    float m[8];
+    int arg[8];
+    max2x2_vec(x, ((bh * 2) * W + 2 * ow) * C + cg * 8, (long)W * C, C, m, arg);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)m[j];
+    *reinterpret_cast<u32x4*>(y + p * C + cg * 8) = __builtin_bit_cast(u32x4, o);
+  }
+}
+
+__global__ void __launch_bounds__(256) maxpool_bwd_vec_kernel(const bf16* __restrict__ x,
+                                                              const bf16* __restrict__ gy, int N, int H,
+                                                              int W, int C, bf16* __restrict__ gx) {
+  const int OH = H / 2, OW = W / 2, CG = C / 8;
+  const long n = (long)N * OH * OW * CG;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int cg = (int)(e % CG);
+    const long p = e / CG;
+    const int ow = (int)(p % OW);
+    const long bh = p / OW;
+    const long base = ((bh * 2) * W + 2 * ow) * C + cg * 8;
+    float m[8];
+    int arg[8];
+    max2x2_vec(x, base, (long)W * C, C, m, arg);
+    const bf16x8 g = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(gy + p * C + cg * 8));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = arg[j] == k ? g[j] : (bf16)0.f;
+      *reinterpret_cast<u32x4*>(gx + base + (k >> 1) * (long)W * C + (k & 1) * C) = __builtin_bit_cast(u32x4, o);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ L2 normalise over channels
 // y = x / max(||x||, eps);  dx = (dy - y * <dy, y>) / max(||x||, eps)  (norm > eps),
 // dx = dy / eps otherwise (F.normalize's clamp_min has zero gradient below eps)
 __global__ void __launch_bounds__(256) l2norm_fwd_kernel(const bf16* __restrict__ x, long P, int C, float eps,
-                                                         bf16* __restrict__ y) {
+                                                         const bf16* __restrict__ res, bf16* __restrict__ y) {
   for (long p = blockIdx.x * 256L + threadIdx.x; p < P; p += (long)gridDim.x * 256) {
     float s = 0.f;
     for (int c = 0; c < C; ++c) {
@@ -228,7 +299,9 @@ __global__ void __launch_bounds__(256) l2norm_fwd_kernel(const bf16* __restrict_
       s += v * v;
     }
     const float inv = 1.f / fmaxf(sqrtf(s), eps);
-    for (int c = 0; c < C; ++c) y[p * C + c] = (bf16)((float)x[p * C + c] * inv);
+    // res: the CompressionNetwork's residual input added in the same pass (networks.py:236)
+    for (int c = 0; c < C; ++c)
+      y[p * C + c] = (bf16)((float)x[p * C + c] * inv + (res ? (float)res[p * C + c] : 0.f));
   }
 }
 
@@ -340,6 +413,17 @@ int p2p_avgpool3s2(const void* x, int N, int H, int W, int C, int OH, int OW, vo
 }
 
 int p2p_maxpool2(const void* x, const void* gy, int N, int H, int W, int C, void* out, hipStream_t st) {
+  if (C % 8 == 0 && H % 2 == 0 && W % 2 == 0) {
+    const long n = (long)N * (H / 2) * (W / 2) * (C / 8);
+    if (!gy)
+      hipLaunchKernelGGL(p2p::maxpool_fwd_vec_kernel, dim3(p2p::mgrid(n)), dim3(256), 0, st,
+                         static_cast<const p2p::bf16*>(x), N, H, W, C, static_cast<p2p::bf16*>(out));
+    else
+      hipLaunchKernelGGL(p2p::maxpool_bwd_vec_kernel, dim3(p2p::mgrid(n)), dim3(256), 0, st,
+                         static_cast<const p2p::bf16*>(x), static_cast<const p2p::bf16*>(gy), N, H, W, C,
+                         static_cast<p2p::bf16*>(out));
+    return (int)hipGetLastError();
+  }
   if (!gy) {
     const long n = (long)N * (H / 2) * (W / 2) * C;
     hipLaunchKernelGGL(p2p::maxpool_fwd_kernel, dim3(p2p::mgrid(n)), dim3(256), 0, st,
@@ -353,10 +437,12 @@ int p2p_maxpool2(const void* x, const void* gy, int N, int H, int W, int C, void
   return (int)hipGetLastError();
 }
 
-int p2p_l2norm(const void* x, const void* gy, long P, int C, float eps, void* out, hipStream_t st) {
+int p2p_l2norm(const void* x, const void* gy, long P, int C, float eps, const void* res, void* out,
+               hipStream_t st) {
   if (!gy)
     hipLaunchKernelGGL(p2p::l2norm_fwd_kernel, dim3(p2p::mgrid(P)), dim3(256), 0, st,
-                       static_cast<const p2p::bf16*>(x), P, C, eps, static_cast<p2p::bf16*>(out));
+                       static_cast<const p2p::bf16*>(x), P, C, eps, static_cast<const p2p::bf16*>(res),
+                       static_cast<p2p::bf16*>(out));
   else
     hipLaunchKernelGGL(p2p::l2norm_bwd_kernel, dim3(p2p::mgrid(P)), dim3(256), 0, st,
                        static_cast<const p2p::bf16*>(x), static_cast<const p2p::bf16*>(gy), P, C, eps,

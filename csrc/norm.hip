@@ -13,7 +13,9 @@
 //      with the unbiased variance (PyTorch semantics).
 //   3. norm_apply     y = act((x - mean) * rstd * gamma + beta), 16-B loads/stores.
 // Backward (dx = rstd*g*(dy - mean(dy) - xhat*mean(dy*xhat)), dgamma/dbeta for affine)
-//   1. norm_bwd_partial : block partial sums of dy and dy*xhat (recomputed from x)
+//   1. norm_bwd_partial : block partial sums of dy and dy*xhat (recomputed from x) -- ONE
+//      pass serves dgamma/dbeta and dx (gamma is constant per channel, the finalize scales);
+//      a fused shared-slope PReLU also reduces its slope gradient here
 //   2. norm_bwd_finalize: per (n,c) coefficients; per-channel dgamma/dbeta (summed over n)
 //   3. norm_bwd_apply   : dx = A*dy + B + Cc*xhat
 #include "fp8_dev.h"
@@ -303,9 +305,10 @@ __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict_
 // LeakyReLU the backward recomputes z from x and the saved statistics, so the act' gate
 // (dy_eff = dy * act'(z)) costs no extra pass over memory.  Tanh / sigmoid (family-R
 // output layer only) go through the separate act kernel before this one.
-__device__ __forceinline__ float act_gate(float z, int act) {
+__device__ __forceinline__ float act_gate(float z, int act, float pw) {
   if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
   if (act == ACT_LRELU) return z > 0.f ? 1.f : LRELU_SLOPE;
+  if (act == ACT_PRELU_T) return z > 0.f ? 1.f : pw;
   return 1.f;
 }
 
@@ -343,13 +346,14 @@ __device__ __forceinline__ void block_rows_reduce(const float* s1, const float* 
   }
 }
 
-// ws: [N][nchunks][C] sum(dy_eff * gs), [N][nchunks][C] sum(dy_eff * gs * xhat);
-// gs = gamma (dx pass) or 1 (dgamma / dbeta pass: scale_gamma = 0)
+// ws: [N][nchunks][C] sum(dy_eff), [N][nchunks][C] sum(dy_eff * xhat); PReLU: pws[n][chunk]
+// = sum(dy * z * [z <= 0]) over the block (the slope gradient, deterministic block order)
 template <int ACT>
 __global__ void __launch_bounds__(256) norm_bwd_partial_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ dy, NormGeom g,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
-    const float* __restrict__ beta, int scale_gamma, float* __restrict__ ws) {
+    const float* __restrict__ beta, const float* __restrict__ prelu_w, float* __restrict__ ws,
+    float* __restrict__ pws) {
   const int n = blockIdx.y, cb = blockIdx.x;
   const int CP = g.C >> 3;
   const int RP = 256 / CP;
@@ -358,14 +362,15 @@ __global__ void __launch_bounds__(256) norm_bwd_partial_kernel(
   const int p0 = cb * g.chunk;
   const int p1 = min(g.HW, p0 + g.chunk);
   const long off = (long)n * g.HW * g.C + cg * 8;
-  float mu[8], rs[8], ga[8], be[8], gs[8], s1[8], s2[8];
+  float mu[8], rs[8], ga[8], be[8], s1[8], s2[8];
+  float s3 = 0.f;
+  const float pw = ACT == ACT_PRELU_T ? prelu_w[0] : 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     mu[j] = mean[(long)n * g.C + cg * 8 + j];
     rs[j] = rstd[(long)n * g.C + cg * 8 + j];
     ga[j] = gamma ? gamma[cg * 8 + j] : 1.f;
     be[j] = gamma ? beta[cg * 8 + j] : 0.f;
-    gs[j] = scale_gamma ? ga[j] : 1.f;
     s1[j] = s2[j] = 0.f;
   }
   if (tr < RP) {
@@ -376,7 +381,9 @@ __global__ void __launch_bounds__(256) norm_bwd_partial_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float xh = (fx[j] - mu[j]) * rs[j];
-        const float d = fd[j] * act_gate(xh * ga[j] + be[j], ACT) * gs[j];
+        const float z = xh * ga[j] + be[j];
+        if constexpr (ACT == ACT_PRELU_T) s3 += z <= 0.f ? fd[j] * z : 0.f;
+        const float d = fd[j] * act_gate(z, ACT, pw);
         s1[j] += d;
         s2[j] += d * xh;
       }
@@ -405,6 +412,15 @@ __global__ void __launch_bounds__(256) norm_bwd_partial_kernel(
     ws[o] = o1[c];
     ws[(long)g.N * g.nchunks * g.C + o] = o2[c];
   }
+  if constexpr (ACT == ACT_PRELU_T) {
+    // fixed-order block reduction of the slope partial: wave shuffles, then 4 wave sums
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s3 += __shfl_xor(s3, m);
+    __syncthreads();
+    if ((tid & 63) == 0) red1[tid >> 6] = s3;
+    __syncthreads();
+    if (tid == 0) pws[(long)n * g.nchunks + cb] = (red1[0] + red1[1]) + (red1[2] + red1[3]);
+  }
 }
 
 // coef: [N][C] A, [N][C] B, [N][C] Cc  with dx = A*dy_eff + B + Cc*xhat
@@ -427,8 +443,8 @@ __global__ void __launch_bounds__(256) norm_bwd_finalize_kernel(const float* __r
   const float ga = gamma ? gamma[c] : 1.f;
   const long NC = (long)g.N * g.C;
   coef[i] = r * ga;
-  coef[NC + i] = -r * sdy * inv;
-  coef[2 * NC + i] = -r * sdx * inv;
+  coef[NC + i] = -r * ga * sdy * inv;   // partial sums are of the un-scaled dy_eff
+  coef[2 * NC + i] = -r * ga * sdx * inv;
 }
 
 // d(gamma) = sum(dy_eff * xhat), d(beta) = sum(dy_eff) over every group of the channel
@@ -453,8 +469,8 @@ template <int ACT>
 __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ dy, NormGeom g,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
-    const float* __restrict__ beta, const float* __restrict__ coef, bf16* __restrict__ dx,
-    Fp8Shadow sh) {
+    const float* __restrict__ beta, const float* __restrict__ prelu_w, const float* __restrict__ coef,
+    bf16* __restrict__ dx, Fp8Shadow sh) {
   const int n = blockIdx.y, cb = blockIdx.x;
   const int CP = g.C >> 3;
   const int RP = 256 / CP;
@@ -465,6 +481,7 @@ __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
   const int p1 = min(g.HW, p0 + g.chunk);
   const long NC = (long)g.N * g.C;
   float mu[8], rs[8], ga[8], be[8], ca[8], cx[8], c0[8];
+  const float pw = ACT == ACT_PRELU_T ? prelu_w[0] : 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const long ci = (long)n * g.C + cg * 8 + j;
@@ -487,7 +504,7 @@ __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float xh = (fx[j] - mu[j]) * rs[j];
-      const float d = ACT ? fd[j] * act_gate(xh * ga[j] + be[j], ACT) : fd[j];
+      const float d = ACT ? fd[j] * act_gate(xh * ga[j] + be[j], ACT, pw) : fd[j];
       fd[j] = ca[j] * d + c0[j] + cx[j] * xh;
     }
     const u32x4 o = pack8(fd);
@@ -542,10 +559,12 @@ static inline NormGeom make_geom(int N, int HW, int C) {
 
 extern "C" {
 
+int p2p_sum_partials(const float* ws, int nb, float scale, float* out, hipStream_t st);
+
 // workspace floats needed by p2p_norm_fwd / p2p_norm_bwd (incl. the fused bias-grad partials)
 long p2p_norm_ws_floats(int N, int HW, int C) {
   p2p::NormGeom g = p2p::make_geom(N, HW, C);
-  return 2L * N * g.nchunks * C + 3L * N * C;
+  return 2L * N * g.nchunks * C + 3L * N * C + (long)N * g.nchunks;
 }
 
 int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* gamma,
@@ -615,41 +634,45 @@ int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const
   return (int)hipGetLastError();
 }
 
-// act: ReLU / LeakyReLU fused by the forward (0 = none); dsum (optional, [C] fp32): the
-// column sums of dx (bias gradient of the producing conv), which are exactly zero.
+// act: ReLU / LeakyReLU fused by the forward (0 = none); prelu_w: the fused shared-slope
+// PReLU (its slope gradient -> *dprelu, written not accumulated); dsum (optional, [C] fp32):
+// the column sums of dx (bias gradient of the producing conv), which are exactly zero.
 int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const float* mean,
-                 const float* rstd, const float* gamma, const float* beta, int act, float* dgamma,
-                 float* dbeta, float* ws, void* dx, float* dsum, void* q, int* qsite, int qfmt,
-                 hipStream_t st) {
+                 const float* rstd, const float* gamma, const float* beta, int act,
+                 const float* prelu_w, float* dprelu, float* dgamma, float* dbeta, float* ws, void* dx,
+                 float* dsum, void* q, int* qsite, int qfmt, hipStream_t st) {
   using namespace p2p;
   NormGeom g = make_geom(N, HW, C);
   float* coef = ws + 2L * N * g.nchunks * C;
+  float* pws = coef + 3L * N * C;
   const bf16* xb = static_cast<const bf16*>(x);
   const bf16* db = static_cast<const bf16*>(dy);
+  const int a = prelu_w ? ACT_PRELU_T : act;
+  if (!dgamma && !dx && !dprelu) return 0;
+  with_act(a, [&](auto t) {
+    hipLaunchKernelGGL((norm_bwd_partial_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st, xb,
+                       db, g, mean, rstd, gamma, beta, prelu_w, ws, pws);
+  });
+  if (dprelu) {
+    const int rc = p2p_sum_partials(pws, N * g.nchunks, 1.f, dprelu, st);
+    if (rc) return rc;
+  }
   if (dgamma) {
-    with_act(act, [&](auto t) {
-      hipLaunchKernelGGL((norm_bwd_partial_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st, xb,
-                         db, g, mean, rstd, gamma, beta, 0, ws);
-    });
     if (fin_wide(g) || N > 8)
       hipLaunchKernelGGL((norm_param_grad_kernel<8, 32>), dim3((C + 7) / 8), dim3(256), 0, st, ws, g, dgamma, dbeta);
     else
       hipLaunchKernelGGL((norm_param_grad_kernel<32, 8>), dim3((C + 31) / 32), dim3(256), 0, st, ws, g, dgamma, dbeta);
   }
   if (dx) {
-    with_act(act, [&](auto t) {
-      hipLaunchKernelGGL((norm_bwd_partial_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st, xb,
-                         db, g, mean, rstd, gamma, beta, 1, ws);
-    });
     if (fin_wide(g))
       hipLaunchKernelGGL((norm_bwd_finalize_kernel<8, 32>), dim3((C + 7) / 8, N), dim3(256), 0, st, ws, g, rstd,
                          gamma, coef);
     else
       hipLaunchKernelGGL((norm_bwd_finalize_kernel<32, 8>), dim3((C + 31) / 32, N), dim3(256), 0, st, ws, g, rstd,
                          gamma, coef);
-    with_act(act, [&](auto t) {
+    with_act(a, [&](auto t) {
       hipLaunchKernelGGL((norm_bwd_apply_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st, xb, db,
-                         g, mean, rstd, gamma, beta, coef, static_cast<bf16*>(dx),
+                         g, mean, rstd, gamma, beta, prelu_w, coef, static_cast<bf16*>(dx),
                          Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
     });
     if (dsum) (void)hipMemsetAsync(dsum, 0, sizeof(float) * C, st);

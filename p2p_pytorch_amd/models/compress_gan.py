@@ -52,6 +52,13 @@ def pixel_unshuffle(x, downscale_factor):
     return ops.pixel_unshuffle(x, downscale_factor)
 
 
+class PixelShuffle(nn.PixelShuffle):
+    """Depth-to-space on the op layer (NHWC HIP kernel on the native path)."""
+
+    def forward(self, x):
+        return ops.pixel_shuffle(x, self.upscale_factor)
+
+
 class ConvLayer(nn.Module):
     """ReflectionPad2d(k//2) + Conv2d(k, stride) -- pad folded into the conv."""
 
@@ -92,7 +99,7 @@ class ResidualBlock(nn.Module):
 
     def forward(self, x):
         out = self.in2(self.conv2(self.in1(self.conv1(x))))
-        return ops.act(out + x, "relu")
+        return ops.add_act(out, x, "relu")
 
 
 class ExpandNetwork(nn.Module):
@@ -127,15 +134,16 @@ class ExpandNetwork(nn.Module):
         # pixel-unshuffle(2) followed by nearest x2: the conv sees 12 channels at full res.
         y = self.inversePixel(x)
         y = ops.conv2d(y, self.conv1.conv2d.weight, self.conv1.conv2d.bias, 1, 4, "reflect", 2)
-        y = self.relu(self.in1_e(y))
-        y = self.relu(self.in2_e(self.conv2(y)))
-        y = self.relu(self.in3_e(self.conv3(y)))
+        pw = self.relu.weight            # PReLU fused into the BN passes (fwd and bwd)
+        y = self.in1_e(y, prelu=pw)
+        y = self.in2_e(self.conv2(y), prelu=pw)
+        y = self.in3_e(self.conv3(y), prelu=pw)
         res = y
         for k in range(1, 10):
             res = getattr(self, f"res{k}")(res)
-        y = ops.act(res + y, "lrelu")
-        y = self.relu(self.in3_d(self.deconv3(y)))
-        y = self.relu(self.in2_d(self.deconv2(y)))
+        y = ops.add_act(res, y, "lrelu")
+        y = self.in3_d(self.deconv3(y), prelu=pw)
+        y = self.in2_d(self.deconv2(y), prelu=pw)
         return self.in1_d(self.deconv1(y))
 
 
@@ -148,11 +156,13 @@ class CompressionNetwork(nn.Module):
         self.conv_block1 = nn.Sequential(ConvLayer(64, 64, kernel_size=3, stride=1),
                                          BatchNorm2d(64), PReLU())
         self.conv_block2 = nn.Sequential(ConvLayer(64, 12, kernel_size=3, stride=2),
-                                         nn.PixelShuffle(2))
+                                         PixelShuffle(2))
 
     def forward(self, x):
-        res = self.conv_block2(self.conv_block1(self.conv_input(x)))
-        return x + ops.l2_normalize_channels(res)
+        conv, bn, act = self.conv_block1
+        h = bn(conv(self.conv_input(x)), prelu=act.weight)   # BN + PReLU: one pass
+        res = self.conv_block2(h)
+        return ops.l2_normalize_channels(res, residual=x)
 
 
 # ----------------------------------------------------------------- spectral norm

@@ -126,14 +126,15 @@ class BatchNorm2d(nn.BatchNorm2d):
         super().__init__(num_features, eps=eps, momentum=momentum, affine=affine)
         self.act = act
 
-    def forward(self, x):
+    def forward(self, x, prelu=None):
+        """``prelu``: slope Parameter of a following shared-slope PReLU, fused in."""
         training = self.training or not self.track_running_stats
         if self.training and self.track_running_stats:
             self.num_batches_tracked.add_(1)
         return ops.batch_norm(x, self.running_mean if self.track_running_stats else None,
                               self.running_var if self.track_running_stats else None,
                               self.weight, self.bias, training, self.momentum, self.eps, self.act,
-                              qkey=id(self))
+                              qkey=id(self), prelu_weight=prelu)
 
 
 class Act(nn.Module):

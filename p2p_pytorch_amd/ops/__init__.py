@@ -54,11 +54,14 @@ def instance_norm(x, eps=1e-5, act=None, weight=None, bias=None, qkey=None):
 
 
 def batch_norm(x, running_mean, running_var, weight, bias, training, momentum=0.1, eps=1e-5,
-               act=None, qkey=None):
+               act=None, qkey=None, prelu_weight=None):
+    """``prelu_weight``: a shared-slope PReLU applied to the output (fused into the apply pass
+    and, in the backward, into the norm's partial-sum pass -- slope gradient included)."""
     if _native.use_native(x):
         return _hip().batch_norm(x, running_mean, running_var, weight, bias, training, momentum,
-                                 eps, act, qkey=qkey)
-    return ref.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps, act)
+                                 eps, act, prelu_weight=prelu_weight, qkey=qkey)
+    y = ref.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps, act)
+    return y if prelu_weight is None else ref.prelu(y, prelu_weight)
 
 
 def prelu(x, weight):
@@ -73,6 +76,15 @@ def act(x, name):
     if _native.use_native(x):
         return _hip().act(x, name)
     return ref.apply_act(x, name)
+
+
+def add_act(a, b, name):
+    """act(a + b) -- one fused pass on the native path (residual joins)."""
+    if name is None:
+        return a + b
+    if _native.use_native(a):
+        return _hip().add_act(a, b, name)
+    return ref.apply_act(a + b, name)
 
 
 def dropout(x, p, training, salt=None):
@@ -131,10 +143,12 @@ def avg_pool3_s2(x):
     return ref.avg_pool3_s2(x)
 
 
-def l2_normalize_channels(x, eps=1e-12):
+def l2_normalize_channels(x, eps=1e-12, residual=None):
+    """x / ||x||_2 over channels, plus ``residual`` (fused into the same pass when native)."""
     if _native.use_native(x):
-        return _hip().l2_normalize_channels(x, eps)
-    return ref.l2_normalize_channels(x, eps)
+        return _hip().l2_normalize_channels(x, eps, residual)
+    y = ref.l2_normalize_channels(x, eps)
+    return y if residual is None else y + residual
 
 
 def pixel_shuffle(x, r):

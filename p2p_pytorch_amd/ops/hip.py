@@ -705,8 +705,14 @@ class NormFn(torch.autograd.Function):
         gy = to_nhwc_bf16(gy)
         gpw = None
         fused_act = 0
-        if prelu_w is not None:
-            # y = prelu(z); dz = dy * (z > 0 ? 1 : w); dw = sum(dy * z * [z <= 0])
+        pw = None
+        if prelu_w is not None and training:
+            # y = prelu(z): the kernels recompute z from x, gate dz = dy * (z > 0 ? 1 : w) and
+            # reduce dw = sum(dy * z * [z <= 0]) in the same partial-sum pass
+            pw = prelu_w.detach().float().contiguous()
+            if ctx.needs_input_grad[3]:
+                gpw = torch.empty(1, device=x.device, dtype=torch.float32)
+        elif prelu_w is not None:
             z = _norm_recompute(x, mean, rstd, gamma, beta, batch)
             zf = z.float()
             neg = zf <= 0
@@ -746,7 +752,12 @@ class NormFn(torch.autograd.Function):
             if not fresh:
                 qd = _f8.shadow_buffer(x, _f8.E5M2)
                 qargs = (dsite, qd, _f8.E5M2)
-        dx = P().norm_bwd(x, gy, mean, rstd, g, b, fused_act, dg, db, need_x, batch, dsum, *qargs)
+        if qargs:
+            dx = P().norm_bwd(x, gy, mean, rstd, g, b, fused_act, dg, db, need_x, batch, dsum,
+                              *qargs, prelu_w=pw, dprelu=gpw if pw is not None else None)
+        else:
+            dx = P().norm_bwd(x, gy, mean, rstd, g, b, fused_act, dg, db, need_x, batch, dsum,
+                              prelu_w=pw, dprelu=gpw if pw is not None else None)
         if need_x:
             _stash_colsum(dx, dsum)
             if qd is not None:
@@ -856,6 +867,29 @@ class ActFn(torch.autograd.Function):
 
 def act(x, name):
     return ActFn.apply(x, name)
+
+
+class AddActFn(torch.autograd.Function):
+    """y = act(a + b) in one pass (act kernel mode 3); the gradient gates on the output sign,
+    which equals the sign of a + b for relu / lrelu, and flows unchanged to both inputs."""
+
+    @staticmethod
+    def forward(ctx, a, b, name):
+        a, b = to_nhwc_bf16(a), to_nhwc_bf16(b)
+        y = P().act(a, b, _act_code(name), 3)
+        ctx.name = name
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (y,) = ctx.saved_tensors
+        g = P().act(to_nhwc_bf16(gy), y, _act_code(ctx.name), 2)
+        return g, g, None
+
+
+def add_act(a, b, name):
+    return AddActFn.apply(a, b, name)
 
 
 class DropoutFn(torch.autograd.Function):
@@ -1054,21 +1088,24 @@ def max_pool2(x):
 
 
 class L2NormFn(torch.autograd.Function):
+    """y = x / ||x||_C (+ res): the residual add rides in the same pass."""
+
     @staticmethod
-    def forward(ctx, x, eps):
+    def forward(ctx, x, eps, res):
         x = _nhwc(x)
-        ctx.eps = eps
+        ctx.eps, ctx.has_res = eps, res is not None
         ctx.save_for_backward(x)
-        return P().l2norm(x, None, eps)
+        return P().l2norm(x, None, eps, _nhwc(res) if res is not None else None)
 
     @staticmethod
     def backward(ctx, gy):
         (x,) = ctx.saved_tensors
-        return P().l2norm(x, _nhwc(gy), ctx.eps), None
+        gy = _nhwc(gy)
+        return P().l2norm(x, gy, ctx.eps), None, (gy if ctx.has_res else None)
 
 
-def l2_normalize_channels(x, eps=1e-12):
-    return L2NormFn.apply(x, float(eps))
+def l2_normalize_channels(x, eps=1e-12, residual=None):
+    return L2NormFn.apply(x, float(eps), residual)
 
 
 class PixelShuffleFn(torch.autograd.Function):
