@@ -678,6 +678,44 @@ void conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, con
   a.M = (int)(N * OH * OW);
   a.Kq = (int)(KH * KW * C);
   a.zero = zero_page(p1);
+  hipStream_t st = cur_stream(p1);
+  // 9x9 stride-1 layers with 16 / 32 input and <= 32 output channels: halo-tile wgrad
+  // (csrc/halo_wgrad.hip), one fp32 slab per persistent block
+  if (!p2 && !q2 && p_act == 0 && q_act == 0 && KH == 9 && KW == 9 && stride == 1 && !flip &&
+      (C == 16 || C == 32) && R % 8 == 0 && (R <= 16 || (C == 16 && R == 32)) &&
+      std::getenv("P2P_NO_HALO") == nullptr) {
+    p2p::HaloWArgs h{};
+    h.gy = static_cast<const __bf16*>(p1.data_ptr());
+    h.x = static_cast<const __bf16*>(q1.data_ptr());
+    h.R = (int)R;
+    h.C = (int)C;
+    h.N = (int)N;
+    h.H = (int)H;
+    h.W = (int)W;
+    h.up = (int)up;
+    h.pad = (int)pad;
+    h.reflect = (int)reflect;
+    h.OH = (int)OH;
+    h.OW = (int)OW;
+    h.zero = static_cast<const __bf16*>(a.zero);
+    h.tiles_x = (int)((OW + 15) / 16);
+    h.tiles_y = (int)((OH + 15) / 16);
+    h.ntiles = (int)N * h.tiles_x * h.tiles_y;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int blocks = std::max(1, std::min(h.ntiles, cus));
+    Tensor ws = at::empty({(int64_t)blocks * R * a.Kq}, p1.options().dtype(at::kFloat));
+    h.ws = ws.data_ptr<float>();
+    const int rc = p2p_halo_wgrad(&h, 9, blocks, st);
+    if (rc != -2) {
+      check_rc(rc, "conv_wgrad(halo)");
+      check_rc(p2p_wgrad_reduce(h.ws, blocks, (int)R, 9, 9, (int)C, (int)Rr, (int)Cr, dw.data_ptr<float>(),
+                                (float)scale, (int)accumulate, 0, st),
+               "wgrad_reduce(halo)");
+      return;
+    }
+  }
   int wbr = 128, wbq = 128;
   p2p_conv_wgrad_tile(&a, &wbr, &wbq);
   const int64_t tiles = ((R + wbr - 1) / wbr) * ((a.Kq + wbq - 1) / wbq);
@@ -691,7 +729,6 @@ void conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, con
   a.splits = (int)splits;
   Tensor ws = at::empty({splits * slab}, p1.options().dtype(at::kFloat));
   a.ws = ws.data_ptr<float>();
-  hipStream_t st = cur_stream(p1);
   check_rc(p2p_conv_wgrad(&a, st), "conv_wgrad");
   check_rc(p2p_wgrad_reduce(a.ws, a.splits, a.R, a.KH, a.KW, a.C, flip ? (int)Cr : (int)Rr,
                             flip ? (int)Rr : (int)Cr, dw.data_ptr<float>(), (float)scale,

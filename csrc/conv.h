@@ -144,9 +144,22 @@ struct HaloKArgs {
   int tiles_x, tiles_y, ntiles;
 };
 
+// Halo-tile weight gradient of the same 9x9 stride-1 layers (csrc/halo_wgrad.hip): per-block
+// fp32 slabs ws[block][R][K*K*C] (summed by p2p_wgrad_reduce).
+struct HaloWArgs {
+  const __bf16* gy;    // NHWC [N][OH][OW][R]  (R in {8, 16, 32})
+  const __bf16* x;     // NHWC [N][H][W][C]    (C in {16, 32})
+  int R, C, N, H, W, up, pad, reflect;
+  int OH, OW;
+  float* ws;
+  const __bf16* zero;
+  int tiles_x, tiles_y, ntiles;
+};
+
 }  // namespace p2p
 
 extern "C" {
+int p2p_halo_wgrad(const p2p::HaloWArgs* a, int KS, int blocks, hipStream_t st);
 int p2p_halo_kxk(const p2p::HaloKArgs* a, int KS, int blocks, hipStream_t st);
 int p2p_halo_pk8(const p2p::HaloPk8Args* a, int blocks, hipStream_t st);
 int p2p_halo_union(const p2p::HaloArgs* a, int relu, int blocks, hipStream_t st);
