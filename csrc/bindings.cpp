@@ -62,7 +62,7 @@ int p2p_weight_prep_pairs(int count, const float* const* w, void* const* out0, v
                           const int* A, const int* B, const int* T, const int* Xa, const int* Xb,
                           int* const* site, hipStream_t st);
 int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, int reflect,
-                 const void* xb, int act, void* dx, hipStream_t st);
+                 const void* xb, int act, const void* res, void* dx, hipStream_t st);
 int p2p_pad_channels(const void* a, int Ca, const void* b, int Cb, long P, int Co, void* out,
                      hipStream_t st);
 int p2p_slice_channels(const void* in, int Ci, int c0, long P, int C, void* out, hipStream_t st);
@@ -421,9 +421,11 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   }
   // stride-1 9x9 convs with 8-32 input channels and <= 32 outputs (family R's full-res
   // layers): the halo-tile direct conv (csrc/halo_kxk.hip); MODE 1 stride 1 = flipped taps
-  if (rc == -2 && !fp8 && C2 == 0 && KH == 9 && KW == 9 && stride == 1 && (C1 == 8 || C1 == 16 || C1 == 32) &&
-      Cout <= 32 && Csplit == Cout && act_in == 0 && act_bwd == 0 && !a.res1 && !a.q_out && !a.stats &&
-      (mode == 0 || (up == 1 && !reflect && pad <= 8)) && std::getenv("P2P_NO_HALO") == nullptr) {
+  const bool halo_geo = (KH == 9 && KW == 9 && (C1 == 8 || C1 == 16 || C1 == 32) && Cout <= 32) ||
+                        (KH == 3 && KW == 3 && ((C1 == 64 && Cout <= 32) || (C1 == 8 && Cout > 48 && Cout <= 64)));
+  if (rc == -2 && !fp8 && C2 == 0 && halo_geo && stride == 1 && Csplit == Cout && act_in == 0 && act_bwd == 0 &&
+      !a.res1 && !a.q_out && !a.stats && (mode == 0 || (up == 1 && !reflect && pad <= KH - 1)) &&
+      std::getenv("P2P_NO_HALO") == nullptr) {
     p2p::HaloKArgs h{};
     h.x = static_cast<const __bf16*>(x1.data_ptr());
     h.C = (int)C1;
@@ -449,7 +451,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       int dev = 0, cus = 256;
       (void)hipGetDevice(&dev);
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      rc = p2p_halo_kxk(&h, 9, std::max(1, std::min(h.ntiles, cus)), st);
+      rc = p2p_halo_kxk(&h, (int)KH, std::max(1, std::min(h.ntiles, cus)), st);
       if (rc == 0) splits = 1;   // no split-K partials to finalize: the halo kernel wrote y
     }
   }
@@ -681,8 +683,9 @@ void conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, con
   hipStream_t st = cur_stream(p1);
   // 9x9 stride-1 layers with 16 / 32 input and <= 32 output channels: halo-tile wgrad
   // (csrc/halo_wgrad.hip), one fp32 slab per persistent block
-  if (!p2 && !q2 && p_act == 0 && q_act == 0 && KH == 9 && KW == 9 && stride == 1 && !flip &&
-      (C == 16 || C == 32) && R % 8 == 0 && (R <= 16 || (C == 16 && R == 32)) &&
+  const bool halo_geo = (KH == 9 && KW == 9 && (C == 16 || C == 32) && (R <= 16 || (C == 16 && R == 32))) ||
+                        (KH == 3 && KW == 3 && C == 64 && R <= 32);
+  if (!p2 && !q2 && p_act == 0 && q_act == 0 && halo_geo && stride == 1 && !flip && R % 8 == 0 &&
       std::getenv("P2P_NO_HALO") == nullptr) {
     p2p::HaloWArgs h{};
     h.gy = static_cast<const __bf16*>(p1.data_ptr());
@@ -707,10 +710,10 @@ void conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, con
     const int blocks = std::max(1, std::min(h.ntiles, cus));
     Tensor ws = at::empty({(int64_t)blocks * R * a.Kq}, p1.options().dtype(at::kFloat));
     h.ws = ws.data_ptr<float>();
-    const int rc = p2p_halo_wgrad(&h, 9, blocks, st);
+    const int rc = p2p_halo_wgrad(&h, (int)KH, blocks, st);
     if (rc != -2) {
       check_rc(rc, "conv_wgrad(halo)");
-      check_rc(p2p_wgrad_reduce(h.ws, blocks, (int)R, 9, 9, (int)C, (int)Rr, (int)Cr, dw.data_ptr<float>(),
+      check_rc(p2p_wgrad_reduce(h.ws, blocks, (int)R, (int)KH, (int)KW, (int)C, (int)Rr, (int)Cr, dw.data_ptr<float>(),
                                 (float)scale, (int)accumulate, 0, st),
                "wgrad_reduce(halo)");
       return;
@@ -1146,7 +1149,7 @@ Tensor pixel_shuffle(const Tensor& x, int64_t r, int64_t dir) {
 
 // pad_fold: gradient of a virtual reflect/zero-padded + nearest-upsampled input -> real input
 Tensor pad_fold(const Tensor& dxp, int64_t H, int64_t W, int64_t pad, int64_t up, int64_t reflect,
-                const optional<Tensor>& xb, int64_t act) {
+                const optional<Tensor>& xb, int64_t act, const optional<Tensor>& res) {
   TORCH_CHECK(dxp.is_cuda() && dxp.scalar_type() == at::kBFloat16 && dxp.dim() == 4, "pad_fold: dxp");
   TORCH_CHECK(dxp.is_contiguous(at::MemoryFormat::ChannelsLast), "pad_fold: NHWC input");
   const int64_t N = dxp.size(0), C = dxp.size(1);
@@ -1154,9 +1157,14 @@ Tensor pad_fold(const Tensor& dxp, int64_t H, int64_t W, int64_t pad, int64_t up
   TORCH_CHECK(dxp.size(2) == H * up + 2 * pad && dxp.size(3) == W * up + 2 * pad, "pad_fold: geometry");
   TORCH_CHECK(!act || (xb && xb->is_contiguous(at::MemoryFormat::ChannelsLast) && xb->size(1) == C),
               "pad_fold: xb");
+  if (res)
+    TORCH_CHECK(res->scalar_type() == at::kBFloat16 && res->is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    res->size(0) == N && res->size(1) == C && res->size(2) == H && res->size(3) == W,
+                "pad_fold: res must match dx");
   Tensor dx = empty_nhwc(N, C, H, W, dxp);
   check_rc(p2p_pad_fold(dxp.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)pad, (int)up, (int)reflect,
-                        act ? xb->data_ptr() : nullptr, (int)act, dx.data_ptr(), cur_stream(dxp)),
+                        act ? xb->data_ptr() : nullptr, (int)act, res ? res->data_ptr() : nullptr, dx.data_ptr(),
+                        cur_stream(dxp)),
            "pad_fold");
   return dx;
 }
@@ -1425,7 +1433,8 @@ TORCH_LIBRARY(p2p, m) {
   m.def("maxpool2(Tensor x, Tensor? gy) -> Tensor");
   m.def("l2norm(Tensor x, Tensor? gy, float eps, Tensor? res=None) -> Tensor");
   m.def("pixel_shuffle(Tensor x, int r, int dir) -> Tensor");
-  m.def("pad_fold(Tensor dxp, int H, int W, int pad, int up, int reflect, Tensor? xb, int act) -> Tensor");
+  m.def("pad_fold(Tensor dxp, int H, int W, int pad, int up, int reflect, Tensor? xb, int act, "
+        "Tensor? res=None) -> Tensor");
   m.def("weight_prep_pairs(Tensor[] w, int[] xa, int[] xb, Tensor(a!)? sites=None, int[]? site_idx=None) -> Tensor[]");
   m.def("weight_prep_multi(Tensor[] w, int[] swap, int[] xp, int[] yp) -> Tensor[]");
   m.def("norm_fwd(Tensor x, float eps, Tensor? gamma, Tensor? beta, Tensor? prelu_w, int act, "

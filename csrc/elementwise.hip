@@ -136,6 +136,7 @@ __device__ __forceinline__ int fold_taps(int u, int pad, int Hu, bool reflect, i
 __global__ void __launch_bounds__(256) pad_fold_kernel(const bf16* __restrict__ dxp, int N, int H, int W,
                                                        int C, int pad, int up, int reflect,
                                                        const bf16* __restrict__ xb, int act,
+                                                       const bf16* __restrict__ res,
                                                        bf16* __restrict__ dx) {
   const int CP = C >> 3;
   const int Hu = H * up, Wu = W * up;
@@ -169,6 +170,12 @@ __global__ void __launch_bounds__(256) pad_fold_kernel(const bf16* __restrict__ 
       unpack8e(*reinterpret_cast<const u32x4*>(xb + pix * C + cg * 8), xf);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] *= act_grad_from_input(xf[j], act);
+    }
+    if (res) {   // the other consumer's gradient of this input (residual blocks), after the gate
+      float rf[8];
+      unpack8e(*reinterpret_cast<const u32x4*>(res + pix * C + cg * 8), rf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += rf[j];
     }
     *reinterpret_cast<u32x4*>(dx + pix * C + cg * 8) = pack8e(acc);
   }
@@ -453,11 +460,12 @@ int p2p_pad_channels(const void* a, int Ca, const void* b, int Cb, long P, int C
 }
 
 int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, int reflect,
-                 const void* xb, int act, void* dx, hipStream_t st) {
+                 const void* xb, int act, const void* res, void* dx, hipStream_t st) {
   using namespace p2p;
   const long total = (long)N * H * W * (C / 8);
   hipLaunchKernelGGL(pad_fold_kernel, dim3(egrid(total)), dim3(256), 0, st, static_cast<const bf16*>(dxp), N,
-                     H, W, C, pad, up, reflect, static_cast<const bf16*>(xb), act, static_cast<bf16*>(dx));
+                     H, W, C, pad, up, reflect, static_cast<const bf16*>(xb), act, static_cast<const bf16*>(res),
+                     static_cast<bf16*>(dx));
   return (int)hipGetLastError();
 }
 

@@ -51,10 +51,12 @@ __device__ __forceinline__ bf16x8 lds_frag(const bf16* base_unit, bool swap) {
 template <int KS, int CIN>
 struct HaloK {
   static constexpr int KK = KS * KS;
-  static constexpr int TPS = 32 / CIN;               // taps per MFMA K-slice
-  static constexpr int S = (KK + TPS - 1) / TPS;     // K-slices
+  // an MFMA K-slice is 32 / CIN taps (CIN <= 32) or 1/SPT of a tap (CIN = 32 * SPT)
+  static constexpr int TPS = CIN <= 32 ? 32 / CIN : 1;
+  static constexpr int SPT = CIN <= 32 ? 1 : CIN / 32;
+  static constexpr int S = CIN <= 32 ? (KK + TPS - 1) / TPS : KK * SPT;   // K-slices
   static constexpr int CPP = CIN / 8;                // 16-B chunks per pixel
-  static constexpr int LSH = CPP == 4 ? 2 : (CPP == 2 ? 3 : 4);   // log2(16 / CPP)
+  static constexpr int LSH = CPP == 8 ? 1 : (CPP == 4 ? 2 : (CPP == 2 ? 3 : 4));   // log2(16 / CPP)
   static constexpr int HT = 16;
   static constexpr int HP = HT + KS - 1;             // halo edge
   static constexpr int HPIX = HP * HP;
@@ -85,16 +87,18 @@ __global__ void __launch_bounds__(256) halo_kxk_kernel(HaloKArgs a) {
 
   // ---- resident weights: unit ((s * NBLK + nb) * 16 + n) * 4 + slot holds logical k-chunk
   // c = slot ^ ((n >> 2) & 3) of slice s: tap s * TPS + 8c / CIN, channels (8c % CIN) + 0..7
+  // (CIN > 32: tap s / SPT, channels 8 * ((s % SPT) * 4 + c) + 0..7)
   for (int e0 = wid * 64; e0 < BUNITS_PAD; e0 += 256) {
     const int e = e0 + lane;
     const int n = (e >> 2) & 15, sn = e >> 6;
     const int nb = sn % NBLK, s = sn / NBLK;
     const int c = (e & 3) ^ ((n >> 2) & 3);
-    const int t = s * G::TPS + (8 * c) / CIN;
+    const int t = CIN <= 32 ? s * G::TPS + (8 * c) / CIN : s / G::SPT;
+    const int ch = CIN <= 32 ? (8 * c) % CIN : 8 * ((s % G::SPT) * 4 + c);
     const int co = nb * 16 + n;
     const int tw = a.flip ? G::KK - 1 - t : t;
     const bool ok = e < BUNITS && co < a.Cout && t < G::KK;
-    glds16k(ok ? a.w + ((long)co * G::KK + tw) * CIN + (8 * c) % CIN : a.zero, Bs + e0 * 8);
+    glds16k(ok ? a.w + ((long)co * G::KK + tw) * CIN + ch : a.zero, Bs + e0 * 8);
   }
 
   // ---- per-lane halo units (fixed across tiles)
@@ -145,7 +149,7 @@ __global__ void __launch_bounds__(256) halo_kxk_kernel(HaloKArgs a) {
   const int px = lane & 15, kq = lane >> 4;
   const bool hswap = kq & 1;
   // this lane's tap within a slice and chunk within the tap
-  const int tsub = kq / G::CPP, csub = kq % G::CPP;
+  const int tsub = CIN <= 32 ? kq / G::CPP : 0, csub0 = CIN <= 32 ? kq % G::CPP : kq;
   const int bslot = kq ^ ((px >> 2) & 3);
   int rowbase[4];
 #pragma unroll
@@ -165,11 +169,12 @@ __global__ void __launch_bounds__(256) halo_kxk_kernel(HaloKArgs a) {
     const bf16* A = As + stage * (G::STAGE_UNITS * 8);
     // the lane's tap walks t = s * TPS + tsub incrementally (loop-carried: the compiler must
     // not hoist 81 per-slice offsets into registers across the tile loop)
-    int dx = tsub % KS, toff = (tsub / KS) * G::HP + tsub % KS;
+    int dx = tsub % KS, toff = (tsub / KS) * G::HP + tsub % KS, sub = 0;
     const bf16* bp = Bs + (px * 4 + bslot) * 8;
 #pragma unroll 2
     for (int s = 0; s < G::S; ++s) {
-      const int to = s * G::TPS + tsub < G::KK ? toff : 0;   // padding tap: zero weights
+      const int to = CIN > 32 || s * G::TPS + tsub < G::KK ? toff : 0;   // padding tap: zero weights
+      const int csub = csub0 + sub * 4;
       bf16x8 bfr[NBLK];
 #pragma unroll
       for (int nb = 0; nb < NBLK; ++nb) bfr[nb] = lds_frag(bp + nb * 16 * 4 * 8, hswap);
@@ -181,12 +186,16 @@ __global__ void __launch_bounds__(256) halo_kxk_kernel(HaloKArgs a) {
           acc[i][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[nb], acc[i][nb], 0, 0, 0);
       }
       bp += NBLK * 16 * 4 * 8;
+      if (CIN > 32 && ++sub < G::SPT) continue;
+      sub = 0;
       dx += G::TPS;
       toff += G::TPS;
-      if (dx >= KS) {
-        dx -= KS;
-        toff += G::HP - KS;
-      }
+#pragma unroll
+      for (int w = 0; w < (G::TPS + KS - 1) / KS; ++w)   // TPS may exceed KS (3x3, 8 ch)
+        if (dx >= KS) {
+          dx -= KS;
+          toff += G::HP - KS;
+        }
     }
     __builtin_amdgcn_s_barrier();   // every wave done reading this stage
     // ---- epilogue: bias + act -> bf16 staging [256 px][LDCS] -> 16-B NHWC stores
@@ -245,14 +254,27 @@ static int launch_halo_kxk(const HaloKArgs& a, int blocks, hipStream_t st) {
 // returns -2 when the geometry is not covered (caller falls back to the implicit GEMM)
 extern "C" int p2p_halo_kxk(const p2p::HaloKArgs* a, int KS, int blocks, hipStream_t st) {
   using namespace p2p;
-  if (KS != 9 || a->Cout % 8 || a->Cout > 32 || a->Cout <= 0) return -2;
+  if (a->Cout % 8 || a->Cout <= 0 || a->Cout > 64) return -2;
   if (a->up != 1 && a->up != 2) return -2;
   if (a->reflect && (a->pad >= a->H * a->up || a->pad >= a->W * a->up)) return -2;
-  const bool wide = a->Cout > 16;
-  switch (a->C) {
-    case 32: return wide ? -2 : launch_halo_kxk<9, 32, 1>(*a, blocks, st);
-    case 16: return wide ? launch_halo_kxk<9, 16, 2>(*a, blocks, st) : launch_halo_kxk<9, 16, 1>(*a, blocks, st);
-    case 8: return wide ? launch_halo_kxk<9, 8, 2>(*a, blocks, st) : launch_halo_kxk<9, 8, 1>(*a, blocks, st);
-    default: return -2;
+  const int nblk = (a->Cout + 15) / 16;
+  if (KS == 9) {
+    if (nblk > 2) return -2;
+    const bool wide = nblk == 2;
+    switch (a->C) {
+      case 32: return wide ? -2 : launch_halo_kxk<9, 32, 1>(*a, blocks, st);
+      case 16: return wide ? launch_halo_kxk<9, 16, 2>(*a, blocks, st) : launch_halo_kxk<9, 16, 1>(*a, blocks, st);
+      case 8: return wide ? launch_halo_kxk<9, 8, 2>(*a, blocks, st) : launch_halo_kxk<9, 8, 1>(*a, blocks, st);
+      default: return -2;
+    }
   }
+  if (KS == 3) {
+    // 64-channel inputs into <= 32 outputs (G.deconv2, VGG conv1_1's input gradient) and
+    // the 8-channel image into 64 (VGG conv1_1)
+    if (a->C == 64 && nblk == 1) return launch_halo_kxk<3, 64, 1>(*a, blocks, st);
+    if (a->C == 64 && nblk == 2) return launch_halo_kxk<3, 64, 2>(*a, blocks, st);
+    if (a->C == 8 && nblk == 4) return launch_halo_kxk<3, 8, 4>(*a, blocks, st);
+    return -2;
+  }
+  return -2;
 }

@@ -42,8 +42,13 @@ __device__ __forceinline__ s16x4 tr_read(const char* lds_byte) {
 
 // 16-B unit index of (pixel, chunk) in an image with CH channels per pixel (16 or 32)
 template <int CH>
+__device__ __forceinline__ int wmask(int hp) {   // chunk XOR of a pixel (CH >= 32)
+  if constexpr (CH == 64) return (((hp >> 1) & 1) << 1) | (((hp >> 3) & 1) << 2);
+  else return ((hp >> 3) & 1) << 1;
+}
+template <int CH>
 __device__ __forceinline__ int wunit(int hp, int c) {
-  if constexpr (CH == 32) return hp * 4 + (c ^ (((hp >> 3) & 1) << 1));
+  if constexpr (CH >= 32) return hp * (CH / 8) + (c ^ wmask<CH>(hp));
   else return (hp ^ (((hp >> 3) & 1) << 2)) * 2 + c;
 }
 
@@ -62,8 +67,9 @@ struct HaloW {
   static constexpr int XUNITS = XLD * 256;
   static constexpr int STAGE_UNITS = XUNITS + GLD * 256;
   static constexpr int STAGE_BYTES = STAGE_UNITS * 16;
-  static constexpr int TPW = (KK + 3) / 4;   // taps per wave
   static constexpr int CB = CIN / 16, RB = RL / 16;
+  static constexpr int ITEMS = KK * CB;          // (tap, 16-channel block) pairs
+  static constexpr int IPW = (ITEMS + 3) / 4;    // items per wave: i = wid + 4u
 };
 
 template <int KS, int CIN, int RL>
@@ -79,9 +85,9 @@ __global__ void __launch_bounds__(256) halo_wgrad_kernel(HaloWArgs a) {
   for (int j = 0; j < G::XLD; ++j) {
     const int e = (j * 4 + wid) * 64 + lane;
     int hp, c;
-    if constexpr (CIN == 32) {
-      hp = e >> 2;
-      c = (e & 3) ^ (((hp >> 3) & 1) << 1);
+    if constexpr (CIN >= 32) {
+      hp = e / G::XCPP;
+      c = (e % G::XCPP) ^ wmask<CIN>(hp);
     } else {
       const int slot = e >> 1;
       hp = slot ^ (((slot >> 3) & 1) << 2);   // the swizzle is an involution
@@ -97,7 +103,7 @@ __global__ void __launch_bounds__(256) halo_wgrad_kernel(HaloWArgs a) {
     const int e = (j * 4 + wid) * 64 + lane;
     if constexpr (RL == 32) {
       gp[j] = e >> 2;
-      gc[j] = (e & 3) ^ (((gp[j] >> 3) & 1) << 1);
+      gc[j] = (e & 3) ^ wmask<32>(gp[j]);
     } else {
       const int slot = e >> 1;
       gp[j] = slot ^ (((slot >> 3) & 1) << 2);
@@ -138,13 +144,11 @@ __global__ void __launch_bounds__(256) halo_wgrad_kernel(HaloWArgs a) {
     }
   };
 
-  f32x4 acc[G::TPW][G::CB][G::RB];
+  f32x4 acc[G::IPW][G::RB];
 #pragma unroll
-  for (int u = 0; u < G::TPW; ++u)
+  for (int u = 0; u < G::IPW; ++u)
 #pragma unroll
-    for (int cb = 0; cb < G::CB; ++cb)
-#pragma unroll
-      for (int rb = 0; rb < G::RB; ++rb) acc[u][cb][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int rb = 0; rb < G::RB; ++rb) acc[u][rb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // transposed-read lane roles: group g = lane / 16 takes k = 8g .. 8g + 7 of a 32-pixel
   // K-step (tile rows 2j + (g >> 1), columns 8 (g & 1) + 4 r + q, r = read 0 / 1);
@@ -176,21 +180,19 @@ __global__ void __launch_bounds__(256) halo_wgrad_kernel(HaloWArgs a) {
       }
       const int xbase = (2 * j + prow) * G::HP + pcol;
 #pragma unroll
-      for (int u = 0; u < G::TPW; ++u) {
-        const int t = wid + 4 * u;
-        if (u == G::TPW - 1 && t >= G::KK) break;   // wave-uniform: EXEC stays full
+      for (int u = 0; u < G::IPW; ++u) {
+        const int item = wid + 4 * u;
+        if (u == G::IPW - 1 && item >= G::ITEMS) break;   // wave-uniform: EXEC stays full
+        const int t = item / G::CB, cb = item % G::CB;
         const int hp = xbase + (t / KS) * G::HP + (t % KS);
+        const s16x4 a0 = tr_read(X + wunit<CIN>(hp, cb * 2 + pch) * 16 + phalf);
+        const s16x4 a1 = tr_read(X + wunit<CIN>(hp + 4, cb * 2 + pch) * 16 + phalf);
+        const bf16x8 af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
-        for (int cb = 0; cb < G::CB; ++cb) {
-          const s16x4 a0 = tr_read(X + wunit<CIN>(hp, cb * 2 + pch) * 16 + phalf);
-          const s16x4 a1 = tr_read(X + wunit<CIN>(hp + 4, cb * 2 + pch) * 16 + phalf);
-          const bf16x8 af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
-#pragma unroll
-          for (int rb = 0; rb < G::RB; ++rb) {
-            const bf16x8 bfr =
-                __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0[rb], b1[rb], 0, 1, 2, 3, 4, 5, 6, 7));
-            acc[u][cb][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[u][cb][rb], 0, 0, 0);
-          }
+        for (int rb = 0; rb < G::RB; ++rb) {
+          const bf16x8 bfr =
+              __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0[rb], b1[rb], 0, 1, 2, 3, 4, 5, 6, 7));
+          acc[u][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[u][rb], 0, 0, 0);
         }
       }
     }
@@ -201,18 +203,17 @@ __global__ void __launch_bounds__(256) halo_wgrad_kernel(HaloWArgs a) {
   float* slab = a.ws + (long)blockIdx.x * a.R * (G::KK * CIN);
   const int col = lane & 15, kq = lane >> 4;
 #pragma unroll
-  for (int u = 0; u < G::TPW; ++u) {
-    const int t = wid + 4 * u;
-    if (t >= G::KK) break;
+  for (int u = 0; u < G::IPW; ++u) {
+    const int item = wid + 4 * u;
+    if (item >= G::ITEMS) break;
+    const int t = item / G::CB, cb = item % G::CB;
 #pragma unroll
     for (int rb = 0; rb < G::RB; ++rb) {
       const int co = rb * 16 + col;
       if (co >= a.R) continue;
 #pragma unroll
-      for (int cb = 0; cb < G::CB; ++cb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          slab[(long)co * (G::KK * CIN) + t * CIN + cb * 16 + kq * 4 + r] = acc[u][cb][rb][r];
+      for (int r = 0; r < 4; ++r)
+        slab[(long)co * (G::KK * CIN) + t * CIN + cb * 16 + kq * 4 + r] = acc[u][rb][r];
     }
   }
 }
@@ -237,10 +238,16 @@ static int launch_halo_wgrad(const HaloWArgs& a, int blocks, hipStream_t st) {
 // returns -2 when the geometry is not covered (caller falls back to the GEMM wgrad)
 extern "C" int p2p_halo_wgrad(const p2p::HaloWArgs* a, int KS, int blocks, hipStream_t st) {
   using namespace p2p;
-  if (KS != 9 || (a->up != 1 && a->up != 2)) return -2;
+  if (a->up != 1 && a->up != 2) return -2;
   if (a->reflect && (a->pad >= a->H * a->up || a->pad >= a->W * a->up)) return -2;
-  if (a->C == 32 && a->R <= 16) return launch_halo_wgrad<9, 32, 16>(*a, blocks, st);
-  if (a->C == 16 && a->R <= 16) return launch_halo_wgrad<9, 16, 16>(*a, blocks, st);
-  if (a->C == 16 && a->R == 32) return launch_halo_wgrad<9, 16, 32>(*a, blocks, st);
+  if (KS == 9) {
+    if (a->C == 32 && a->R <= 16) return launch_halo_wgrad<9, 32, 16>(*a, blocks, st);
+    if (a->C == 16 && a->R <= 16) return launch_halo_wgrad<9, 16, 16>(*a, blocks, st);
+    if (a->C == 16 && a->R == 32) return launch_halo_wgrad<9, 16, 32>(*a, blocks, st);
+  }
+  if (KS == 3 && a->C == 64) {
+    if (a->R <= 16) return launch_halo_wgrad<3, 64, 16>(*a, blocks, st);
+    if (a->R == 32) return launch_halo_wgrad<3, 64, 32>(*a, blocks, st);
+  }
   return -2;
 }

@@ -96,10 +96,13 @@ class ResidualBlock(nn.Module):
         self.relu = nn.ReLU()
         self.conv2 = ConvLayer(channels, channels, kernel_size=3, stride=1)
         self.in2 = BatchNorm2d(channels, affine=True)
+        # x is read by conv1 and by the residual add: the add's gradient for x is folded into
+        # conv1's input-gradient pass (HIP path) instead of an autograd accumulate
+        self.conv1.conv2d.skip_grad = "take"
 
     def forward(self, x):
         out = self.in2(self.conv2(self.in1(self.conv1(x))))
-        return ops.add_act(out, x, "relu")
+        return ops.add_act(out, x, "relu", defer_b=True)
 
 
 class ExpandNetwork(nn.Module):

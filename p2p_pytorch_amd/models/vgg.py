@@ -61,6 +61,13 @@ class Vgg19(nn.Module):
                 seq.add_module(str(idx), feats[idx])
             setattr(self, f"slice{k}", seq)
         self._init(weights_path or os.environ.get("P2P_VGG19_WEIGHTS"))
+        # ReLU' of every conv whose output is not a loss tap moves into the next conv's dgrad
+        # epilogue (a max-pool in between passes it through: the pooled value is the arg-max
+        # input, so relu'(pool(y)) is relu'(y) where the gradient lands) -- no separate gate
+        # pass in the perceptual loss's backward (HIP path; the oracle ignores the flags)
+        for prod, cons in ((2, 5), (7, 10), (12, 14), (14, 16), (16, 19), (21, 23), (23, 25), (25, 28)):
+            feats[prod].out_gated = True
+            feats[cons].grad_gate = "relu"
         if not requires_grad:
             for p in self.parameters():
                 p.requires_grad = False

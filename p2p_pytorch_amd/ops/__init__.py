@@ -78,12 +78,13 @@ def act(x, name):
     return ref.apply_act(x, name)
 
 
-def add_act(a, b, name):
-    """act(a + b) -- one fused pass on the native path (residual joins)."""
+def add_act(a, b, name, defer_b=False):
+    """act(a + b) -- one fused pass on the native path (residual joins).  ``defer_b`` (HIP
+    path): hand b's gradient to the conv that also reads b (its ``skip_grad="take"``)."""
     if name is None:
         return a + b
     if _native.use_native(a):
-        return _hip().add_act(a, b, name)
+        return _hip().add_act(a, b, name, defer_b)
     return ref.apply_act(a + b, name)
 
 

@@ -436,8 +436,14 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
             Hp, Wp = H * cfg.up + 2 * p, W * cfg.up + 2 * p
             dxp = _conv_call(gyp, None, None, None, 1, KH, KW, s, 0, 0, 1, 0, Hp, Wp, Cp,
                              0, Cp, None, None, 0, C1, False, weight, 1, Cp, Coutp, "gy")[0]
+            res = None
+            if cfg.skip_grad == "take" and q2 is None and need_x1 and Cp == C1:
+                res = _DEFERRED.pop(q1.data_ptr(), None)   # the residual add's gradient
+                if res is not None and res.shape != (q1.shape[0], Cp, H, W):
+                    _DEFERRED[q1.data_ptr()] = res   # not fusable: added below instead
+                    res = None
             outs = [P().pad_fold(dxp, H, W, p, cfg.up, int(cfg.reflect),
-                                 q1 if act_in else None, act_in)]
+                                 q1 if act_in else None, act_in, res)]
         elif cfg.transposed:
             outs = _conv_call(gyp, None, None, None, 0, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
                               split, q1 if act_in else None,
@@ -871,11 +877,18 @@ def act(x, name):
 
 class AddActFn(torch.autograd.Function):
     """y = act(a + b) in one pass (act kernel mode 3); the gradient gates on the output sign,
-    which equals the sign of a + b for relu / lrelu, and flows unchanged to both inputs."""
+    which equals the sign of a + b for relu / lrelu, and flows unchanged to both inputs.
+    ``defer_b``: b's gradient is parked in ``_DEFERRED`` for the conv that also reads b
+    (``skip_grad="take"``: a residual block's first conv), which adds it in its dgrad
+    epilogue / pad fold -- no autograd accumulate kernel for the residual input."""
 
     @staticmethod
-    def forward(ctx, a, b, name):
-        a, b = to_nhwc_bf16(a), to_nhwc_bf16(b)
+    def forward(ctx, a, b, name, defer_b=False):
+        a = to_nhwc_bf16(a)
+        ctx.defer_key = None
+        if defer_b and b.dtype == torch.bfloat16 and b.is_contiguous(memory_format=CL):
+            ctx.defer_key = b.data_ptr()   # the storage the consuming conv reads (no copy)
+        b = to_nhwc_bf16(b)
         y = P().act(a, b, _act_code(name), 3)
         ctx.name = name
         ctx.save_for_backward(y)
@@ -885,11 +898,16 @@ class AddActFn(torch.autograd.Function):
     def backward(ctx, gy):
         (y,) = ctx.saved_tensors
         g = P().act(to_nhwc_bf16(gy), y, _act_code(ctx.name), 2)
-        return g, g, None
+        if ctx.defer_key is not None and ctx.needs_input_grad[1]:
+            if ctx.defer_key in _DEFERRED:
+                raise RuntimeError("skip_grad: a deferred gradient of this tensor is pending")
+            _DEFERRED[ctx.defer_key] = g
+            return g, None, None, None
+        return g, g, None, None
 
 
-def add_act(a, b, name):
-    return AddActFn.apply(a, b, name)
+def add_act(a, b, name, defer_b=False):
+    return AddActFn.apply(a, b, name, defer_b)
 
 
 class DropoutFn(torch.autograd.Function):

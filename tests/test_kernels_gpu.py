@@ -604,29 +604,32 @@ def test_avg_pool3_s2(C, H, W):
     assert rel_err(yh, yr) < 1e-2 and rel_err(gh, gr) < 1e-2
 
 
-HALO_K9_CASES = [
-    # (N, Cin, H, W, Cout, pad_mode, up): family R's 9x9 layers on the halo-tile kernel
-    (2, 32, 40, 36, 3, "reflect", 1),     # G.deconv1 (+ its dgrad: 8-ch gy, flipped taps)
-    (2, 12, 20, 18, 32, "reflect", 2),    # G.conv1 on the unshuffled image, nearest x2
-    (2, 16, 33, 35, 16, "zeros", 1),      # partial tiles, zero pad
+HALO_CASES = [
+    # (N, Cin, H, W, Cout, pad_mode, up, k): family R's full-resolution layers on the
+    # halo-tile kernels (csrc/halo_kxk.hip forward / flipped-tap dgrad, halo_wgrad.hip)
+    (2, 32, 40, 36, 3, "reflect", 1, 9),     # G.deconv1 (+ its dgrad: 8-ch gy, flipped taps)
+    (2, 12, 20, 18, 32, "reflect", 2, 9),    # G.conv1 on the unshuffled image, nearest x2
+    (2, 16, 33, 35, 16, "zeros", 1, 9),      # partial tiles, zero pad
+    (2, 64, 20, 18, 32, "reflect", 2, 3),    # G.deconv2 (64 -> 32, x2), wgrad 3x3 / 64 ch
+    (2, 3, 34, 30, 64, "zeros", 1, 3),       # VGG conv1_1 (image -> 64) + its 64 -> 8 dgrad
 ]
 
 
-@pytest.mark.parametrize("case", HALO_K9_CASES)
+@pytest.mark.parametrize("case", HALO_CASES)
 def test_halo_k9_conv(case, monkeypatch):
-    """9x9 stride-1 conv forward + input / weight gradients on the halo path vs fp32 (and vs
+    """Stride-1 conv forward + input / weight gradients on the halo paths vs fp32 (and vs
     the implicit-GEMM fallback, P2P_NO_HALO=1)."""
-    N, C, H, W, Co, mode, up = case
+    N, C, H, W, Co, mode, up, k = case
     g = torch.Generator(device=DEV).manual_seed(3)
     x = rand_img(N, C, H, W, seed=41)
-    w = (torch.randn(Co, C, 9, 9, device=DEV, generator=g) * 0.05).to(torch.bfloat16).float()
+    w = (torch.randn(Co, C, k, k, device=DEV, generator=g) * (0.4 / k)).to(torch.bfloat16).float()
     b = torch.randn(Co, device=DEV, generator=g) * 0.1
     gy_shape = (N, Co, H * up, W * up)
     gy = rand_img(*gy_shape, seed=42)
 
     def run():
         hx, hw, hb = _leaf(x), _leaf(w), _leaf(b)
-        y = ops.conv2d(hx, hw, hb, 1, 4, mode, up)
+        y = ops.conv2d(hx, hw, hb, 1, k // 2, mode, up)
         y.backward(gy)
         return y.float(), hx.grad.float(), hw.grad.float(), hb.grad.float()
 
@@ -635,7 +638,7 @@ def test_halo_k9_conv(case, monkeypatch):
     yf, gxf, gwf, gbf = run()
     monkeypatch.delenv("P2P_NO_HALO")
     rx, rw, rb = _leaf(x.float()), _leaf(w), _leaf(b)
-    ry = ref.conv2d(rx, rw, rb, 1, 4, mode, up)
+    ry = ref.conv2d(rx, rw, rb, 1, k // 2, mode, up)
     ry.backward(gy.float())
     assert yh.shape == ry.shape
     assert rel_err(yh, ry) < 1e-2, rel_err(yh, ry)
