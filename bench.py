@@ -65,6 +65,10 @@ def parse():
     p.add_argument("--precision", default=os.environ.get("P2P_PRECISION", "bf16"), choices=["bf16", "fp8"],
                    help="(native) conv GEMM operands: bf16, or fp8 (e4m3 fwd / e5m2 dgrad, bf16 wgrad; "
                         "BASELINE config 5)")
+    p.add_argument("--c_phase_backward", type=int, default=1, choices=[0, 1],
+                   help="(--family ref) run the reference's C-phase backward (locc.backward(),"
+                        " train.py:400-402) even though with the reference's optimizer_c it updates"
+                        " nothing -- 1 (default) times the reference's full step")
     p.add_argument("--json_out", default=None)
     return p.parse_args()
 
@@ -127,7 +131,8 @@ def main():
         autocast = None
     if ref:
         from p2p_pytorch_amd.engine.compress_gan import CompressGANStep
-        trainer = CompressGANStep(netG, netD, netC, reducer_g=reducer_g, reducer_d=reducer_d)
+        trainer = CompressGANStep(netG, netD, netC, reducer_g=reducer_g, reducer_d=reducer_d,
+                                  c_phase_backward=bool(args.c_phase_backward))
     else:
         trainer = Pix2PixStep(netG, netD, lr=2e-4, beta1=0.5, gan_mode=args.gan_mode,
                               lambda_L1=args.lamb, reducer_g=reducer_g, reducer_d=reducer_d,
@@ -231,6 +236,7 @@ def main():
                    "image_size": S, "parallelism": f"dp{world}", "impl": args.impl,
                    "gan_mode": args.gan_mode, "lambda_L1": args.lamb,
                    "hipgraph": bool(use_graph),
+                   **({"c_phase_backward": bool(args.c_phase_backward)} if ref else {}),
                    "conv_precision": ("fp8 e4m3 fwd / e5m2 dgrad, bf16 wgrad + first/last layers"
                                       if args.precision == "fp8" else "bf16")},
         "max_mem_gib": (round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)

@@ -422,7 +422,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   // stride-1 9x9 convs with 8-32 input channels and <= 32 outputs (family R's full-res
   // layers): the halo-tile direct conv (csrc/halo_kxk.hip); MODE 1 stride 1 = flipped taps
   const bool halo_geo = (KH == 9 && KW == 9 && (C1 == 8 || C1 == 16 || C1 == 32) && Cout <= 32) ||
-                        (KH == 3 && KW == 3 && ((C1 == 64 && Cout <= 32) || (C1 == 8 && Cout > 48 && Cout <= 64)));
+                        (KH == 3 && KW == 3 && C1 == 64 && Cout <= 32);
   if (rc == -2 && !fp8 && C2 == 0 && halo_geo && stride == 1 && Csplit == Cout && act_in == 0 && act_bwd == 0 &&
       !a.res1 && !a.q_out && !a.stats && (mode == 0 || (up == 1 && !reflect && pad <= KH - 1)) &&
       std::getenv("P2P_NO_HALO") == nullptr) {

@@ -59,7 +59,10 @@ struct HaloK {
   static constexpr int LSH = CPP == 8 ? 1 : (CPP == 4 ? 2 : (CPP == 2 ? 3 : 4));   // log2(16 / CPP)
   static constexpr int HT = 16;
   static constexpr int HP = HT + KS - 1;             // halo edge
-  static constexpr int HPIX = HP * HP;
+  // LDS row stride (pixels): a wave's 4 output rows are 4 apart, so 4 * HPS = 0 mod 16 keeps
+  // the chunk swizzle (pixel bits < 4) identical on all four -- one address per K-slice
+  static constexpr int HPS = (HP + 3) / 4 * 4;
+  static constexpr int HPIX = HP * HPS;
   static constexpr int HUNITS = HPIX * CPP;
   static constexpr int HLD = (HUNITS + 255) / 256;   // glds per lane per stage
   static constexpr int STAGE_UNITS = HLD * 256;
@@ -81,7 +84,8 @@ __global__ void __launch_bounds__(256) halo_kxk_kernel(HaloKArgs a) {
   bf16* As = reinterpret_cast<bf16*>(smem);                                 // 2 stages
   bf16* Bs = reinterpret_cast<bf16*>(smem + 2 * G::STAGE_BYTES);            // [S][NBLK][16][4 units]
   bf16* Ed = reinterpret_cast<bf16*>(smem + 2 * G::STAGE_BYTES + BUNITS_PAD * 16);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int my_tiles = (a.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
   if (my_tiles <= 0) return;
 
@@ -107,8 +111,9 @@ __global__ void __launch_bounds__(256) halo_kxk_kernel(HaloKArgs a) {
   for (int j = 0; j < G::HLD; ++j) {
     const int e = (j * 4 + wid) * 64 + lane;
     const int hp = e / G::CPP;
-    hy[j] = hp < G::HPIX ? hp / G::HP : -100000;
-    hx[j] = hp - (hp / G::HP) * G::HP;
+    const int hxx = hp % G::HPS;
+    hy[j] = hp < G::HPIX && hxx < G::HP ? hp / G::HPS : -100000;   // padding column: zero
+    hx[j] = hxx;
     hc[j] = (e % G::CPP) ^ ((hp >> G::LSH) & (G::CPP - 1));
   }
   const int VH = a.H * a.up, VW = a.W * a.up;
@@ -131,10 +136,8 @@ __global__ void __launch_bounds__(256) halo_kxk_kernel(HaloKArgs a) {
       if (a.reflect) {
         iy = iy < 0 ? -iy : (iy >= VH ? 2 * (VH - 1) - iy : iy);
         ix = ix < 0 ? -ix : (ix >= VW ? 2 * (VW - 1) - ix : ix);
-        inb = hy[j] >= 0 && (unsigned)iy < (unsigned)VH && (unsigned)ix < (unsigned)VW;
-      } else {
-        inb = (unsigned)iy < (unsigned)VH && (unsigned)ix < (unsigned)VW;
       }
+      inb = hy[j] >= 0 && (unsigned)iy < (unsigned)VH && (unsigned)ix < (unsigned)VW;
       const int sy = a.up == 2 ? iy >> 1 : iy, sx = a.up == 2 ? ix >> 1 : ix;
       const bf16* g = inb ? a.x + ((long)(n * a.H + sy) * a.W + sx) * CIN + hc[j] * 8 : a.zero;
       glds16k(g, dst + (j * 4 + wid) * 64 * 8);
@@ -151,9 +154,10 @@ __global__ void __launch_bounds__(256) halo_kxk_kernel(HaloKArgs a) {
   // this lane's tap within a slice and chunk within the tap
   const int tsub = CIN <= 32 ? kq / G::CPP : 0, csub0 = CIN <= 32 ? kq % G::CPP : kq;
   const int bslot = kq ^ ((px >> 2) & 3);
-  int rowbase[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) rowbase[i] = (wid * 4 + i) * G::HP + px;
+  // the wave's output rows are wid + 4i (i < 4): row i's A fragment sits ISTRIDE elements
+  // after row 0's (same swizzle, see HPS)
+  constexpr int ISTRIDE = 4 * G::HPS * G::CPP * 8;
+  const int rowbase = wid * G::HPS + px;
 
   issue(0, 0);
   for (int it = 0; it < my_tiles; ++it) {
@@ -169,7 +173,7 @@ __global__ void __launch_bounds__(256) halo_kxk_kernel(HaloKArgs a) {
     const bf16* A = As + stage * (G::STAGE_UNITS * 8);
     // the lane's tap walks t = s * TPS + tsub incrementally (loop-carried: the compiler must
     // not hoist 81 per-slice offsets into registers across the tile loop)
-    int dx = tsub % KS, toff = (tsub / KS) * G::HP + tsub % KS, sub = 0;
+    int dx = tsub % KS, toff = (tsub / KS) * G::HPS + tsub % KS, sub = 0;
     const bf16* bp = Bs + (px * 4 + bslot) * 8;
 #pragma unroll 2
     for (int s = 0; s < G::S; ++s) {
@@ -178,9 +182,10 @@ __global__ void __launch_bounds__(256) halo_kxk_kernel(HaloKArgs a) {
       bf16x8 bfr[NBLK];
 #pragma unroll
       for (int nb = 0; nb < NBLK; ++nb) bfr[nb] = lds_frag(bp + nb * 16 * 4 * 8, hswap);
+      const bf16* a0 = A + G::aslot(rowbase + to, csub) * 8;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const bf16x8 af = lds_frag(A + G::aslot(rowbase[i] + to, csub) * 8, hswap);
+        const bf16x8 af = lds_frag(a0 + i * ISTRIDE, hswap);
 #pragma unroll
         for (int nb = 0; nb < NBLK; ++nb)
           acc[i][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[nb], acc[i][nb], 0, 0, 0);
@@ -194,7 +199,7 @@ __global__ void __launch_bounds__(256) halo_kxk_kernel(HaloKArgs a) {
       for (int w = 0; w < (G::TPS + KS - 1) / KS; ++w)   // TPS may exceed KS (3x3, 8 ch)
         if (dx >= KS) {
           dx -= KS;
-          toff += G::HP - KS;
+          toff += G::HPS - KS;
         }
     }
     __builtin_amdgcn_s_barrier();   // every wave done reading this stage
@@ -210,7 +215,7 @@ __global__ void __launch_bounds__(256) halo_kxk_kernel(HaloKArgs a) {
       for (int i = 0; i < 4; ++i) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int q = (wid * 4 + i) * 16 + kq * 4 + r;
+          const int q = (wid + 4 * i) * 16 + kq * 4 + r;
           Cs[q * LDCS + co] = (bf16)act_fwd(acc[i][nb][r] + bj, a.act_out);
         }
         acc[i][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -269,11 +274,11 @@ extern "C" int p2p_halo_kxk(const p2p::HaloKArgs* a, int KS, int blocks, hipStre
     }
   }
   if (KS == 3) {
-    // 64-channel inputs into <= 32 outputs (G.deconv2, VGG conv1_1's input gradient) and
-    // the 8-channel image into 64 (VGG conv1_1)
+    // 64-channel inputs into <= 32 outputs (G.deconv2, VGG conv1_1's input gradient).  The
+    // 8-channel image into 64 (VGG conv1_1) measured 1.6x slower than the implicit GEMM: its
+    // 3 K-slices per tile leave the 64-channel epilogue stores exposed
     if (a->C == 64 && nblk == 1) return launch_halo_kxk<3, 64, 1>(*a, blocks, st);
     if (a->C == 64 && nblk == 2) return launch_halo_kxk<3, 64, 2>(*a, blocks, st);
-    if (a->C == 8 && nblk == 4) return launch_halo_kxk<3, 8, 4>(*a, blocks, st);
     return -2;
   }
   return -2;

@@ -59,7 +59,10 @@ struct HaloW {
   static constexpr int KK = KS * KS;
   static constexpr int HT = 16;
   static constexpr int HP = HT + KS - 1;
-  static constexpr int HPIX = HP * HP;
+  // LDS row stride (pixels): K-steps advance 2 rows, so 2 * HPS = 0 mod 16 leaves every
+  // swizzle (pixel bits < 4) unchanged -- the read offsets are computed once per kernel
+  static constexpr int HPS = (HP + 7) / 8 * 8;
+  static constexpr int HPIX = HP * HPS;
   static constexpr int XCPP = CIN / 8;
   static constexpr int GCPP = RL / 8;
   static constexpr int XLD = (HPIX * XCPP + 255) / 256;
@@ -76,7 +79,8 @@ template <int KS, int CIN, int RL>
 __global__ void __launch_bounds__(256) halo_wgrad_kernel(HaloWArgs a) {
   using G = HaloW<KS, CIN, RL>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int my_tiles = (a.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
 
   // ---- per-lane staging units (fixed across tiles)
@@ -93,8 +97,9 @@ __global__ void __launch_bounds__(256) halo_wgrad_kernel(HaloWArgs a) {
       hp = slot ^ (((slot >> 3) & 1) << 2);   // the swizzle is an involution
       c = e & 1;
     }
-    hy[j] = hp < G::HPIX ? hp / G::HP : -100000;
-    hx[j] = hp - (hp / G::HP) * G::HP;
+    const int hxx = hp % G::HPS;
+    hy[j] = hp < G::HPIX && hxx < G::HP ? hp / G::HPS : -100000;   // padding column: zero
+    hx[j] = hxx;
     hc[j] = c;
   }
   int gp[G::GLD], gc[G::GLD];
@@ -157,6 +162,25 @@ __global__ void __launch_bounds__(256) halo_wgrad_kernel(HaloWArgs a) {
   const int prow = g >> 1, pcol = 8 * (g & 1) + q;
   const int pch = (p >> 1), phalf = (p & 1) * 8;   // chunk within a 16-channel block, byte half
 
+  // read offsets (bytes) of K-step 0; K-step j adds j * XSTEP / YSTEP (same swizzle)
+  constexpr int XSTEP = 2 * G::HPS * G::XCPP * 16, YSTEP = 32 * G::GCPP * 16;
+  int ax0[G::IPW], ax1[G::IPW];
+#pragma unroll
+  for (int u = 0; u < G::IPW; ++u) {
+    const int item = min(wid + 4 * u, G::ITEMS - 1);
+    const int t = item / G::CB, cb = item % G::CB;
+    const int hp = prow * G::HPS + pcol + (t / KS) * G::HPS + (t % KS);
+    ax0[u] = wunit<CIN>(hp, cb * 2 + pch) * 16 + phalf;
+    ax1[u] = wunit<CIN>(hp + 4, cb * 2 + pch) * 16 + phalf;
+  }
+  int gy0[G::RB], gy1[G::RB];
+#pragma unroll
+  for (int rb = 0; rb < G::RB; ++rb) {
+    const int gpx = prow * 16 + pcol;
+    gy0[rb] = wunit<RL>(gpx, rb * 2 + pch) * 16 + phalf;
+    gy1[rb] = wunit<RL>(gpx + 4, rb * 2 + pch) * 16 + phalf;
+  }
+
   if (my_tiles > 0) issue(0, 0);
   for (int it = 0; it < my_tiles; ++it) {
     const int stage = it & 1;
@@ -170,30 +194,24 @@ __global__ void __launch_bounds__(256) halo_wgrad_kernel(HaloWArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     const char* X = smem + stage * G::STAGE_BYTES;
     const char* Y = X + G::XUNITS * 16;
+#pragma unroll
     for (int j = 0; j < 8; ++j) {
-      s16x4 b0[G::RB], b1[G::RB];
-      const int gpx = (2 * j + prow) * 16 + pcol;
+      bf16x8 bfr[G::RB];
 #pragma unroll
       for (int rb = 0; rb < G::RB; ++rb) {
-        b0[rb] = tr_read(Y + wunit<RL>(gpx, rb * 2 + pch) * 16 + phalf);
-        b1[rb] = tr_read(Y + wunit<RL>(gpx + 4, rb * 2 + pch) * 16 + phalf);
+        const s16x4 b0 = tr_read(Y + gy0[rb] + j * YSTEP);
+        const s16x4 b1 = tr_read(Y + gy1[rb] + j * YSTEP);
+        bfr[rb] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
       }
-      const int xbase = (2 * j + prow) * G::HP + pcol;
 #pragma unroll
       for (int u = 0; u < G::IPW; ++u) {
-        const int item = wid + 4 * u;
-        if (u == G::IPW - 1 && item >= G::ITEMS) break;   // wave-uniform: EXEC stays full
-        const int t = item / G::CB, cb = item % G::CB;
-        const int hp = xbase + (t / KS) * G::HP + (t % KS);
-        const s16x4 a0 = tr_read(X + wunit<CIN>(hp, cb * 2 + pch) * 16 + phalf);
-        const s16x4 a1 = tr_read(X + wunit<CIN>(hp + 4, cb * 2 + pch) * 16 + phalf);
+        if (u == G::IPW - 1 && wid + 4 * u >= G::ITEMS) break;   // wave-uniform: EXEC stays full
+        const s16x4 a0 = tr_read(X + ax0[u] + j * XSTEP);
+        const s16x4 a1 = tr_read(X + ax1[u] + j * XSTEP);
         const bf16x8 af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
-        for (int rb = 0; rb < G::RB; ++rb) {
-          const bf16x8 bfr =
-              __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0[rb], b1[rb], 0, 1, 2, 3, 4, 5, 6, 7));
-          acc[u][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[u][rb], 0, 0, 0);
-        }
+        for (int rb = 0; rb < G::RB; ++rb)
+          acc[u][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[rb], acc[u][rb], 0, 0, 0);
       }
     }
     __builtin_amdgcn_s_barrier();   // every wave done with this stage before it is refilled

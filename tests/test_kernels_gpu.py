@@ -611,7 +611,7 @@ HALO_CASES = [
     (2, 12, 20, 18, 32, "reflect", 2, 9),    # G.conv1 on the unshuffled image, nearest x2
     (2, 16, 33, 35, 16, "zeros", 1, 9),      # partial tiles, zero pad
     (2, 64, 20, 18, 32, "reflect", 2, 3),    # G.deconv2 (64 -> 32, x2), wgrad 3x3 / 64 ch
-    (2, 3, 34, 30, 64, "zeros", 1, 3),       # VGG conv1_1 (image -> 64) + its 64 -> 8 dgrad
+    (2, 3, 34, 30, 64, "zeros", 1, 3),       # VGG conv1_1: its 64 -> 8 dgrad (flipped taps)
 ]
 
 
