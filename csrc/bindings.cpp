@@ -163,7 +163,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                              bool want_stats, const optional<Tensor>& qs_x1,
                              const optional<Tensor>& qs_x2, const optional<Tensor>& qs_w,
                              const optional<Tensor>& y_qsite, int64_t y_qfmt,
-                             const optional<Tensor>& res) {
+                             const optional<Tensor>& res, const optional<Tensor>& alpha) {
   check_act(x1, "conv_fwd x1", true);
   // fp8 operands: x e4m3 (activations) or e5m2 (gradients), weight image e4m3, each with
   // an fp8 scale site (csrc/fp8.hip); outputs stay bf16
@@ -227,6 +227,10 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   a.Cout = (int)Cout;
   a.w = w.data_ptr();
   a.bias = bias ? bias->data_ptr<float>() : nullptr;
+  if (alpha)
+    TORCH_CHECK(alpha->is_cuda() && alpha->scalar_type() == at::kFloat && alpha->numel() == 1,
+                "conv_fwd: alpha must be a 1-element fp32 GPU tensor");
+  a.alpha = alpha ? alpha->data_ptr<float>() : nullptr;
   a.act_out = (int)act_out;
   a.y1 = y1.data_ptr();
   a.y2 = y2.defined() ? y2.data_ptr() : nullptr;
@@ -262,6 +266,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       C2 % 64 == 0) {
     TORCH_CHECK(!fp8, "conv_fwd: fp8 is not supported on the tiny-Cout col path");
     TORCH_CHECK(!res, "conv_fwd: no residual on the tiny-Cout col path");
+    TORCH_CHECK(!alpha, "conv_fwd: no alpha on the tiny-Cout col path");
     // col[i][t*Cvp + co]: each tap's outputs padded to Cvp (4 / 8 / 16) so col2im reads
     // one aligned vector per tap
     const int64_t T = KH * KW;
@@ -388,7 +393,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   int rc = -2;
   // packed 8-channel image convs (4x4 s2 p1): the halo-tile kernel (csrc/halo_pk8.hip)
   if (mode == 0 && !fp8 && C1 == 8 && C2 == 0 && KH == 4 && KW == 4 && stride == 2 && pad == 1 && !reflect &&
-      up == 1 && act_in == 0 && splits == 1 && !a.stats && !a.q_out && !a.res1 && (Cout == 64 || Cout == 128) &&
+      up == 1 && act_in == 0 && splits == 1 && !a.stats && !a.q_out && !a.res1 && !a.alpha && (Cout == 64 || Cout == 128) &&
       std::getenv("P2P_NO_HALO") == nullptr) {
     p2p::HaloPk8Args h{};
     h.x = static_cast<const __bf16*>(x1.data_ptr());
@@ -424,7 +429,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   const bool halo_geo = (KH == 9 && KW == 9 && (C1 == 8 || C1 == 16 || C1 == 32) && Cout <= 32) ||
                         (KH == 3 && KW == 3 && C1 == 64 && Cout <= 32);
   if (rc == -2 && !fp8 && C2 == 0 && halo_geo && stride == 1 && Csplit == Cout && act_in == 0 && act_bwd == 0 &&
-      !a.res1 && !a.q_out && !a.stats && (mode == 0 || (up == 1 && !reflect && pad <= KH - 1)) &&
+      !a.res1 && !a.q_out && !a.stats && !a.alpha && (mode == 0 || (up == 1 && !reflect && pad <= KH - 1)) &&
       std::getenv("P2P_NO_HALO") == nullptr) {
     p2p::HaloKArgs h{};
     h.x = static_cast<const __bf16*>(x1.data_ptr());
@@ -1409,7 +1414,8 @@ TORCH_LIBRARY(p2p, m) {
   m.def("conv_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, int mode, int KH, int KW, int stride, "
         "int pad, int reflect, int up, int act_in, int OH, int OW, int Cout, int act_out, int Csplit, "
         "Tensor? xb1, Tensor? xb2, int act_bwd, int Cvalid=0, bool want_stats=False, Tensor? qs_x1=None, "
-        "Tensor? qs_x2=None, Tensor? qs_w=None, Tensor(a!)? y_qsite=None, int y_qfmt=0, Tensor? res=None) -> Tensor[]");
+        "Tensor? qs_x2=None, Tensor? qs_w=None, Tensor(a!)? y_qsite=None, int y_qfmt=0, Tensor? res=None, "
+        "Tensor? alpha=None) -> Tensor[]");
   m.def("fp8_quant(Tensor x, Tensor(a!) site, int fmt, int use_cur=0) -> Tensor");
   m.def("sn_power_iter(Tensor w, Tensor(a!) u, Tensor(b!) v) -> Tensor");
   m.def("fp8_amax(Tensor x, Tensor(a!) site, int slot) -> ()");

@@ -21,6 +21,8 @@ struct ConvFwdArgs {
   int OH, OW, Cout;
   const void* w;   // bf16 [Cout][KH][KW][C]
   const float* bias;  // [Cout] or null
+  const float* alpha; // device scalar multiplying the accumulator before the bias (null = 1):
+                      // spectral norm's 1 / sigma without materialising W / sigma
   int act_out;
   void* y1;        // bf16 output, channels [0, Csplit): NHWC with ld = Csplit
   void* y2;        // bf16 output, channels [Csplit, Cout): ld = Cout - Csplit (may be null)

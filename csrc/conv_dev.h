@@ -126,6 +126,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
   constexpr int LDC = BN + 8;
   // the activation is dispatched ONCE per tile (compile-time body per code), not by a
   // wave-uniform branch per accumulator element
+  const float al = a.alpha ? a.alpha[0] : 1.f;
   auto stage_tile = [&](auto act_tag) __attribute__((always_inline)) {
     constexpr int ACT = decltype(act_tag)::value;
 #pragma unroll
@@ -138,7 +139,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
         const int rowb = wm * TM * 16 + i * 16 + (lane >> 4) * 4;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          Cs[(rowb + r) * LDC + coll] = (bf16)act_fwd(acc[i][j][r] + bj, ACT);
+          Cs[(rowb + r) * LDC + coll] = (bf16)act_fwd(acc[i][j][r] * al + bj, ACT);
       }
     }
   };

@@ -276,6 +276,11 @@ __global__ void __launch_bounds__(256) conv_finalize_kernel(ConvFwdArgs a, long 
       }
     }
     float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    if (a.alpha) {
+      const float al = a.alpha[0];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= al;
+    }
     if (a.bias) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += a.bias[co + j];

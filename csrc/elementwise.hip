@@ -433,6 +433,77 @@ static inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) 
 
 }  // namespace p2p
 
+namespace p2p {
+// Stride-1, no-upsample fold (the residual blocks' reflect-pad dgrads): one thread per (pixel,
+// 4 chunks of 8 channels), the pixel's 1-4 source positions resolved once, 4 independent 16-B
+// loads per source in flight, int32 indexing (host-checked sizes).
+__global__ void __launch_bounds__(256) pad_fold_s1_kernel(const bf16* __restrict__ dxp, int N, int H, int W,
+                                                          int C, int pad, int reflect,
+                                                          const bf16* __restrict__ xb, int act,
+                                                          const bf16* __restrict__ res,
+                                                          bf16* __restrict__ dx) {
+  const int CQ = C >> 5;   // groups of 4 chunks per pixel
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+  const int total = N * H * W * CQ;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
+    const int cq = e % CQ;
+    const int pix = e / CQ;
+    const int x = pix % W;
+    const int t = pix / W;
+    const int y = t % H, n = t / H;
+    int qy[3], qx[3], ny = 0, nx = 0;
+    qy[ny++] = y + pad;
+    qx[nx++] = x + pad;
+    if (reflect) {
+      if (y >= 1 && y <= pad) qy[ny++] = pad - y;                       // reflected top rows
+      if (y >= H - 1 - pad && y <= H - 2) qy[ny++] = 2 * (H - 1) + pad - y;   // bottom rows
+      if (x >= 1 && x <= pad) qx[nx++] = pad - x;
+      if (x >= W - 1 - pad && x <= W - 2) qx[nx++] = 2 * (W - 1) + pad - x;
+    }
+    float acc[4][8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+    for (int i = 0; i < ny; ++i)
+      for (int k2 = 0; k2 < nx; ++k2) {
+        const bf16* src = dxp + ((n * Hp + qy[i]) * Wp + qx[k2]) * C + cq * 32;
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const u32x4*>(src + k * 8);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float f[8];
+          unpack8e(v[k], f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[k][j] += f[j];
+        }
+      }
+    const int o = pix * C + cq * 32;
+    if (act) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float xf[8];
+        unpack8e(*reinterpret_cast<const u32x4*>(xb + o + k * 8), xf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[k][j] *= act_grad_from_input(xf[j], act);
+      }
+    }
+    if (res) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float rf[8];
+        unpack8e(*reinterpret_cast<const u32x4*>(res + o + k * 8), rf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[k][j] += rf[j];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) *reinterpret_cast<u32x4*>(dx + o + k * 8) = pack8e(acc[k]);
+  }
+}
+}  // namespace p2p
+
 extern "C" {
 
 int p2p_act(const void* a, const void* b, long n, int act, int mode, void* out, hipStream_t st) {
@@ -462,6 +533,16 @@ int p2p_pad_channels(const void* a, int Ca, const void* b, int Cb, long P, int C
 int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, int reflect,
                  const void* xb, int act, const void* res, void* dx, hipStream_t st) {
   using namespace p2p;
+  const long padded = (long)N * (H + 2 * pad) * (W + 2 * pad) * C;
+  if (up == 1 && C % 32 == 0 && pad < H - 1 && pad < W - 1 && padded < (1L << 31)) {
+    const long work = (long)N * H * W * (C / 32);
+    long b = (work + 255) / 256;
+    b = b > 8192 ? 8192 : (b < 1 ? 1 : b);
+    hipLaunchKernelGGL(pad_fold_s1_kernel, dim3((unsigned)b), dim3(256), 0, st, static_cast<const bf16*>(dxp), N,
+                       H, W, C, pad, reflect, static_cast<const bf16*>(xb), act, static_cast<const bf16*>(res),
+                       static_cast<bf16*>(dx));
+    return (int)hipGetLastError();
+  }
   const long total = (long)N * H * W * (C / 8);
   hipLaunchKernelGGL(pad_fold_kernel, dim3(egrid(total)), dim3(256), 0, st, static_cast<const bf16*>(dxp), N,
                      H, W, C, pad, up, reflect, static_cast<const bf16*>(xb), act, static_cast<const bf16*>(res),

@@ -534,8 +534,22 @@ __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
   if (sh.q) fp8_amax_commit(qmax, sh.site);
 }
 
-// finalize-pass launches: many chunks per group -> 8 channels x 32 chunk-lanes per block
+// finalize-pass launches: many chunks per group -> 8 channels x 32 chunk-lanes per block;
+// batch norm over N*H*W (thousands of chunks per channel) -> one channel x 256 chunk-lanes
+// per block (the merge was latency-bound: 64 dependent merges per lane, 16 blocks busy)
 static inline bool fin_wide(const NormGeom& g) { return g.nchunks >= 64; }
+static inline bool fin_huge(const NormGeom& g) { return g.nchunks >= 512; }
+
+// launch a finalize-style kernel with the (channels, chunk-lanes) split chosen by nchunks
+#define P2P_FIN_LAUNCH(KERNEL, g, ny, st, ...)                                                            \
+  do {                                                                                                   \
+    if (fin_huge(g))                                                                                     \
+      hipLaunchKernelGGL((KERNEL<1, 256>), dim3((g).C, ny), dim3(256), 0, st, __VA_ARGS__);              \
+    else if (fin_wide(g))                                                                                \
+      hipLaunchKernelGGL((KERNEL<8, 32>), dim3(((g).C + 7) / 8, ny), dim3(256), 0, st, __VA_ARGS__);     \
+    else                                                                                                 \
+      hipLaunchKernelGGL((KERNEL<32, 8>), dim3(((g).C + 31) / 32, ny), dim3(256), 0, st, __VA_ARGS__);   \
+  } while (0)
 
 static inline NormGeom make_geom(int N, int HW, int C) {
   NormGeom g;
@@ -575,12 +589,7 @@ int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* ga
   NormGeom g = make_geom(N, HW, C);
   hipLaunchKernelGGL(norm_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
                      static_cast<const bf16*>(x), g, ws);
-  if (fin_wide(g))
-    hipLaunchKernelGGL((norm_finalize_kernel<8, 32>), dim3((C + 7) / 8, N), dim3(256), 0, st, ws, g, eps, mean,
-                       rstd, run_mean, run_var, momentum);
-  else
-    hipLaunchKernelGGL((norm_finalize_kernel<32, 8>), dim3((C + 31) / 32, N), dim3(256), 0, st, ws, g, eps, mean,
-                       rstd, run_mean, run_var, momentum);
+  P2P_FIN_LAUNCH(norm_finalize_kernel, g, N, st, ws, g, eps, mean, rstd, run_mean, run_var, momentum);
   if (y)
     with_act(prelu_w ? ACT_PRELU_T : act, [&](auto t) {
       hipLaunchKernelGGL((norm_apply_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st,
@@ -605,12 +614,7 @@ int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, cons
   pg.C = C;
   pg.chunk = HW / nchunks;
   pg.nchunks = nchunks;
-  if (fin_wide(pg))
-    hipLaunchKernelGGL((norm_finalize_kernel<8, 32>), dim3((C + 7) / 8, N), dim3(256), 0, st, partials, pg, eps,
-                       mean, rstd, run_mean, run_var, momentum);
-  else
-    hipLaunchKernelGGL((norm_finalize_kernel<32, 8>), dim3((C + 31) / 32, N), dim3(256), 0, st, partials, pg, eps,
-                       mean, rstd, run_mean, run_var, momentum);
+  P2P_FIN_LAUNCH(norm_finalize_kernel, pg, N, st, partials, pg, eps, mean, rstd, run_mean, run_var, momentum);
   NormGeom g = make_geom(N, HW, C);
   with_act(prelu_w ? ACT_PRELU_T : act, [&](auto t) {
     hipLaunchKernelGGL((norm_apply_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st,
@@ -658,18 +662,15 @@ int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const floa
     if (rc) return rc;
   }
   if (dgamma) {
-    if (fin_wide(g) || N > 8)
+    if (fin_huge(g))
+      hipLaunchKernelGGL((norm_param_grad_kernel<1, 256>), dim3(C), dim3(256), 0, st, ws, g, dgamma, dbeta);
+    else if (fin_wide(g) || N > 8)
       hipLaunchKernelGGL((norm_param_grad_kernel<8, 32>), dim3((C + 7) / 8), dim3(256), 0, st, ws, g, dgamma, dbeta);
     else
       hipLaunchKernelGGL((norm_param_grad_kernel<32, 8>), dim3((C + 31) / 32), dim3(256), 0, st, ws, g, dgamma, dbeta);
   }
   if (dx) {
-    if (fin_wide(g))
-      hipLaunchKernelGGL((norm_bwd_finalize_kernel<8, 32>), dim3((C + 7) / 8, N), dim3(256), 0, st, ws, g, rstd,
-                         gamma, coef);
-    else
-      hipLaunchKernelGGL((norm_bwd_finalize_kernel<32, 8>), dim3((C + 31) / 32, N), dim3(256), 0, st, ws, g, rstd,
-                         gamma, coef);
+    P2P_FIN_LAUNCH(norm_bwd_finalize_kernel, g, N, st, ws, g, rstd, gamma, coef);
     with_act(a, [&](auto t) {
       hipLaunchKernelGGL((norm_bwd_apply_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st, xb, db,
                          g, mean, rstd, gamma, beta, prelu_w, coef, static_cast<bf16*>(dx),

@@ -225,8 +225,19 @@ class SpectralNorm(nn.Module):
 
     def forward(self, x):
         m = self.module
+        w = getattr(m, self.name + "_bar")
+        pad_mode = getattr(m, "pad_mode", "zeros")
+        if w.is_cuda and _native.use_native(w) and pad_mode == "zeros" and m.padding[0] == m.padding[1]:
+            # 1 / sigma stays a device scalar applied in the conv epilogues (ops/hip.py SNConvFn)
+            u = getattr(m, self.name + "_u")
+            v = getattr(m, self.name + "_v")
+            with torch.autocast(device_type=w.device.type, enabled=False):
+                sigma = ops_hip().spectral_sigma(w.reshape(w.shape[0], -1), u, v, self.power_iterations)
+                scale = sigma.reciprocal()
+            return ops_hip().sn_conv2d(x, w, m.bias, scale, m.stride, m.padding,
+                                       getattr(m, "act_in", None), getattr(m, "act_out", None))
         w = self.normalized_weight()
-        return ops.conv2d(x, w, m.bias, m.stride, m.padding, getattr(m, "pad_mode", "zeros"), 1,
+        return ops.conv2d(x, w, m.bias, m.stride, m.padding, pad_mode, 1,
                           getattr(m, "act_in", None), getattr(m, "act_out", None))
 
 

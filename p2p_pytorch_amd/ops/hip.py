@@ -139,7 +139,7 @@ def _weight_image_fp8(w: torch.Tensor, swap: int, xp: int, yp: int):
 
 def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout, act_out,
                Csplit, xb1, xb2, act_bwd, Cvalid, want, weight=None, swap=0, xp=0, yp=0, role="x",
-               y_qkey=None, res=None):
+               y_qkey=None, res=None, alpha=None):
     """conv_fwd on bf16 operands, or -- fp8 precision and a geometry the fp8 kernel takes --
     on fp8 ones: x (role 'x': activations, e4m3; 'gy': gradients, e5m2) quantised with
     delayed scaling (or taken from the producer's fused shadow), the weight image with
@@ -160,7 +160,8 @@ def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, 
         a1, s1 = _f8.quant(x1, (k, role, 1), fmt)
         a2, s2 = _f8.quant(x2, (k, role, 2), fmt) if x2 is not None else (None, None)
         return P().conv_fwd(a1, a2, w8, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout,
-                            act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, s1, s2, sw, *yq, res=res)
+                            act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, s1, s2, sw, *yq, res=res,
+                            alpha=alpha)
     if wimg is None:
         wimg = _weight_image(weight, swap, xp, yp)
     yq = ()
@@ -168,7 +169,7 @@ def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, 
         ysite, fresh = _f8.producer_site(x1.device, y_qkey)
         yq = (None, None, None, None, 0) if fresh else (None, None, None, ysite, _f8.E4M3)
     return P().conv_fwd(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout,
-                        act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, *yq, res=res)
+                        act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, *yq, res=res, alpha=alpha)
 
 
 def prepare_weights(*modules):
@@ -413,7 +414,65 @@ class ConvFn(torch.autograd.Function):
         return gx1, gx2, gw, gb, None
 
 
-def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, need_b):
+class SNConvFn(torch.autograd.Function):
+    """y = act(conv(x, w_bar * s) + b) with s = 1 / sigma a DEVICE scalar (spectral norm,
+    /root/reference/networks.py:543-549): the kernels scale the accumulator by s in the
+    epilogue (conv.h ``alpha``), so W / sigma is never materialised and the bf16 weight image
+    of w_bar is cast once per step for all of the step's D forwards.
+
+    Backward: dx = dgrad(gy_eff, w_bar) * s (epilogue again); with G = wgrad(gy_eff, x),
+    dL/dw_bar = s * G and dL/ds = <G, w_bar>, which autograd chains through s = 1 / sigma(w_bar)
+    -- the same gradient as the reference's ``w / sigma``."""
+
+    @staticmethod
+    def forward(ctx, x, w_bar, bias, scale, cfg: _ConvCfg):
+        if cfg.transposed or cfg.reflect or cfg.up != 1:
+            raise NotImplementedError("SNConvFn: plain zero-padded convs only")
+        q1, _, C1, _, Cp, packed = _prep_inputs(x, None)
+        N, _, H, W = q1.shape
+        KH, KW, st, p = cfg.KH, cfg.KW, cfg.stride, cfg.pad
+        Cout = w_bar.shape[0]
+        OH = (H + 2 * p - KH) // st + 1
+        OW = (W + 2 * p - KW) // st + 1
+        Coutp = _pad8(Cout)
+        sc = scale.detach().float().reshape(1).contiguous()
+        outs = _conv_call(q1, None, None, _bias_padded(bias, Coutp), 0, KH, KW, st, p, 0, 1,
+                          _act_code(cfg.act_in), OH, OW, Coutp, _act_code(cfg.act_out), Coutp, None,
+                          None, 0, Cout, False, w_bar, 0, Coutp, Cp, alpha=sc)
+        y = outs[0]
+        if Coutp != Cout:
+            y = P().slice_channels(y, 0, Cout)
+        ctx.cfg = cfg
+        ctx.geo = (C1, 0, Cp, packed, Cout, Coutp, H, W)
+        ctx.has_bias = bias is not None
+        keep_y = cfg.act_out not in (None, "none")
+        ctx.save_for_backward(q1, w_bar, sc, y if keep_y else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        q1, w_bar, sc, y = ctx.saved_tensors
+        need_w = ctx.needs_input_grad[1] or ctx.needs_input_grad[3]
+        gx, _, G, gb = _conv_backward(ctx.cfg, ctx.geo, q1, None, w_bar, y, gy,
+                                      ctx.needs_input_grad[0], False, need_w,
+                                      ctx.has_bias and ctx.needs_input_grad[2], alpha=sc)
+        gw = G * sc if ctx.needs_input_grad[1] else None
+        gs = (G * w_bar.detach()).sum().reshape(1) if ctx.needs_input_grad[3] else None
+        return gx, gw, gb, gs, None
+
+
+def sn_conv2d(x, w_bar, bias, scale, stride=1, padding=0, act_in=None, act_out=None):
+    """Spectral-norm conv: ``conv2d(x, w_bar * scale)`` with ``scale`` (1 / sigma, a 1-element
+    tensor carrying its own gradient) applied in the conv epilogues."""
+    s, s2 = _pair(stride)
+    p, p2 = _pair(padding)
+    if s != s2 or p != p2:
+        raise NotImplementedError("anisotropic stride/padding")
+    cfg = _ConvCfg(False, w_bar.shape[2], w_bar.shape[3], s, p, False, 1, act_in, act_out)
+    return SNConvFn.apply(x, w_bar, bias, scale, cfg)
+
+
+def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, need_b, alpha=None):
     """Input / weight / bias gradients of one fused conv (ConvFn's backward, shared with the
     image head): dgrad with the input-activation gate, concat split and skip-gradient
     hand-off in its epilogue; wgrad; bias = column sums (or the norm's exact zero)."""
@@ -459,7 +518,7 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
             outs = _conv_call(gyp, None, None, None, 1, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
                               split, q1 if act_in else None,
                               q2 if (act_in and q2 is not None) else None, act_in, C1 + C2,
-                              False, weight, 1, Cp, Coutp, "gy", res=res)
+                              False, weight, 1, Cp, Coutp, "gy", res=res, alpha=alpha)
         if q2 is not None:
             gx1, gx2 = outs[0], outs[1]
         elif packed:

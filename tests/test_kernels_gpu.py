@@ -4,6 +4,8 @@ The HIP side runs bf16 activations (fp32 accumulate, fp32 master weights); the o
 the identical math in fp32 on the *same bf16-rounded inputs*, so the tolerance only has
 to absorb bf16 output rounding and accumulation order.
 """
+import copy
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -825,3 +827,34 @@ def test_image_metrics_kernel(dtype, cl, ref_compat, hw):
     assert torch.allclose(p[:2].cpu(), rp[:2], rtol=0, atol=1e-4), (p, rp)
     assert torch.allclose(s.cpu().double(), rs.double(), rtol=0, atol=1e-6), (s, rs)
     assert abs(s[2].item() - 1.0) < 1e-12
+
+
+@pytest.mark.parametrize("cin,cout,k,s", [(64, 128, 4, 2), (256, 512, 4, 1)])
+def test_spectral_norm_conv_epilogue_scale(cin, cout, k, s):
+    """SpectralNorm conv with 1/sigma applied in the conv epilogues (SNConvFn, no W/sigma
+    tensor) vs the reference formulation conv(x, w / sigma) in fp32: output, input gradient
+    and the weight_bar gradient (both the direct and the sigma path)."""
+    from p2p_pytorch_amd.models.compress_gan import SpectralNorm
+    torch.manual_seed(5)
+    conv = torch.nn.Conv2d(cin, cout, k, stride=s, padding=2)
+    sn = SpectralNorm(conv).to(DEV)
+    sn_ref = copy.deepcopy(sn)
+    x = rand_img(2, cin, 18, 18, seed=51)
+    hx = _leaf(x)
+    y = sn(hx)
+    gy = rand_img(*y.shape, seed=52)
+    y.backward(gy)
+    _native.set_backend("torch")
+    try:
+        rx = _leaf(x.float())
+        ry = sn_ref(rx)
+        ry.backward(gy.float())
+    finally:
+        _native.set_backend("native")
+    assert y.shape == ry.shape
+    assert rel_err(y, ry) < 2e-2
+    assert rel_err(hx.grad, rx.grad) < 3e-2
+    gw, rgw = sn.module.weight_bar.grad, sn_ref.module.weight_bar.grad
+    assert rel_err(gw, rgw) < 3e-2, rel_err(gw, rgw)
+    # u / v advanced identically (one power iteration each)
+    assert torch.allclose(sn.module.weight_u, sn_ref.module.weight_u, rtol=1e-3, atol=1e-5)
