@@ -78,6 +78,8 @@ class CompressGANStep:
         self.train_c = train_c
         self.opt_c = make_adam(net_c.parameters(), lr=lr, betas=(beta1, 0.999))
         self.c_phase_backward = c_phase_backward
+        if hasattr(net_d, "set_feature_grad_gate"):
+            net_d.set_feature_grad_gate(True)   # the feature-matching L1 below applies lrelu
         self.image_pool = image_pool
         self.reducer_g, self.reducer_d, self.reducer_c = reducer_g, reducer_d, reducer_c
         self.nan_guard = nan_guard
@@ -143,10 +145,11 @@ class CompressGANStep:
         set_requires_grad(self._d_trainable, True)
         loss_g_gan = self.criterionGAN(pred_fake_g, True)
         loss_feat = 0.0
+        fgate = getattr(D, "feature_grad_gate", None)   # D's lrelu' rides in these gradients
         for i in range(len(pred_fake_g)):
             for j in range(len(pred_fake_g[i]) - 1):
                 loss_feat = loss_feat + self.d_weights * self.feat_weights * ops.l1(
-                    pred_fake_g[i][j], pred_real[i][j].detach()) * self.lambda_feat
+                    pred_fake_g[i][j], pred_real[i][j].detach(), gate_a=fgate) * self.lambda_feat
         content = self.criterionVGG(fake_b, real_b) * self.lambda_vgg
         tv = calc_tv_Loss(fake_b)
         loss_g = loss_g_gan + loss_feat + content + tv * self.lambda_tv

@@ -235,7 +235,8 @@ class SpectralNorm(nn.Module):
                 sigma = ops_hip().spectral_sigma(w.reshape(w.shape[0], -1), u, v, self.power_iterations)
                 scale = sigma.reciprocal()
             return ops_hip().sn_conv2d(x, w, m.bias, scale, m.stride, m.padding,
-                                       getattr(m, "act_in", None), getattr(m, "act_out", None))
+                                       getattr(m, "act_in", None), getattr(m, "act_out", None),
+                                       getattr(m, "grad_gate", None), getattr(m, "out_gated", False))
         w = self.normalized_weight()
         return ops.conv2d(x, w, m.bias, m.stride, m.padding, pad_mode, 1,
                           getattr(m, "act_in", None), getattr(m, "act_out", None))
@@ -261,11 +262,25 @@ class NLayerDiscriminatorSN(nn.Module):
         seq.append([SpectralNorm(Conv2d(nf_prev, nf, kw, stride=1, padding=padw, act_out="lrelu"))])
         seq.append([Conv2d(nf, 1, kw, stride=1, padding=padw,
                            act_out="sigmoid" if use_sigmoid else None)])
+        self._chain = [s[0].module if isinstance(s[0], SpectralNorm) else s[0] for s in seq]
+        self.feature_grad_gate = None
         if getIntermFeat:
             for k, s in enumerate(seq):
                 setattr(self, f"model{k}", nn.Sequential(*s))
         else:
             self.model = nn.Sequential(*[m for s in seq for m in s])
+
+    def set_feature_grad_gate(self, on=True):
+        """Opt-in (the family-R training step enables it): every LeakyReLU derivative moves
+        into the next conv's dgrad epilogue (HIP path) -- no separate gate pass per layer.
+        Only valid when every OTHER consumer of the intermediate features applies lrelu' to
+        its own gradient, as the step's feature-matching L1 does (``ops.l1(..., gate_a=
+        self.feature_grad_gate)``).  The oracle path ignores the flags."""
+        for prod, cons in zip(self._chain[:-1], self._chain[1:]):
+            if getattr(prod, "act_out", None) == "lrelu":
+                prod.out_gated = bool(on)
+                cons.grad_gate = "lrelu" if on else None
+        self.feature_grad_gate = "lrelu" if on else None
 
     def forward(self, x):
         if self.getIntermFeat:
@@ -287,13 +302,22 @@ class MultiscaleDiscriminator(nn.Module):
         self.num_D = num_D
         self.n_layers = n_layers
         self.getIntermFeat = getIntermFeat
+        self.feature_grad_gate = None
+        self._subs = []   # plain list (not registered): the per-scale gate chains
         for i in range(num_D):
             d = NLayerDiscriminatorSN(input_nc, ndf, n_layers, norm_layer, use_sigmoid, getIntermFeat)
+            self._subs.append(d)
             if getIntermFeat:
                 for j in range(n_layers + 2):
                     setattr(self, f"scale{i}_layer{j}", getattr(d, f"model{j}"))
             else:
                 setattr(self, f"layer{i}", d.model)
+
+    def set_feature_grad_gate(self, on=True):
+        """See NLayerDiscriminatorSN.set_feature_grad_gate."""
+        for d in self._subs:
+            d.set_feature_grad_gate(on)
+        self.feature_grad_gate = "lrelu" if on else None
 
     def downsample(self, x):
         if isinstance(x, (tuple, list)):  # virtual concat: pool each half

@@ -114,9 +114,11 @@ def bce_const(prob, target):
     return ref.bce_const(prob, target)
 
 
-def l1(a, b):
+def l1(a, b, gate_a=None):
+    """``gate_a`` (HIP path): the gradient of ``a`` also carries that activation's derivative
+    (its producer is ``out_gated``); the oracle's producers apply their own activation."""
     if _native.use_native(a):
-        return _hip().l1(a, b)
+        return _hip().l1(a, b, gate_a)
     return ref.l1(a, b)
 
 

