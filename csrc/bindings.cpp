@@ -249,6 +249,10 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   a.ws = nullptr;
   a.splits = 1;
   a.zero = zero_page(x1);
+  {
+    const char* cm = std::getenv("P2P_CLASS_MAJOR");
+    a.cls_major = (cm && cm[0] == '1') ? 1 : 0;
+  }
   a.stats = nullptr;
   a.stats_nchunks = 0;
   a.fp8 = fp8;

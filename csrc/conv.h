@@ -69,6 +69,7 @@ struct ConvFwdArgs {
   const void* pk_f;
   float d2s_scale;
   float* l1_part;
+  int cls_major;   // MODE 1 block order A/B knob (P2P_CLASS_MAJOR=1: all tiles of class 0 first)
 };
 
 // Weight gradient: C[R][Kq] = sum_m P[m][R] * im2col(Q)[m][Kq], written to per-split

@@ -83,11 +83,17 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
 
-  const int cls = blockIdx.z / a.splits;
-  const int split = blockIdx.z % a.splits;
-  const ClassGeom g = class_geom<MODE>(a, cls);
+  // MODE 1: the stride^2 parity classes of one (m, n) tile are adjacent block ids (class
+  // fastest), so after the XCD remap they run together on one XCD and share the input rows
+  // in its L2 -- class-major order re-read the whole input from HBM once per class
+  const int classes = MODE == 1 ? a.stride * a.stride : 1;
+  const int split = blockIdx.z;
   const int ntiles = (a.Cout + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_cls = gridDim.x / classes;
+  const int cls = MODE == 1 ? (a.cls_major ? bid0 / per_cls : bid0 % classes) : 0;
+  const int bid = MODE == 1 ? (a.cls_major ? bid0 % per_cls : bid0 / classes) : bid0;
+  const ClassGeom g = class_geom<MODE>(a, cls);
   const int mt = bid / ntiles, nt = bid % ntiles;
   const int m0 = mt * BM, n0 = nt * BN;
   if (m0 >= g.Mc) return;
@@ -484,7 +490,7 @@ static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   }
   const long mtiles = (mmax + BM - 1) / BM;
   const long ntiles = (a.Cout + BN - 1) / BN;
-  dim3 grid((unsigned)(mtiles * ntiles), 1, (unsigned)(classes * a.splits));
+  dim3 grid((unsigned)(mtiles * ntiles * classes), 1, (unsigned)a.splits);
   hipLaunchKernelGGL((conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU, F8, PK8>), grid, dim3(WM * WN * 64), smem,
                      st, a);
   return (int)hipGetLastError();

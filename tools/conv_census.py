@@ -122,11 +122,13 @@ def main():
         alt = {}
         if name == "conv_fwd" and args.variants:
             for v in args.variants.split(","):
-                os.environ["P2P_CONV_VARIANT"] = v
+                # "g5" -> P2P_CONV_VARIANT=g5; "NAME=VAL" -> that environment variable
+                key, val = v.split("=", 1) if "=" in v else ("P2P_CONV_VARIANT", v)
+                os.environ[key] = val
                 try:
                     alt[v] = timed()
                 finally:
-                    os.environ.pop("P2P_CONV_VARIANT", None)
+                    os.environ.pop(key, None)
         rows.append((geo, ms, flop, alt))
     agg = collections.OrderedDict()
     altagg = collections.defaultdict(lambda: collections.Counter())
