@@ -649,6 +649,9 @@ static int wgrad_glds_shape(const p2p::ConvWgradArgs* a) {
   // 4 = 256x256 (half the VALU + LDS fragment traffic per MFMA of 1 / 2)
   if (v && v[0] == 'g' && v[1] == '5' && a->R % 256 == 0 && a->Kq % 256 == 0) return 4;
   if (a->R >= 256) return 1;
+  // 5 = 128x128 on 4 waves, 2-stage (two blocks per CU): Kq = 128, e.g. the packed 8-channel
+  // image conv's wgrad (16 taps x 8 channels), which fell back to the register-staged kernel
+  if (a->Kq == 128) return 5;
   return a->Kq >= 256 ? 2 : 0;
 }
 
@@ -658,6 +661,7 @@ extern "C" int p2p_conv_wgrad_tile(const p2p::ConvWgradArgs* a, int* tr, int* tq
   if (shape == 2) { *tr = 128; *tq = 256; return shape; }
   if (shape == 3) { *tr = 64; *tq = 128; return shape; }
   if (shape == 4) { *tr = 256; *tq = 256; return shape; }
+  if (shape == 5) { *tr = 128; *tq = 128; return shape; }
   *tr = a->R <= 16 ? 16 : (a->R <= 64 ? 64 : 128);
   *tq = 128;
   return 0;
@@ -703,6 +707,11 @@ extern "C" int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t st) {
       const int smem4 = 2 * (256 + 256) * WBM * 2;
       dim3 grid4(((a->R + 255) / 256) * ((a->Kq + 255) / 256), a->splits, 1);
       return wg_launch_rm<256, 256, 2, 4, 2>(rm, *a, grid4, smem4, st);
+    }
+    if (shape == 5) {  // 128x128, 4 waves, 2-stage ring (64 KB LDS: two blocks per CU)
+      const int smem5 = 2 * (128 + 128) * WBM * 2;
+      dim3 grid5(((a->R + 127) / 128) * ((a->Kq + 127) / 128), a->splits, 1);
+      return wg_launch_rm<128, 128, 2, 2, 2>(rm, *a, grid5, smem5, st);
     }
     if (shape == 1) return wg_launch_rm<256, 128, 4, 2, STG>(rm, *a, grid, smem, st);
     if (shape == 2) return wg_launch_rm<128, 256, 2, 4, STG>(rm, *a, grid, smem, st);

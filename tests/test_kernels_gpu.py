@@ -65,6 +65,9 @@ CONV_CASES = [
     ("bottleneck_splitk", 2, 512, 0, 4, 512, 4, 2, 1, "lrelu", None, True),
     ("one_by_one", 2, 64, 0, 16, 128, 1, 1, 0, "lrelu", None, True),
     ("concat_64+64", 2, 64, 64, 16, 64, 3, 1, 1, "relu", None, False),
+    # 8-channel input, 128 outputs, 4x4: the 128x128 glds wgrad tile (Kq = 128)
+    ("c8_r128_wgrad128", 4, 8, 0, 64, 128, 4, 2, 1, None, None, True),
+    ("c8_r128_relu_in", 4, 8, 0, 64, 128, 4, 2, 1, "relu", None, True),
 ]
 
 
