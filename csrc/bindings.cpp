@@ -39,6 +39,11 @@ int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const floa
                  const float* rstd, const float* gamma, const float* beta, int act,
                  const float* prelu_w, float* dprelu, float* dgamma, float* dbeta, float* ws, void* dx,
                  float* dsum, void* q, int* qsite, int qfmt, hipStream_t st);
+int p2p_norm_bwd_partials(const void* x, const void* dy, int N, int HW, int C, int nchunks,
+                          const float* partials, const float* mean, const float* rstd,
+                          const float* gamma, const float* beta, int act, float* dgamma, float* dbeta,
+                          float* coef, void* dx, float* dsum, void* q, int* qsite, int qfmt,
+                          hipStream_t st);
 int p2p_act(const void* a, const void* b, long n, int act, int mode, void* out, hipStream_t st);
 int p2p_dropout(const void* x, long n, float p, const int64_t* seed, unsigned salt, void* y,
                 hipStream_t st);
@@ -163,7 +168,10 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                              bool want_stats, const optional<Tensor>& qs_x1,
                              const optional<Tensor>& qs_x2, const optional<Tensor>& qs_w,
                              const optional<Tensor>& y_qsite, int64_t y_qfmt,
-                             const optional<Tensor>& res, const optional<Tensor>& alpha) {
+                             const optional<Tensor>& res, const optional<Tensor>& alpha,
+                             const optional<Tensor>& nb_x, const optional<Tensor>& nb_mean,
+                             const optional<Tensor>& nb_rstd, const optional<Tensor>& nb_gamma,
+                             const optional<Tensor>& nb_beta, int64_t nb_act, int64_t nb_half, bool nb_batch) {
   check_act(x1, "conv_fwd x1", true);
   // fp8 operands: x e4m3 (activations) or e5m2 (gradients), weight image e4m3, each with
   // an fp8 scale site (csrc/fp8.hip); outputs stay bf16
@@ -252,6 +260,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   {
     const char* cm = std::getenv("P2P_CLASS_MAJOR");
     a.cls_major = (cm && cm[0] == '1') ? 1 : 0;
+    const char* es = std::getenv("P2P_EPI_SERIAL");
+    a.epi_serial = (es && es[0] == '1') ? 1 : 0;
   }
   a.stats = nullptr;
   a.stats_nchunks = 0;
@@ -384,6 +394,47 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       a.stats_nchunks = (int)nch;
     }
   }
+  // fused norm-backward partials (dgrad epilogue): half nb_half (1 = channels [0, Csplit),
+  // 2 = [Csplit, Cout)) is the gradient of a norm's output; same tile constraints as stats
+  Tensor nbp;
+  a.nb_ws = nullptr;
+  // the packed-image halo kernel (below) beats the generic tile with fused partials: keep it
+  const bool pk8_halo = mode == 0 && !fp8 && C1 == 8 && C2 == 0 && KH == 4 && KW == 4 && stride == 2 && pad == 1 &&
+                        (Cout == 64 || Cout == 128) && std::getenv("P2P_NO_HALO") == nullptr;
+  if (nb_x && nb_half && glds_ok && splits == 1 && !fp8 && !want_stats && !pk8_halo) {
+    const int64_t c0 = nb_half == 1 ? 0 : Csplit;
+    const int64_t nC = nb_half == 1 ? Csplit : Cout - Csplit;
+    bool ok = nC > 0 && nC % 8 == 0 && (nb_half == 1 || Csplit < Cout);
+    int64_t hwq = OH * OW;
+    if (mode == 1) {
+      ok = ok && OH % stride == 0 && OW % stride == 0;
+      hwq = (OH / stride) * (OW / stride);
+    }
+    ok = ok && hwq % bm == 0;
+    if (ok) {
+      check_act(*nb_x, "conv_fwd nb_x");
+      TORCH_CHECK(nb_x->size(0) == N && nb_x->size(1) == nC && nb_x->size(2) == OH && nb_x->size(3) == OW,
+                  "conv_fwd: nb_x must match the gradient half");
+      const int64_t groups = nb_batch ? 1 : N;
+      TORCH_CHECK(nb_mean && nb_rstd && nb_mean->numel() == groups * nC && nb_rstd->numel() == groups * nC &&
+                      nb_mean->scalar_type() == at::kFloat && nb_rstd->scalar_type() == at::kFloat,
+                  "conv_fwd: nb mean / rstd");
+      if (nb_gamma) TORCH_CHECK(nb_beta && nb_gamma->numel() == nC && nb_beta->numel() == nC, "conv_fwd: nb affine");
+      const int64_t nch = classes * (hwq / bm);
+      nbp = at::empty({2, N, nch, nC}, x1.options().dtype(at::kFloat));
+      a.nb_x = nb_x->data_ptr();
+      a.nb_mean = nb_mean->data_ptr<float>();
+      a.nb_rstd = nb_rstd->data_ptr<float>();
+      a.nb_gamma = nb_gamma ? nb_gamma->data_ptr<float>() : nullptr;
+      a.nb_beta = nb_gamma ? nb_beta->data_ptr<float>() : nullptr;
+      a.nb_act = (int)nb_act;
+      a.nb_batch = nb_batch ? 1 : 0;
+      a.nb_c0 = (int)c0;
+      a.nb_C = (int)nC;
+      a.nb_nchunks = (int)nch;
+      a.nb_ws = nbp.data_ptr<float>();
+    }
+  }
   // fp8 shadow of y (the next conv's operand) from the epilogue: plain single-output GEMMs
   Tensor yq;
   if (y_qsite && splits == 1 && Csplit == Cout && !act_bwd) {
@@ -397,7 +448,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   int rc = -2;
   // packed 8-channel image convs (4x4 s2 p1): the halo-tile kernel (csrc/halo_pk8.hip)
   if (mode == 0 && !fp8 && C1 == 8 && C2 == 0 && KH == 4 && KW == 4 && stride == 2 && pad == 1 && !reflect &&
-      up == 1 && act_in == 0 && splits == 1 && !a.stats && !a.q_out && !a.res1 && !a.alpha && (Cout == 64 || Cout == 128) &&
+      up == 1 && act_in == 0 && splits == 1 && !a.stats && !a.nb_ws && !a.q_out && !a.res1 && !a.alpha && (Cout == 64 || Cout == 128) &&
       std::getenv("P2P_NO_HALO") == nullptr) {
     p2p::HaloPk8Args h{};
     h.x = static_cast<const __bf16*>(x1.data_ptr());
@@ -433,7 +484,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   const bool halo_geo = (KH == 9 && KW == 9 && (C1 == 8 || C1 == 16 || C1 == 32) && Cout <= 32) ||
                         (KH == 3 && KW == 3 && C1 == 64 && Cout <= 32);
   if (rc == -2 && !fp8 && C2 == 0 && halo_geo && stride == 1 && Csplit == Cout && act_in == 0 && act_bwd == 0 &&
-      !a.res1 && !a.q_out && !a.stats && !a.alpha && (mode == 0 || (up == 1 && !reflect && pad <= KH - 1)) &&
+      !a.res1 && !a.q_out && !a.stats && !a.nb_ws && !a.alpha && (mode == 0 || (up == 1 && !reflect && pad <= KH - 1)) &&
       std::getenv("P2P_NO_HALO") == nullptr) {
     p2p::HaloKArgs h{};
     h.x = static_cast<const __bf16*>(x1.data_ptr());
@@ -469,6 +520,10 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     a.stats = nullptr;
     stats = Tensor();
   }
+  if (rc == -2 && a.nb_ws) {  // the register-staged kernel shares the epilogue, but keep it simple
+    a.nb_ws = nullptr;
+    nbp = Tensor();
+  }
   TORCH_CHECK(!(fp8 && rc == -2), "conv_fwd: no fp8 kernel for this geometry (Cout ", Cout, ", C1 ", C1, ", C2 ",
               C2, ", act_in ", act_in, ")");
   if (rc == -2) {
@@ -485,6 +540,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   std::vector<Tensor> out{y1};
   if (y2.defined()) out.push_back(y2);
   if (stats.defined()) out.push_back(stats);
+  if (nbp.defined()) out.push_back(nbp);  // dgrad calls only (no stats / fp8 shadow there)
   if (yq.defined()) out.push_back(yq);   // always last (fp8 dtype)
   return out;
 }
@@ -941,7 +997,7 @@ Tensor norm_bwd(const Tensor& x, const Tensor& dy, const Tensor& mean, const Ten
                 const optional<Tensor>& dgamma, const optional<Tensor>& dbeta, bool need_dx,
                 bool batch, const optional<Tensor>& dsum, const optional<Tensor>& qsite,
                 const optional<Tensor>& q_out, int64_t qfmt, const optional<Tensor>& prelu_w,
-                const optional<Tensor>& dprelu) {
+                const optional<Tensor>& dprelu, const optional<Tensor>& partials) {
   check_act(x, "norm_bwd x");
   if (prelu_w)
     TORCH_CHECK(prelu_w->numel() == 1 && prelu_w->scalar_type() == at::kFloat && prelu_w->is_cuda(),
@@ -964,9 +1020,28 @@ Tensor norm_bwd(const Tensor& x, const Tensor& dy, const Tensor& mean, const Ten
   const int gN = batch ? 1 : (int)N;
   const int gHW = batch ? (int)(N * HW) : (int)HW;
   if (dsum) TORCH_CHECK(dsum->numel() == C && dsum->scalar_type() == at::kFloat, "norm_bwd: dsum");
-  Tensor ws = at::empty({p2p_norm_ws_floats(gN, gHW, (int)C)}, x.options().dtype(at::kFloat));
   Tensor dx;
   if (need_dx) dx = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (partials) {
+    // [2][N][nch][C] sum(d) / sum(d * xhat) from the consumer conv's dgrad epilogue
+    TORCH_CHECK(!prelu_w && partials->dim() == 4 && partials->size(0) == 2 && partials->size(1) == N &&
+                    partials->size(3) == C && partials->scalar_type() == at::kFloat,
+                "norm_bwd: partials shape");
+    const int nch = (int)(batch ? N * partials->size(2) : partials->size(2));
+    Tensor coef = at::empty({3 * gN * C}, x.options().dtype(at::kFloat));
+    check_rc(p2p_norm_bwd_partials(x.data_ptr(), dy.data_ptr(), gN, gHW, (int)C, nch, partials->data_ptr<float>(),
+                                   mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                                   gamma ? gamma->data_ptr<float>() : nullptr,
+                                   beta ? beta->data_ptr<float>() : nullptr, (int)act,
+                                   dgamma ? dgamma->data_ptr<float>() : nullptr,
+                                   dbeta ? dbeta->data_ptr<float>() : nullptr, coef.data_ptr<float>(),
+                                   need_dx ? dx.data_ptr() : nullptr,
+                                   (need_dx && dsum) ? dsum->data_ptr<float>() : nullptr, qp, qs, (int)qfmt,
+                                   cur_stream(x)),
+             "norm_bwd(partials)");
+    return dx;
+  }
+  Tensor ws = at::empty({p2p_norm_ws_floats(gN, gHW, (int)C)}, x.options().dtype(at::kFloat));
   check_rc(p2p_norm_bwd(x.data_ptr(), dy.data_ptr(), gN, gHW, (int)C, mean.data_ptr<float>(),
                         rstd.data_ptr<float>(), gamma ? gamma->data_ptr<float>() : nullptr,
                         beta ? beta->data_ptr<float>() : nullptr, (int)act,
@@ -1419,7 +1494,9 @@ TORCH_LIBRARY(p2p, m) {
         "int pad, int reflect, int up, int act_in, int OH, int OW, int Cout, int act_out, int Csplit, "
         "Tensor? xb1, Tensor? xb2, int act_bwd, int Cvalid=0, bool want_stats=False, Tensor? qs_x1=None, "
         "Tensor? qs_x2=None, Tensor? qs_w=None, Tensor(a!)? y_qsite=None, int y_qfmt=0, Tensor? res=None, "
-        "Tensor? alpha=None) -> Tensor[]");
+        "Tensor? alpha=None, Tensor? nb_x=None, Tensor? nb_mean=None, Tensor? nb_rstd=None, "
+        "Tensor? nb_gamma=None, Tensor? nb_beta=None, int nb_act=0, int nb_half=0, bool nb_batch=False) "
+        "-> Tensor[]");
   m.def("fp8_quant(Tensor x, Tensor(a!) site, int fmt, int use_cur=0) -> Tensor");
   m.def("sn_power_iter(Tensor w, Tensor(a!) u, Tensor(b!) v) -> Tensor");
   m.def("fp8_amax(Tensor x, Tensor(a!) site, int slot) -> ()");
@@ -1455,7 +1532,7 @@ TORCH_LIBRARY(p2p, m) {
   m.def("norm_bwd(Tensor x, Tensor dy, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, int act, "
         "Tensor(a!)? dgamma, Tensor(b!)? dbeta, bool need_dx, bool batch, Tensor(c!)? dsum, "
         "Tensor(d!)? qsite=None, Tensor(e!)? q_out=None, int qfmt=0, Tensor? prelu_w=None, "
-        "Tensor(f!)? dprelu=None) -> Tensor");
+        "Tensor(f!)? dprelu=None, Tensor? partials=None) -> Tensor");
   m.def("act(Tensor a, Tensor? b, int act, int mode) -> Tensor");
   m.def("dropout(Tensor x, float p, Tensor seed, int salt) -> Tensor");
   m.def("pad_channels(Tensor a, Tensor? b, int Co) -> Tensor");

@@ -70,6 +70,19 @@ struct ConvFwdArgs {
   float d2s_scale;
   float* l1_part;
   int cls_major;   // MODE 1 block order A/B knob (P2P_CLASS_MAJOR=1: all tiles of class 0 first)
+  // Norm-backward partial sums fused into a dgrad epilogue (null nb_ws = off): the output
+  // channels [nb_c0, nb_c0 + nb_C) are the gradient dz of a norm's output z = act(xhat*g + b)
+  // (xhat = (x - mean) * rstd, x = nb_x [N][OH][OW][nb_C]); every BM-row tile (one image /
+  // parity class, host-checked like ``stats``) writes sum(d) and sum(d * xhat), d = dz *
+  // act'(z), per channel to nb_ws[{0,1}][n][chunk][nb_C] -- the norm backward's partial pass.
+  const void* nb_x;
+  const float* nb_mean;   // [N][nb_C] (instance) or [nb_C] (batch, nb_batch = 1)
+  const float* nb_rstd;
+  const float* nb_gamma;  // null = no affine
+  const float* nb_beta;
+  int nb_act, nb_batch, nb_c0, nb_C, nb_nchunks;
+  float* nb_ws;
+  int epi_serial;   // A/B knob (P2P_EPI_SERIAL=1): the store loop without grouped operand prefetch
 };
 
 // Weight gradient: C[R][Kq] = sum_m P[m][R] * im2col(Q)[m][Kq], written to per-split

@@ -681,4 +681,43 @@ int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const floa
   return (int)hipGetLastError();
 }
 
+// backward from per-chunk partials [2][N][nchunks][C] of sum(d) / sum(d * xhat) produced by the
+// consumer conv's dgrad epilogue (conv_dev.h nb_*): the partial pass over (x, dy) is gone;
+// finalize (+ the affine parameter gradients) and apply as in p2p_norm_bwd.  coef: [3][N][C].
+int p2p_norm_bwd_partials(const void* x, const void* dy, int N, int HW, int C, int nchunks,
+                          const float* partials, const float* mean, const float* rstd,
+                          const float* gamma, const float* beta, int act, float* dgamma, float* dbeta,
+                          float* coef, void* dx, float* dsum, void* q, int* qsite, int qfmt,
+                          hipStream_t st) {
+  using namespace p2p;
+  if (nchunks <= 0 || HW % nchunks) return -1;
+  NormGeom pg;
+  pg.N = N;
+  pg.HW = HW;
+  pg.C = C;
+  pg.chunk = HW / nchunks;
+  pg.nchunks = nchunks;
+  if (dgamma) {
+    if (fin_huge(pg))
+      hipLaunchKernelGGL((norm_param_grad_kernel<1, 256>), dim3(C), dim3(256), 0, st, partials, pg, dgamma, dbeta);
+    else if (fin_wide(pg) || N > 8)
+      hipLaunchKernelGGL((norm_param_grad_kernel<8, 32>), dim3((C + 7) / 8), dim3(256), 0, st, partials, pg, dgamma,
+                         dbeta);
+    else
+      hipLaunchKernelGGL((norm_param_grad_kernel<32, 8>), dim3((C + 31) / 32), dim3(256), 0, st, partials, pg, dgamma,
+                         dbeta);
+  }
+  if (dx) {
+    P2P_FIN_LAUNCH(norm_bwd_finalize_kernel, pg, N, st, partials, pg, rstd, gamma, coef);
+    NormGeom g = make_geom(N, HW, C);
+    with_act(act, [&](auto t) {
+      hipLaunchKernelGGL((norm_bwd_apply_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st,
+                         static_cast<const bf16*>(x), static_cast<const bf16*>(dy), g, mean, rstd, gamma, beta,
+                         nullptr, coef, static_cast<bf16*>(dx), Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
+    });
+    if (dsum) (void)hipMemsetAsync(dsum, 0, sizeof(float) * C, st);
+  }
+  return (int)hipGetLastError();
+}
+
 }  // extern "C"

@@ -25,6 +25,7 @@ see ``ops/reference.py`` for the fp32 oracle each kernel is tested against.
 from __future__ import annotations
 
 import itertools
+import os
 
 import torch
 
@@ -32,6 +33,8 @@ from .. import _native
 from . import fp8 as _f8
 
 ACT = {None: 0, "none": 0, "relu": 1, "lrelu": 2, "tanh": 3, "sigmoid": 4}
+# P2P_NB_FUSE=0: norm backward runs its own partial pass (A/B knob for the dgrad-epilogue fusion)
+_NB_FUSE = os.environ.get("P2P_NB_FUSE", "1") != "0"
 CL = torch.channels_last
 
 _gen = [0]
@@ -48,6 +51,8 @@ def begin_step():
     _gen[0] += 1
     _colsum_stash.clear()
     _stats_stash.clear()
+    _norm_out.clear()
+    _nbp_stash.clear()
     _DEFERRED.clear()   # a backward that raised part-way must not leak parked skip gradients
     if _f8._pools:
         _f8.begin_step()
@@ -78,6 +83,40 @@ def _stash_stats(y, st):
 def _take_stats(x):
     ent = _stats_stash.pop((x.data_ptr(), tuple(x.shape)), None)
     return None if ent is None else ent[1]
+
+
+# Norm-backward partial sums fused into the consumer conv's dgrad epilogue.  NormFn.forward
+# registers its output z with what the partial pass needs (x, mean, rstd, affine, act); a conv
+# reading z as a whole input half passes that to its dgrad, whose epilogue emits sum(d) and
+# sum(d * xhat) per tile (conv_dev.h nb_*); the partials are parked keyed by the gradient
+# tensor and NormFn.backward takes them only if it receives exactly that tensor (an
+# autograd-accumulated gradient is a new tensor: the norm then runs its own partial pass).
+_norm_out: dict = {}
+_nbp_stash: dict = {}
+
+
+def _register_norm_out(z, info):
+    if len(_norm_out) >= 256:
+        _norm_out.pop(next(iter(_norm_out)))
+    _norm_out[(z.data_ptr(), tuple(z.shape))] = (z, info)
+
+
+def _norm_lookup(t):
+    if t is None:
+        return None
+    ent = _norm_out.get((t.data_ptr(), tuple(t.shape)))
+    return None if ent is None or ent[0] is not t else ent[1]
+
+
+def _stash_nbp(g, parts):
+    if len(_nbp_stash) >= 256:
+        _nbp_stash.pop(next(iter(_nbp_stash)))
+    _nbp_stash[(g.data_ptr(), tuple(g.shape))] = (g, parts)
+
+
+def _take_nbp(g):
+    ent = _nbp_stash.pop((g.data_ptr(), tuple(g.shape)), None)
+    return None if ent is None or ent[0] is not g else ent[1]
 
 
 def _take_colsum(gy):
@@ -139,14 +178,16 @@ def _weight_image_fp8(w: torch.Tensor, swap: int, xp: int, yp: int):
 
 def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout, act_out,
                Csplit, xb1, xb2, act_bwd, Cvalid, want, weight=None, swap=0, xp=0, yp=0, role="x",
-               y_qkey=None, res=None, alpha=None):
+               y_qkey=None, res=None, alpha=None, nb=None):
     """conv_fwd on bf16 operands, or -- fp8 precision and a geometry the fp8 kernel takes --
     on fp8 ones: x (role 'x': activations, e4m3; 'gy': gradients, e5m2) quantised with
     delayed scaling (or taken from the producer's fused shadow), the weight image with
     current scaling.  ``y_qkey``: also emit an e4m3 shadow of the output from the epilogue
     (the output feeds other fp8 convs directly) -- appended last to the returned list.
     ``wimg`` may be None (built on demand for the bf16 path).  ``res``: bf16 tensor added to
-    the (unsplit) output in the epilogue, after the act' gate."""
+    the (unsplit) output in the epilogue, after the act' gate.  ``nb`` = (half, norm info): the
+    dgrad epilogue also emits that half's norm-backward partials (bf16 path only), appended
+    as the last output."""
     C1 = x1.shape[1]
     C2 = 0 if x2 is None else x2.shape[1]
     if weight is not None and _f8.enabled() and _f8.conv_ok(C1, C2, Cout, act_in):
@@ -168,8 +209,14 @@ def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, 
     if y_qkey is not None and _f8.enabled():
         ysite, fresh = _f8.producer_site(x1.device, y_qkey)
         yq = (None, None, None, None, 0) if fresh else (None, None, None, ysite, _f8.E4M3)
+    kw = {}
+    if nb is not None and not yq:
+        half, (nx, nmean, nrstd, ng, nbeta, nact, nbatch) = nb
+        kw = dict(nb_x=nx, nb_mean=nmean, nb_rstd=nrstd, nb_gamma=ng, nb_beta=nbeta, nb_act=nact,
+                  nb_half=half, nb_batch=nbatch)
     return P().conv_fwd(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout,
-                        act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, *yq, res=res, alpha=alpha)
+                        act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, *yq, res=res, alpha=alpha,
+                        **kw)
 
 
 def prepare_weights(*modules):
@@ -390,6 +437,7 @@ class ConvFn(torch.autograd.Function):
         ctx.geo = (C1, C2, Cp, packed, Cout, Coutp, H, W)
         ctx.has_x2 = x2 is not None
         ctx.has_bias = bias is not None
+        ctx.nb = (None if packed else _norm_lookup(q1), _norm_lookup(q2))
         keep_y = cfg.act_out not in (None, "none") and not cfg.out_gated
         ctx.save_for_backward(q1, q2, weight, y if keep_y else None)
         return y
@@ -410,7 +458,7 @@ class ConvFn(torch.autograd.Function):
         gx1, gx2, gw, gb = _conv_backward(ctx.cfg, ctx.geo, q1, q2, weight, y, gy, need_x1,
                                           ctx.has_x2 and ctx.needs_input_grad[1],
                                           ctx.needs_input_grad[2],
-                                          ctx.has_bias and ctx.needs_input_grad[3])
+                                          ctx.has_bias and ctx.needs_input_grad[3], nb=ctx.nb)
         return gx1, gx2, gw, gb, None
 
 
@@ -474,10 +522,29 @@ def sn_conv2d(x, w_bar, bias, scale, stride=1, padding=0, act_in=None, act_out=N
     return SNConvFn.apply(x, w_bar, bias, scale, cfg)
 
 
-def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, need_b, alpha=None):
+def _nb_half(cfg, q2, nb, res_fused):
+    """Which input half's dgrad epilogue emits norm-backward partials: one whose gradient this
+    conv completes (not a deferred skip half; a "take" half only when its parked gradient is
+    added in the epilogue)."""
+    if nb is None:
+        return None
+    nb1, nb2 = nb
+    if (nb1 is not None and cfg.skip_grad != "defer" and (cfg.skip_grad != "take" or res_fused)):
+        return (1, nb1)
+    if nb2 is not None and q2 is not None:
+        return (2, nb2)
+    return None
+
+
+def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, need_b, alpha=None,
+                   nb=None):
     """Input / weight / bias gradients of one fused conv (ConvFn's backward, shared with the
     image head): dgrad with the input-activation gate, concat split and skip-gradient
-    hand-off in its epilogue; wgrad; bias = column sums (or the norm's exact zero)."""
+    hand-off in its epilogue; wgrad; bias = column sums (or the norm's exact zero).
+    ``nb``: (x1, x2) norm-output infos (``_norm_lookup``) -- the dgrad epilogue emits the
+    norm-backward partials of a half that is a norm's output."""
+    nbh = None
+    nbp = None
     C1, C2, Cp, packed, Cout, Coutp, H, W = geo
     gy = to_nhwc_bf16(gy)
     if cfg.act_out not in (None, "none") and not cfg.out_gated:
@@ -506,10 +573,11 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
             outs = [P().pad_fold(dxp, H, W, p, cfg.up, int(cfg.reflect),
                                  q1 if act_in else None, act_in, res)]
         elif cfg.transposed:
+            nbh = _nb_half(cfg, q2, nb, False) if not packed else None
             outs = _conv_call(gyp, None, None, None, 0, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
                               split, q1 if act_in else None,
                               q2 if (act_in and q2 is not None and cfg.gate_x2) else None,
-                              act_in, C1 + C2, False, weight, 0, Cp, Coutp, "gy")
+                              act_in, C1 + C2, False, weight, 0, Cp, Coutp, "gy", nb=nbh)
         else:
             res = None
             if cfg.skip_grad == "take" and q2 is None and not packed and need_x1:
@@ -517,10 +585,15 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
                 if res is not None and (res.shape != (q1.shape[0], Cp, H, W) or Cp != C1):
                     _DEFERRED[q1.data_ptr()] = res   # not fusable: added below instead
                     res = None
+            take_ok = res is not None or q1.data_ptr() not in _DEFERRED
+            nbh = _nb_half(cfg, q2, nb, take_ok) if not packed else None
             outs = _conv_call(gyp, None, None, None, 1, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
                               split, q1 if act_in else None,
                               q2 if (act_in and q2 is not None) else None, act_in, C1 + C2,
-                              False, weight, 1, Cp, Coutp, "gy", res=res, alpha=alpha)
+                              False, weight, 1, Cp, Coutp, "gy", res=res, alpha=alpha, nb=nbh)
+        nouts = 2 if q2 is not None else 1
+        if nbh is not None and len(outs) > nouts:
+            nbp = outs[nouts]
         if q2 is not None:
             gx1, gx2 = outs[0], outs[1]
         elif packed:
@@ -529,6 +602,10 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
             gx2 = P().slice_channels(g, C1, C2) if need_x2 else None
         else:
             gx1 = outs[0]
+        if nbp is not None:
+            g_half = gx1 if nbh[0] == 1 else gx2
+            if g_half is not None:
+                _stash_nbp(g_half, nbp)
         if not need_x1:
             gx1 = None
         if not need_x2:
@@ -626,6 +703,7 @@ class ImageHeadFn(torch.autograd.Function):
         ctx.geo = (skip.shape[1], u.shape[1], skip.shape[1] + u.shape[1], False, 3, 8,
                    skip.shape[2], skip.shape[3])
         ctx.save_for_backward(skip, u, weight, af, ab)
+        ctx.nb = (None, _norm_lookup(u))
         ctx.mark_non_differentiable(l1)
         af._p2p_packed = (3, 3)
         af._p2p_head = (ab, float(scale))
@@ -646,7 +724,7 @@ class ImageHeadFn(torch.autograd.Function):
         gx1, gx2, gw, gb = _conv_backward(cfg, ctx.geo, skip, u, weight, None, dz,
                                           ctx.needs_input_grad[0], ctx.needs_input_grad[1],
                                           ctx.needs_input_grad[2],
-                                          ctx.has_bias and ctx.needs_input_grad[3])
+                                          ctx.has_bias and ctx.needs_input_grad[3], nb=ctx.nb)
         if gb is not None:
             gb = gb[:3].contiguous()
         return gx1, gx2, gw, gb, None, None, None
@@ -761,6 +839,8 @@ class NormFn(torch.autograd.Function):
             rstd = torch.rsqrt(run_var.float() + eps).view(1, -1)
             y = P().norm_apply(x, mean, rstd, g, b, pw, _act_code(act), True)
         ctx.cfg = (eps, act, batch, training)
+        if training and pw is None and act in (None, "none", "relu", "lrelu") and _NB_FUSE:
+            _register_norm_out(y, (x, mean, rstd, g, b, _act_code(act), bool(batch)))
         keep_y = act not in (None, "none") and (act not in ("relu", "lrelu") or not training)
         ctx.save_for_backward(x, mean, rstd, gamma, beta, prelu_w, y if keep_y else None)
         return y
@@ -819,7 +899,11 @@ class NormFn(torch.autograd.Function):
             if not fresh:
                 qd = _f8.shadow_buffer(x, _f8.E5M2)
                 qargs = (dsite, qd, _f8.E5M2)
-        if qargs:
+        parts = _take_nbp(gy) if pw is None else None
+        if parts is not None:
+            dx = P().norm_bwd(x, gy, mean, rstd, g, b, fused_act, dg, db, need_x, batch, dsum,
+                              *(qargs or (None, None, 0)), partials=parts)
+        elif qargs:
             dx = P().norm_bwd(x, gy, mean, rstd, g, b, fused_act, dg, db, need_x, batch, dsum,
                               *qargs, prelu_w=pw, dprelu=gpw if pw is not None else None)
         else:

@@ -1,0 +1,169 @@
+"""Norm-backward partial sums fused into the consumer conv's dgrad epilogue (conv_dev.h nb_*).
+
+The fused path must compute the same input / parameter gradients as the norm's own partial
+pass (only the fp32 summation order of the per-channel sums differs), and it must actually
+run for the layer shapes it targets: encoder conv -> IN(lrelu) -> strided conv (MODE-1
+dgrad), decoder ConvT(cat(skip, relu(IN(.)))) (second half of a split MODE-0 dgrad), and
+batch norm with affine + ReLU.  Checked op-level against the unfused path and the fp32
+oracle, and at model level on the U-Net-256 generator.  Batches are sized so the dgrads
+run without split-K (the fusion needs whole tiles; split-K layers keep the partial pass).
+"""
+import pytest
+import torch
+
+from p2p_pytorch_amd import _native, ops
+from p2p_pytorch_amd.ops import hip
+from p2p_pytorch_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _native_backend():
+    _native.set_backend("native")
+    assert _native.load(), _native.load_error()
+    yield
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def bf(x):
+    return x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+
+def _rand(*shape, seed, scale=1.0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return torch.randn(*shape, device=DEV, generator=g) * scale
+
+
+class _Count:
+    def __init__(self, monkeypatch):
+        self.hits = 0
+        orig = hip._take_nbp
+
+        def take(g):
+            p = orig(g)
+            self.hits += p is not None
+            return p
+        monkeypatch.setattr(hip, "_take_nbp", take)
+
+
+def _run(monkeypatch, fused, fn):
+    monkeypatch.setattr(hip, "_NB_FUSE", fused)
+    hip.begin_step()
+    out = fn()
+    assert not hip._nbp_stash, "every parked partial must be taken by its norm"
+    return out
+
+
+def test_nb_encoder_instance_lrelu(monkeypatch):
+    x = bf(_rand(64, 64, 64, 64, seed=1))
+    w1 = _rand(128, 64, 4, 4, seed=2, scale=(1 / 1024) ** 0.5)
+    w2 = _rand(256, 128, 4, 4, seed=3, scale=(1 / 2048) ** 0.5)
+    gy = bf(_rand(64, 256, 16, 16, seed=4))
+
+    def fn():
+        hx, hw1, hw2 = x.clone().requires_grad_(True), w1.clone().requires_grad_(True), w2.clone().requires_grad_(True)
+        h = ops.conv2d(hx, hw1, None, 2, 1, stats=True)
+        z = ops.instance_norm(h, act="lrelu")
+        y = ops.conv2d(z, hw2, None, 2, 1)
+        y.backward(gy)
+        return hx.grad.float(), hw1.grad.float(), hw2.grad.float()
+
+    cnt = _Count(monkeypatch)
+    fused = _run(monkeypatch, True, fn)
+    assert cnt.hits == 1, "the fused partials were not used"
+    plain = _run(monkeypatch, False, fn)
+    assert cnt.hits == 1
+    for a, b in zip(fused, plain):
+        assert rel_err(a, b) < 1e-2
+    # fp32 oracle on the same bf16 inputs
+    rx = x.float().requires_grad_(True)
+    h = ref.conv2d(rx, w1.to(torch.bfloat16).float(), None, 2, 1)
+    z = ref.instance_norm(h, 1e-5, "lrelu")
+    ref.conv2d(z, w2.to(torch.bfloat16).float(), None, 2, 1).backward(gy.float())
+    # the fusion only reorders fp32 sums: as close to the oracle as the unfused bf16 path
+    assert rel_err(fused[0], rx.grad) <= 1.1 * rel_err(plain[0], rx.grad) + 1e-3
+
+
+def test_nb_decoder_split_half_relu(monkeypatch):
+    """ConvT(cat(skip, u)) with u = relu(IN(ConvT(.))): the up half (second output half of
+    the MODE-0 dgrad, no ReLU' gate of its own) carries the norm's partials."""
+    skip = bf(_rand(64, 64, 32, 32, seed=11))
+    v = bf(_rand(64, 128, 16, 16, seed=12))
+    wi = _rand(128, 64, 4, 4, seed=13, scale=(1 / 512) ** 0.5)
+    wo = _rand(128, 32, 4, 4, seed=14, scale=(1 / 512) ** 0.5)
+    gy = bf(_rand(64, 32, 64, 64, seed=15))
+
+    def fn():
+        hv, hwi, hwo = v.clone().requires_grad_(True), wi.clone().requires_grad_(True), wo.clone().requires_grad_(True)
+        u = ops.instance_norm(ops.conv_transpose2d(hv, hwi, None, 2, 1, "relu", None, stats=True), act="relu")
+        y = ops.conv_transpose2d((skip, u), hwo, None, 2, 1, "relu", None, gate_x2=False)
+        y.backward(gy)
+        return hv.grad.float(), hwi.grad.float(), hwo.grad.float()
+
+    cnt = _Count(monkeypatch)
+    fused = _run(monkeypatch, True, fn)
+    assert cnt.hits == 1, "the fused partials were not used"
+    plain = _run(monkeypatch, False, fn)
+    for a, b in zip(fused, plain):
+        assert rel_err(a, b) < 1e-2
+
+
+def test_nb_batch_norm_affine_relu(monkeypatch):
+    x = bf(_rand(64, 64, 64, 64, seed=21))
+    w1 = _rand(128, 64, 4, 4, seed=22, scale=(1 / 1024) ** 0.5)
+    w2 = _rand(128, 128, 4, 4, seed=23, scale=(1 / 2048) ** 0.5)
+    gam = 1 + _rand(128, seed=24, scale=0.1)
+    bet = _rand(128, seed=25, scale=0.1)
+    gy = bf(_rand(64, 128, 16, 16, seed=26))
+
+    def fn():
+        hx, hg, hb = x.clone().requires_grad_(True), gam.clone().requires_grad_(True), bet.clone().requires_grad_(True)
+        rm, rv = torch.zeros(128, device=DEV), torch.ones(128, device=DEV)
+        h = ops.conv2d(hx, w1, None, 2, 1, stats=True)
+        z = ops.batch_norm(h, rm, rv, hg, hb, True, act="relu")
+        ops.conv2d(z, w2, None, 2, 1).backward(gy)
+        return hx.grad.float(), hg.grad.float(), hb.grad.float()
+
+    cnt = _Count(monkeypatch)
+    fused = _run(monkeypatch, True, fn)
+    assert cnt.hits == 1, "the fused partials were not used"
+    plain = _run(monkeypatch, False, fn)
+    for a, b in zip(fused, plain):
+        assert rel_err(a, b) < 1e-2
+
+
+def test_nb_unet256_generator_grads(monkeypatch):
+    """Model level: U-Net-256 generator gradients with and without the fusion, each against
+    the fp32 eager oracle (8 chained bf16 layers amplify any reordering of the sums, so the
+    two bf16 runs are compared by their distance from fp32, per parameter)."""
+    from p2p_pytorch_amd.models import define_G
+    torch.manual_seed(0)
+    G = define_G(netG="unet_256", gpu_id=DEV, verbose=False, use_dropout=False)
+    A = bf(torch.rand(16, 3, 256, 256, device=DEV) * 2 - 1)
+
+    def fn():
+        G.zero_grad(set_to_none=True)
+        G(A).float().square().mean().backward()
+        hip.assert_no_deferred()
+        return {n: p.grad.detach().float().clone() for n, p in G.named_parameters()}
+
+    cnt = _Count(monkeypatch)
+    fused = _run(monkeypatch, True, fn)
+    assert cnt.hits >= 4, cnt.hits
+    plain = _run(monkeypatch, False, fn)
+    _native.set_backend("torch")
+    try:
+        G.zero_grad(set_to_none=True)
+        G(A.float()).square().mean().backward()
+        oracle = {n: p.grad.detach().float().clone() for n, p in G.named_parameters()}
+    finally:
+        _native.set_backend("native")
+    for n in fused:
+        ef, ep = rel_err(fused[n], oracle[n]), rel_err(plain[n], oracle[n])
+        assert ef <= 1.5 * ep + 0.01, (n, ef, ep)
