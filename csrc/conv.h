@@ -78,11 +78,11 @@ struct ConvFwdArgs {
   const void* nb_x;
   const float* nb_mean;   // [N][nb_C] (instance) or [nb_C] (batch, nb_batch = 1)
   const float* nb_rstd;
-  const float* nb_gamma;  // null = no affine
+  const float* nb_gamma;  // unused: the host fuses non-affine norms only
   const float* nb_beta;
   int nb_act, nb_batch, nb_c0, nb_C, nb_nchunks;
   float* nb_ws;
-  int epi_serial;   // A/B knob (P2P_EPI_SERIAL=1): the store loop without grouped operand prefetch
+  int epi_serial;   // A/B knob (P2P_EPI_SERIAL=1): gate / skip-gradient dgrads on the plain epilogue, not EXT
 };
 
 // Weight gradient: C[R][Kq] = sum_m P[m][R] * im2col(Q)[m][Kq], written to per-split

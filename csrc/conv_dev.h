@@ -74,10 +74,153 @@ __device__ __forceinline__ float d2s_pixel(int mode, long P, const bf16* c, cons
   return l1;
 }
 
+// Store loop of the EXT dgrad epilogue (see conv_epilogue): the bf16 tile is staged in Cs.
+// Per output chunk: act'(x) gate, + the parked skip gradient, store, and -- for the channels
+// of a norm's output (nb_*) -- sum(d) / sum(d * xhat) with d = dz * act'(xhat) (non-affine
+// norms; the host only fuses those).  A thread's 8-channel chunk is fixed (NT % CPR == 0);
+// its operand loads are issued two rows ahead so their latencies overlap.
+template <int BM, int BN, int MODE, int NT, typename PixF>
+__device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const ClassGeom& g, int m0, int n0,
+                                                  char* smem, const bf16* Cs, int LDC, int HWq, int s,
+                                                  PixF&& out_pix) {
+  constexpr int CPR = BN / 8;
+  static_assert(NT % CPR == 0, "a thread's 8-channel chunk is fixed across the store loop");
+  const int tid = threadIdx.x;
+  const int co_t = n0 + (tid % CPR) * 8;
+  const bool first_t = co_t < a.Csplit;
+  const int ld_t = first_t ? a.Csplit : a.Cout - a.Csplit;
+  const int cof_t = first_t ? co_t : co_t - a.Csplit;
+  const bf16* xb_t = static_cast<const bf16*>(first_t ? a.xb1 : a.xb2);
+  const bool gate_t = a.act_bwd && xb_t;   // a null half is gated by its producer's backward
+  const bool res_t = a.res1 && first_t;    // host: res1 only with Csplit == Cout
+  bf16* y_t = static_cast<bf16*>(first_t ? a.y1 : a.y2);
+  const bf16* res_p = static_cast<const bf16*>(a.res1);
+  const bf16* nbx_p = static_cast<const bf16*>(a.nb_x);
+  const int nb_co = co_t - a.nb_c0;
+  const bool nb_on = a.nb_ws != nullptr && nb_co >= 0 && nb_co < a.nb_C;
+  const float nb_slope = a.nb_act ? neg_slope(a.nb_act) : 1.f;
+  // xhat = x * rs + c1 (c1 = -mean * rstd)
+  float rs[8], c1[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    rs[j] = c1[j] = s1[j] = s2[j] = 0.f;
+    if (nb_on) {
+      const long si = a.nb_batch ? nb_co + j : (long)(m0 / HWq) * a.nb_C + nb_co + j;
+      rs[j] = a.nb_rstd[si];
+      c1[j] = -a.nb_mean[si] * rs[j];
+    }
+  }
+  const u32x4 z4 = {0u, 0u, 0u, 0u};
+  auto ld16 = [](const bf16* p) __attribute__((always_inline)) { return *reinterpret_cast<const u32x4*>(p); };
+  auto finish = [&](int row, long pix, u32x4 xv, u32x4 rv, u32x4 nv) __attribute__((always_inline)) {
+    u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * LDC + (tid % CPR) * 8);
+    if (gate_t) {
+      if (a.act_bwd == ACT_RELU) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t xw = xv[q];
+          uint32_t keep = 0;
+          if ((int16_t)(xw & 0xffffu) > 0) keep |= 0xffffu;
+          if ((int16_t)(xw >> 16) > 0) keep |= 0xffff0000u;
+          v[q] &= keep;
+        }
+      } else {
+        bf16x8 vb = __builtin_bit_cast(bf16x8, v);
+        const bf16x8 xb8 = __builtin_bit_cast(bf16x8, xv);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          vb[q] = (bf16)((float)vb[q] * act_grad_from_input((float)xb8[q], a.act_bwd));
+        v = __builtin_bit_cast(u32x4, vb);
+      }
+    }
+    if (res_t) {
+      bf16x8 vb = __builtin_bit_cast(bf16x8, v);
+      const bf16x8 rb = __builtin_bit_cast(bf16x8, rv);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) vb[q] = (bf16)((float)vb[q] + (float)rb[q]);
+      v = __builtin_bit_cast(u32x4, vb);
+    }
+    *reinterpret_cast<u32x4*>(y_t + pix * ld_t + cof_t) = v;
+    if (nb_on) {   // from the stored bf16 dz, as the unfused partial pass reads it
+      const bf16x8 dz = __builtin_bit_cast(bf16x8, v);
+      const bf16x8 xn = __builtin_bit_cast(bf16x8, nv);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float xh = (float)xn[q] * rs[q] + c1[q];
+        const float d = (float)dz[q] * (xh > 0.f ? 1.f : nb_slope);
+        s1[q] += d;
+        s2[q] += d * xh;
+      }
+    }
+  };
+  constexpr int IT = (BM * CPR) / NT;   // rows per thread
+  constexpr int RSTEP = NT / CPR;
+  if constexpr (IT >= 2 && (BM * CPR) % NT == 0 && IT % 2 == 0) {
+    if (co_t < a.Cout) {
+      for (int g0 = 0; g0 < IT; g0 += 2) {
+        long pixv[2];
+        u32x4 xv[2], rv[2], nv[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int m = m0 + tid / CPR + (g0 + u) * RSTEP;
+          const bool ok = m < g.Mc;
+          pixv[u] = ok ? out_pix(m) : -1;
+          xv[u] = (gate_t && ok) ? ld16(xb_t + pixv[u] * ld_t + cof_t) : z4;
+          rv[u] = (res_t && ok) ? ld16(res_p + pixv[u] * ld_t + cof_t) : z4;
+          nv[u] = (nb_on && ok) ? ld16(nbx_p + pixv[u] * a.nb_C + nb_co) : z4;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          if (pixv[u] >= 0) finish(tid / CPR + (g0 + u) * RSTEP, pixv[u], xv[u], rv[u], nv[u]);
+      }
+    }
+  } else {
+    for (int c = tid; c < BM * CPR; c += NT) {
+      const int row = c / CPR;
+      const int m = m0 + row;
+      if (m >= g.Mc || co_t >= a.Cout) continue;
+      const long pix = out_pix(m);
+      finish(row, pix, gate_t ? ld16(xb_t + pix * ld_t + cof_t) : z4, res_t ? ld16(res_p + pix * ld_t + cof_t) : z4,
+             nb_on ? ld16(nbx_p + pix * a.nb_C + nb_co) : z4);
+    }
+  }
+  if (a.nb_ws) {
+    // per column: the NT / CPR threads sharing its chunk, summed in a fixed order
+    __syncthreads();   // every thread is done with the staged tile
+    float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      red[tid * 16 + q] = s1[q];
+      red[tid * 16 + 8 + q] = s2[q];
+    }
+    __syncthreads();
+    if (tid < BN) {
+      const int cc = tid >> 3, q = tid & 7;
+      const int co = n0 + tid - a.nb_c0;
+      if (co >= 0 && co < a.nb_C) {
+        float S1 = 0.f, S2 = 0.f;
+        for (int k = 0; k < NT / CPR; ++k) {
+          S1 += red[(cc + CPR * k) * 16 + q];
+          S2 += red[(cc + CPR * k) * 16 + 8 + q];
+        }
+        const int img = m0 / HWq;
+        const int cls = g.ry * s + g.rx;
+        const int chunk = cls * (HWq / BM) + (m0 - img * HWq) / BM;
+        const long o = ((long)img * a.nb_nchunks + chunk) * a.nb_C + co;
+        a.nb_ws[o] = S1;
+        a.nb_ws[(long)a.N * a.nb_nchunks * a.nb_C + o] = S2;
+      }
+    }
+  }
+}
+
 // bias + output activation in registers, the bf16 tile staged through LDS, 16-B stores
 // with the optional act'(x) multiply (dgrad) and the concat channel split; split-K tiles
 // accumulate fp32 atomics instead.
-template <int BM, int BN, int WM, int WN, int MODE, int NT>
+// EXT (dgrad kernels with an act' gate, a parked skip gradient or fused norm-backward partials):
+// the store loop prefetches those operands two rows at a time and accumulates the partials.  A
+// separate instantiation: its registers would halve the occupancy of the plain store loop.
+template <int BM, int BN, int WM, int WN, int MODE, int NT, bool EXT = false>
 __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassGeom& g,
                                               f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
                                               int n0, char* smem, const FastDiv& fd_hwq,
@@ -216,45 +359,24 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
     }
   }
 
+  if constexpr (!EXT) {
   constexpr int CPR = BN / 8;  // 8-channel chunks per row
-  static_assert(NT % CPR == 0, "a thread's 8-channel chunk is fixed across the store loop");
   const Fp8Shadow qsh{static_cast<uint8_t*>(a.q_out), a.q_site, a.q_fmt};
   const float qsc = qsh.q ? fp8_shadow_scale(qsh) : 0.f;
   float qmax = 0.f;
-  // fused norm-backward partials: this thread's fixed chunk of 8 channels
-  const int nb_co = n0 + (tid % CPR) * 8 - a.nb_c0;
-  const bool nb_on = a.nb_ws != nullptr && nb_co >= 0 && nb_co < a.nb_C;
-  float nb_mu[8], nb_rs[8], nb_ga[8], nb_be[8], nb_s1[8], nb_s2[8];
-  if (a.nb_ws) {
-    const int img = m0 / HWq;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int ci = nb_on ? nb_co + j : 0;
-      const long si = a.nb_batch ? ci : (long)img * a.nb_C + ci;
-      nb_mu[j] = a.nb_mean[si];
-      nb_rs[j] = a.nb_rstd[si];
-      nb_ga[j] = a.nb_gamma ? a.nb_gamma[ci] : 1.f;
-      nb_be[j] = a.nb_gamma ? a.nb_beta[ci] : 0.f;
-      nb_s1[j] = nb_s2[j] = 0.f;
-    }
-  }
-  // the thread's 8-channel chunk is fixed across the store loop: its column constants once
-  const int co_t = n0 + (tid % CPR) * 8;
-  const bool first_t = co_t < a.Csplit;
-  const int ld_t = first_t ? a.Csplit : a.Cout - a.Csplit;
-  const int cof_t = first_t ? co_t : co_t - a.Csplit;
-  const bf16* xb_t = static_cast<const bf16*>(first_t ? a.xb1 : a.xb2);
-  const bool gate_t = a.act_bwd && xb_t;   // a null half is gated by its producer's backward
-  const bool res_t = a.res1 && first_t;    // host: res1 only with Csplit == Cout
-  bf16* y_t = static_cast<bf16*>(first_t ? a.y1 : a.y2);
-  const bf16* res_p = static_cast<const bf16*>(a.res1);
-  const bf16* nbx_p = static_cast<const bf16*>(a.nb_x);
-  const u32x4 z4 = {0u, 0u, 0u, 0u};
-  // one output chunk from the staged tile and its prefetched operands: act' gate (xv), the
-  // other consumer's gradient (rv), store, norm-backward partials (nv = the norm's input)
-  auto finish = [&](int row, long pix, u32x4 xv, u32x4 rv, u32x4 nv) __attribute__((always_inline)) {
-    u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * LDC + (tid % CPR) * 8);
-    if (gate_t) {
+  for (int c = tid; c < BM * CPR; c += NT) {
+    const int row = c / CPR, cc = c - row * CPR;
+    const int m = m0 + row;
+    const int co = n0 + cc * 8;
+    if (m >= g.Mc || co >= a.Cout) continue;
+    const long pix = out_pix(m);
+    u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * LDC + cc * 8);
+    const bool first = co < a.Csplit;
+    const int ld = first ? a.Csplit : a.Cout - a.Csplit;
+    const int cof = first ? co : co - a.Csplit;
+    const bf16* xb = static_cast<const bf16*>(first ? a.xb1 : a.xb2);
+    if (a.act_bwd && xb) {   // a null half is gated by its producer's backward instead
+      const u32x4 xv = *reinterpret_cast<const u32x4*>(xb + pix * ld + cof);
       if (a.act_bwd == ACT_RELU) {
         // zero the gradient where x <= 0 (bf16 sign / zero test on the int pipe)
 #pragma unroll
@@ -274,26 +396,15 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
         v = __builtin_bit_cast(u32x4, vb);
       }
     }
-    if (res_t) {
+    if (a.res1 && first) {   // host: res1 only with Csplit == Cout
       bf16x8 vb = __builtin_bit_cast(bf16x8, v);
-      const bf16x8 rb = __builtin_bit_cast(bf16x8, rv);
+      const bf16x8 rb = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(a.res1) + pix * ld + cof);
 #pragma unroll
       for (int q = 0; q < 8; ++q) vb[q] = (bf16)((float)vb[q] + (float)rb[q]);
       v = __builtin_bit_cast(u32x4, vb);
     }
-    *reinterpret_cast<u32x4*>(y_t + pix * ld_t + cof_t) = v;
-    if (nb_on) {   // d = dz * act'(z) from the stored bf16 dz (as the unfused partial pass reads it)
-      const bf16x8 dz = __builtin_bit_cast(bf16x8, v);
-      const bf16x8 xn = __builtin_bit_cast(bf16x8, nv);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float xh = ((float)xn[q] - nb_mu[q]) * nb_rs[q];
-        const float z = xh * nb_ga[q] + nb_be[q];
-        const float d = (float)dz[q] * (a.nb_act ? (z > 0.f ? 1.f : neg_slope(a.nb_act)) : 1.f);
-        nb_s1[q] += d;
-        nb_s2[q] += d * xh;
-      }
-    }
+    bf16* y = static_cast<bf16*>(first ? a.y1 : a.y2);
+    *reinterpret_cast<u32x4*>(y + pix * ld + cof) = v;
     if (qsh.q) {  // host: only with Csplit == Cout, no act_bwd
       const bf16x8 vb = __builtin_bit_cast(bf16x8, v);
       float r[8];
@@ -302,75 +413,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
         r[q] = (float)vb[q];
         qmax = fmaxf(qmax, fabsf(r[q]));
       }
-      *reinterpret_cast<uint2*>(qsh.q + pix * ld_t + cof_t) = fp8_pack8(r, qsc, qsh.fmt);
-    }
-  };
-  auto ld16 = [](const bf16* p) __attribute__((always_inline)) { return *reinterpret_cast<const u32x4*>(p); };
-  constexpr int IT = (BM * CPR) / NT;   // rows per thread
-  // (only when there is something to prefetch: a plain store loop runs faster ungrouped)
-  if (IT >= 1 && (BM * CPR) % NT == 0 && !a.epi_serial && (gate_t || res_t || nb_on)) {
-    // groups of G rows: the gate / residual / norm-input loads of a group are all issued
-    // before any of its rows is finished, so their latencies overlap instead of serialising
-    constexpr int G = IT < 4 ? (IT < 1 ? 1 : IT) : 4;
-    static_assert(IT < 1 || IT % G == 0, "prefetch groups");
-    constexpr int RSTEP = NT / CPR;
-    if (co_t < a.Cout) {
-      for (int g0 = 0; g0 < IT; g0 += G) {
-        long pixv[G];
-        u32x4 xv[G], rv[G], nv[G];
-#pragma unroll
-        for (int u = 0; u < G; ++u) {
-          const int row = tid / CPR + (g0 + u) * RSTEP;
-          const int m = m0 + row;
-          const bool ok = m < g.Mc;
-          pixv[u] = ok ? out_pix(m) : -1;
-          xv[u] = (gate_t && ok) ? ld16(xb_t + pixv[u] * ld_t + cof_t) : z4;
-          rv[u] = (res_t && ok) ? ld16(res_p + pixv[u] * ld_t + cof_t) : z4;
-          nv[u] = (nb_on && ok) ? ld16(nbx_p + pixv[u] * a.nb_C + nb_co) : z4;
-        }
-#pragma unroll
-        for (int u = 0; u < G; ++u)
-          if (pixv[u] >= 0) finish(tid / CPR + (g0 + u) * RSTEP, pixv[u], xv[u], rv[u], nv[u]);
-      }
-    }
-  } else {
-    for (int c = tid; c < BM * CPR; c += NT) {
-      const int row = c / CPR;
-      const int m = m0 + row;
-      if (m >= g.Mc || co_t >= a.Cout) continue;
-      const long pix = out_pix(m);
-      finish(row, pix, gate_t ? ld16(xb_t + pix * ld_t + cof_t) : z4, res_t ? ld16(res_p + pix * ld_t + cof_t) : z4,
-             nb_on ? ld16(nbx_p + pix * a.nb_C + nb_co) : z4);
+      *reinterpret_cast<uint2*>(qsh.q + pix * ld + cof) = fp8_pack8(r, qsc, qsh.fmt);
     }
   }
   if (qsh.q) fp8_amax_commit(qmax, qsh.site);
-  if (a.nb_ws) {
-    // per column: the NT / CPR threads sharing its chunk, summed in a fixed order
-    __syncthreads();   // every thread is done with the staged tile
-    float* red = reinterpret_cast<float*>(smem);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      red[tid * 16 + q] = nb_s1[q];
-      red[tid * 16 + 8 + q] = nb_s2[q];
-    }
-    __syncthreads();
-    if (tid < BN) {
-      const int cc = tid >> 3, q = tid & 7;
-      const int co = n0 + tid - a.nb_c0;
-      if (co >= 0 && co < a.nb_C) {
-        float S1 = 0.f, S2 = 0.f;
-        for (int k = 0; k < NT / CPR; ++k) {
-          S1 += red[(cc + CPR * k) * 16 + q];
-          S2 += red[(cc + CPR * k) * 16 + 8 + q];
-        }
-        const int img = m0 / HWq;
-        const int cls = g.ry * s + g.rx;
-        const int chunk = cls * (HWq / BM) + (m0 - img * HWq) / BM;
-        const long o = ((long)img * a.nb_nchunks + chunk) * a.nb_C + co;
-        a.nb_ws[o] = S1;
-        a.nb_ws[(long)a.N * a.nb_nchunks * a.nb_C + o] = S2;
-      }
-    }
+  } else {
+    conv_epilogue_ext<BM, BN, MODE, NT>(a, g, m0, n0, smem, Cs, LDC, HWq, s, out_pix);
   }
 }
 

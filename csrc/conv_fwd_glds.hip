@@ -62,7 +62,8 @@ __device__ __forceinline__ u32x4 relu_fp8x16(u32x4 v) {
 // PK8 (non-FASTK, MODE 0, bf16): the packed 8-channel image inputs (C1 == 8, no second
 // source, KW | 8) -- one 16-B chunk is exactly one tap, so a row's chunk keeps its tap offset
 // (ty0 + kt * 8 / KW, tx) from tile to tile and the loader needs no per-tile divisions.
-template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU, int F8, bool PK8 = false>
+template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU, int F8, bool PK8 = false,
+          bool EXT = false>
 __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs a) {
   static_assert(!PK8 || (!FASTK && MODE == 0 && F8 == 0), "PK8: packed bf16 image convs");
   using T = typename std::conditional<F8 != 0, uint8_t, bf16>::type;
@@ -460,10 +461,11 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
     }
   }
   __syncthreads();  // every wave done with the ring before the epilogue reuses the LDS
-  conv_epilogue<BM, BN, WM, WN, MODE, NT>(a, g, acc, m0, n0, smem, fd_hwq, fd_wq);
+  conv_epilogue<BM, BN, WM, WN, MODE, NT, EXT>(a, g, acc, m0, n0, smem, fd_hwq, fd_wq);
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU, int F8, bool PK8 = false>
+template <int BM, int BN, int WM, int WN, int MODE, int STAGES, bool FASTK, bool RELU, int F8, bool PK8 = false,
+          bool EXT = false>
 static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   if ((BM / WM / 16) * (BN / WN / 16) > 16 && a.splits > 1) return -2;   // no split-K epilogue in big wave tiles
   constexpr int pipe = STAGES * (BM + BN) * BK * 2;
@@ -472,7 +474,7 @@ static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU, F8, PK8>),
+        reinterpret_cast<const void*>(&conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU, F8, PK8, EXT>),
         hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
@@ -491,12 +493,12 @@ static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   const long mtiles = (mmax + BM - 1) / BM;
   const long ntiles = (a.Cout + BN - 1) / BN;
   dim3 grid((unsigned)(mtiles * ntiles * classes), 1, (unsigned)a.splits);
-  hipLaunchKernelGGL((conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU, F8, PK8>), grid, dim3(WM * WN * 64), smem,
+  hipLaunchKernelGGL((conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU, F8, PK8, EXT>), grid, dim3(WM * WN * 64), smem,
                      st, a);
   return (int)hipGetLastError();
 }
 
-template <int MODE, bool FASTK, bool RELU, int F8, bool PK8 = false>
+template <int MODE, bool FASTK, bool RELU, int F8, bool PK8 = false, bool EXT = false>
 static int dispatch_glds2(const ConvFwdArgs& a, int variant, hipStream_t st) {
   if constexpr (F8 != 0) {
     // fp8: the bf16 winners only (256x256 / 256x128 for wide layers, 128x64 below)
@@ -516,30 +518,30 @@ static int dispatch_glds2(const ConvFwdArgs& a, int variant, hipStream_t st) {
     if (a.Cout > 32) return launch_glds<128, 64, 2, 2, MODE, 2, FASTK, RELU, F8, true>(a, st);
     return -2;
   }
-  if (a.Cout > 128 && variant == 5) return launch_glds<256, 256, 2, 4, MODE, 2, FASTK, RELU, F8>(a, st);
+  if (a.Cout > 128 && variant == 5) return launch_glds<256, 256, 2, 4, MODE, 2, FASTK, RELU, F8, false, EXT>(a, st);
   // 7 = 256x32 on 4 waves of 64x32: the skinny union GEMMs of the packed-image layers
   // (d1 forward / c1 dgrad: 4 parity classes x 3 image channels, padded to 32 columns)
   if (variant == 7) {
     if constexpr (MODE == 0 && FASTK) {
-      if (a.Cout <= 32) return launch_glds<256, 32, 4, 1, MODE, 2, FASTK, RELU, F8>(a, st);
+      if (a.Cout <= 32) return launch_glds<256, 32, 4, 1, MODE, 2, FASTK, RELU, F8, false, EXT>(a, st);
     }
     return -2;
   }
   // 8 = 256x64 on 2 waves of 128x64, 9 = 256x128 on 4 waves of 128x64: the 256x256 tile's
   // per-wave operand reuse (384 B of LDS fragments per MFMA) for N = 64 / 128 layers
-  if (variant == 8 && a.Cout <= 64) return launch_glds<256, 64, 2, 1, MODE, 2, FASTK, RELU, F8>(a, st);
+  if (variant == 8 && a.Cout <= 64) return launch_glds<256, 64, 2, 1, MODE, 2, FASTK, RELU, F8, false, EXT>(a, st);
   if (variant == 9 && a.Cout > 64 && a.Cout <= 128)
-    return launch_glds<256, 128, 2, 2, MODE, 2, FASTK, RELU, F8>(a, st);
+    return launch_glds<256, 128, 2, 2, MODE, 2, FASTK, RELU, F8, false, EXT>(a, st);
   if (a.Cout > 64) {
-    if (variant == 5) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU, F8>(a, st);
-    if (variant == 2) return launch_glds<128, 128, 2, 2, MODE, 2, FASTK, RELU, F8>(a, st);
-    if (variant == 3) return launch_glds<128, 128, 2, 2, MODE, 3, FASTK, RELU, F8>(a, st);
-    if (variant == 4) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU, F8>(a, st);
+    if (variant == 5) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU, F8, false, EXT>(a, st);
+    if (variant == 2) return launch_glds<128, 128, 2, 2, MODE, 2, FASTK, RELU, F8, false, EXT>(a, st);
+    if (variant == 3) return launch_glds<128, 128, 2, 2, MODE, 3, FASTK, RELU, F8, false, EXT>(a, st);
+    if (variant == 4) return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU, F8, false, EXT>(a, st);
   } else if (a.Cout > 32) {
-    if (variant == 6) return launch_glds<256, 64, 4, 1, MODE, 2, FASTK, RELU, F8>(a, st);
-    if (variant == 2) return launch_glds<128, 64, 2, 2, MODE, 2, FASTK, RELU, F8>(a, st);
-    if (variant == 3) return launch_glds<128, 64, 2, 2, MODE, 3, FASTK, RELU, F8>(a, st);
-    if (variant == 4) return launch_glds<256, 64, 4, 2, MODE, 3, FASTK, RELU, F8>(a, st);
+    if (variant == 6) return launch_glds<256, 64, 4, 1, MODE, 2, FASTK, RELU, F8, false, EXT>(a, st);
+    if (variant == 2) return launch_glds<128, 64, 2, 2, MODE, 2, FASTK, RELU, F8, false, EXT>(a, st);
+    if (variant == 3) return launch_glds<128, 64, 2, 2, MODE, 3, FASTK, RELU, F8, false, EXT>(a, st);
+    if (variant == 4) return launch_glds<256, 64, 4, 2, MODE, 3, FASTK, RELU, F8, false, EXT>(a, st);
   }
   return -2;
   }
@@ -559,6 +561,13 @@ static int dispatch_glds(const ConvFwdArgs& a, int variant, hipStream_t st) {
     if (!fastk && a.C1 == 8 && a.C2 == 0 && a.KW <= 8 && 8 % a.KW == 0 && variant != 1)
       return dispatch_glds2<MODE, false, false, F8, true>(a, variant, st);
   }
+  if constexpr (F8 == 0) {
+    // dgrads with an act' gate / parked skip gradient / fused norm partials: the EXT epilogue
+    if (a.nb_ws || ((a.act_bwd || a.res1) && !a.epi_serial))
+      return fastk ? dispatch_glds2<MODE, true, false, F8, false, true>(a, variant, st)
+                   : dispatch_glds2<MODE, false, false, F8, false, true>(a, variant, st);
+  }
+  if (a.nb_ws) return -2;   // (fp8 / input-ReLU convs never carry fused norm partials)
   return fastk ? dispatch_glds2<MODE, true, false, F8>(a, variant, st)
                : dispatch_glds2<MODE, false, false, F8>(a, variant, st);
 }
