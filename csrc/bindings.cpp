@@ -401,7 +401,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   // the packed-image halo kernel (below) beats the generic tile with fused partials: keep it
   const bool pk8_halo = mode == 0 && !fp8 && C1 == 8 && C2 == 0 && KH == 4 && KW == 4 && stride == 2 && pad == 1 &&
                         (Cout == 64 || Cout == 128) && std::getenv("P2P_NO_HALO") == nullptr;
-  if (nb_x && nb_half && !nb_gamma && glds_ok && splits == 1 && !fp8 && !want_stats && !pk8_halo) {
+  if (nb_x && nb_half && !nb_gamma && glds_ok && splits == 1 && fp8 != 1 && !want_stats && !pk8_halo) {
     const int64_t c0 = nb_half == 1 ? 0 : Csplit;
     const int64_t nC = nb_half == 1 ? Csplit : Cout - Csplit;
     bool ok = nC > 0 && nC % 8 == 0 && (nb_half == 1 || Csplit < Cout);

@@ -502,12 +502,12 @@ template <int MODE, bool FASTK, bool RELU, int F8, bool PK8 = false, bool EXT = 
 static int dispatch_glds2(const ConvFwdArgs& a, int variant, hipStream_t st) {
   if constexpr (F8 != 0) {
     // fp8: the bf16 winners only (256x256 / 256x128 for wide layers, 128x64 below)
-    if (a.Cout > 128 && variant == 5) return launch_glds<256, 256, 2, 4, MODE, 2, FASTK, RELU, F8>(a, st);
+    if (a.Cout > 128 && variant == 5) return launch_glds<256, 256, 2, 4, MODE, 2, FASTK, RELU, F8, false, EXT>(a, st);
     if (a.Cout > 64) {
-      if (variant == 2) return launch_glds<128, 128, 2, 2, MODE, 2, FASTK, RELU, F8>(a, st);
-      return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU, F8>(a, st);
+      if (variant == 2) return launch_glds<128, 128, 2, 2, MODE, 2, FASTK, RELU, F8, false, EXT>(a, st);
+      return launch_glds<256, 128, 4, 2, MODE, 3, FASTK, RELU, F8, false, EXT>(a, st);
     }
-    if (a.Cout > 32) return launch_glds<128, 64, 2, 2, MODE, 2, FASTK, RELU, F8>(a, st);
+    if (a.Cout > 32) return launch_glds<128, 64, 2, 2, MODE, 2, FASTK, RELU, F8, false, EXT>(a, st);
     return -2;
   } else {
   // variant: 2 = 2-stage 128-row tile, 3 = 3-stage 128-row tile, 4 = 3-stage 256x128 8 waves,
@@ -561,8 +561,9 @@ static int dispatch_glds(const ConvFwdArgs& a, int variant, hipStream_t st) {
     if (!fastk && a.C1 == 8 && a.C2 == 0 && a.KW <= 8 && 8 % a.KW == 0 && variant != 1)
       return dispatch_glds2<MODE, false, false, F8, true>(a, variant, st);
   }
-  if constexpr (F8 == 0) {
-    // dgrads with an act' gate / parked skip gradient / fused norm partials: the EXT epilogue
+  if constexpr (F8 != 1) {
+    // dgrads (bf16 or e5m2 gradient operands) with an act' gate / parked skip gradient / fused
+    // norm partials: the EXT epilogue
     if (a.nb_ws || ((a.act_bwd || a.res1) && !a.epi_serial))
       return fastk ? dispatch_glds2<MODE, true, false, F8, false, true>(a, variant, st)
                    : dispatch_glds2<MODE, false, false, F8, false, true>(a, variant, st);

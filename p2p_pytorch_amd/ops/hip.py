@@ -202,21 +202,24 @@ def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, 
         a2, s2 = _f8.quant(x2, (k, role, 2), fmt) if x2 is not None else (None, None)
         return P().conv_fwd(a1, a2, w8, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout,
                             act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, s1, s2, sw, *yq, res=res,
-                            alpha=alpha)
+                            alpha=alpha, **_nb_kwargs(nb if not yq else None))
     if wimg is None:
         wimg = _weight_image(weight, swap, xp, yp)
     yq = ()
     if y_qkey is not None and _f8.enabled():
         ysite, fresh = _f8.producer_site(x1.device, y_qkey)
         yq = (None, None, None, None, 0) if fresh else (None, None, None, ysite, _f8.E4M3)
-    kw = {}
-    if nb is not None and not yq:
-        half, (nx, nmean, nrstd, ng, nbeta, nact, nbatch) = nb
-        kw = dict(nb_x=nx, nb_mean=nmean, nb_rstd=nrstd, nb_gamma=ng, nb_beta=nbeta, nb_act=nact,
-                  nb_half=half, nb_batch=nbatch)
     return P().conv_fwd(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout,
                         act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, *yq, res=res, alpha=alpha,
-                        **kw)
+                        **_nb_kwargs(nb if not yq else None))
+
+
+def _nb_kwargs(nb):
+    if nb is None:
+        return {}
+    half, (nx, nmean, nrstd, ng, nbeta, nact, nbatch) = nb
+    return dict(nb_x=nx, nb_mean=nmean, nb_rstd=nrstd, nb_gamma=ng, nb_beta=nbeta, nb_act=nact,
+                nb_half=half, nb_batch=nbatch)
 
 
 def prepare_weights(*modules):
