@@ -171,7 +171,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                              const optional<Tensor>& res, const optional<Tensor>& alpha,
                              const optional<Tensor>& nb_x, const optional<Tensor>& nb_mean,
                              const optional<Tensor>& nb_rstd, const optional<Tensor>& nb_gamma,
-                             const optional<Tensor>& nb_beta, int64_t nb_act, int64_t nb_half, bool nb_batch) {
+                             const optional<Tensor>& nb_beta, int64_t nb_act, int64_t nb_half, bool nb_batch,
+                             bool nb_colsum) {
   check_act(x1, "conv_fwd x1", true);
   // fp8 operands: x e4m3 (activations) or e5m2 (gradients), weight image e4m3, each with
   // an fp8 scale site (csrc/fp8.hip); outputs stay bf16
@@ -401,7 +402,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   // the packed-image halo kernel (below) beats the generic tile with fused partials: keep it
   const bool pk8_halo = mode == 0 && !fp8 && C1 == 8 && C2 == 0 && KH == 4 && KW == 4 && stride == 2 && pad == 1 &&
                         (Cout == 64 || Cout == 128) && std::getenv("P2P_NO_HALO") == nullptr;
-  if (nb_x && nb_half && !nb_gamma && glds_ok && splits == 1 && fp8 != 1 && !want_stats && !pk8_halo) {
+  if ((nb_x || nb_colsum) && nb_half && !nb_gamma && glds_ok && splits == 1 && fp8 != 1 && !want_stats &&
+      !pk8_halo) {
     const int64_t c0 = nb_half == 1 ? 0 : Csplit;
     const int64_t nC = nb_half == 1 ? Csplit : Cout - Csplit;
     bool ok = nC > 0 && nC % 8 == 0 && (nb_half == 1 || Csplit < Cout);
@@ -411,7 +413,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       hwq = (OH / stride) * (OW / stride);
     }
     ok = ok && hwq % bm == 0;
-    if (ok) {
+    if (ok && !nb_colsum) {
       check_act(*nb_x, "conv_fwd nb_x");
       TORCH_CHECK(nb_x->size(0) == N && nb_x->size(1) == nC && nb_x->size(2) == OH && nb_x->size(3) == OW,
                   "conv_fwd: nb_x must match the gradient half");
@@ -419,12 +421,15 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       TORCH_CHECK(nb_mean && nb_rstd && nb_mean->numel() == groups * nC && nb_rstd->numel() == groups * nC &&
                       nb_mean->scalar_type() == at::kFloat && nb_rstd->scalar_type() == at::kFloat,
                   "conv_fwd: nb mean / rstd");
+    }
+    if (ok) {
       if (nb_gamma) TORCH_CHECK(nb_beta && nb_gamma->numel() == nC && nb_beta->numel() == nC, "conv_fwd: nb affine");
       const int64_t nch = classes * (hwq / bm);
       nbp = at::empty({2, N, nch, nC}, x1.options().dtype(at::kFloat));
-      a.nb_x = nb_x->data_ptr();
-      a.nb_mean = nb_mean->data_ptr<float>();
-      a.nb_rstd = nb_rstd->data_ptr<float>();
+      a.nb_colsum = nb_colsum ? 1 : 0;
+      a.nb_x = nb_colsum ? nullptr : nb_x->data_ptr();
+      a.nb_mean = nb_colsum ? nullptr : nb_mean->data_ptr<float>();
+      a.nb_rstd = nb_colsum ? nullptr : nb_rstd->data_ptr<float>();
       a.nb_gamma = nb_gamma ? nb_gamma->data_ptr<float>() : nullptr;
       a.nb_beta = nb_gamma ? nb_beta->data_ptr<float>() : nullptr;
       a.nb_act = (int)nb_act;
@@ -1495,7 +1500,8 @@ TORCH_LIBRARY(p2p, m) {
         "Tensor? xb1, Tensor? xb2, int act_bwd, int Cvalid=0, bool want_stats=False, Tensor? qs_x1=None, "
         "Tensor? qs_x2=None, Tensor? qs_w=None, Tensor(a!)? y_qsite=None, int y_qfmt=0, Tensor? res=None, "
         "Tensor? alpha=None, Tensor? nb_x=None, Tensor? nb_mean=None, Tensor? nb_rstd=None, "
-        "Tensor? nb_gamma=None, Tensor? nb_beta=None, int nb_act=0, int nb_half=0, bool nb_batch=False) "
+        "Tensor? nb_gamma=None, Tensor? nb_beta=None, int nb_act=0, int nb_half=0, bool nb_batch=False, "
+        "bool nb_colsum=False) "
         "-> Tensor[]");
   m.def("fp8_quant(Tensor x, Tensor(a!) site, int fmt, int use_cur=0) -> Tensor");
   m.def("sn_power_iter(Tensor w, Tensor(a!) u, Tensor(b!) v) -> Tensor");

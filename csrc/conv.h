@@ -82,6 +82,8 @@ struct ConvFwdArgs {
   const float* nb_beta;
   int nb_act, nb_batch, nb_c0, nb_C, nb_nchunks;
   float* nb_ws;
+  int nb_colsum;    // 1: plain column sums sum(dz) of the half (the bias gradient of the conv
+                    // that produced it), no norm input read: nb_ws[0] only, nb_x / stats unused
   int epi_serial;   // A/B knob (P2P_EPI_SERIAL=1): gate / skip-gradient dgrads on the plain epilogue, not EXT
 };
 

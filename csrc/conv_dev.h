@@ -98,13 +98,14 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
   const bf16* nbx_p = static_cast<const bf16*>(a.nb_x);
   const int nb_co = co_t - a.nb_c0;
   const bool nb_on = a.nb_ws != nullptr && nb_co >= 0 && nb_co < a.nb_C;
-  const float nb_slope = a.nb_act ? neg_slope(a.nb_act) : 1.f;
+  const bool nb_x_on = nb_on && !a.nb_colsum;   // colsum mode: d = dz, xhat = 0 (rs = c1 = 0)
+  const float nb_slope = (a.nb_act && !a.nb_colsum) ? neg_slope(a.nb_act) : 1.f;
   // xhat = x * rs + c1 (c1 = -mean * rstd)
   float rs[8], c1[8], s1[8], s2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     rs[j] = c1[j] = s1[j] = s2[j] = 0.f;
-    if (nb_on) {
+    if (nb_on && !a.nb_colsum) {
       const long si = a.nb_batch ? nb_co + j : (long)(m0 / HWq) * a.nb_C + nb_co + j;
       rs[j] = a.nb_rstd[si];
       c1[j] = -a.nb_mean[si] * rs[j];
@@ -167,7 +168,7 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
           pixv[u] = ok ? out_pix(m) : -1;
           xv[u] = (gate_t && ok) ? ld16(xb_t + pixv[u] * ld_t + cof_t) : z4;
           rv[u] = (res_t && ok) ? ld16(res_p + pixv[u] * ld_t + cof_t) : z4;
-          nv[u] = (nb_on && ok) ? ld16(nbx_p + pixv[u] * a.nb_C + nb_co) : z4;
+          nv[u] = (nb_x_on && ok) ? ld16(nbx_p + pixv[u] * a.nb_C + nb_co) : z4;
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u)
@@ -181,7 +182,7 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
       if (m >= g.Mc || co_t >= a.Cout) continue;
       const long pix = out_pix(m);
       finish(row, pix, gate_t ? ld16(xb_t + pix * ld_t + cof_t) : z4, res_t ? ld16(res_p + pix * ld_t + cof_t) : z4,
-             nb_on ? ld16(nbx_p + pix * a.nb_C + nb_co) : z4);
+             nb_x_on ? ld16(nbx_p + pix * a.nb_C + nb_co) : z4);
     }
   }
   if (a.nb_ws) {

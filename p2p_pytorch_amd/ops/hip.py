@@ -93,6 +93,10 @@ def _take_stats(x):
 # autograd-accumulated gradient is a new tensor: the norm then runs its own partial pass).
 _norm_out: dict = {}
 _nbp_stash: dict = {}
+# the same hand-off for a biased conv output read whole by one conv (its act' already applied
+# by that consumer, or no activation): the consumer's dgrad epilogue emits the column sums of
+# the gradient -- the producer's bias gradient -- parked in _colsum_stash
+_CS = ("colsum",)
 
 
 def _register_norm_out(z, info):
@@ -217,7 +221,10 @@ def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, 
 def _nb_kwargs(nb):
     if nb is None:
         return {}
-    half, (nx, nmean, nrstd, ng, nbeta, nact, nbatch) = nb
+    half, info = nb
+    if info is _CS:
+        return dict(nb_half=half, nb_colsum=True)
+    nx, nmean, nrstd, ng, nbeta, nact, nbatch = info
     return dict(nb_x=nx, nb_mean=nmean, nb_rstd=nrstd, nb_gamma=ng, nb_beta=nbeta, nb_act=nact,
                 nb_half=half, nb_batch=nbatch)
 
@@ -441,6 +448,9 @@ class ConvFn(torch.autograd.Function):
         ctx.has_x2 = x2 is not None
         ctx.has_bias = bias is not None
         ctx.nb = (None if packed else _norm_lookup(q1), _norm_lookup(q2))
+        if (_NB_FUSE and bias is not None and bias.requires_grad and Coutp == Cout
+                and (cfg.act_out in (None, "none") or cfg.out_gated)):
+            _register_norm_out(y, _CS)
         keep_y = cfg.act_out not in (None, "none") and not cfg.out_gated
         ctx.save_for_backward(q1, q2, weight, y if keep_y else None)
         return y
@@ -608,7 +618,10 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
         if nbp is not None:
             g_half = gx1 if nbh[0] == 1 else gx2
             if g_half is not None:
-                _stash_nbp(g_half, nbp)
+                if nbh[1] is _CS:
+                    _stash_colsum(g_half, nbp[0].sum((0, 1)))
+                else:
+                    _stash_nbp(g_half, nbp)
         if not need_x1:
             gx1 = None
         if not need_x2:
@@ -639,7 +652,7 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
             P().conv_wgrad(gyp, None, 0, q1, q2, act_in, KH, KW, s, p, int(cfg.reflect),
                            cfg.up, gw, 1.0, 0)
     if need_b:
-        gb = _take_colsum(gy) if cfg.act_out in (None, "none") else None
+        gb = _take_colsum(gy) if (cfg.act_out in (None, "none") or cfg.out_gated) else None
         if gb is None:
             gb = torch.empty(Cout, device=gy.device, dtype=torch.float32)
             P().colsum(gyp, gb, 1.0, False)

@@ -171,3 +171,37 @@ def test_nb_unet256_generator_grads(monkeypatch):
     for n in fused:
         ef, ep = rel_err(fused[n], oracle[n]), rel_err(plain[n], oracle[n])
         assert ef <= 1.5 * ep + 0.01, (n, ef, ep)
+
+
+def test_fused_bias_colsum(monkeypatch):
+    """A biased conv whose LeakyReLU' is applied by its consumer's dgrad (out_gated /
+    grad_gate, the U-Net's outermost conv / the PatchGAN's first conv): the consumer's dgrad
+    epilogue emits the gradient's column sums, which become the producer's bias gradient."""
+    x = bf(_rand(64, 32, 64, 64, seed=31))
+    w1 = _rand(64, 32, 4, 4, seed=32, scale=(1 / 512) ** 0.5)
+    b1 = _rand(64, seed=33, scale=0.1)
+    w2 = _rand(128, 64, 4, 4, seed=34, scale=(1 / 1024) ** 0.5)
+    gy = bf(_rand(64, 128, 16, 16, seed=35))
+    taken = []
+    orig = hip._take_colsum
+
+    def take(g):
+        r = orig(g)
+        taken.append(r is not None)
+        return r
+    monkeypatch.setattr(hip, "_take_colsum", take)
+
+    def fn():
+        hw1, hb1 = w1.clone().requires_grad_(True), b1.clone().requires_grad_(True)
+        h = ops.conv2d(x, hw1, hb1, 2, 1, act_out="lrelu", out_gated=True)
+        ops.conv2d(h, w2, None, 2, 1, grad_gate="lrelu").backward(gy)
+        return hw1.grad.float(), hb1.grad.float()
+
+    taken.clear()
+    fused = _run(monkeypatch, True, fn)
+    assert taken == [True], taken
+    taken.clear()
+    plain = _run(monkeypatch, False, fn)
+    assert taken == [False], taken
+    assert rel_err(fused[0], plain[0]) < 1e-2
+    assert rel_err(fused[1], plain[1]) < 1e-2
