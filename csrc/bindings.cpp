@@ -453,7 +453,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   int rc = -2;
   // packed 8-channel image convs (4x4 s2 p1): the halo-tile kernel (csrc/halo_pk8.hip)
   if (mode == 0 && !fp8 && C1 == 8 && C2 == 0 && KH == 4 && KW == 4 && stride == 2 && pad == 1 && !reflect &&
-      up == 1 && act_in == 0 && splits == 1 && !a.stats && !a.nb_ws && !a.q_out && !a.res1 && !a.alpha && (Cout == 64 || Cout == 128) &&
+      up == 1 && act_in == 0 && splits == 1 && !a.stats && !a.nb_ws && !a.res1 && !a.alpha && (Cout == 64 || Cout == 128) &&
       std::getenv("P2P_NO_HALO") == nullptr) {
     p2p::HaloPk8Args h{};
     h.x = static_cast<const __bf16*>(x1.data_ptr());
@@ -474,6 +474,9 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     h.tiles_x = (int)((OW + 15) / 16);
     h.tiles_y = (int)((OH + 15) / 16);
     h.ntiles = (int)N * h.tiles_x * h.tiles_y;
+    h.q = static_cast<uint8_t*>(a.q_out);
+    h.q_site = a.q_site;
+    h.q_fmt = a.q_fmt;
     const bool gate_ok = act_bwd == 0 || act_bwd == 1;
     if (gate_ok && (act_bwd == 0 || Cout == 128) && OH == (H + 2 - 4) / 2 + 1 && OW == (W + 2 - 4) / 2 + 1) {
       if (act_bwd == 0) h.xb1 = h.xb2 = nullptr;

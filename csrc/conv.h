@@ -145,6 +145,9 @@ struct HaloPk8Args {
   const __bf16* xb2;
   const __bf16* zero;
   int tiles_x, tiles_y, ntiles;
+  uint8_t* q;          // optional fp8 shadow of the (Cout 64, unsplit) output, null = off
+  int* q_site;
+  int q_fmt;
 };
 
 // Halo-tile direct conv for stride-1 KxK convs with few channels (csrc/halo_kxk.hip): input

@@ -43,8 +43,11 @@ __device__ __forceinline__ int unit_of(int hy, int hx) { return (hy * 2 + (hx & 
 
 // TN = 8 (128 channels) keeps 128 accumulators + 8 B fragments live: one block per CU
 // (512-register budget, no spill); TN = 4 runs two blocks per CU
-template <int TN, int ACT, bool GATE>
+// QS: also write the e4m3 / e5m2 shadow of the output (fp8 precision: the next conv's operand)
+template <int TN, int ACT, bool GATE, bool QS = false>
 __global__ void __launch_bounds__(256, TN >= 8 ? 1 : 2) halo_pk8_kernel(HaloPk8Args a) {
+  float qsc = 0.f, qmax = 0.f;
+  if constexpr (QS) qsc = fp8_shadow_scale(Fp8Shadow{a.q, a.q_site, a.q_fmt});
   constexpr int NC = TN * 16;              // output channels of the block (== Cout)
   constexpr int PC = 32;                   // channels per epilogue piece
   constexpr int LDC = PC + 8;              // staging row (80 B: 16-B aligned, spread banks)
@@ -188,23 +191,34 @@ __global__ void __launch_bounds__(256, TN >= 8 ? 1 : 2) halo_pk8_kernel(HaloPk8A
           }
         }
         *reinterpret_cast<u32x4*>(yb + pix[q] * ld + cof0 + cc * 8) = v;
+        if constexpr (QS) {   // host: unsplit output (ld == Cout)
+          const bf16x8 vb = __builtin_bit_cast(bf16x8, v);
+          float r[8];
+#pragma unroll
+          for (int w = 0; w < 8; ++w) {
+            r[w] = (float)vb[w];
+            qmax = fmaxf(qmax, fabsf(r[w]));
+          }
+          *reinterpret_cast<uint2*>(a.q + pix[q] * ld + cof0 + cc * 8) = fp8_pack8(r, qsc, a.q_fmt);
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
   }
+  if constexpr (QS) fp8_amax_commit(qmax, a.q_site);
 }
 
-template <int TN, int ACT, bool GATE>
+template <int TN, int ACT, bool GATE, bool QS = false>
 static int launch_pk8(const HaloPk8Args& a, int blocks, hipStream_t st) {
   constexpr int smem = (2 * SUNITS + TN * 16 * 16) * 16;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo_pk8_kernel<TN, ACT, GATE>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo_pk8_kernel<TN, ACT, GATE, QS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
-  hipLaunchKernelGGL((halo_pk8_kernel<TN, ACT, GATE>), dim3(blocks), dim3(256), smem, st, a);
+  hipLaunchKernelGGL((halo_pk8_kernel<TN, ACT, GATE, QS>), dim3(blocks), dim3(256), smem, st, a);
   return (int)hipGetLastError();
 }
 
@@ -215,6 +229,12 @@ extern "C" int p2p_halo_pk8(const p2p::HaloPk8Args* a, int blocks, hipStream_t s
   using namespace p2p;
   const bool gate = a->xb1 != nullptr || a->xb2 != nullptr;
   if (a->Csplit % 32) return -2;   // epilogue pieces never straddle the split
+  if (a->q && (a->Cout != 64 || gate || a->Csplit != a->Cout)) return -2;
+  if (a->Cout == 64 && !gate && a->q) {
+    if (a->act_out == ACT_LRELU) return launch_pk8<4, ACT_LRELU, false, true>(*a, blocks, st);
+    if (a->act_out == ACT_RELU) return launch_pk8<4, ACT_RELU, false, true>(*a, blocks, st);
+    return -2;
+  }
   if (a->Cout == 64 && !gate) {
     if (a->act_out == ACT_LRELU) return launch_pk8<4, ACT_LRELU, false>(*a, blocks, st);
     if (a->act_out == ACT_NONE) return launch_pk8<4, ACT_NONE, false>(*a, blocks, st);
