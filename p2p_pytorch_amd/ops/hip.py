@@ -112,6 +112,10 @@ def _norm_lookup(t):
     return None if ent is None or ent[0] is not t else ent[1]
 
 
+# Invariant both stashes rely on: an entry holds a reference to the gradient tensor, so autograd
+# never accumulates a second consumer's gradient INTO it in place (its InputBuffer only reuses a
+# buffer it holds the last reference to) -- a summed gradient is always a new tensor, whose key
+# or identity does not match, and the consumer of the stash recomputes instead.
 def _stash_nbp(g, parts):
     if len(_nbp_stash) >= 256:
         _nbp_stash.pop(next(iter(_nbp_stash)))
