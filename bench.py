@@ -174,19 +174,11 @@ def main():
                  and (world == 1 or (pdist.backend() == "nccl"
                                      and os.environ.get("P2P_GRAPH_MULTI", "1") != "0")))
     if use_graph:
-        from p2p_pytorch_amd.engine.graph import CapturedStep
-        ok = 1.0
-        try:
-            # capture runs its own warmup steps on a side stream, then records one step
-            step = CapturedStep(step_fn, real_A, real_B, warmup=2)
-        except Exception as e:  # noqa: BLE001 - any capture failure: eager on every rank
-            print(f"[bench] rank {rank}: graph capture failed ({type(e).__name__}: {e}); eager",
-                  file=sys.stderr, flush=True)
-            ok = 0.0
-        if world > 1:
-            ok = pdist.min_scalar(ok, dev)
-        if ok < 1.0:
-            step, use_graph = step_fn, False
+        from p2p_pytorch_amd.engine.graph import capture_agreed
+        # capture runs its own warmup steps on a side stream, then records one step
+        step, use_graph = capture_agreed(
+            step_fn, real_A, real_B, warmup=2,
+            log=lambda m: print(f"[bench] rank {rank}: {m}", file=sys.stderr, flush=True))
     t_w = time.perf_counter()
     for i in range(args.warmup):
         losses = step(real_A, real_B)
@@ -206,6 +198,24 @@ def main():
     dt = time.perf_counter() - t0
     dt_max = pdist.max_scalar(dt, dev)
     loss_vals = {k: float(v) for k, v in losses.items()}
+    comm = None
+    if reducer_g is not None:
+        # after (never inside) the timed region: ONE eager step with the reducers' collectives
+        # on a timed side stream -> per-network all-reduce busy ms, the part left exposed
+        # after backward's last kernel, and the overlap fraction (max over ranks)
+        comm = {"dtype": args.comm_dtype, "bucket_mb": args.bucket_mb}
+        for r in (reducer_g, reducer_d):
+            r.enable_timing()
+        trainer.step(real_A, real_B)
+        sync()
+        for tag, r in (("G", reducer_g), ("D", reducer_d)):
+            st = r.comm_stats()
+            r.enable_timing(False)
+            if st:
+                comm[tag] = {"comm_ms": round(pdist.max_scalar(st["comm_ms"], dev), 3),
+                             "exposed_ms": round(pdist.max_scalar(st["exposed_ms"], dev), 3),
+                             "overlap": round(pdist.min_scalar(st["overlap"], dev), 3),
+                             "buckets": st["buckets"]}
     finite = all(v == v and abs(v) != float("inf") for v in loss_vals.values())
 
     img_s = world * B * args.steps / dt_max
@@ -241,8 +251,7 @@ def main():
                                       if args.precision == "fp8" else "bf16")},
         "max_mem_gib": (round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)
                         if dev.type == "cuda" else None),
-        "comm": ({"dtype": args.comm_dtype, "bucket_mb": args.bucket_mb}
-                 if reducer_g is not None else None),
+        "comm": comm,
         "losses_finite": finite,
         "losses": loss_vals,
     }

@@ -77,6 +77,16 @@ def has_scheduler_state(path) -> bool:
     return "scheduler_g" in torch.load(path, map_location="cpu", weights_only=True, mmap=True)
 
 
+def scheduler_offset(path):
+    """The ``epoch_count`` offset the saved schedulers' lambda was built with (the run that
+    wrote the file records it as ``sched_epoch_count``; files from before that default to
+    1), or None when ``path`` carries no scheduler state (a reference-written file)."""
+    state = torch.load(path, map_location="cpu", weights_only=True, mmap=True)
+    if "scheduler_g" not in state:
+        return None
+    return int(state.get("sched_epoch_count", 1))
+
+
 def load_checkpoint(path, net_g=None, net_c=None, net_d=None, opt_g=None, opt_d=None,
                     sched_g=None, sched_d=None, device=None, strict=True, opt_c=None,
                     sched_c=None):

@@ -110,3 +110,33 @@ class CapturedStep:
                 dst.copy_(src, non_blocking=True)
         self.graph.replay()
         return self.static_out
+
+
+def capture_agreed(step_fn, *example_inputs, warmup: int = 2, log=None):
+    """Capture ``step_fn`` as a :class:`CapturedStep` when it is safe on every rank, else run
+    eager on every rank.  Returns ``(step, captured)``.
+
+    * Only RCCL process groups are captured at world > 1: gloo (the CPU / one-GPU rehearsal
+      backend) stages collectives through the host and cannot be captured, and a failed
+      capture can leave the process in capture mode.
+    * A capture that raises on ANY rank makes every rank fall back to eager (``min_scalar``
+      consensus): collectives must match, so one rank replaying a graph while another runs
+      eager would hang until the watchdog.
+    """
+    from ..parallel import dist as pdist
+    world = pdist.world_size()
+    dev = example_inputs[0].device
+    if dev.type != "cuda" or (world > 1 and pdist.backend() != "nccl"):
+        return step_fn, False
+    ok, step = 1.0, step_fn
+    try:
+        step = CapturedStep(step_fn, *example_inputs, warmup=warmup)
+    except Exception as e:  # noqa: BLE001 - any capture failure: eager on every rank
+        if log is not None:
+            log(f"graph capture failed ({type(e).__name__}: {e}); running eager")
+        ok = 0.0
+    if world > 1:
+        ok = pdist.min_scalar(ok, dev)
+    if ok < 1.0:
+        return step_fn, False
+    return step, True

@@ -28,10 +28,12 @@ class FusedAdam(torch.optim.Optimizer):
         self._lr_t = [torch.tensor([float(g["lr"])], device=dev) for g in self.param_groups]
         self._step_t = [torch.zeros(1, device=dev) for _ in self.param_groups]
         # moments allocated up front (not on first step): the state tensors exist before any
-        # warmup, so a graph capture can snapshot and restore them (engine/graph.py)
+        # warmup, so a graph capture can snapshot and restore them (engine/graph.py); only
+        # for trainable parameters (spectral norm's weight_u / weight_v never get a grad)
         for g in self.param_groups:
             for p in g["params"]:
-                self._init_state(p)
+                if p.requires_grad:
+                    self._init_state(p)
 
     def _init_state(self, p):
         st = self.state[p]

@@ -35,7 +35,8 @@ Mechanism
   * ``force_comm=True`` issues the collectives even at world size 1 (exercises the RCCL
     and capture path on a single GPU).
   * ``enable_timing()`` (logging only): collectives are issued from a side stream
-    bracketed by HIP events, and ``comm_stats()`` reports the last backward's collective
+    bracketed by HIP events (CPU / gloo groups: host clock from launch to the collective's
+    completion callback), and ``comm_stats()`` reports the last backward's collective
     busy time, the part of it left exposed after backward's last kernel, and the overlap
     fraction -- the JSONL "comm ms / overlap %" of SURVEY.md section 5.5.
   * Bucket size: xGMI is point-to-point (7 links x ~153 GB/s per GPU); RCCL's ring /
@@ -45,6 +46,8 @@ Mechanism
 from __future__ import annotations
 
 import contextlib
+import threading
+import time
 
 import torch
 import torch.distributed as dist
@@ -75,6 +78,28 @@ class _StreamJoin:
 
     def wait(self):
         torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+
+
+class _HostEvent:
+    """Host-clock stand-in for a timing HIP event on CPU (gloo) process groups: ``record`` now,
+    or ``record`` from a collective's completion callback; ``elapsed_time`` in ms."""
+    __slots__ = ("t", "_done")
+
+    def __init__(self):
+        self.t = None
+        self._done = threading.Event()
+
+    def record(self, *_):
+        self.t = time.perf_counter()
+        self._done.set()
+        return self
+
+    def synchronize(self):
+        if not self._done.wait(timeout=60.0):
+            raise RuntimeError("GradReducer timing: a collective never completed")
+
+    def elapsed_time(self, other):
+        return (other.t - self.t) * 1e3
 
 
 class GradReducer:
@@ -190,6 +215,18 @@ class GradReducer:
         if not self.comm:
             b.work = True
             return
+        if self._timing and not b.flat.is_cuda:
+            # CPU process group: host clock from the launch to the collective's completion
+            # callback (gloo completes it on its own thread while backward continues)
+            buf = b.flat
+            if b.cbuf is not None:
+                torch.mul(b.flat, 1.0 / self.world, out=b.cbuf)
+                buf = b.cbuf
+            e0, e1 = _HostEvent().record(), _HostEvent()
+            b.work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            b.work.get_future().then(lambda _f, e=e1: e.record())
+            b.events = (e0, e1)
+            return
         timed = self._timing and not torch.cuda.is_current_stream_capturing() and b.flat.is_cuda
         cur = torch.cuda.current_stream(b.flat.device) if b.flat.is_cuda else None
         if timed:
@@ -248,10 +285,12 @@ class GradReducer:
         """Complete the reduction of this backward: launch stragglers, wait (stream-ordered),
         average, and reset bookkeeping for the next backward."""
         end_bwd = None
-        if self._timing and self.comm and self.buckets and self.buckets[0].flat.is_cuda \
-                and not torch.cuda.is_current_stream_capturing():
-            end_bwd = torch.cuda.Event(enable_timing=True)
-            end_bwd.record()
+        if self._timing and self.comm and self.buckets:
+            if not self.buckets[0].flat.is_cuda:
+                end_bwd = _HostEvent().record()
+            elif not torch.cuda.is_current_stream_capturing():
+                end_bwd = torch.cuda.Event(enable_timing=True)
+                end_bwd.record()
         for b in self.buckets:
             if b.work is None:
                 self._launch(b)
@@ -279,7 +318,8 @@ class GradReducer:
         if not self._last or not self._last[0]:
             return {}
         evs, end_bwd = self._last
-        evs[-1][1].synchronize()
+        for _, e1 in evs:
+            e1.synchronize()
         end_bwd.synchronize()
         ref = evs[0][0]
         spans = sorted((ref.elapsed_time(e0), ref.elapsed_time(e1)) for e0, e1 in evs)

@@ -96,6 +96,9 @@ def main():
             C = x1.shape[1] + (x2.shape[1] if x2 is not None else 0)
             taps = KH * KW if mode == 0 else KH * KW / (s * s)
             flop = 2.0 * x1.shape[0] * OH * OW * Cout * taps * C
+            # ideal HBM bytes: every operand read once, the output written once
+            byts = 2.0 * (x1.numel() + (x2.numel() if x2 is not None else 0) + w.numel()
+                          + x1.shape[0] * OH * OW * Cout)
             geo = f"fwd m{mode} N{x1.shape[0]} C{C} {x1.shape[2]}x{x1.shape[3]} -> {Cout} k{KH} s{s} p{pad}" \
                   f"{' refl' if refl else ''}{' up2' if up == 2 else ''} -> {OH}x{OW}"
         else:
@@ -104,6 +107,8 @@ def main():
             Cq = q1.shape[1] + (q2.shape[1] if q2 is not None else 0)
             M = p1.shape[0] * p1.shape[2] * p1.shape[3]
             flop = 2.0 * M * R * KH * KW * Cq
+            byts = 2.0 * (p1.numel() + (p2_.numel() if p2_ is not None else 0) + q1.numel()
+                          + (q2.numel() if q2 is not None else 0)) + 4.0 * R * KH * KW * Cq
             geo = f"wgrad R{R} C{Cq} k{KH} s{s} p{pad}{' refl' if refl else ''}{' up2' if up == 2 else ''}" \
                   f" M{M} (p {p1.shape[2]}x{p1.shape[3]}, q {q1.shape[2]}x{q1.shape[3]})"
         fn = getattr(real, name)
@@ -129,29 +134,34 @@ def main():
                     alt[v] = timed()
                 finally:
                     os.environ.pop(key, None)
-        rows.append((geo, ms, flop, alt))
+        rows.append((geo, ms, flop, alt, byts))
     agg = collections.OrderedDict()
     altagg = collections.defaultdict(lambda: collections.Counter())
-    for geo, ms, flop, alt in rows:
-        e = agg.setdefault(geo, [0, 0.0, 0.0])
+    for geo, ms, flop, alt, byts in rows:
+        e = agg.setdefault(geo, [0, 0.0, 0.0, 0.0])
         e[0] += 1
         e[1] += ms
         e[2] += flop
+        e[3] += byts
         for v, t in alt.items():
             altagg[geo][v] += t
     tot = sum(v[1] for v in agg.values())
     print(f"{len(rows)} conv calls, {tot:.2f} ms replayed in isolation "
           f"({sum(v[2] for v in agg.values()) / 1e12:.2f} TFLOP)")
-    print(f"{'ms':>8} {'%':>5} {'n':>3} {'TF/s':>7}  geometry")
-    for geo, (n, ms, flop) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:args.top]:
+    print("ideal MB = every operand read once + output written once (the HBM floor of the call);"
+          " floor ms = that at 6.3 TB/s")
+    print(f"{'ms':>8} {'%':>5} {'n':>3} {'TF/s':>7} {'idealMB':>8} {'floor':>6}  geometry")
+    for geo, (n, ms, flop, byts) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:args.top]:
         extra = "".join(f"  [{v}: {t:.3f}]" for v, t in altagg[geo].items())
-        print(f"{ms:8.3f} {100 * ms / tot:5.1f} {n:3d} {flop / ms / 1e9:7.1f}  {geo}{extra}")
+        print(f"{ms:8.3f} {100 * ms / tot:5.1f} {n:3d} {flop / ms / 1e9:7.1f} {byts / n / 1e6:8.1f} "
+              f"{byts / 6.3e9:6.3f}  {geo}{extra}")
     print("\nother HIP ops of the step (calls, Melements of the first tensor argument):")
     for k, n in others.most_common():
         print(f"  {n:4d} {other_elems[k] / 1e6:10.1f}  {k}")
     if args.json:
         with open(args.json, "w") as f:
-            json.dump([{"geometry": g, "calls": v[0], "ms": v[1], "flop": v[2]} for g, v in agg.items()],
+            json.dump([{"geometry": g, "calls": v[0], "ms": v[1], "flop": v[2], "ideal_bytes": v[3]}
+                       for g, v in agg.items()],
                       f, indent=1)
 
 

@@ -113,7 +113,7 @@ def main(argv=None):
     from p2p_pytorch_amd.data import (DevicePairCache, SyntheticPairs, get_test_set,
                                       get_training_set)
     from p2p_pytorch_amd.data.image_io import save_img
-    from p2p_pytorch_amd.engine.checkpoint import (checkpoint_path, has_scheduler_state,
+    from p2p_pytorch_amd.engine.checkpoint import (checkpoint_path, scheduler_offset,
                                                    latest_checkpoint, save_checkpoint)
     from p2p_pytorch_amd.engine.checkpoint import load_checkpoint as load_full_checkpoint
     from p2p_pytorch_amd.engine.metrics import image_metrics
@@ -182,11 +182,15 @@ def main(argv=None):
     for net in (net_g, net_d, net_c):
         if net is not None:
             pdist.broadcast_module(net)
-    reducer_g = reducer_d = None
+    reducer_g = reducer_d = reducer_c = None
     if world > 1:
         from p2p_pytorch_amd.parallel import GradReducer
         reducer_g = GradReducer(net_g, bucket_mb=opt.bucket_mb)
         reducer_d = GradReducer(net_d, bucket_mb=opt.bucket_mb)
+        if net_c is not None and opt.train_c:
+            # --train_c steps an Adam over C: its gradients are all-reduced like G's and D's
+            # (and the NaN-skip decision is agreed through this reducer)
+            reducer_c = GradReducer(net_c, bucket_mb=opt.bucket_mb)
 
     if pix2pix:
         from p2p_pytorch_amd.engine.pix2pix import Pix2PixStep
@@ -202,7 +206,7 @@ def main(argv=None):
         trainer = CompressGANStep(net_g, net_d, net_c, lr=opt.lr, beta1=opt.beta1, bits=opt.bits,
                                   n_layers_d=opt.n_layers_D, image_pool=ImagePool(0),
                                   train_c=opt.train_c, c_phase_backward=opt.c_phase_backward,
-                                  reducer_g=reducer_g, reducer_d=reducer_d,
+                                  reducer_g=reducer_g, reducer_d=reducer_d, reducer_c=reducer_c,
                                   nan_guard=not opt.no_nan_guard)
         opt_g, opt_d = trainer.opt_g, trainer.opt_d
     # the reference's third optimizer / scheduler pair (train.py:243-246, :441-443): over C
@@ -222,12 +226,16 @@ def main(argv=None):
                                   opt.epoch_count - 1)
         if not os.path.exists(ck_path):
             raise SystemExit(f"=> No checkpoint found at '{ck_path}'")
-    # a restored scheduler already counts the finished epochs (last_epoch): its lambda must
-    # not add epoch_count on top; a reference-written file (no scheduler state) starts a
-    # fresh scheduler whose lambda is offset by epoch_count, as in the reference
-    sched_opt = opt
-    if ck_path and has_scheduler_state(ck_path):
-        sched_opt = argparse.Namespace(**{**vars(opt), "epoch_count": 1})
+    # a restored scheduler already counts the finished epochs (last_epoch): its lambda keeps
+    # the offset of the run that built it (saved as sched_epoch_count), not this run's
+    # epoch_count; a reference-written file (no scheduler state) starts a fresh scheduler
+    # whose lambda is offset by epoch_count, as in the reference
+    sched_epoch_count = opt.epoch_count
+    if ck_path:
+        off = scheduler_offset(ck_path)
+        if off is not None:
+            sched_epoch_count = off
+    sched_opt = argparse.Namespace(**{**vars(opt), "epoch_count": sched_epoch_count})
     sched_g = get_scheduler(opt_g, sched_opt)
     sched_d = get_scheduler(opt_d, sched_opt)
     sched_c = get_scheduler(opt_c, sched_opt) if opt_c is not None else None
@@ -246,11 +254,12 @@ def main(argv=None):
     if timing and use_cuda:
         from p2p_pytorch_amd.utils import PhaseTimer
         trainer.timer = PhaseTimer()
-        for r in (reducer_g, reducer_d):
+        for r in (reducer_g, reducer_d, reducer_c):
             if r is not None:
                 r.enable_timing()
     wd_s = opt.watchdog_s if opt.watchdog_s is not None else (1800.0 if world > 1 else 0.0)
     watchdog = StepWatchdog(wd_s).start()
+    graph_tried = False
     for epoch in range(start_epoch, num_epoch):
         net_g.train()
         net_d.train()
@@ -270,9 +279,14 @@ def main(argv=None):
         for iteration, batch in enumerate(batches, 1):
             real_a = batch[0].to(device, act_dtype).contiguous(memory_format=torch.channels_last)
             real_b = batch[1].to(device, act_dtype).contiguous(memory_format=torch.channels_last)
-            if opt.graph and use_cuda and step_fn is trainer.step:
-                from p2p_pytorch_amd.engine.graph import CapturedStep
-                step_fn = CapturedStep(trainer.step, real_a, real_b)
+            if opt.graph and use_cuda and step_fn is trainer.step and not graph_tried:
+                # RCCL groups only, and every rank agrees on graph vs eager (a capture that
+                # fails on one rank must not leave the others blocked in its collectives)
+                from p2p_pytorch_amd.engine.graph import capture_agreed
+                graph_tried = True
+                step_fn, _ = capture_agreed(
+                    trainer.step, real_a, real_b,
+                    log=lambda m: print(f"[train] rank {rank}: {m}", file=sys.stderr, flush=True))
             losses = step_fn(real_a, real_b)
             watchdog.beat()
             for k, v in losses.items():   # device-side running sums, no host sync
@@ -285,7 +299,7 @@ def main(argv=None):
                 extra = {}   # every rank drains its timers; rank 0 logs
                 if getattr(trainer, "timer", None) is not None:
                     extra["phase_ms"] = {k: v / count for k, v in trainer.timer.report().items()}
-                    for tag, r in (("G", reducer_g), ("D", reducer_d)):
+                    for tag, r in (("G", reducer_g), ("D", reducer_d), ("C", reducer_c)):
                         st = r.comm_stats() if r is not None else {}
                         if st:
                             extra[f"comm_{tag}"] = st
@@ -328,7 +342,8 @@ def main(argv=None):
             # one random test image's input / target / prediction / compressed view is dumped
             # to in.png, tar.png, pred.png, comp.png (train.py:462, :469-473; the reference's
             # inclusive randint bound can miss every image, quirk A14)
-            rande = random.randint(0, max(n_eval - 1, 0))
+            # drawn from rank 0's shard (i = 0 mod world): rank 0 writes the images
+            rande = random.randrange(0, max(n_eval, 1), world)
             with torch.no_grad():
                 for i in range(rank, n_eval, world):
                     inp, tgt = test_set[i]
@@ -373,7 +388,8 @@ def main(argv=None):
         if epoch % opt.epochsave == 0:
             path = checkpoint_path(opt.checkpoint_dir, opt.dataset or "synthetic", opt.name, epoch)
             save_checkpoint(path, epoch, net_g, net_c, net_d, opt_g, opt_d, sched_g, sched_d,
-                            losslogger, rank=rank, opt_c=opt_c, sched_c=sched_c)
+                            losslogger, rank=rank, opt_c=opt_c, sched_c=sched_c,
+                            extra={"sched_epoch_count": sched_epoch_count})
             pdist.barrier()
             if rank == 0:
                 print("Checkpoint saved to {}".format(path))
