@@ -579,7 +579,7 @@ std::vector<Tensor> union_weight(const Tensor& w, int64_t co_off, int64_t nv, in
 // (returns the device scalar lam_scale * sum|fake - pk_a[3..5]|), mode 2 = head gradient.
 Tensor conv_d2s(const Tensor& x1, const optional<Tensor>& x2, const Tensor& w, const Tensor& bias, int64_t act_in,
                 int64_t act_out, int64_t mode, Tensor out, const Tensor& pk_a, const optional<Tensor>& pk_f,
-                double scale) {
+                double scale, const optional<Tensor>& wscale) {
   check_act(x1, "conv_d2s x1");
   check_act(pk_a, "conv_d2s pk_a");
   check_act(out, "conv_d2s out");
@@ -608,6 +608,12 @@ Tensor conv_d2s(const Tensor& x1, const optional<Tensor>& x2, const Tensor& w, c
     check_act(*pk_f, "conv_d2s pk_f");
     TORCH_CHECK(pk_f->sizes() == out.sizes(), "conv_d2s: pk_f shape");
   }
+  const float* wsc = nullptr;
+  if (wscale) {
+    TORCH_CHECK(mode == 2 && wscale->is_cuda() && wscale->scalar_type() == at::kFloat && wscale->numel() == 1,
+                "conv_d2s: wscale is a 1-element fp32 device tensor (head gradient only)");
+    wsc = wscale->data_ptr<float>();
+  }
   hipStream_t st = cur_stream(x1);
   if (nrows == 16) {
     // halo-tile kernel: persistent blocks (one per CU) over 16x16 tiles of the input grid
@@ -627,6 +633,7 @@ Tensor conv_d2s(const Tensor& x1, const optional<Tensor>& x2, const Tensor& w, c
     h.pk_a = static_cast<const __bf16*>(pk_a.data_ptr());
     h.pk_f = mode == 2 ? static_cast<const __bf16*>(pk_f->data_ptr()) : nullptr;
     h.scale = (float)scale;
+    h.wscale = wsc;
     h.zero = static_cast<const __bf16*>(zero_page(x1));
     h.tiles_x = (int)((W + 15) / 16);
     h.tiles_y = (int)((H + 15) / 16);
@@ -678,6 +685,7 @@ Tensor conv_d2s(const Tensor& x1, const optional<Tensor>& x2, const Tensor& w, c
   a.pk_a = pk_a.data_ptr();
   a.pk_f = mode == 2 ? pk_f->data_ptr() : nullptr;
   a.d2s_scale = (float)scale;
+  a.d2s_w = wsc;
   const int64_t blocks = (N * H * W + 255) / 256;
   Tensor part, l1;
   if (mode == 1) {
@@ -1518,7 +1526,7 @@ TORCH_LIBRARY(p2p, m) {
   m.def("weight_prep(Tensor w, int swap, int Xp, int Yp, Tensor? scale) -> Tensor");
   m.def("union_weight(Tensor w, int co_off, int nv, int Nrows, int Cpad, Tensor? bias) -> Tensor[]");
   m.def("conv_d2s(Tensor x1, Tensor? x2, Tensor w, Tensor bias, int act_in, int act_out, int mode, "
-        "Tensor(a!) out, Tensor pk_a, Tensor? pk_f, float scale) -> Tensor");
+        "Tensor(a!) out, Tensor pk_a, Tensor? pk_f, float scale, Tensor? wscale=None) -> Tensor");
   m.def("prelu_fwd(Tensor x, Tensor w) -> Tensor");
   m.def("prelu_bwd(Tensor x, Tensor gy, Tensor w, bool need_x) -> Tensor[]");
   m.def("tv_fwd(Tensor x) -> Tensor");

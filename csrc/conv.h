@@ -68,6 +68,7 @@ struct ConvFwdArgs {
   const void* pk_a;
   const void* pk_f;
   float d2s_scale;
+  const float* d2s_w;   // mode 2: device multiplier of the sign term (dL/dl1; null = 1)
   float* l1_part;
   int cls_major;   // MODE 1 block order A/B knob (P2P_CLASS_MAJOR=1: all tiles of class 0 first)
   // Norm-backward partial sums fused into a dgrad epilogue (null nb_ws = off): the output
@@ -125,6 +126,7 @@ struct HaloArgs {
   const __bf16* pk_a;
   const __bf16* pk_f;
   float scale;
+  const float* wscale; // mode 2: device multiplier of the sign term (dL/dl1; null = 1)
   float* l1_part;      // [blocks] (mode 1)
   const __bf16* zero;
   int tiles_x, tiles_y, ntiles;

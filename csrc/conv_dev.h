@@ -46,7 +46,8 @@ __device__ __forceinline__ ClassGeom class_geom(const ConvFwdArgs& a, int cls) {
 
 // One packed output pixel P of the depth-to-space epilogue (conv.h ``d2s``) from its three
 // GEMM values c[0..2]: mode 1 writes (pk_a[0..2], c, 0, 0) and returns sum|c - pk_a[3..5]|;
-// mode 2 writes ((c + scale * sign(f - b)) * (1 - f^2), 0 ...) with f = pk_f[3..5], b = pk_a[3..5].
+// mode 2 writes ((c + scale * sign(f - b)) * (1 - f^2), 0 ...) with f = pk_f[3..5], b = pk_a[3..5]
+// (scale already multiplied by the device weight dL/dl1 by the caller).
 __device__ __forceinline__ float d2s_pixel(int mode, long P, const bf16* c, const bf16* pk_a, const bf16* pk_f,
                                            float scale, bf16* out) {
   const bf16x8 ab = *reinterpret_cast<const bf16x8*>(pk_a + P * 8);
@@ -299,6 +300,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
   if (a.d2s) {  // depth-to-space packed image (d1 forward / its head gradient)
     const int Ho = 2 * a.OH, Wo = 2 * a.OW;
     float l1 = 0.f;
+    const float d2s_sc = a.d2s_scale * (a.d2s == 2 && a.d2s_w ? *a.d2s_w : 1.f);
     for (int it = tid; it < BM * 4; it += NT) {
       const int row = it >> 2, cls = it & 3;
       const int m = m0 + row;
@@ -309,7 +311,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
       const int qx = r - qy * g.Wq;
       const long P = ((long)n * Ho + 2 * qy + (cls >> 1)) * Wo + 2 * qx + (cls & 1);
       l1 += d2s_pixel(a.d2s, P, Cs + row * LDC + cls * 4, static_cast<const bf16*>(a.pk_a),
-                      static_cast<const bf16*>(a.pk_f), a.d2s_scale, static_cast<bf16*>(a.y1));
+                      static_cast<const bf16*>(a.pk_f), d2s_sc, static_cast<bf16*>(a.y1));
     }
     if (a.d2s == 1 && a.l1_part) {
       float* red = reinterpret_cast<float*>(smem + BM * LDC * 2);

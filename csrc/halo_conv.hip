@@ -105,6 +105,8 @@ __global__ void __launch_bounds__(256) halo_union_kernel(HaloArgs a) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float l1 = 0.f;
+  // mode 2: the L1 sign term's weight = scale x dL/dl1 (a device scalar written by autograd)
+  const float l1w = a.scale * (a.mode == 2 && a.wscale ? *a.wscale : 1.f);
   const int px = lane & 15, kq = lane >> 4;
 
   issue(0, 0);
@@ -192,7 +194,7 @@ __global__ void __launch_bounds__(256) halo_union_kernel(HaloArgs a) {
           for (int j = 0; j < 3; ++j) {
             const float f = (float)af[q][3 + j], b = (float)ab[q][3 + j];
             const float sg = (float)(f > b) - (float)(f < b);
-            o[j] = (bf16)(((float)c[j] + a.scale * sg) * (1.f - f * f));
+            o[j] = (bf16)(((float)c[j] + l1w * sg) * (1.f - f * f));
           }
         }
         *reinterpret_cast<bf16x8*>(a.out + P[q] * 8) = o;

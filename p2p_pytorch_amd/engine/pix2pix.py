@@ -162,8 +162,9 @@ class Pix2PixStep:
         with self._phase("G_loss_fwd"):
             pred_fake = netD(fake_pk)
             loss_G_GAN = self.criterionGAN(pred_fake, True)
-            # the L1 term's gradient is injected by the fused first-D-conv dgrad (weight 1)
-            loss_G = loss_G_GAN + loss_G_L1
+            # the L1 term's gradient is fused into D's first-conv dgrad; the tap hands that
+            # kernel dL/d(L1) on the device (any weighting of the L1 term is honoured)
+            loss_G = loss_G_GAN + hip.head_l1_tap(loss_G_L1)
         with self._phase("G_bwd_opt"):
             self._zero(self.opt_G, self.reducer_g)
             loss_G.backward()

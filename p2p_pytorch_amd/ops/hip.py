@@ -691,15 +691,57 @@ def _head_dgrad_ok(cfg, weight, x):
 
 def _head_dgrad(head, af, weight, gy):
     """d(loss)/d(pre-tanh fake) in slots 0..2 of a packed tensor: the first D conv's input
-    gradient on the fake channels (3..5) as a 3x3 union GEMM, + the L1 sign term, x tanh'."""
-    ab, scale = head
+    gradient on the fake channels (3..5) as a 3x3 union GEMM, + the L1 sign term, x tanh'.
+
+    The L1 term's weight is dL/d(l1), read by the kernel from a device scalar that the L1
+    value's gradient tap (``head_l1_tap``) writes -- so any recomposition or rescaling of the
+    loss is honoured.  If no tap has delivered that weight yet (the L1 value is not in the
+    loss, or it was not tapped), the term is left out here (weight 0) and ImageHeadFn's
+    backward adds it with the weight autograd hands it."""
+    ab, scale, state = head
     img, _ = P().union_weight(weight.detach().float().contiguous(), 3, 3, UNION_ROWS,
                               gy.shape[1], None)
     zb = torch.zeros(UNION_ROWS, device=gy.device, dtype=torch.float32)
     dz = torch.empty_like(af, memory_format=CL)
-    P().conv_d2s(gy, None, img, zb, 0, 0, 2, dz, ab, af, float(scale))
+    tapped = state.tap_ran
+    P().conv_d2s(gy, None, img, zb, 0, 0, 2, dz, ab, af, float(scale) if tapped else 0.0,
+                 state.weight if tapped else None)
     dz._p2p_dz = True
+    dz._p2p_l1_in = tapped
     return dz
+
+
+class _HeadL1State:
+    """Per-forward hand-off between the L1 value's gradient tap and the head's fused dgrad."""
+    __slots__ = ("weight", "tap_ran")
+
+    def __init__(self, device):
+        self.weight = torch.ones(1, device=device, dtype=torch.float32)
+        self.tap_ran = False
+
+
+class _L1TapFn(torch.autograd.Function):
+    """Identity on the image head's L1 value whose backward stores dL/d(l1) on the device for
+    the fused head dgrad.  Apply it where the loss is composed (after D's forward): autograd
+    runs ready nodes latest-created first, so the tap's backward runs before D's backward
+    reaches the head dgrad (``_head_dgrad`` checks that on the host)."""
+
+    @staticmethod
+    def forward(ctx, l1, state):
+        ctx.state = state
+        return l1.view_as(l1)
+
+    @staticmethod
+    def backward(ctx, g):
+        ctx.state.weight.copy_(g.detach().reshape(1).float())
+        ctx.state.tap_ran = True
+        return g, None
+
+
+def head_l1_tap(l1):
+    """Tap the L1 value returned by the packed image head (no-op for any other tensor)."""
+    state = getattr(l1, "_p2p_head_l1", None)
+    return l1 if state is None else _L1TapFn.apply(l1, state)
 
 
 class ImageHeadFn(torch.autograd.Function):
@@ -724,19 +766,28 @@ class ImageHeadFn(torch.autograd.Function):
                    skip.shape[2], skip.shape[3])
         ctx.save_for_backward(skip, u, weight, af, ab)
         ctx.nb = (None, _norm_lookup(u))
-        ctx.mark_non_differentiable(l1)
+        state = _HeadL1State(skip.device)
         af._p2p_packed = (3, 3)
-        af._p2p_head = (ab, float(scale))
+        af._p2p_head = (ab, float(scale), state)
+        l1._p2p_head_l1 = state
         return af, l1
 
     @staticmethod
-    def backward(ctx, gaf, _gl1):
+    def backward(ctx, gaf, gl1):
         skip, u, weight, af, ab = ctx.saved_tensors
         if getattr(gaf, "_p2p_dz", False):
             dz = gaf                       # fused by the consumer (_head_dgrad)
+            if not gaf._p2p_l1_in and gl1 is not None:
+                # the dgrad ran before any tap delivered dL/dl1: add the L1 term here
+                f = af[:, 3:6].float()
+                t = gl1.float() * ctx.scale * torch.sign(f - ab[:, 3:6].float()) * (1 - f * f)
+                dz = dz.clone(memory_format=CL)
+                dz[:, 0:3] = (dz[:, 0:3].float() + t).to(torch.bfloat16)
         else:                              # any other consumer: the same math, unfused
             f = af[:, 3:6].float()
-            g = gaf[:, 3:6].float() + ctx.scale * torch.sign(f - ab[:, 3:6].float())
+            g = gaf[:, 3:6].float()
+            if gl1 is not None:
+                g = g + gl1.float() * ctx.scale * torch.sign(f - ab[:, 3:6].float())
             dz = torch.zeros_like(af, memory_format=CL)
             dz[:, 0:3] = (g * (1 - f * f)).to(torch.bfloat16)
         cfg = _ConvCfg(True, 4, 4, 2, 1, False, 1, ctx.cfg.act_in, None,

@@ -77,3 +77,69 @@ def test_head_gradient(rows):
     got = dz.float()
     assert (got[:, 3:8] == 0).all()
     assert rel(got[:, 0:3], ref) < 2e-2
+
+
+@pytest.mark.parametrize("rows", [16, 32])
+def test_head_gradient_device_weight(rows):
+    """The L1 sign term scaled by a device scalar (dL/dl1 written by the loss's gradient tap)."""
+    N, H = 2, 32
+    g = torch.Generator(device=DEV).manual_seed(3)
+    gy = bf(torch.randn(N, 64, H, H, device=DEV, generator=g))
+    w = torch.randn(64, 6, 4, 4, device=DEV, generator=g) * 0.05
+    af = bf(torch.rand(N, 8, 2 * H, 2 * H, device=DEV, generator=g) * 1.6 - 0.8)
+    ab = bf(torch.rand(N, 8, 2 * H, 2 * H, device=DEV, generator=g) * 2 - 1)
+    img, _ = hip.P().union_weight(w, 3, 3, rows, 64, None)
+    zb = torch.zeros(rows, device=DEV)
+    dz = torch.empty_like(af, memory_format=torch.channels_last)
+    scale, wdev = 0.01, torch.tensor([-2.5], device=DEV)
+    hip.P().conv_d2s(gy, None, img, zb, 0, 0, 2, dz, ab, af, scale, wdev)
+    dx = F.conv_transpose2d(gy.float(), w, None, 2, 1)[:, 3:6]
+    f, t = af.float()[:, 3:6], ab.float()[:, 3:6]
+    ref = (dx - 2.5 * scale * torch.sign(f - t)) * (1 - f * f)
+    assert rel(dz.float()[:, 0:3], ref) < 2e-2
+
+
+def _g_grads(G, D, A, B, packed, tap, w_gan, w_l1, lam):
+    from p2p_pytorch_amd.models import GANLoss
+    from p2p_pytorch_amd.ops import l1
+    crit = GANLoss(gan_mode="vanilla")
+    hip.begin_step()
+    hip.prepare_weights(G, D)
+    G.zero_grad(set_to_none=True)
+    N, _, H, W = A.shape
+    if packed:
+        dd = torch.empty(2 * N, 8, H, W, device=DEV, dtype=torch.bfloat16,
+                         memory_format=torch.channels_last)
+        hip.P().pad_channels_into(A, B, dd.narrow(0, N, N))
+        dd._p2p_packed = (3, 3)
+        fake, loss_l1 = G.forward_packed(dd, lam / float(N * 3 * H * W))
+        gan = crit(D(fake), True)
+        loss = w_gan * gan + w_l1 * (hip.head_l1_tap(loss_l1) if tap else loss_l1)
+    else:
+        fake = G(A)
+        gan = crit(D((A, fake)), True)
+        loss = w_gan * gan + w_l1 * l1(fake, B) * lam
+    loss.backward()
+    return {n: p.grad.detach().float().clone() for n, p in G.named_parameters()}
+
+
+@pytest.mark.parametrize("tap", [True, False])
+def test_packed_head_honours_loss_weights(tap):
+    """W5: the packed image head's fused L1 gradient follows the loss's weighting (tapped:
+    the weight reaches the fused dgrad on the device; untapped: the head's backward adds the
+    term) -- G's gradients match the unpacked path under a non-unit recomposition."""
+    from p2p_pytorch_amd.models import define_D, define_G
+    from p2p_pytorch_amd.models.pix2pix import UnetGenerator
+    torch.manual_seed(0)
+    G = define_G(netG="unet_64", gpu_id=DEV, verbose=False, use_dropout=False)
+    D = define_D(6, 64, norm="instance", netD="basic", gpu_id=DEV, verbose=False)
+    for p in D.parameters():
+        p.requires_grad_(False)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    A = bf(torch.rand(2, 3, 64, 64, device=DEV, generator=g) * 2 - 1)
+    B = bf(torch.rand(2, 3, 64, 64, device=DEV, generator=g) * 2 - 1)
+    assert isinstance(G, UnetGenerator) and G.packed_ok(A)
+    ref = _g_grads(G, D, A, B, False, tap, 0.5, 3.0, 100.0)
+    got = _g_grads(G, D, A, B, True, tap, 0.5, 3.0, 100.0)
+    for n in ref:
+        assert rel(got[n], ref[n]) < 5e-2, n
