@@ -38,7 +38,7 @@ int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const
 int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const float* mean,
                  const float* rstd, const float* gamma, const float* beta, int act,
                  const float* prelu_w, float* dprelu, float* dgamma, float* dbeta, float* ws, void* dx,
-                 float* dsum, void* q, int* qsite, int qfmt, hipStream_t st);
+                 float* dsum, void* q, int* qsite, int qfmt, int frozen, hipStream_t st);
 int p2p_norm_bwd_partials(const void* x, const void* dy, int N, int HW, int C, int nchunks,
                           const float* partials, const float* mean, const float* rstd,
                           const float* gamma, const float* beta, int act, float* dgamma, float* dbeta,
@@ -83,6 +83,7 @@ int p2p_adam_max_tensors();
 int p2p_union_weight(const float* w, int CinT, int CoutT, int co_off, int nv, int Nrows, int Cpad,
                      const float* bias, void* out, float* bias_out, hipStream_t st);
 int p2p_sum_partials(const float* ws, int nb, float scale, float* out, hipStream_t st);
+int p2p_guard_flag(const float* const* v, int n, float* flag, float* counter, hipStream_t st);
 int p2p_adam(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
              const long* n, const float* lr, const float* step, const float* skip, float b1, float b2,
              float eps, float wd, hipStream_t st);
@@ -368,13 +369,22 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   if (tiles < 256 && ktiles >= 8) {
     splits = (int)std::min<int64_t>((512 + tiles - 1) / tiles, ktiles / 4);
     splits = std::max(1, std::min(splits, 32));
+    // no empty split: the kernel gives split s the k tiles [s*kps, (s+1)*kps), and every
+    // split's slab must be written whole (it is not zero-filled)
+    for (int it = 0; it < 4; ++it) {
+      const int64_t kps = (ktiles + splits - 1) / splits;
+      splits = (int)((ktiles + kps - 1) / kps);
+    }
   }
   Tensor ws;
   if (splits > 1) {
-    // P2P_DETERMINISTIC=1: per-split slabs reduced in order instead of fp32 atomics
-    const char* dv = std::getenv("P2P_DETERMINISTIC");
-    a.det = (dv && dv[0] == '1') ? 1 : 0;
-    ws = at::zeros({a.det ? splits : 1, N * OH * OW, Cout}, obf.options().dtype(at::kFloat));
+    // per-split fp32 slabs (plain stores, no zero fill) summed in split order by
+    // conv_finalize: deterministic, and no atomics; P2P_SPLITK_ATOMIC=1 restores the
+    // fp32-atomic accumulation into one zero-filled buffer (A/B only)
+    const char* av = std::getenv("P2P_SPLITK_ATOMIC");
+    a.det = (av && av[0] == '1') ? 0 : 1;
+    ws = a.det ? at::empty({splits, N * OH * OW, Cout}, obf.options().dtype(at::kFloat))
+               : at::zeros({1, N * OH * OW, Cout}, obf.options().dtype(at::kFloat));
     a.ws = ws.data_ptr<float>();
     a.splits = splits;
   }
@@ -1013,8 +1023,9 @@ Tensor norm_bwd(const Tensor& x, const Tensor& dy, const Tensor& mean, const Ten
                 const optional<Tensor>& dgamma, const optional<Tensor>& dbeta, bool need_dx,
                 bool batch, const optional<Tensor>& dsum, const optional<Tensor>& qsite,
                 const optional<Tensor>& q_out, int64_t qfmt, const optional<Tensor>& prelu_w,
-                const optional<Tensor>& dprelu, const optional<Tensor>& partials) {
+                const optional<Tensor>& dprelu, const optional<Tensor>& partials, bool frozen) {
   check_act(x, "norm_bwd x");
+  TORCH_CHECK(!frozen || (!partials && !dsum), "norm_bwd: frozen statistics take no partials / dsum");
   if (prelu_w)
     TORCH_CHECK(prelu_w->numel() == 1 && prelu_w->scalar_type() == at::kFloat && prelu_w->is_cuda(),
                 "norm_bwd: prelu_w must be a 1-element fp32 GPU tensor");
@@ -1067,7 +1078,7 @@ Tensor norm_bwd(const Tensor& x, const Tensor& dy, const Tensor& mean, const Ten
                         dbeta ? dbeta->data_ptr<float>() : nullptr, ws.data_ptr<float>(),
                         need_dx ? dx.data_ptr() : nullptr,
                         (need_dx && dsum) ? dsum->data_ptr<float>() : nullptr, qp, qs, (int)qfmt,
-                        cur_stream(x)),
+                        frozen ? 1 : 0, cur_stream(x)),
            "norm_bwd");
   return dx;
 }
@@ -1505,6 +1516,25 @@ void adam(at::TensorList p, at::TensorList g, at::TensorList m, at::TensorList v
 
 }  // namespace
 
+// NaN / Inf guard: fp32 flag (1 = some loss is not finite) and counter += flag, one launch
+Tensor guard_flag(const std::vector<Tensor>& losses, const optional<Tensor>& counter) {
+  TORCH_CHECK(!losses.empty() && losses.size() <= 8, "guard_flag: 1..8 loss scalars");
+  const float* v[8] = {};
+  for (size_t i = 0; i < losses.size(); ++i) {
+    TORCH_CHECK(losses[i].is_cuda() && losses[i].scalar_type() == at::kFloat && losses[i].numel() == 1,
+                "guard_flag: fp32 one-element GPU tensors");
+    v[i] = losses[i].data_ptr<float>();
+  }
+  if (counter)
+    TORCH_CHECK(counter->is_cuda() && counter->scalar_type() == at::kFloat && counter->numel() == 1,
+                "guard_flag: counter is a one-element fp32 GPU tensor");
+  Tensor flag = at::empty({}, losses[0].options());
+  check_rc(p2p_guard_flag(v, (int)losses.size(), flag.data_ptr<float>(),
+                          counter ? counter->data_ptr<float>() : nullptr, cur_stream(losses[0])),
+           "guard_flag");
+  return flag;
+}
+
 TORCH_LIBRARY(p2p, m) {
   m.def("conv_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, int mode, int KH, int KW, int stride, "
         "int pad, int reflect, int up, int act_in, int OH, int OW, int Cout, int act_out, int Csplit, "
@@ -1549,13 +1579,14 @@ TORCH_LIBRARY(p2p, m) {
   m.def("norm_bwd(Tensor x, Tensor dy, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, int act, "
         "Tensor(a!)? dgamma, Tensor(b!)? dbeta, bool need_dx, bool batch, Tensor(c!)? dsum, "
         "Tensor(d!)? qsite=None, Tensor(e!)? q_out=None, int qfmt=0, Tensor? prelu_w=None, "
-        "Tensor(f!)? dprelu=None, Tensor? partials=None) -> Tensor");
+        "Tensor(f!)? dprelu=None, Tensor? partials=None, bool frozen=False) -> Tensor");
   m.def("act(Tensor a, Tensor? b, int act, int mode) -> Tensor");
   m.def("dropout(Tensor x, float p, Tensor seed, int salt) -> Tensor");
   m.def("pad_channels(Tensor a, Tensor? b, int Co) -> Tensor");
   m.def("pad_channels_into(Tensor a, Tensor? b, Tensor(a!) out) -> ()");
   m.def("slice_channels(Tensor x, int c0, int C) -> Tensor");
   m.def("colsum(Tensor x, Tensor(a!) out, float scale, bool accumulate) -> ()");
+  m.def("guard_flag(Tensor[] losses, Tensor(a!)? counter) -> Tensor");
   m.def("loss_fwd(Tensor a, Tensor? b, int kind, float t, float scale) -> Tensor");
   m.def("loss_bwd(Tensor a, Tensor? b, int kind, float t, float scale, Tensor gout, bool need_a, "
         "bool need_b) -> Tensor[]");
@@ -1565,6 +1596,7 @@ TORCH_LIBRARY(p2p, m) {
 
 TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("conv_fwd", conv_fwd);
+  m.impl("guard_flag", guard_flag);
   m.impl("fp8_quant", fp8_quant);
   m.impl("sn_power_iter", sn_power_iter);
   m.impl("fp8_amax", fp8_amax);

@@ -646,8 +646,11 @@ static int wgrad_glds_shape(const p2p::ConvWgradArgs* a) {
     return 0;
   const char* v = std::getenv("P2P_CONV_VARIANT");
   if (v && v[0] == 'v') return 0;
-  // 4 = 256x256 (half the VALU + LDS fragment traffic per MFMA of 1 / 2)
-  if (v && v[0] == 'g' && v[1] == '5' && a->R % 256 == 0 && a->Kq % 256 == 0) return 4;
+  // 4 = 256x256 (half the VALU + LDS fragment traffic per MFMA of 1 / 2); P2P_WGRAD_TILE=256
+  // selects it for the weight gradients alone (census A/B)
+  const char* wt = std::getenv("P2P_WGRAD_TILE");
+  const bool w256 = (v && v[0] == 'g' && v[1] == '5') || (wt && wt[0] == '2' && wt[1] == '5');
+  if (w256 && a->R % 256 == 0 && a->Kq % 256 == 0) return 4;
   if (a->R >= 256) return 1;
   // 5 = 128x128 on 4 waves, 2-stage (two blocks per CU): Kq = 128, e.g. the packed 8-channel
   // image conv's wgrad (16 taps x 8 channels), which fell back to the register-staged kernel

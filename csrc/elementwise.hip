@@ -511,6 +511,26 @@ __global__ void __launch_bounds__(256) pad_fold_s1_kernel(const bf16* __restrict
 }
 }  // namespace p2p
 
+namespace p2p {
+// NaN / Inf guard of a training step: flag = 1 if any of the n fp32 loss scalars is not finite
+// (else 0), and the guard's device counter += flag -- one launch instead of the
+// isfinite / not / any / max / add chain of aten kernels per optimizer step
+struct GuardArgs {
+  const float* v[8];
+  int n;
+};
+__global__ void guard_flag_kernel(GuardArgs a, float* flag, float* counter) {
+  if (threadIdx.x != 0) return;
+  float bad = 0.f;
+  for (int i = 0; i < a.n; ++i) {
+    const float x = *a.v[i];
+    if (!(fabsf(x) <= 3.402823466e38f)) bad = 1.f;   // NaN fails every comparison
+  }
+  *flag = bad;
+  if (counter) *counter += bad;
+}
+}  // namespace p2p
+
 extern "C" {
 
 int p2p_act(const void* a, const void* b, long n, int act, int mode, void* out, hipStream_t st) {
@@ -607,6 +627,16 @@ int p2p_loss_fwd(const void* a, const void* b, int is_f32, long n, int kind, flo
     hipLaunchKernelGGL(loss_partial_kernel, dim3(nb), dim3(256), 0, st, a, b, is_f32, n, kind, t, ws);
   }
   hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, ws, nb, scale, out);
+  return (int)hipGetLastError();
+}
+
+int p2p_guard_flag(const float* const* v, int n, float* flag, float* counter, hipStream_t st) {
+  using namespace p2p;
+  if (n < 1 || n > 8) return -1;
+  GuardArgs a{};
+  for (int i = 0; i < n; ++i) a.v[i] = v[i];
+  a.n = n;
+  hipLaunchKernelGGL(guard_flag_kernel, dim3(1), dim3(64), 0, st, a, flag, counter);
   return (int)hipGetLastError();
 }
 

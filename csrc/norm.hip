@@ -447,6 +447,18 @@ __global__ void __launch_bounds__(256) norm_bwd_finalize_kernel(const float* __r
   coef[2 * NC + i] = -r * ga * sdx * inv;
 }
 
+// eval-mode (frozen statistics) backward: x -> xhat is a fixed affine map, so
+// dx = rstd * gamma * dy_eff (no mean terms) -- the apply kernel with B = Cc = 0
+__global__ void __launch_bounds__(256) norm_frozen_coef_kernel(int NC, int C, const float* __restrict__ rstd,
+                                                               const float* __restrict__ gamma,
+                                                               float* __restrict__ coef) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= NC) return;
+  coef[i] = rstd[i] * (gamma ? gamma[i % C] : 1.f);
+  coef[NC + i] = 0.f;
+  coef[2 * NC + i] = 0.f;
+}
+
 // d(gamma) = sum(dy_eff * xhat), d(beta) = sum(dy_eff) over every group of the channel
 template <int FIN_CT, int FIN_J>
 __global__ void __launch_bounds__(256) norm_param_grad_kernel(const float* __restrict__ ws, NormGeom g,
@@ -644,7 +656,7 @@ int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const
 int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const float* mean,
                  const float* rstd, const float* gamma, const float* beta, int act,
                  const float* prelu_w, float* dprelu, float* dgamma, float* dbeta, float* ws, void* dx,
-                 float* dsum, void* q, int* qsite, int qfmt, hipStream_t st) {
+                 float* dsum, void* q, int* qsite, int qfmt, int frozen, hipStream_t st) {
   using namespace p2p;
   NormGeom g = make_geom(N, HW, C);
   float* coef = ws + 2L * N * g.nchunks * C;
@@ -653,10 +665,13 @@ int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const floa
   const bf16* db = static_cast<const bf16*>(dy);
   const int a = prelu_w ? ACT_PRELU_T : act;
   if (!dgamma && !dx && !dprelu) return 0;
-  with_act(a, [&](auto t) {
-    hipLaunchKernelGGL((norm_bwd_partial_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st, xb,
-                       db, g, mean, rstd, gamma, beta, prelu_w, ws, pws);
-  });
+  // frozen (eval-mode BN): the partial sums serve only the parameter / slope gradients
+  if (!frozen || dgamma || dprelu) {
+    with_act(a, [&](auto t) {
+      hipLaunchKernelGGL((norm_bwd_partial_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st, xb,
+                         db, g, mean, rstd, gamma, beta, prelu_w, ws, pws);
+    });
+  }
   if (dprelu) {
     const int rc = p2p_sum_partials(pws, N * g.nchunks, 1.f, dprelu, st);
     if (rc) return rc;
@@ -670,13 +685,19 @@ int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const floa
       hipLaunchKernelGGL((norm_param_grad_kernel<32, 8>), dim3((C + 31) / 32), dim3(256), 0, st, ws, g, dgamma, dbeta);
   }
   if (dx) {
-    P2P_FIN_LAUNCH(norm_bwd_finalize_kernel, g, N, st, ws, g, rstd, gamma, coef);
+    if (frozen)
+      hipLaunchKernelGGL(norm_frozen_coef_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, N * C, C, rstd, gamma,
+                         coef);
+    else
+      P2P_FIN_LAUNCH(norm_bwd_finalize_kernel, g, N, st, ws, g, rstd, gamma, coef);
     with_act(a, [&](auto t) {
       hipLaunchKernelGGL((norm_bwd_apply_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st, xb, db,
                          g, mean, rstd, gamma, beta, prelu_w, coef, static_cast<bf16*>(dx),
                          Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
     });
-    if (dsum) (void)hipMemsetAsync(dsum, 0, sizeof(float) * C, st);
+    // a normalised group's dx sums to exactly zero (the producer's bias gradient); not so
+    // under frozen statistics -- the caller computes that column sum itself
+    if (dsum && !frozen) (void)hipMemsetAsync(dsum, 0, sizeof(float) * C, st);
   }
   return (int)hipGetLastError();
 }

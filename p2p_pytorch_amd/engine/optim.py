@@ -101,12 +101,15 @@ def guarded_step(opt, reducer, skipped, *losses):
     device (FusedAdam: no host sync; agreed across ranks by a 4-byte MAX all-reduce) and is
     added to the ``skipped`` device counter, which is returned (created on first use)."""
     from ..utils.guards import nonfinite
-    flag = nonfinite(*losses)
-    if reducer is not None:
-        reducer.all_reduce_max_(flag)
+    agree = reducer is not None and reducer.comm and reducer.world > 1
     if skipped is None:
-        skipped = torch.zeros((), device=flag.device)
-    skipped.add_(flag)
+        skipped = torch.zeros((), device=losses[0].device)
+    if not agree:
+        flag = nonfinite(*losses, counter=skipped)     # flag + count in one launch
+    else:
+        flag = nonfinite(*losses)
+        reducer.all_reduce_max_(flag)
+        skipped.add_(flag)
     if isinstance(opt, FusedAdam):
         opt.step(skip=flag)
     elif float(flag) == 0.0:   # stock optimizer: host decision (eager baseline / CPU)

@@ -111,6 +111,8 @@ def bce_logits_const(pred, target):
 
 
 def bce_const(prob, target):
+    if _native.use_native(prob):
+        return _hip().bce_const(prob, target)
     return ref.bce_const(prob, target)
 
 

@@ -673,9 +673,10 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
 # generator's pre-tanh gradient (L1 sign term and tanh' fused in), so no 3-channel tensor,
 # channel pad / slice, col2im, tanh' or L1 kernel remains.
 #
-# Contract: the L1 value returned by image_head enters the loss LINEARLY with weight 1 (the
-# trainer's ``loss_G = loss_G_GAN + loss_G_L1``); its gradient lambda * sign(fake - B) / n is
-# injected by the fused dgrad, not routed through autograd.
+# The L1 value returned by image_head is an ordinary differentiable output: its gradient
+# lambda * sign(fake - B) / n times dL/d(L1) is fused into D's first-conv dgrad, which reads
+# dL/d(L1) from a device scalar that ``head_l1_tap`` (applied where the loss is composed)
+# fills during backward; untapped, ImageHeadFn's backward adds the term itself.
 
 
 # union GEMM columns: 16 = the halo-tile kernel (csrc/halo_conv.hip); 32 = the implicit-GEMM
@@ -924,21 +925,13 @@ class NormFn(torch.autograd.Function):
         gpw = None
         fused_act = 0
         pw = None
-        if prelu_w is not None and training:
+        if prelu_w is not None:
             # y = prelu(z): the kernels recompute z from x, gate dz = dy * (z > 0 ? 1 : w) and
             # reduce dw = sum(dy * z * [z <= 0]) in the same partial-sum pass
             pw = prelu_w.detach().float().contiguous()
             if ctx.needs_input_grad[3]:
                 gpw = torch.empty(1, device=x.device, dtype=torch.float32)
-        elif prelu_w is not None:
-            z = _norm_recompute(x, mean, rstd, gamma, beta, batch)
-            zf = z.float()
-            neg = zf <= 0
-            if ctx.needs_input_grad[3]:
-                gpw = (gy.float() * zf * neg).sum().reshape(1)
-            gy = (gy.float() * torch.where(neg, prelu_w.float(), torch.ones_like(zf))).to(
-                torch.bfloat16).contiguous(memory_format=CL)
-        elif act in ("relu", "lrelu") and training:
+        elif act in ("relu", "lrelu"):
             fused_act = _act_code(act)  # gate recomputed inside the norm backward kernels
         elif act not in (None, "none"):
             gy = P().act(gy, y, _act_code(act), 2)
@@ -950,19 +943,11 @@ class NormFn(torch.autograd.Function):
         g = gamma.detach().float().contiguous() if gamma is not None else None
         b = beta.detach().float().contiguous() if beta is not None else None
         if not training:
-            # eval-mode BN: affine map with frozen statistics
-            if act not in (None, "none") and prelu_w is None:
-                gy = P().act(gy, y, _act_code(act), 2)
-            dx = None
-            if need_x:
-                scale = rstd.view(-1) * (g if g is not None else 1.0)
-                dx = (gy.float() * scale.view(1, -1, 1, 1)).to(torch.bfloat16).contiguous(
-                    memory_format=CL)
-            if dg is not None:
-                xh = (x.float() - mean.view(1, -1, 1, 1)) * rstd.view(1, -1, 1, 1)
-                dg = (gy.float() * xh).sum((0, 2, 3))
-                db = gy.float().sum((0, 2, 3))
-            return dx, dg, db, gpw, None, None, None, None, None, None, None, None
+            # eval-mode BN: an affine map with frozen statistics -- the same HIP passes with
+            # dx = rstd * gamma * dz (no mean terms) and the parameter / slope gradients
+            dx = P().norm_bwd(x, gy, mean, rstd, g, b, fused_act, dg, db, need_x, True, None,
+                              prelu_w=pw, dprelu=gpw, frozen=True)
+            return (dx if need_x else None), dg, db, gpw, None, None, None, None, None, None, None, None
         dsum = torch.empty(x.shape[1], device=x.device, dtype=torch.float32) if need_x else None
         qargs, qd, dsite, fresh = (), None, None, False
         if ctx.qkey is not None and need_x:
@@ -987,18 +972,6 @@ class NormFn(torch.autograd.Function):
             elif fresh:
                 _f8.bootstrap_shadow(dx, (ctx.qkey, "dx"), _f8.E5M2)
         return (dx if need_x else None), dg, db, gpw, None, None, None, None, None, None, None, None
-
-
-def _norm_recompute(x, mean, rstd, gamma, beta, batch):
-    # pre-activation normalised value z = xhat * gamma + beta (for the PReLU backward)
-    N, C = x.shape[:2]
-    if batch:
-        z = (x.float() - mean.view(1, C, 1, 1)) * rstd.view(1, C, 1, 1)
-    else:
-        z = (x.float() - mean.view(N, C, 1, 1)) * rstd.view(N, C, 1, 1)
-    if gamma is not None:
-        z = z * gamma.float().view(1, C, 1, 1) + beta.float().view(1, C, 1, 1)
-    return z
 
 
 class _PadCFn(torch.autograd.Function):

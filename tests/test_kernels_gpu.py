@@ -265,6 +265,36 @@ def test_batch_norm_train_and_eval():
     assert rel_err(ye, rye) < 2e-2
 
 
+@pytest.mark.parametrize("act", [None, "lrelu", "prelu"])
+def test_batch_norm_eval_backward(act):
+    """Eval-mode (frozen running statistics) BN backward on the HIP norm passes: dx =
+    rstd * gamma * gate(dy), d(gamma), d(beta) and the shared PReLU slope gradient."""
+    N, C, H = 4, 64, 16
+    x = bf(torch.randn(N, C, H, H, device=DEV) * 2 + 0.5)
+    g = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV) * 0.3
+    rm = torch.randn(C, device=DEV) * 0.5
+    rv = torch.rand(C, device=DEV) + 0.5
+    w = torch.full((1,), 0.25, device=DEV)
+    hx, hg, hb, hw = _leaf(x), _leaf(g), _leaf(b), _leaf(w)
+    kw = {"prelu_weight": hw} if act == "prelu" else ({"act": act} if act else {})
+    y = ops.batch_norm(hx, rm.clone(), rv.clone(), hg, hb, False, 0.1, 1e-5, **kw)
+    gy = rand_img(N, C, H, H, seed=41)
+    y.backward(gy)
+    rx, rg, rb, rw = _leaf(x.float()), _leaf(g), _leaf(b), _leaf(w)
+    ry = F.batch_norm(rx, rm.clone(), rv.clone(), rg, rb, False, 0.1, 1e-5)
+    if act == "prelu":
+        ry = F.prelu(ry, rw)
+    elif act == "lrelu":
+        ry = F.leaky_relu(ry, 0.2)
+    ry.backward(gy.float())
+    assert rel_err(y, ry) < 2e-2
+    assert rel_err(hx.grad, rx.grad) < 2e-2
+    assert rel_err(hg.grad, rg.grad) < 2e-2 and rel_err(hb.grad, rb.grad) < 2e-2
+    if act == "prelu":
+        assert rel_err(hw.grad, rw.grad) < 1e-2
+
+
 @pytest.mark.parametrize("C", [32, 64, 3])
 def test_batch_norm_fused_prelu(C):
     """BN + shared-slope PReLU in one apply pass; backward gate and slope gradient reduced in
@@ -880,3 +910,14 @@ def test_l1_gated_lrelu_gradient():
     ref_g = 2.0 * torch.sign(af - bf_) * torch.where(af > 0, 1.0, 0.2) / af.numel()
     assert abs(v.item() - ref_v.item()) <= 1e-3 * abs(ref_v.item())
     assert rel_err(ha.grad, ref_g) < 1e-2
+
+
+def test_guard_flag_kernel():
+    """The NaN / Inf guard on the HIP path: flag and counter from one kernel."""
+    from p2p_pytorch_amd.utils.guards import nonfinite
+    one, nan, inf = (torch.tensor(v, device=DEV) for v in (1.0, float("nan"), float("-inf")))
+    cnt = torch.zeros((), device=DEV)
+    assert float(nonfinite(one, one * 2, counter=cnt)) == 0.0 and float(cnt) == 0.0
+    assert float(nonfinite(one, nan, counter=cnt)) == 1.0 and float(cnt) == 1.0
+    assert float(nonfinite(inf, counter=cnt)) == 1.0 and float(cnt) == 2.0
+    assert float(nonfinite(torch.tensor(3.0e38, device=DEV))) == 0.0

@@ -166,11 +166,18 @@ def test_nb_unet256_generator_grads(monkeypatch):
         G.zero_grad(set_to_none=True)
         G(A.float()).square().mean().backward()
         oracle = {n: p.grad.detach().float().clone() for n, p in G.named_parameters()}
+        G.zero_grad(set_to_none=True)      # stock kernels under bf16 autocast: the dtype's error
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            G(A.float()).float().square().mean().backward()
+        eager = {n: p.grad.detach().float().clone() for n, p in G.named_parameters()}
     finally:
         _native.set_backend("native")
     for n in fused:
         ef, ep = rel_err(fused[n], oracle[n]), rel_err(plain[n], oracle[n])
+        ee = rel_err(eager[n], oracle[n])
         assert ef <= 1.5 * ep + 0.01, (n, ef, ep)
+        # and absolutely: the unfused native path within twice the eager bf16 error
+        assert ep <= 2 * ee + 0.01, (n, ep, ee)
 
 
 def test_fused_bias_colsum(monkeypatch):

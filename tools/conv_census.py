@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--variants", default="",
                     help="comma list of P2P_CONV_VARIANT values also timed per conv_fwd call (e.g. g2,g3)")
+    ap.add_argument("--wgrad_variants", default="",
+                    help="comma list of NAME=VAL environment settings also timed per conv_wgrad call "
+                         "(e.g. P2P_WGRAD_TILE=256)")
     args = ap.parse_args()
 
     import p2p_pytorch_amd as p2p
@@ -125,8 +128,9 @@ def main():
             return e0.elapsed_time(e1) / args.reps
         ms = timed()
         alt = {}
-        if name == "conv_fwd" and args.variants:
-            for v in args.variants.split(","):
+        vlist = args.variants if name == "conv_fwd" else args.wgrad_variants
+        if vlist:
+            for v in vlist.split(","):
                 # "g5" -> P2P_CONV_VARIANT=g5; "NAME=VAL" -> that environment variable
                 key, val = v.split("=", 1) if "=" in v else ("P2P_CONV_VARIANT", v)
                 os.environ[key] = val

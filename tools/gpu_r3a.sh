@@ -20,5 +20,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 echo smoke ok
 timeout -k 10 300 python bench.py > $O/bench_default.jsonl 2> $O/bench_default.err || exit $?
 cut -c1-300 $O/bench_default.jsonl
-timeout -k 10 400 python tools/conv_census.py --family pix2pix --batch 256 --top 60 --json $O/census_b256.json > $O/census_b256.txt 2>&1 || exit $?
+timeout -k 10 600 python tools/conv_census.py --family pix2pix --batch 256 --top 60 --wgrad_variants P2P_WGRAD_TILE=256 --json $O/census_b256.json > $O/census_b256.txt 2>&1 || exit $?
 head -70 $O/census_b256.txt
+P2P_LIB=p2p_pytorch_amd/_C/exp_normfrag.so timeout -k 10 400 python tools/conv_census.py --family pix2pix --batch 256 --top 60 --json $O/census_b256_normfrag.json > $O/census_b256_normfrag.txt 2>&1 || exit $?
+head -12 $O/census_b256_normfrag.txt

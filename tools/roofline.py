@@ -1,21 +1,38 @@
 #!/usr/bin/env python
-"""Per-kernel roofline table from tools/gpu_roofline.sh's counter passes.
+"""Per-kernel roofline table from tools/gpu_roofline.sh's counter passes, with the MFMA
+counters CALIBRATED on a kernel of known MFMA count (tools/probes/mfma_count_probe.hip).
 
-    python tools/roofline.py gpurun_out/roof --steps 3
+    python tools/roofline.py gpurun_out/roof --steps 3 --probe gpurun_out/r3a/probe_pmc
 
-Per kernel name (sorted by total time per step): calls / step, mean us, achieved MFMA
-TFLOP/s (SQ_INSTS_MFMA x 16384 FLOP -- every conv MFMA is v_mfma_f32_16x16x32_bf16),
-MFMA busy fraction (SQ_VALU_MFMA_BUSY_CYCLES / SQ_BUSY_CYCLES, as reported), LDS bank-
-conflict cycles per LDS instruction, HBM bytes (2 x FETCH_SIZE: gfx950 tallies 128-B reads
-at 64 B -- MI355X_MICROARCH.md; + WRITE_SIZE), achieved GB/s and arithmetic intensity.
+Columns per kernel name (sorted by time per step): calls / step, mean us, achieved MFMA
+TFLOP/s, MFMA busy as a true % of the chip's SIMD-cycles, LDS bank-conflict cycles per LDS
+instruction, HBM bytes per call (2 x FETCH_SIZE: gfx950 tallies 128-B reads at 64 B --
+MI355X_MICROARCH.md -- + WRITE_SIZE), achieved GB/s and arithmetic intensity.
+
+Calibration (from the probe's own counter pass; its kernels issue exactly
+2048 blocks x 4 waves x 4096 x 4 MFMAs, bf16 16x16x32 in k_bf16, e4m3 16x16x128 in k_fp8):
+  * inst_scale  = SQ_INSTS_MFMA / expected wave-MFMAs          (how the counter tallies)
+  * busy_per_mfma (bf16 / fp8) = SQ_VALU_MFMA_BUSY_CYCLES / expected wave-MFMAs
+  * clock = GRBM_GUI_ACTIVE / 8 / duration  (GRBM sums the 8 XCDs; MI355X_MICROARCH.md)
+  * MFMA busy % = 100 x (busy cycles / busy_per_mfma_bf16 x 16) / (1024 SIMDs x kernel cycles)
+    -- i.e. MFMA-pipe cycles (16 per bf16 16x16x32, 32 per fp8 16x16x128) over the SIMD-cycles
+    the kernel had; the probe's own row must read its FLOP-derived utilisation.
+FLOPs per MFMA instruction: 16384 (bf16 16x16x32), 65536 (fp8 16x16x128, the conv kernels'
+F8 template argument != 0).
 """
 from __future__ import annotations
 
 import collections
 import csv
 import glob
+import json
 import os
+import re
 import sys
+
+SIMDS = 1024           # 256 CUs x 4
+XCDS = 8
+PROBE_WAVE_MFMAS = 2048 * 4 * 4096 * 4
 
 
 def load(d):
@@ -37,11 +54,54 @@ def load(d):
     return vals, dur
 
 
+def mean(v):
+    return sum(v) / len(v) if v else None
+
+
+def calibrate(probe_dir):
+    """Calibration constants from the probe's counter pass (see module docstring)."""
+    vals, dur = load(probe_dir)
+    cal = {}
+    for k, c in vals.items():
+        tag = "bf16" if "k_bf16" in k else ("fp8" if "k_fp8" in k else None)
+        if tag is None:
+            continue
+        ns = mean(dur.get(k, []))
+        inst, busy, grbm = mean(c.get("SQ_INSTS_MFMA")), mean(c.get("SQ_VALU_MFMA_BUSY_CYCLES")), \
+            mean(c.get("GRBM_GUI_ACTIVE"))
+        flop = PROBE_WAVE_MFMAS * (16384 if tag == "bf16" else 65536)
+        clock = grbm / XCDS / ns if grbm and ns else None              # GHz
+        pipe = PROBE_WAVE_MFMAS * (16 if tag == "bf16" else 32)       # MFMA-pipe SIMD-cycles
+        cal[tag] = {
+            "ns": ns, "tflops": flop / ns / 1e3 if ns else None, "clock_ghz": clock,
+            "inst_scale": inst / PROBE_WAVE_MFMAS if inst else None,
+            "busy_per_mfma": busy / PROBE_WAVE_MFMAS if busy else None,
+            "util_true": pipe / (SIMDS * grbm / XCDS) if grbm else None,
+        }
+    return cal
+
+
+def is_fp8(kernel):
+    m = re.search(r"conv_fwd_glds_kernel<([^>]*)>", kernel)
+    if m:
+        args = [x.strip() for x in m.group(1).split(",")]
+        return len(args) > 8 and args[8] not in ("0",)
+    return False
+
+
 def short(k):
-    return k.replace("void p2p::", "").replace("p2p::", "").split("(")[0][:64]
+    return k.replace("void p2p::", "").replace("p2p::", "").split("(")[0][:72]
 
 
-def main(root, steps):
+def main(root, steps, probe):
+    cal = calibrate(probe) if probe else {}
+    if cal:
+        print("calibration (tools/probes/mfma_count_probe.hip, known MFMA counts):")
+        print("```")
+        print(json.dumps(cal, indent=1))
+        print("```")
+    inst_scale = cal.get("bf16", {}).get("inst_scale") or 1.0
+    busy_bf16 = cal.get("bf16", {}).get("busy_per_mfma") or 16.0
     sq, dur = load(os.path.join(root, "sq"))
     fe, _ = load(os.path.join(root, "fetch"))
     wr, _ = load(os.path.join(root, "write"))
@@ -52,36 +112,44 @@ def main(root, steps):
         n = len(ds)
         mean_ns = sum(ds) / n
         c = sq.get(k, {})
-
-        def m(cs, name):
-            v = cs.get(name)
-            return sum(v) / len(v) if v else None
-
-        mf = m(c, "SQ_INSTS_MFMA")
-        busy, mbusy = m(c, "SQ_BUSY_CYCLES"), m(c, "SQ_VALU_MFMA_BUSY_CYCLES")
-        lds, conf = m(c, "SQ_INSTS_LDS"), m(c, "SQ_LDS_BANK_CONFLICT")
-        fetch = m(fe.get(k, {}), "FETCH_SIZE")
-        write = m(wr.get(k, {}), "WRITE_SIZE")
-        flop = mf * 16384 if mf else 0.0
+        mf = mean(c.get("SQ_INSTS_MFMA", []))
+        busy = mean(c.get("SQ_VALU_MFMA_BUSY_CYCLES", []))
+        grbm = mean(c.get("GRBM_GUI_ACTIVE", []))
+        lds, conf = mean(c.get("SQ_INSTS_LDS", [])), mean(c.get("SQ_LDS_BANK_CONFLICT", []))
+        fetch = mean(fe.get(k, {}).get("FETCH_SIZE", []))
+        write = mean(wr.get(k, {}).get("WRITE_SIZE", []))
+        fpi = 65536 if is_fp8(k) else 16384
+        flop = (mf / inst_scale) * fpi if mf else 0.0
+        # MFMA-pipe SIMD-cycles: the busy counter in units of one bf16 16x16x32 (16 cycles)
+        pipe = busy / busy_bf16 * 16 if busy else None
+        util = 100.0 * pipe / (SIMDS * grbm / XCDS) if pipe and grbm else None
+        clock = grbm / XCDS / mean_ns if grbm else None
         byts = ((2 * fetch if fetch else 0.0) + (write or 0.0)) * 1024
-        rows.append((sum(ds) / steps, k, n / steps, mean_ns, flop, mbusy / busy if busy and mbusy else None,
-                     conf / lds if lds and conf is not None else None, byts))
+        rows.append((sum(ds) / steps, k, n / steps, mean_ns, flop, util,
+                     conf / lds if lds and conf is not None else None, byts, clock))
     rows.sort(reverse=True)
     tot = sum(r[0] for r in rows) or 1.0
-    print("| kernel | %step | calls/step | us/call | MFMA TF/s | MFMA busy | LDS confl/instr | HBM MB/call | GB/s | FLOP/B |")
-    print("|---|---|---|---|---|---|---|---|---|---|")
-    for t, k, calls, mean_ns, flop, mb, cf, byts in rows[:40]:
+    print()
+    print("| kernel | %step | calls/step | us/call | MFMA TF/s | MFMA busy % | LDS confl/instr | "
+          "HBM MB/call | GB/s | FLOP/B | clock GHz |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|")
+    for t, k, calls, mean_ns, flop, util, cf, byts, clock in rows[:45]:
         tf = flop / mean_ns / 1e3 if mean_ns else 0.0
         gbs = byts / mean_ns if mean_ns else 0.0
         ai = flop / byts if byts else 0.0
         print(f"| {short(k)} | {100 * t / tot:.1f} | {calls:.1f} | {mean_ns / 1e3:.1f} | {tf:.0f} | "
-              f"{'-' if mb is None else f'{mb:.2f}'} | {'-' if cf is None else f'{cf:.2f}'} | "
-              f"{byts / 1e6:.1f} | {gbs:.0f} | {ai:.1f} |")
+              f"{'-' if util is None else f'{util:.1f}'} | {'-' if cf is None else f'{cf:.2f}'} | "
+              f"{byts / 1e6:.1f} | {gbs:.0f} | {ai:.1f} | {'-' if clock is None else f'{clock:.2f}'} |")
 
 
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     steps = 3
+    probe = None
     if "--steps" in sys.argv:
         steps = float(sys.argv[sys.argv.index("--steps") + 1])
-    main(args[0] if args else "gpurun_out/roof", steps)
+        args = [a for a in args if a != sys.argv[sys.argv.index("--steps") + 1]]
+    if "--probe" in sys.argv:
+        probe = sys.argv[sys.argv.index("--probe") + 1]
+        args = [a for a in args if a != probe]
+    main(args[0] if args else "gpurun_out/roof", steps, probe)
