@@ -714,23 +714,36 @@ Tensor conv_d2s(const Tensor& x1, const optional<Tensor>& x2, const Tensor& w, c
 }
 
 // ------------------------------------------------------------------ conv wgrad
-void conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, const Tensor& q1,
+// fp8 (qs_p / qs_q given): p / q are OCP fp8 shadows (p_fmt / q_fmt 0 = e4m3, 1 = e5m2) with
+// their scale sites; returns false (nothing launched) when the fp8 kernel does not take the
+// geometry -- the caller then runs the bf16 path.  bf16 always returns true.
+bool conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, const Tensor& q1,
                 const optional<Tensor>& q2, int64_t q_act, int64_t KH, int64_t KW, int64_t stride,
                 int64_t pad, int64_t reflect, int64_t up, Tensor dw, double scale,
-                int64_t accumulate, int64_t flip) {
-  check_act(p1, "conv_wgrad p1");
-  check_act(q1, "conv_wgrad q1");
+                int64_t accumulate, int64_t flip, const optional<Tensor>& qs_p,
+                const optional<Tensor>& qs_q, int64_t p_fmt, int64_t q_fmt, const optional<Tensor>& qs_p2,
+                const optional<Tensor>& qs_q2) {
+  const bool f8 = qs_p.has_value() || qs_q.has_value();
+  TORCH_CHECK(!f8 || (qs_p && qs_q && !flip && p1.element_size() == 1 && q1.element_size() == 1 &&
+                      (!p2 || p2->element_size() == 1) && (!q2 || q2->element_size() == 1)),
+              "conv_wgrad fp8: both operands fp8 with both scale sites");
+  if (f8) {
+    check_site(*qs_p);
+    check_site(*qs_q);
+  }
+  check_act(p1, "conv_wgrad p1", f8);
+  check_act(q1, "conv_wgrad q1", f8);
   const int64_t N = p1.size(0), OH = p1.size(2), OW = p1.size(3);
   int64_t R2 = 0, C2 = 0;
   if (p2) {
-    check_act(*p2, "conv_wgrad p2");
+    check_act(*p2, "conv_wgrad p2", f8);
     TORCH_CHECK(p2->size(0) == N && p2->size(2) == OH && p2->size(3) == OW, "wgrad p concat shape");
     R2 = p2->size(1);
   }
   const int64_t H = q1.size(2), W = q1.size(3);
   TORCH_CHECK(q1.size(0) == N, "conv_wgrad: batch mismatch");
   if (q2) {
-    check_act(*q2, "conv_wgrad q2");
+    check_act(*q2, "conv_wgrad q2", f8);
     TORCH_CHECK(q2->size(0) == N && q2->size(2) == H && q2->size(3) == W, "wgrad q concat shape");
     C2 = q2->size(1);
   }
@@ -772,6 +785,38 @@ void conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, con
   a.Kq = (int)(KH * KW * C);
   a.zero = zero_page(p1);
   hipStream_t st = cur_stream(p1);
+  if (f8) {
+    a.f8 = 1;
+    a.p_fmt = (int)p_fmt;
+    a.q_fmt = (int)q_fmt;
+    a.qs_p = qs_p->data_ptr<int>();
+    a.qs_q = qs_q->data_ptr<int>();
+    if (qs_p2) {
+      check_site(*qs_p2);
+      a.qs_p2 = qs_p2->data_ptr<int>();
+    }
+    if (qs_q2) {
+      check_site(*qs_q2);
+      a.qs_q2 = qs_q2->data_ptr<int>();
+    }
+    int tr = 0, tq = 0;
+    if (!p2p_conv_wgrad_f8_tile(&a, &tr, &tq) || !((p_fmt == 1 && q_fmt == 0) || (p_fmt == 0 && q_fmt == 1)))
+      return false;
+    const int64_t tiles = ((R + tr - 1) / tr) * ((a.Kq + tq - 1) / tq);
+    const int64_t stages = ((int64_t)a.M + 127) / 128;
+    int64_t splits = std::max<int64_t>(1, 512 / std::max<int64_t>(tiles, 1));
+    splits = std::min<int64_t>(splits, std::max<int64_t>(1, stages / 8));
+    const int64_t slab = R * (int64_t)a.Kq;
+    splits = std::max<int64_t>(1, std::min<int64_t>(splits, (64ll << 20) / std::max<int64_t>(slab, 1)));
+    a.splits = (int)splits;
+    Tensor ws = at::empty({splits * slab}, p1.options().dtype(at::kFloat));
+    a.ws = ws.data_ptr<float>();
+    check_rc(p2p_conv_wgrad(&a, st), "conv_wgrad(fp8)");
+    check_rc(p2p_wgrad_reduce(a.ws, a.splits, a.R, a.KH, a.KW, a.C, (int)Rr, (int)Cr, dw.data_ptr<float>(),
+                              (float)scale, (int)accumulate, 0, st),
+             "wgrad_reduce(fp8)");
+    return true;
+  }
   // 9x9 stride-1 layers with 16 / 32 input and <= 32 output channels: halo-tile wgrad
   // (csrc/halo_wgrad.hip), one fp32 slab per persistent block
   const bool halo_geo = (KH == 9 && KW == 9 && (C == 16 || C == 32) && (R <= 16 || (C == 16 && R == 32))) ||
@@ -807,7 +852,7 @@ void conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, con
       check_rc(p2p_wgrad_reduce(h.ws, blocks, (int)R, (int)KH, (int)KW, (int)C, (int)Rr, (int)Cr, dw.data_ptr<float>(),
                                 (float)scale, (int)accumulate, 0, st),
                "wgrad_reduce(halo)");
-      return;
+      return true;
     }
   }
   int wbr = 128, wbq = 128;
@@ -828,6 +873,7 @@ void conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, con
                             flip ? (int)Rr : (int)Cr, dw.data_ptr<float>(), (float)scale,
                             (int)accumulate, (int)flip, st),
            "wgrad_reduce");
+  return true;
 }
 
 // ------------------------------------------------------------------ weight prep
@@ -1552,7 +1598,8 @@ TORCH_LIBRARY(p2p, m) {
   m.def("fp8_dequant(Tensor q, Tensor site) -> Tensor");
   m.def("conv_wgrad(Tensor p1, Tensor? p2, int p_act, Tensor q1, Tensor? q2, int q_act, int KH, int KW, "
         "int stride, int pad, int reflect, int up, Tensor(a!) dw, float scale, int accumulate, "
-        "int flip=0) -> ()");
+        "int flip=0, Tensor? qs_p=None, Tensor? qs_q=None, int p_fmt=0, int q_fmt=0, Tensor? qs_p2=None, "
+        "Tensor? qs_q2=None) -> bool");
   m.def("weight_prep(Tensor w, int swap, int Xp, int Yp, Tensor? scale) -> Tensor");
   m.def("union_weight(Tensor w, int co_off, int nv, int Nrows, int Cpad, Tensor? bias) -> Tensor[]");
   m.def("conv_d2s(Tensor x1, Tensor? x2, Tensor w, Tensor bias, int act_in, int act_out, int mode, "

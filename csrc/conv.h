@@ -109,6 +109,14 @@ struct ConvWgradArgs {
   int M;           // N*OH*OW
   int Kq;          // KH*KW*C
   const void* zero;  // zero page for the global_load_lds variant
+  // fp8 operands (f8 = 1): P and Q are 1-byte OCP fp8 tensors (p_fmt / q_fmt: 0 = e4m3,
+  // 1 = e5m2) with per-tensor E8M0 dequant exponents in word 2 of their scale sites
+  int f8;
+  int p_fmt, q_fmt;
+  const int* qs_p;    // P (first concat half)
+  const int* qs_q;    // Q (first concat half)
+  const int* qs_p2;   // second concat halves' sites (null = the first half's)
+  const int* qs_q2;
 };
 
 // Halo-tile union conv (csrc/halo_conv.hip): the conv_d2s GEMM with a resident 16-column
@@ -199,6 +207,7 @@ int p2p_fp8_amax_multi(int count, const float* const* x, const long* n, int* con
 int p2p_fp8_dequant(const void* q, long n, const int* site, int fmt, void* y, hipStream_t st);
 int p2p_conv_wgrad_tile_rows(int R);
 int p2p_conv_wgrad_tile(const p2p::ConvWgradArgs* a, int* tile_r, int* tile_q);
+int p2p_conv_wgrad_f8_tile(const p2p::ConvWgradArgs* a, int* tile_r, int* tile_q);
 int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int KW, int C, int Rr, int Cr,
                      float* dw, float scale, int accumulate, int flip, hipStream_t stream);
 int p2p_col2im(int mode, const void* col, int ldc, int N, int H, int W, int OH, int OW, int KH, int KW,

@@ -585,6 +585,257 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// fp8 weight gradient (gfx950 v_mfma_scale_f32_16x16x128_f8f6f4): P and Q are the OCP fp8
+// shadows the forward / dgrad already quantised (activations e4m3, gradients e5m2), with
+// per-tensor power-of-two scales handed to the MFMA as E8M0 operands (free dequant).
+// The reduction (pixel) dimension is the outer dimension of both operands, so both are read
+// k-transposed out of LDS with ds_read_b64_tr_b8: per 16-lane group an 8-row x 16-column byte
+// block, lane i receiving column i of the 8 rows (probe: tools/probes/ds_read_tr_b8_probe.hip).
+// A stage is 128 pixels (one 128-deep MFMA K step); LDS sub-tiles are [128 rows][128 B]
+// with the 16-B chunk XOR-swizzled by f8x(row) so the 16 rows x 16 B a half-wave reads per
+// transposed load hit all 64 banks once; the swizzle is applied on the glds SOURCE side.
+__device__ __forceinline__ int f8x(int row) { return ((row >> 1) & 3) | (((row >> 4) & 1) << 2); }
+
+// lane's byte address of transposed-read block 0 of a 16-column fragment at column cb
+__device__ __forceinline__ uint32_t tr8_lane_addr(const uint8_t* sub, int cb, int lane) {
+  const int q = lane >> 4, i = lane & 15;
+  const int row = 16 * q + (i >> 1);
+  return lds_addr(sub + row * 128 + ((((cb & 127) >> 4) ^ f8x(row)) << 4) + 8 * (i & 1));
+}
+
+typedef int i32x8w __attribute__((ext_vector_type(8)));
+
+// the 32 K bytes of one lane: K [16q, 16q+16) -> bytes 0..15, K [64+16q, +16) -> 16..31
+__device__ __forceinline__ i32x8w tr8_frag(uint32_t addr) {
+  uint64_t b0, b1, b2, b3;
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:0" : "=v"(b0) : "v"(addr));
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:1024" : "=v"(b1) : "v"(addr));
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:8192" : "=v"(b2) : "v"(addr));
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:9216" : "=v"(b3) : "v"(addr));
+  i32x8w v = {(int)(uint32_t)b0, (int)(uint32_t)(b0 >> 32), (int)(uint32_t)b1, (int)(uint32_t)(b1 >> 32),
+              (int)(uint32_t)b2, (int)(uint32_t)(b2 >> 32), (int)(uint32_t)b3, (int)(uint32_t)(b3 >> 32)};
+  return v;
+}
+
+__device__ __forceinline__ i32x8w relu_f8x32(i32x8w v) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t w = (uint32_t)v[k];
+    const uint32_t neg = (w >> 7) & 0x01010101u;
+    v[k] = (int)(w & ~(neg * 0xffu));
+  }
+  return v;
+}
+
+// RM: bit 0 = ReLU on the P fragments, bit 1 = on the Q fragments (fp8 sign bits);
+// PF / QF: the MFMA operand formats of P / Q (0 = e4m3, 1 = e5m2)
+template <int TBR, int TBQ, int WM, int WN, int STAGES, int RM, int PF, int QF>
+__global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_f8_kernel(ConvWgradArgs a) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int TM = TBR / WM / 16, TN = TBQ / WN / 16;
+  constexpr int SROWS = 128;                          // pixels per stage (one K step)
+  constexpr int SUBB = SROWS * 128;                   // bytes per [128][128 B] sub-tile
+  constexpr int PSUB = TBR / 128, QSUB = TBQ / 128;
+  constexpr int PL = PSUB * 1024 / NT, QL = QSUB * 1024 / NT;   // glds per thread per stage
+  constexpr int LOADS = PL + QL;
+  static_assert(PL >= 1 && QL >= 1 && (PSUB * 1024) % NT == 0 && (QSUB * 1024) % NT == 0,
+                "every wave issues the same glds count");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint8_t* Ps = reinterpret_cast<uint8_t*>(smem);    // [STAGES][PSUB][128][128]
+  uint8_t* Qs = Ps + STAGES * PSUB * SUBB;            // [STAGES][QSUB][128][128]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int qtiles = (a.Kq + TBQ - 1) / TBQ;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int rt = bid / qtiles, qt = bid % qtiles;
+  const int r0 = rt * TBR, q0 = qt * TBQ;
+
+  const int stages = (a.M + SROWS - 1) / SROWS;
+  const int sps = (stages + a.splits - 1) / a.splits;
+  const int s0 = blockIdx.y * sps;
+  const int s1 = min(stages, s0 + sps);
+
+  const uint8_t* __restrict__ p1 = static_cast<const uint8_t*>(a.p1);
+  const uint8_t* __restrict__ p2 = static_cast<const uint8_t*>(a.p2);
+  const uint8_t* __restrict__ q1 = static_cast<const uint8_t*>(a.q1);
+  const uint8_t* __restrict__ q2 = static_cast<const uint8_t*>(a.q2);
+  const uint8_t* zero = static_cast<const uint8_t*>(a.zero);
+  const int ep1 = a.qs_p ? a.qs_p[2] : 127, eq1 = a.qs_q ? a.qs_q[2] : 127;
+  const int ep2 = a.qs_p2 ? a.qs_p2[2] : ep1, eq2 = a.qs_q2 ? a.qs_q2[2] : eq1;
+
+  int p_row[PL], p_lds[PL], p_ld[PL];
+  const uint8_t* p_base[PL];
+#pragma unroll
+  for (int i = 0; i < PL; ++i) {
+    const int q = tid + NT * i;
+    const int sub = q >> 10, rem = q & 1023;
+    const int row = rem >> 3, slot = rem & 7;
+    const int col = r0 + sub * 128 + ((slot ^ f8x(row)) << 4);
+    const bool first = col < a.R1;
+    p_row[i] = col < a.R ? row : -1;
+    p_base[i] = first ? p1 + col : p2 + (col - a.R1);
+    p_ld[i] = first ? a.R1 : a.R2;
+    p_lds[i] = sub * SUBB + ((q & ~63) & 1023) * 16;
+  }
+  int q_row[QL], q_lds[QL], q_kh[QL], q_kw[QL], q_ld[QL];
+  const uint8_t* q_base[QL];
+#pragma unroll
+  for (int i = 0; i < QL; ++i) {
+    const int q = tid + NT * i;
+    const int sub = q >> 10, rem = q & 1023;
+    const int row = rem >> 3, slot = rem & 7;
+    const int kq = q0 + sub * 128 + ((slot ^ f8x(row)) << 4);
+    int tap = 0, ci = 0;
+    const bool ok = kq < a.Kq;
+    if (ok) {
+      tap = kq / a.C;
+      ci = kq - tap * a.C;
+    }
+    q_kh[i] = tap / a.KW;
+    q_kw[i] = tap - q_kh[i] * a.KW;
+    const bool first = ci < a.C1;
+    q_base[i] = first ? q1 + ci : q2 + (ci - a.C1);
+    q_ld[i] = first ? a.C1 : a.C2;
+    q_row[i] = ok ? row : -1;
+    q_lds[i] = sub * SUBB + ((q & ~63) & 1023) * 16;
+  }
+  const int ush = a.up == 2 ? 1 : 0;
+  const int Hu = a.H << ush, Wu = a.W << ush;
+  const int OHW = a.OH * a.OW;
+  const FastDiv fd_ohw = make_fastdiv((uint32_t)OHW), fd_ow = make_fastdiv((uint32_t)a.OW);
+  int q_n[QL], q_oh[QL], q_ow[QL];
+#pragma unroll
+  for (int i = 0; i < QL; ++i) {
+    const int m = s0 * SROWS + (q_row[i] >= 0 ? q_row[i] : 0);
+    q_n[i] = (int)fdiv((uint32_t)m, fd_ohw);
+    const int rem = m - q_n[i] * OHW;
+    q_oh[i] = (int)fdiv((uint32_t)rem, fd_ow);
+    q_ow[i] = rem - q_oh[i] * a.OW;
+  }
+  const int d_n = SROWS / OHW, d_rem = SROWS % OHW;
+  const int d_h = d_rem / a.OW, d_w = d_rem % a.OW;
+
+  auto issue = [&](int st, int stage) {
+    uint8_t* Pst = Ps + stage * PSUB * SUBB;
+    uint8_t* Qst = Qs + stage * QSUB * SUBB;
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+      const int m = st * SROWS + p_row[i];
+      const bool ok = p_row[i] >= 0 && m < a.M;
+      const uint8_t* gp = ok ? p_base[i] + (long)m * p_ld[i] : zero;
+      __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)(Pst + p_lds[i]), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < QL; ++i) {
+      if (st != s0) {
+        int ow = q_ow[i] + d_w, oh = q_oh[i] + d_h, n = q_n[i] + d_n;
+        if (ow >= a.OW) {
+          ow -= a.OW;
+          ++oh;
+        }
+        if (oh >= a.OH) {
+          oh -= a.OH;
+          ++n;
+        }
+        q_ow[i] = ow;
+        q_oh[i] = oh;
+        q_n[i] = n;
+      }
+      const int m = st * SROWS + (q_row[i] >= 0 ? q_row[i] : 0);
+      int uy = q_oh[i] * a.stride - a.pad + q_kh[i];
+      int ux = q_ow[i] * a.stride - a.pad + q_kw[i];
+      if (a.reflect) {
+        uy = reflect_idx(uy, Hu);
+        ux = reflect_idx(ux, Wu);
+      }
+      const bool ok = q_row[i] >= 0 && m < a.M && (unsigned)uy < (unsigned)Hu && (unsigned)ux < (unsigned)Wu;
+      const int pix = (q_n[i] * a.H + (uy >> ush)) * a.W + (ux >> ush);
+      const uint8_t* gp = ok ? q_base[i] + (long)pix * q_ld[i] : zero;
+      __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)(Qst + q_lds[i]), 16, 0, 0);
+    }
+  };
+
+  // per fragment: LDS address and the E8M0 dequant exponent of its concat half (a 16-column
+  // fragment lies inside one half: host guarantees R1 % 16 == 0 and C1 % 16 == 0)
+  uint32_t fa_lane[TM], fb_lane[TN];
+  int fa_e[TM], fb_e[TN];
+#pragma unroll
+  for (int i2 = 0; i2 < TM; ++i2) {
+    const int cb = wm * (TBR / WM) + i2 * 16;
+    fa_lane[i2] = tr8_lane_addr(Ps + (cb >> 7) * SUBB, cb, lane);
+    fa_e[i2] = r0 + cb < a.R1 ? ep1 : ep2;
+  }
+#pragma unroll
+  for (int j2 = 0; j2 < TN; ++j2) {
+    const int cb = wn * (TBQ / WN) + j2 * 16;
+    fb_lane[j2] = tr8_lane_addr(Qs + (cb >> 7) * SUBB, cb, lane);
+    const int kq = q0 + cb;
+    fb_e[j2] = (kq - (kq / a.C) * a.C) < a.C1 ? eq1 : eq2;
+  }
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int sgi = 0; sgi < STAGES - 1; ++sgi)
+    if (s0 + sgi < s1) issue(s0 + sgi, sgi);
+
+  int stage = 0;
+  for (int st = s0; st < s1; ++st) {
+    if (st + STAGES - 2 < s1) wg_wait_vmcnt<LOADS * (STAGES - 2)>();
+    else wg_wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + STAGES - 1 < s1) {
+      int ns = stage + STAGES - 1;
+      if (ns >= STAGES) ns -= STAGES;
+      issue(st + STAGES - 1, ns);
+    }
+    const uint32_t p_st = (uint32_t)(stage * PSUB * SUBB), q_st = (uint32_t)(stage * QSUB * SUBB);
+    i32x8w af[TM], bfr[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = tr8_frag(fb_lane[j] + q_st);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = tr8_frag(fa_lane[i] + p_st);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (RM & 1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = relu_f8x32(af[i]);
+    }
+    if constexpr (RM & 2) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = relu_f8x32(bfr[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], PF, QF, 0,
+                                                                     fa_e[i], 0, fb_e[j]);
+    stage = stage + 1 == STAGES ? 0 : stage + 1;
+  }
+
+  float* slab = a.ws + (long)blockIdx.y * a.R * a.Kq;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = q0 + wn * (TBQ / WN) + j * 16 + (lane & 15);
+      const int rowb = r0 + wm * (TBR / WM) + i * 16 + (lane >> 4) * 4;
+      if (col < a.Kq) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (rowb + r < a.R) slab[(long)(rowb + r) * a.Kq + col] = acc[i][j][r];
+      }
+    }
+}
+
 // dw[r][ci][kh][kw] (+)= scale * sum_s ws[s][r][(kh*KW+kw)*C + ci]
 // Block = EPB elements x G split-groups; each thread sums a fixed, strided subset of the
 // splits, then the G partials are combined in LDS in a fixed order (deterministic).
@@ -696,8 +947,60 @@ static int wg_launch_rm(int rm, const p2p::ConvWgradArgs& a, dim3 grid, int smem
   }
 }
 
+template <int TBR, int TBQ, int WM, int WN, int STG, int RM, int PF, int QF>
+static int wg8_launch(const p2p::ConvWgradArgs& a, hipStream_t st) {
+  constexpr int smem = STG * (TBR + TBQ) * 128;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&p2p::conv_wgrad_f8_kernel<TBR, TBQ, WM, WN, STG, RM, PF, QF>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  dim3 grid(((a.R + TBR - 1) / TBR) * ((a.Kq + TBQ - 1) / TBQ), a.splits, 1);
+  hipLaunchKernelGGL((p2p::conv_wgrad_f8_kernel<TBR, TBQ, WM, WN, STG, RM, PF, QF>), grid, dim3(WM * WN * 64), smem,
+                     st, a);
+  return (int)hipGetLastError();
+}
+
+// (P, Q) formats: conv wgrad = (e5m2 dY, e4m3 X); transposed-conv wgrad = (e4m3 X, e5m2 dY)
+template <int TBR, int TBQ, int WM, int WN, int STG, int RM>
+static int wg8_launch_fmt(const p2p::ConvWgradArgs& a, hipStream_t st) {
+  if (a.p_fmt == 1 && a.q_fmt == 0) return wg8_launch<TBR, TBQ, WM, WN, STG, RM, 1, 0>(a, st);
+  if (a.p_fmt == 0 && a.q_fmt == 1) return wg8_launch<TBR, TBQ, WM, WN, STG, RM, 0, 1>(a, st);
+  return -2;
+}
+
+template <int TBR, int TBQ, int WM, int WN, int STG>
+static int wg8_launch_rm(int rm, const p2p::ConvWgradArgs& a, hipStream_t st) {
+  switch (rm) {
+    case 1: return wg8_launch_fmt<TBR, TBQ, WM, WN, STG, 1>(a, st);
+    case 2: return wg8_launch_fmt<TBR, TBQ, WM, WN, STG, 2>(a, st);
+    case 3: return wg8_launch_fmt<TBR, TBQ, WM, WN, STG, 3>(a, st);
+    default: return wg8_launch_fmt<TBR, TBQ, WM, WN, STG, 0>(a, st);
+  }
+}
+
+// fp8 wgrad tile: 1 = 256(R) x 128(Kq), 2 = 128 x 256; 0 = not covered (caller: bf16 path)
+extern "C" int p2p_conv_wgrad_f8_tile(const p2p::ConvWgradArgs* a, int* tr, int* tq) {
+  using namespace p2p;
+  if (!a->zero || a->Kq % 128 || a->R % 128 || a->C1 % 16 || a->C2 % 16 || a->R1 % 16 || a->R2 % 16) return 0;
+  if ((a->p_act != ACT_NONE && a->p_act != ACT_RELU) || (a->q_act != ACT_NONE && a->q_act != ACT_RELU)) return 0;
+  if (a->R >= 256) { *tr = 256; *tq = 128; return 1; }
+  if (a->Kq >= 256) { *tr = 128; *tq = 256; return 2; }
+  return 0;
+}
+
 extern "C" int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t st) {
   using namespace p2p;
+  if (a->f8) {
+    int tr = 0, tq = 0;
+    const int shape8 = p2p_conv_wgrad_f8_tile(a, &tr, &tq);
+    if (!shape8) return -2;
+    const int rm = (a->p_act == ACT_RELU ? 1 : 0) | (a->q_act == ACT_RELU ? 2 : 0);
+    if (shape8 == 1) return wg8_launch_rm<256, 128, 4, 2, 3>(rm, *a, st);
+    return wg8_launch_rm<128, 256, 2, 4, 3>(rm, *a, st);
+  }
   const int shape = wgrad_glds_shape(a);
   if (shape) {
     constexpr int STG = 3;

@@ -553,6 +553,35 @@ def _nb_half(cfg, q2, nb, res_fused):
     return None
 
 
+def _wgrad_fp8(cfg, weight, q1, q2, gyp, act_in, gw) -> bool:
+    """fp8 weight gradient (BASELINE config 5): dY e5m2 x X e4m3 on the scaled f8f6f4 MFMA,
+    reading the fp8 copies the forward / dgrad of this conv already made (``_f8.quant`` caches
+    them per step under the same site keys) -- the image-facing layers stay bf16.  Returns
+    False when the geometry is not the fp8 kernel's (the caller runs the bf16 wgrad)."""
+    if not _f8.enabled() or os.environ.get("P2P_FP8_WGRAD", "0") == "0":
+        return False
+    if cfg.reflect or cfg.up != 1 or act_in not in (0, 1):
+        return False
+    C1 = q1.shape[1]
+    C2 = 0 if q2 is None else q2.shape[1]
+    Cout = gyp.shape[1]
+    if not (_f8.conv_ok(C1, C2, Cout, act_in) and C1 % 16 == 0 and C2 % 16 == 0 and Cout % 128 == 0
+            and (C1 + C2) % 128 == 0 and C1 + C2 >= 128):
+        return False
+    k = id(weight)
+    x1q, sx = _f8.quant(q1, (k, "x", 1), _f8.E4M3)
+    x2q = sx2 = None
+    if q2 is not None:     # the concat halves keep their own scales (per-fragment exponents)
+        x2q, sx2 = _f8.quant(q2, (k, "x", 2), _f8.E4M3)
+    gq, sg = _f8.quant(gyp, (k, "gy", 1), _f8.E5M2)
+    KH, KW, s, p = cfg.KH, cfg.KW, cfg.stride, cfg.pad
+    if cfg.transposed:
+        return bool(P().conv_wgrad(x1q, x2q, act_in, gq, None, 0, KH, KW, s, p, 0, 1, gw, 1.0, 0, 0,
+                                   sx, sg, _f8.E4M3, _f8.E5M2, sx2, None))
+    return bool(P().conv_wgrad(gq, None, 0, x1q, x2q, act_in, KH, KW, s, p, 0, 1, gw, 1.0, 0, 0,
+                               sg, sx, _f8.E5M2, _f8.E4M3, None, sx2))
+
+
 def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, need_b, alpha=None,
                    nb=None):
     """Input / weight / bias gradients of one fused conv (ConvFn's backward, shared with the
@@ -643,7 +672,9 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
     if need_w:
         gw = torch.empty_like(weight, dtype=torch.float32, memory_format=torch.contiguous_format)
         act_in = _act_code(cfg.act_in)
-        if cfg.transposed:
+        if _wgrad_fp8(cfg, weight, q1, q2, gyp, act_in, gw):
+            pass
+        elif cfg.transposed:
             P().conv_wgrad(q1, q2, act_in, gyp, None, 0, KH, KW, s, p, 0, 1, gw, 1.0, 0)
         elif (s == 1 and Coutp <= 16 and Cp >= 128 and KH == KW and not cfg.reflect
               and cfg.up == 1):

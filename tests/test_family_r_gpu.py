@@ -99,12 +99,11 @@ def test_family_r_step_gpu_matches_cpu_oracle():
             erre = (ge.cpu().float() - gr.float()).abs().max().item()
             scale = gr.abs().max().item()
             rows.append((n, err, erre, scale))
-            # a single-scalar gradient (the shared PReLU slope: sum of dy * x over every
-            # negative PReLU input of the step, a heavily cancelling sum) has no
-            # per-element statistics: with bf16 activations (eager autocast keeps the BN /
-            # PReLU outputs fp32) its measured error is 17-61 % of its value; bounded here
-            # by its magnitude (right sign and scale) instead of by the eager scalar error
-            floor = 0.75 * scale if gr.numel() == 1 else 1e-2 * scale
+            # the single-scalar shared-PReLU slope gradient (a heavily cancelling sum of
+            # dy * x over every negative PReLU input) takes the same rule: the eager bf16
+            # run's own error on it is large (17-61 % of the value), and the native one
+            # stays within twice that (r3: 0.025 vs eager 0.049 at |grad| 0.084)
+            floor = 1e-2 * scale
             if err > 2 * erre + floor and err > 1e-3 * gscale:
                 bad.append((n, err, erre, scale))
     for net, netg, nete, it in ((G, Gg, Ge, "buffers"), (D, Dg, De, "uv")):

@@ -244,3 +244,54 @@ def test_fused_shadows_equal_standalone_quantisation(producer):
             assert ent is not None, "no dx shadow"
             torch.cuda.synchronize()
             assert torch.equal(ent[1].view(torch.uint8), _expect_fp8(dx, ent[2], 1)), f"dx shadow, step {it}"
+
+
+def _deq(q, site):
+    """fp8 tensor x its power-of-two scale -> exact fp32."""
+    return q.float() * 2.0 ** (int(site[2].item()) - 127)
+
+
+@pytest.mark.parametrize("case", ["conv_s2_relu", "convT_concat", "conv_s1_wide"])
+def test_fp8_wgrad_matches_dequantised_oracle(case):
+    """fp8 weight gradient (e5m2 dY x e4m3 X on the scaled f8f6f4 MFMA, both operands read
+    k-transposed with ds_read_b64_tr_b8) against an fp32 weight gradient of the DEQUANTISED
+    operands: the products are exact in fp32, so the bound only absorbs summation order."""
+    P = _native.ops()
+    if case == "conv_s2_relu":      # U-Net e3-like: 128 -> 256, 4x4 s2 p1, input ReLU
+        N, C1, C2, H, Cout, k, s, p, act, tr = 8, 128, 0, 32, 256, 4, 2, 1, 1, False
+    elif case == "conv_s1_wide":    # PatchGAN c4-like: 256 -> 512, 4x4 s1 p1
+        N, C1, C2, H, Cout, k, s, p, act, tr = 4, 256, 0, 17, 512, 4, 1, 1, 0, False
+    else:                           # U-Net decoder ConvT on a skip concat: (128 | 128) -> 128
+        N, C1, C2, H, Cout, k, s, p, act, tr = 8, 128, 128, 16, 128, 4, 2, 1, 1, True
+    x1 = rand_img(N, C1, H, H, seed=61)
+    x2 = rand_img(N, C2, H, H, seed=62) if C2 else None
+    OH = (H - 1) * s - 2 * p + k if tr else (H + 2 * p - k) // s + 1
+    gy = rand_img(N, Cout, OH, OH, scale=0.01, seed=63)
+    sites = [torch.zeros(4, dtype=torch.int32, device=DEV) for _ in range(3)]
+    qs = []
+    for t, site, fmt in ((x1, sites[0], 0), (x2, sites[1], 0), (gy, sites[2], 1)):
+        if t is None:
+            qs.append(None)
+            continue
+        P.fp8_amax(t, site, 0)
+        qs.append(P.fp8_quant(t, site, fmt, 0))
+    x1q, x2q, gq = qs
+    xd = _deq(x1q, sites[0])
+    if x2q is not None:
+        xd = torch.cat((xd, _deq(x2q, sites[1])), 1)
+    xa = F.relu(xd) if act else xd
+    gd = _deq(gq, sites[2])
+    if tr:
+        w = torch.zeros(C1 + C2, Cout, k, k, device=DEV, requires_grad=True)
+        F.conv_transpose2d(xa, w, None, s, p).backward(gd)
+        gw = torch.empty(C1 + C2, Cout, k, k, device=DEV)
+        ok = P.conv_wgrad(x1q, x2q, act, gq, None, 0, k, k, s, p, 0, 1, gw, 1.0, 0, 0,
+                          sites[0], sites[2], 0, 1, sites[1] if x2q is not None else None, None)
+    else:
+        w = torch.zeros(Cout, C1 + C2, k, k, device=DEV, requires_grad=True)
+        F.conv2d(xa, w, None, s, p).backward(gd)
+        gw = torch.empty(Cout, C1 + C2, k, k, device=DEV)
+        ok = P.conv_wgrad(gq, None, 0, x1q, x2q, act, k, k, s, p, 0, 1, gw, 1.0, 0, 0,
+                          sites[2], sites[0], 1, 0, None, sites[1] if x2q is not None else None)
+    assert ok, "fp8 wgrad kernel did not take the geometry"
+    assert rel_err(gw, w.grad) < 1e-4, rel_err(gw, w.grad)

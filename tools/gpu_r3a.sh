@@ -13,6 +13,8 @@ cat $O/probe.txt
 timeout -s KILL 90 rocprofv3 --kernel-trace --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT \
   --output-format csv -d $O/probe_pmc -o run -- ./tools/probes/bin/mfma_count_probe > $O/probe_pmc.log 2>&1 || exit $?
 echo probe pmc ok
+timeout -k 10 60 ./tools/probes/bin/ds_read_tr_b8_probe > $O/tr_b8.txt 2>&1 || exit $?
+head -3 $O/tr_b8.txt
 timeout -k 10 900 python -u -m pytest tests/ -q -m gpu -x --timeout 240 --timeout-method thread > $O/kt.log 2>&1; rc=$?
 echo "gpu tests rc=$rc: $(tail -1 $O/kt.log)"; grep -E "FAILED|ERROR" $O/kt.log | head -20
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
