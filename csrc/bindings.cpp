@@ -173,7 +173,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                              const optional<Tensor>& nb_x, const optional<Tensor>& nb_mean,
                              const optional<Tensor>& nb_rstd, const optional<Tensor>& nb_gamma,
                              const optional<Tensor>& nb_beta, int64_t nb_act, int64_t nb_half, bool nb_batch,
-                             bool nb_colsum) {
+                             bool nb_colsum, bool nb_gate) {
   check_act(x1, "conv_fwd x1", true);
   // fp8 operands: x e4m3 (activations) or e5m2 (gradients), weight image e4m3, each with
   // an fp8 scale site (csrc/fp8.hip); outputs stay bf16
@@ -443,6 +443,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       a.nb_gamma = nb_gamma ? nb_gamma->data_ptr<float>() : nullptr;
       a.nb_beta = nb_gamma ? nb_beta->data_ptr<float>() : nullptr;
       a.nb_act = (int)nb_act;
+      a.nb_gate = (nb_gate && !nb_colsum && nb_act == 0 && std::getenv("P2P_NB_GATE_LOAD") == nullptr) ? 1 : 0;
       a.nb_batch = nb_batch ? 1 : 0;
       a.nb_c0 = (int)c0;
       a.nb_C = (int)nC;
@@ -1588,7 +1589,7 @@ TORCH_LIBRARY(p2p, m) {
         "Tensor? qs_x2=None, Tensor? qs_w=None, Tensor(a!)? y_qsite=None, int y_qfmt=0, Tensor? res=None, "
         "Tensor? alpha=None, Tensor? nb_x=None, Tensor? nb_mean=None, Tensor? nb_rstd=None, "
         "Tensor? nb_gamma=None, Tensor? nb_beta=None, int nb_act=0, int nb_half=0, bool nb_batch=False, "
-        "bool nb_colsum=False) "
+        "bool nb_colsum=False, bool nb_gate=False) "
         "-> Tensor[]");
   m.def("fp8_quant(Tensor x, Tensor(a!) site, int fmt, int use_cur=0) -> Tensor");
   m.def("sn_power_iter(Tensor w, Tensor(a!) u, Tensor(b!) v) -> Tensor");

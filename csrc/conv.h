@@ -86,6 +86,9 @@ struct ConvFwdArgs {
   int nb_colsum;    // 1: plain column sums sum(dz) of the half (the bias gradient of the conv
                     // that produced it), no norm input read: nb_ws[0] only, nb_x / stats unused
   int epi_serial;   // A/B knob (P2P_EPI_SERIAL=1): gate / skip-gradient dgrads on the plain epilogue, not EXT
+  int nb_gate;      // the act' gate of the nb half reads the norm's output, which IS xhat (non-affine,
+                    // no fused act): compute the gate from the xhat the partials already form,
+                    // instead of loading that output again (one operand stream fewer)
 };
 
 // Weight gradient: C[R][Kq] = sum_m P[m][R] * im2col(Q)[m][Kq], written to per-split

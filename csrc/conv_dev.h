@@ -92,7 +92,6 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
   const int ld_t = first_t ? a.Csplit : a.Cout - a.Csplit;
   const int cof_t = first_t ? co_t : co_t - a.Csplit;
   const bf16* xb_t = static_cast<const bf16*>(first_t ? a.xb1 : a.xb2);
-  const bool gate_t = a.act_bwd && xb_t;   // a null half is gated by its producer's backward
   const bool res_t = a.res1 && first_t;    // host: res1 only with Csplit == Cout
   bf16* y_t = static_cast<bf16*>(first_t ? a.y1 : a.y2);
   const bf16* res_p = static_cast<const bf16*>(a.res1);
@@ -101,6 +100,11 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
   const bool nb_on = a.nb_ws != nullptr && nb_co >= 0 && nb_co < a.nb_C;
   const bool nb_x_on = nb_on && !a.nb_colsum;   // colsum mode: d = dz, xhat = 0 (rs = c1 = 0)
   const float nb_slope = (a.nb_act && !a.nb_colsum) ? neg_slope(a.nb_act) : 1.f;
+  // act' gate (a null half is gated by its producer's backward): from the xhat of the nb
+  // partials when the gated input is the norm's output itself (nb_gate), else loaded
+  const bool gate_nb = a.act_bwd && xb_t && nb_x_on && a.nb_gate;
+  const bool gate_t = a.act_bwd && xb_t && !gate_nb;
+  const float gate_slope = gate_nb ? neg_slope(a.act_bwd) : 0.f;
   // xhat = x * rs + c1 (c1 = -mean * rstd)
   float rs[8], c1[8], s1[8], s2[8];
 #pragma unroll
@@ -134,6 +138,16 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
           vb[q] = (bf16)((float)vb[q] * act_grad_from_input((float)xb8[q], a.act_bwd));
         v = __builtin_bit_cast(u32x4, vb);
       }
+    }
+    if (gate_nb) {
+      bf16x8 vb = __builtin_bit_cast(bf16x8, v);
+      const bf16x8 xn = __builtin_bit_cast(bf16x8, nv);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float xh = (float)xn[q] * rs[q] + c1[q];
+        vb[q] = (bf16)((float)vb[q] * (xh > 0.f ? 1.f : gate_slope));
+      }
+      v = __builtin_bit_cast(u32x4, vb);
     }
     if (res_t) {
       bf16x8 vb = __builtin_bit_cast(bf16x8, v);

@@ -5,8 +5,10 @@ Recipe (MI355X-first, see ``csrc/fp8.hip``):
 * conv forward:  x in OCP e4m3 x weight e4m3 -> bf16 output (bias / act / norm stats fused
   as on the bf16 path);
 * conv dgrad:    dY in e5m2 (gradient range) x weight e4m3 -> bf16 dX;
-* conv wgrad:    stays bf16 (it reads the saved bf16 activations, so no fp8 copy has to
-  live until backward);
+* conv wgrad:    dY e5m2 x X e4m3 on the same scaled MFMA, both operands read k-transposed
+  with ds_read_b64_tr_b8 (csrc/conv_wgrad.hip ``conv_wgrad_f8_kernel``), from the fp8 copies
+  the forward and the dgrad of that conv already made (the per-step quantisation cache keeps
+  them until the backward); ``P2P_FP8_WGRAD=0`` keeps it bf16;
 * first / last layers stay bf16: their channel counts (3 / 6-channel images, 1-channel
   PatchGAN logits) are below the fp8 kernel's 32-channel granularity, which is also the
   usual "keep the image-facing layers in high precision" rule for GANs.

@@ -229,8 +229,11 @@ def _nb_kwargs(nb):
     if info is _CS:
         return dict(nb_half=half, nb_colsum=True)
     nx, nmean, nrstd, ng, nbeta, nact, nbatch = info
+    # the half's act' gate input is the norm's output registered for it (ctx.nb comes from
+    # _norm_lookup of that very input): with no fused act and no affine it IS xhat, so the
+    # epilogue gates from the xhat it already forms instead of re-reading the output
     return dict(nb_x=nx, nb_mean=nmean, nb_rstd=nrstd, nb_gamma=ng, nb_beta=nbeta, nb_act=nact,
-                nb_half=half, nb_batch=nbatch)
+                nb_half=half, nb_batch=nbatch, nb_gate=(ng is None and not nact))
 
 
 def prepare_weights(*modules):
@@ -558,7 +561,7 @@ def _wgrad_fp8(cfg, weight, q1, q2, gyp, act_in, gw) -> bool:
     reading the fp8 copies the forward / dgrad of this conv already made (``_f8.quant`` caches
     them per step under the same site keys) -- the image-facing layers stay bf16.  Returns
     False when the geometry is not the fp8 kernel's (the caller runs the bf16 wgrad)."""
-    if not _f8.enabled() or os.environ.get("P2P_FP8_WGRAD", "0") == "0":
+    if not _f8.enabled() or os.environ.get("P2P_FP8_WGRAD", "1") == "0":
         return False
     if cfg.reflect or cfg.up != 1 or act_in not in (0, 1):
         return False

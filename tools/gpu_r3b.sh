@@ -6,6 +6,8 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r3b
 mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_nb_fuse_gpu.py tests/test_pix2pix_step_gpu.py tests/test_production_shapes_gpu.py -x -q --timeout 240 --timeout-method thread > $O/nb.log 2>&1 || exit $?
+echo "nb/step tests: $(tail -1 $O/nb.log)"
 timeout -k 10 600 python -u -m pytest tests/test_fp8_gpu.py -x -q --timeout 240 --timeout-method thread > $O/fp8.log 2>&1; rc=$?
 echo "fp8 tests rc=$rc: $(tail -1 $O/fp8.log)"
 grep -E "FAILED|Error|assert" $O/fp8.log | head -20
