@@ -376,6 +376,15 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       splits = (int)((ktiles + kps - 1) / kps);
     }
   }
+  // stride-2 4x4 transposed convs onto 32x32 / 64x64 grids (U-Net decoder ConvT, every 4x4
+  // s2 conv's input gradient): the class-shared halo kernel (csrc/conv_s2t.hip).  Its tiles
+  // are BM = 128 rows of one class, which fixes the stats / partial chunk layout below.
+  const bool s2t_ok = mode == 1 && !fp8 && splits == 1 && KH == 4 && KW == 4 && stride == 2 && pad == 1 &&
+                      !reflect && up == 1 && OH == 2 * H && OW == 2 * W && (W == 32 || W == 64) &&
+                      (H * W) % 128 == 0 && Cout % 64 == 0 && C1 % 64 == 0 && C2 % 64 == 0 &&
+                      (act_in == 0 || (act_in == 1 && act_bwd == 0 && !res)) &&
+                      std::getenv("P2P_NO_S2T") == nullptr;
+  if (s2t_ok) bm = 128;
   Tensor ws;
   if (splits > 1) {
     // per-split fp32 slabs (plain stores, no zero fill) summed in split order by
@@ -390,7 +399,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   }
   // fused norm statistics: only on the glds path with whole tiles inside one image/class
   Tensor stats;
-  if (want_stats && glds_ok && splits == 1 && Csplit == Cout && act_out == 0 && !act_bwd) {
+  if (want_stats && (glds_ok || s2t_ok) && splits == 1 && Csplit == Cout && act_out == 0 && !act_bwd) {
     bool ok = true;
     int64_t hwq = OH * OW;
     if (mode == 1) {
@@ -412,7 +421,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   // the packed-image halo kernel (below) beats the generic tile with fused partials: keep it
   const bool pk8_halo = mode == 0 && !fp8 && C1 == 8 && C2 == 0 && KH == 4 && KW == 4 && stride == 2 && pad == 1 &&
                         (Cout == 64 || Cout == 128) && std::getenv("P2P_NO_HALO") == nullptr;
-  if ((nb_x || nb_colsum) && nb_half && !nb_gamma && glds_ok && splits == 1 && fp8 != 1 && !want_stats &&
+  if ((nb_x || nb_colsum) && nb_half && !nb_gamma && (glds_ok || s2t_ok) && splits == 1 && fp8 != 1 && !want_stats &&
       !pk8_halo) {
     const int64_t c0 = nb_half == 1 ? 0 : Csplit;
     const int64_t nC = nb_half == 1 ? Csplit : Cout - Csplit;
@@ -533,6 +542,10 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       rc = p2p_halo_kxk(&h, (int)KH, std::max(1, std::min(h.ntiles, cus)), st);
       if (rc == 0) splits = 1;   // no split-K partials to finalize: the halo kernel wrote y
     }
+  }
+  if (rc == -2 && s2t_ok) {
+    rc = p2p_conv_s2t(&a, st);
+    TORCH_CHECK(rc != -2, "conv_fwd: the s2t kernel refused a geometry the host accepted");
   }
   if (rc == -2 && glds_ok) rc = p2p_conv_fwd_glds(&a, (int)mode, variant, st);
   if (rc == -2 && a.stats) {  // glds refused after all: no fused statistics

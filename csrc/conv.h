@@ -202,6 +202,9 @@ int p2p_conv_finalize(const p2p::ConvFwdArgs* a, hipStream_t stream);
 // global_load_lds pipelined variant (FAST layers, BN in {64, 128}); returns -2 if the
 // configuration is not supported so the caller can fall back to p2p_conv_fwd.
 int p2p_conv_fwd_glds(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t stream);
+// stride-2 4x4 pad-1 transposed convs (MODE 1) onto 32x32 / 64x64 grids on the class-shared
+// halo kernel (conv_s2t.hip); -2 = geometry not covered
+int p2p_conv_s2t(const p2p::ConvFwdArgs* a, hipStream_t stream);
 int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t stream);
 int p2p_fp8_quant(const void* x, long n, int* site, int use_cur, int fmt, void* q, hipStream_t st);
 int p2p_fp8_amax(const void* x, int is_f32, long n, int* site, int slot, hipStream_t st);

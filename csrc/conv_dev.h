@@ -230,23 +230,51 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
   }
 }
 
-// bias + output activation in registers, the bf16 tile staged through LDS, 16-B stores
-// with the optional act'(x) multiply (dgrad) and the concat channel split; split-K tiles
-// accumulate fp32 atomics instead.
-// EXT (dgrad kernels with an act' gate, a parked skip gradient or fused norm-backward partials):
-// the store loop prefetches those operands two rows at a time and accumulates the partials.  A
-// separate instantiation: its registers would halve the occupancy of the plain store loop.
-template <int BM, int BN, int WM, int WN, int MODE, int NT, bool EXT = false>
-__device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassGeom& g,
-                                              f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
-                                              int n0, char* smem, const FastDiv& fd_hwq,
-                                              const FastDiv& fd_wq) {
-  constexpr int TM = BM / WM / 16;
-  constexpr int TN = BN / WN / 16;
+// bias + output activation in registers -> the bf16 tile in LDS (row stride LDC): one wave's
+// TM x TN fragment block at (row0, col0) of the tile.  The activation is dispatched ONCE per
+// tile (compile-time body per code), not by a wave-uniform branch per accumulator element.
+template <int TM, int TN, int LDC>
+__device__ __forceinline__ void conv_stage_tile(const ConvFwdArgs& a, f32x4 (&acc)[TM][TN], bf16* Cs, int row0,
+                                                int col0, int n0, int lane) {
+  const float al = a.alpha ? a.alpha[0] : 1.f;
+  auto stage = [&](auto act_tag) __attribute__((always_inline)) {
+    constexpr int ACT = decltype(act_tag)::value;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int coll = col0 + j * 16 + (lane & 15);
+      const int col = n0 + coll;
+      const float bj = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int rowb = row0 + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(rowb + r) * LDC + coll] = (bf16)act_fwd(acc[i][j][r] * al + bj, ACT);
+      }
+    }
+  };
+  switch (a.act_out) {
+    case ACT_RELU: stage(std::integral_constant<int, ACT_RELU>{}); break;
+    case ACT_LRELU: stage(std::integral_constant<int, ACT_LRELU>{}); break;
+    case ACT_TANH: stage(std::integral_constant<int, ACT_TANH>{}); break;
+    case ACT_SIGMOID: stage(std::integral_constant<int, ACT_SIGMOID>{}); break;
+    default: stage(std::integral_constant<int, ACT_NONE>{}); break;
+  }
+}
+
+// Everything after the staged bf16 tile (Cs, row stride BN + 8, visible to all NT threads):
+// depth-to-space / statistics / the store loop with the act' gate, concat split, skip
+// gradient, fp8 shadow (or the EXT loop with fused norm-backward partials).  red_stats:
+// 2 * NT floats of scratch (d2s / stats); red_nb: NT * 16 floats that may alias Cs (EXT
+// reuses it after a barrier).
+template <int BM, int BN, int MODE, int NT, bool EXT = false>
+__device__ __forceinline__ void conv_epilogue_tail(const ConvFwdArgs& a, const ClassGeom& g, int m0, int n0,
+                                                   const bf16* Cs, float* red_stats, char* red_nb,
+                                                   const FastDiv& fd_hwq, const FastDiv& fd_wq) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid % WN;
   const int HWq = g.Hq * g.Wq;
   const int s = a.stride;
+  constexpr int LDC = BN + 8;
   auto out_pix = [&](int m) __attribute__((always_inline)) -> long {
     if (MODE == 0) return m;
     const int n = (int)fdiv((uint32_t)m, fd_hwq);
@@ -255,61 +283,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
     const int qx = r - qy * g.Wq;
     return ((long)n * a.OH + qy * s + g.ry) * a.OW + qx * s + g.rx;
   };
-
-  // ---- split-K: fp32 atomics straight from the accumulators (tiny-M layers only).  Not
-  // compiled into the big tiles (the host never splits them): its out_pix division loop
-  // is not unrolled there, which made the compiler keep the accumulators in scratch.
-  if constexpr (TM * TN <= 16) if (a.splits > 1) {
-    float* wsb = a.det ? a.ws + (long)(blockIdx.z % a.splits) * a.N * a.OH * a.OW * a.Cout : a.ws;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wn * TN * 16 + j * 16 + (lane & 15);
-        const int rowb = m0 + wm * TM * 16 + i * 16 + (lane >> 4) * 4;
-        if (col >= a.Cout) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = rowb + r;
-          if (m < g.Mc) {
-            if (a.det) wsb[out_pix(m) * a.Cout + col] = acc[i][j][r];
-            else atomicAdd(a.ws + out_pix(m) * a.Cout + col, acc[i][j][r]);
-          }
-        }
-      }
-    return;
-  }
-
-  // ---- epilogue: bias + act in registers, bf16 tile staged in LDS, 16-B stores
-  bf16* Cs = reinterpret_cast<bf16*>(smem);
-  constexpr int LDC = BN + 8;
-  // the activation is dispatched ONCE per tile (compile-time body per code), not by a
-  // wave-uniform branch per accumulator element
-  const float al = a.alpha ? a.alpha[0] : 1.f;
-  auto stage_tile = [&](auto act_tag) __attribute__((always_inline)) {
-    constexpr int ACT = decltype(act_tag)::value;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int coll = wn * TN * 16 + j * 16 + (lane & 15);
-      const int col = n0 + coll;
-      const float bj = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int rowb = wm * TM * 16 + i * 16 + (lane >> 4) * 4;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Cs[(rowb + r) * LDC + coll] = (bf16)act_fwd(acc[i][j][r] * al + bj, ACT);
-      }
-    }
-  };
-  switch (a.act_out) {
-    case ACT_RELU: stage_tile(std::integral_constant<int, ACT_RELU>{}); break;
-    case ACT_LRELU: stage_tile(std::integral_constant<int, ACT_LRELU>{}); break;
-    case ACT_TANH: stage_tile(std::integral_constant<int, ACT_TANH>{}); break;
-    case ACT_SIGMOID: stage_tile(std::integral_constant<int, ACT_SIGMOID>{}); break;
-    default: stage_tile(std::integral_constant<int, ACT_NONE>{}); break;
-  }
-  __syncthreads();
 
   if (a.d2s) {  // depth-to-space packed image (d1 forward / its head gradient)
     const int Ho = 2 * a.OH, Wo = 2 * a.OW;
@@ -328,7 +301,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
                       static_cast<const bf16*>(a.pk_f), d2s_sc, static_cast<bf16*>(a.y1));
     }
     if (a.d2s == 1 && a.l1_part) {
-      float* red = reinterpret_cast<float*>(smem + BM * LDC * 2);
+      float* red = red_stats;
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) l1 += __shfl_xor(l1, off);
       if (lane == 0) red[wid] = l1;
@@ -347,7 +320,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
     // (no E[x^2] - E[x]^2 cancellation); NT / BN threads per column, combined in LDS
     constexpr int TPC = NT / BN;
     static_assert(NT % BN == 0 && BM % TPC == 0, "stats partition");
-    float* red = reinterpret_cast<float*>(smem + BM * LDC * 2);
+    float* red = red_stats;
     const int col = tid % BN, part = tid / BN;
     const float piv = (float)Cs[col];
     float s1 = 0.f, s2 = 0.f;
@@ -435,8 +408,67 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassG
   }
   if (qsh.q) fp8_amax_commit(qmax, qsh.site);
   } else {
-    conv_epilogue_ext<BM, BN, MODE, NT>(a, g, m0, n0, smem, Cs, LDC, HWq, s, out_pix);
+    conv_epilogue_ext<BM, BN, MODE, NT>(a, g, m0, n0, red_nb, Cs, LDC, HWq, s, out_pix);
   }
+}
+
+// bias + output activation in registers, the bf16 tile staged through LDS, 16-B stores
+// with the optional act'(x) multiply (dgrad) and the concat channel split; split-K tiles
+// accumulate fp32 atomics instead.
+// EXT (dgrad kernels with an act' gate, a parked skip gradient or fused norm-backward partials):
+// the store loop prefetches those operands two rows at a time and accumulates the partials.  A
+// separate instantiation: its registers would halve the occupancy of the plain store loop.
+template <int BM, int BN, int WM, int WN, int MODE, int NT, bool EXT = false>
+__device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, const ClassGeom& g,
+                                              f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
+                                              int n0, char* smem, const FastDiv& fd_hwq,
+                                              const FastDiv& fd_wq) {
+  constexpr int TM = BM / WM / 16;
+  constexpr int TN = BN / WN / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int HWq = g.Hq * g.Wq;
+  const int s = a.stride;
+  auto out_pix = [&](int m) __attribute__((always_inline)) -> long {
+    if (MODE == 0) return m;
+    const int n = (int)fdiv((uint32_t)m, fd_hwq);
+    const int r = m - n * HWq;
+    const int qy = (int)fdiv((uint32_t)r, fd_wq);
+    const int qx = r - qy * g.Wq;
+    return ((long)n * a.OH + qy * s + g.ry) * a.OW + qx * s + g.rx;
+  };
+
+  // ---- split-K: fp32 atomics straight from the accumulators (tiny-M layers only).  Not
+  // compiled into the big tiles (the host never splits them): its out_pix division loop
+  // is not unrolled there, which made the compiler keep the accumulators in scratch.
+  if constexpr (TM * TN <= 16) if (a.splits > 1) {
+    float* wsb = a.det ? a.ws + (long)(blockIdx.z % a.splits) * a.N * a.OH * a.OW * a.Cout : a.ws;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * TN * 16 + j * 16 + (lane & 15);
+        const int rowb = m0 + wm * TM * 16 + i * 16 + (lane >> 4) * 4;
+        if (col >= a.Cout) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = rowb + r;
+          if (m < g.Mc) {
+            if (a.det) wsb[out_pix(m) * a.Cout + col] = acc[i][j][r];
+            else atomicAdd(a.ws + out_pix(m) * a.Cout + col, acc[i][j][r]);
+          }
+        }
+      }
+    return;
+  }
+
+  // ---- epilogue: bias + act in registers, bf16 tile staged in LDS, 16-B stores
+  bf16* Cs = reinterpret_cast<bf16*>(smem);
+  constexpr int LDC = BN + 8;
+  conv_stage_tile<TM, TN, LDC>(a, acc, Cs, wm * TM * 16, wn * TN * 16, n0, lane);
+  __syncthreads();
+  conv_epilogue_tail<BM, BN, MODE, NT, EXT>(a, g, m0, n0, Cs, reinterpret_cast<float*>(smem + BM * LDC * 2), smem,
+                                            fd_hwq, fd_wq);
 }
 
 }  // namespace p2p

@@ -1,0 +1,238 @@
+// Stride-2 transposed conv (4x4, pad 1, OH = 2H) -- the U-Net decoder's ConvTranspose2d and
+// the input gradient of every 4x4 stride-2 conv -- on a halo tile shared by the 4 parity
+// classes (VERDICT r2 #1a).
+//
+// The implicit GEMM (conv_fwd_glds.hip MODE 1) runs one GEMM per output parity class: every
+// class tile gathers its own im2col rows, so each input pixel is staged from L2 into LDS
+// 16 times (4 classes x 4 taps) for a 64-column output -- these layers ran at 390-540 TF/s,
+// bound by the L2 -> LDS staging rate (profiles/kernel_experiments_r3.md).  Here a block
+// owns BM = 128 consecutive grid positions q (RH = 128 / W whole rows of the input grid,
+// one image) and 64 output channels of ALL four classes: per 64-channel chunk it stages
+// the (RH + 2) x (W + 2) input halo ONCE (global_load_lds, source-side swizzle, 2-stage
+// ring), and wave c (= class (ry, rx)) reads the A fragments of its 2 x 2 taps out of that
+// one LDS image at shifted pixel offsets.  A waves's B fragments (its class's 4 taps x 64
+// channels, the weights are L2-resident) go global -> VGPR one k-step ahead.  Per wave and
+// chunk: 64 ds_read_b128 + 32 global loads for 256 MFMAs (0.25 LDS reads per MFMA).
+//
+// Tap geometry (conv_dev.h class_geom, s = 2, p = 1): class (ry, rx) reads input row
+// qy + dy - ty with kernel row ky = ky0 + 2 ty, ty in {0, 1}; ky0 = (ry + 1) % 2,
+// dy = (ry + 1 - ky0) / 2 (columns alike).  Halo pixel (hy, hx) = input (qy0 - 1 + hy, hx - 1).
+//
+// Epilogue: each wave stages its class's 128 x 64 bf16 tile into its own LDS region; then
+// the whole block runs the shared GEMM epilogue tail (conv_dev.h) class by class -- bias,
+// activation, statistics for a following norm, act' gate / skip gradient / norm-backward
+// partials of a dgrad, fp8 shadow -- with exactly the per-class BM = 128 tile conventions
+// of the implicit GEMM (stats / partial chunk index), so the host's buffers are the same.
+#include "conv_dev.h"
+
+namespace p2p {
+
+namespace {
+
+__device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(lds_wave_base), 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+constexpr int BM = 128, BN = 64, NT = 256;
+constexpr int TM = BM / 16, TN = BN / 16;   // one wave = one class: 8 x 4 fragments
+constexpr int LDC = BN + 8;
+
+template <int W>
+struct S2TGeom {
+  static constexpr int RH = BM / W;                 // grid rows per tile
+  static constexpr int HW = W + 2, HH = RH + 2;     // halo edge
+  static constexpr int HPIX = HH * HW;
+  static constexpr int UNITS = HPIX * 8;            // 16-B units per 64-channel chunk
+  static constexpr int HLD = (UNITS + NT - 1) / NT; // glds per lane per stage
+  static constexpr int STAGE_BYTES = HLD * NT * 16;
+  static constexpr int EPI_BYTES = 4 * BM * LDC * 2 + 2 * NT * 4;
+  static constexpr int SMEM = 2 * STAGE_BYTES > EPI_BYTES ? 2 * STAGE_BYTES : EPI_BYTES;
+};
+
+}  // namespace
+
+template <int W, bool RELU, bool EXT>
+__global__ void __launch_bounds__(256, 2) conv_s2t_kernel(ConvFwdArgs a) {
+  using G = S2TGeom<W>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntiles_n = a.Cout / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / ntiles_n, nt = bid - mt * ntiles_n;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int HWq = a.H * a.W;
+  const int img = m0 / HWq;
+  const int qy0 = (m0 - img * HWq) / W;
+  const int C = a.C1 + a.C2;
+  const int nch = C / 64;
+
+  char* ring = smem;
+  // halo chunk ch -> ring stage: unit e = j * NT + tid holds logical 16-B chunk
+  // (e & 7) ^ ((hp >> 1) & 7) of halo pixel hp = e >> 3 (source-side swizzle, conv_dev.h swz);
+  // pixels outside the image (or beyond the halo) read the zero page.  Recomputed per issue
+  // (a few VALU per unit, 2-4 issues per block) instead of holding 2 x HLD registers.
+  auto issue = [&](int ch, int stage) {
+    const bool s1 = ch * 64 < a.C1;
+    const bf16* src = static_cast<const bf16*>(s1 ? a.x1 : a.x2);
+    const int cs = s1 ? a.C1 : a.C2;
+    const int coff = s1 ? ch * 64 : ch * 64 - a.C1;
+    char* dst = ring + stage * G::STAGE_BYTES;
+#pragma unroll
+    for (int j = 0; j < G::HLD; ++j) {
+      const int e = j * NT + tid;
+      const int hp = e >> 3;
+      const int hy = hp / G::HW, hx = hp - (hp / G::HW) * G::HW;
+      const int iy = qy0 - 1 + hy, ix = hx - 1;
+      const bool in = hp < G::HPIX && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+      const int kc = (e & 7) ^ ((hp >> 1) & 7);
+      const bf16* g = in ? src + (long)((img * a.H + iy) * a.W + ix) * cs + coff + kc * 8
+                         : static_cast<const bf16*>(a.zero);
+      glds16(g, dst + (j * NT + wid * 64) * 16);
+    }
+  };
+
+  // ---- this wave's class and its tap geometry (wave-uniform: scalar registers)
+  const int cls_w = __builtin_amdgcn_readfirstlane(wid);
+  const int ry = cls_w >> 1, rx = cls_w & 1;
+  const int ky0 = (ry + 1) & 1, kx0 = (rx + 1) & 1;
+  const int dy = (ry + 1 - ky0) >> 1, dx = (rx + 1 - kx0) >> 1;
+  // B fragments by buffer loads: per-lane row offset (output channel n0 + (lane & 15), k block
+  // 8 * (lane >> 4)) in voffset, the (tap, k-step, 16-column block) offset in soffset
+  const int wrow = 16 * C;   // bf16 elements per output channel of the [Cout][4][4][C] image
+  const auto wsrd = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, a.Cout * wrow * 2, 0x00020000);
+  const int bvoff = ((n0 + (lane & 15)) * wrow + 8 * (lane >> 4)) * 2;
+  // A fragment rows: lane row r = lane & 15 of fragment i -> grid position p = 16 i + r
+  //   (ly = p / W, qx = p % W); tap (ty, tx) reads halo pixel (ly + dy - ty + 1, qx + dx - tx + 1)
+  int apix[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int p = 16 * i + (lane & 15);
+    apix[i] = (p / W + dy + 1) * G::HW + (p % W) + dx + 1;
+  }
+  const int kq = lane >> 4;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // B operand of k-step (ch, t, ks): t = ty * 2 + tx, ks = 32-deep half of the chunk
+  auto loadB = [&](int ch, int t, int ks, u32x4 (&b)[TN]) __attribute__((always_inline)) {
+    const int ky = ky0 + 2 * (t >> 1), kx = kx0 + 2 * (t & 1);
+    const int so = ((ky * 4 + kx) * C + ch * 64 + ks * 32) * 2;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      b[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wsrd, bvoff, so + j * 32 * wrow, 0));
+  };
+
+  u32x4 bcur[TN], bnxt[TN];
+  loadB(0, 0, 0, bcur);
+  issue(0, 0);
+  for (int ch = 0; ch < nch; ++ch) {
+    const int stage = ch & 1;
+    if (ch + 1 < nch) {
+      issue(ch + 1, stage ^ 1);
+      wait_vm<G::HLD>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const bf16* A = reinterpret_cast<const bf16*>(ring + stage * G::STAGE_BYTES);
+    // the A addresses are loop-invariant per (tap, k-step, fragment): hoisted out of the chunk
+    // loop they would pin 64 registers (and spill); laundering apix keeps them per step
+#pragma unroll
+    for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(apix[i]));
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      const int t = st >> 1, ks = st & 1;
+      // prefetch the next k-step's B (the next chunk's first after the last)
+      if (st < 7) loadB(ch, (st + 1) >> 1, (st + 1) & 1, bnxt);
+      else if (ch + 1 < nch) loadB(ch + 1, 0, 0, bnxt);
+      const int toff = -(t >> 1) * G::HW - (t & 1);
+      const int kc = ks * 4 + kq;
+      bf16x8 af[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int hp = apix[i] + toff;
+        af[i] = *reinterpret_cast<const bf16x8*>(A + (hp * 8 + (kc ^ ((hp >> 1) & 7))) * 8);
+        if constexpr (RELU) af[i] = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, af[i])));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], __builtin_bit_cast(bf16x8, bcur[j]),
+                                                               acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bcur[j] = bnxt[j];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // every wave done reading this stage before it is re-filled
+  }
+  __syncthreads();
+
+  // ---- epilogue: every wave stages its class tile, then the block stores class by class
+  bf16* Cs0 = reinterpret_cast<bf16*>(smem);
+  conv_stage_tile<TM, TN, LDC>(a, acc, Cs0 + wid * BM * LDC, 0, 0, n0, lane);
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem + 4 * BM * LDC * 2);
+  const FastDiv fd_hwq = make_fastdiv((uint32_t)HWq), fd_wq = make_fastdiv((uint32_t)a.W);
+#pragma unroll 1
+  for (int cls = 0; cls < 4; ++cls) {
+    const ClassGeom g = class_geom<1>(a, cls);
+    bf16* Cs = Cs0 + cls * BM * LDC;
+    conv_epilogue_tail<BM, BN, 1, NT, EXT>(a, g, m0, n0, Cs, red, reinterpret_cast<char*>(Cs), fd_hwq, fd_wq);
+    __syncthreads();
+  }
+}
+
+template <int W, bool RELU, bool EXT>
+static int launch_s2t(const ConvFwdArgs& a, hipStream_t st) {
+  constexpr int smem = S2TGeom<W>::SMEM;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_s2t_kernel<W, RELU, EXT>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  const long mtiles = (long)a.N * a.H * a.W / BM;
+  const long blocks = mtiles * (a.Cout / BN);
+  hipLaunchKernelGGL((conv_s2t_kernel<W, RELU, EXT>), dim3((unsigned)blocks), dim3(NT), smem, st, a);
+  return (int)hipGetLastError();
+}
+
+template <int W>
+static int dispatch_s2t_w(const ConvFwdArgs& a, bool ext, hipStream_t st) {
+  const bool relu = a.act_in == ACT_RELU;
+  if (ext) return relu ? -2 : launch_s2t<W, false, true>(a, st);
+  return relu ? launch_s2t<W, true, false>(a, st) : launch_s2t<W, false, false>(a, st);
+}
+
+}  // namespace p2p
+
+// Geometry gate (the host checks the same before choosing this path, see s2t_ok in
+// bindings.cpp): returns -2 when not covered.
+extern "C" int p2p_conv_s2t(const p2p::ConvFwdArgs* a, hipStream_t st) {
+  using namespace p2p;
+  if (a->fp8 || a->splits != 1 || a->d2s || a->KH != 4 || a->KW != 4 || a->stride != 2 || a->pad != 1 ||
+      a->up != 1 || a->reflect)
+    return -2;
+  if (a->OH != 2 * a->H || a->OW != 2 * a->W || a->Cout % 64 || a->C1 % 64 || a->C2 % 64 || a->C1 + a->C2 < 64)
+    return -2;
+  if ((long)a->H * a->W % 128) return -2;
+  if (a->act_in != ACT_NONE && a->act_in != ACT_RELU) return -2;
+  const bool ext = a->nb_ws || ((a->act_bwd || a->res1) && !a->epi_serial);
+  if (ext && a->act_in) return -2;
+  switch (a->W) {
+    case 32: return dispatch_s2t_w<32>(*a, ext, st);
+    case 64: return dispatch_s2t_w<64>(*a, ext, st);
+    default: return -2;
+  }
+}

@@ -113,6 +113,15 @@ class CompressGANStep:
     def _quant(self, x):
         return _STEQuantize.apply(x, self.bits) if self.train_c else ops.quantize(x, self.bits)
 
+    @staticmethod
+    def _wgrad_overlap(x, reducer):
+        """G's conv weight gradients on the side stream (ops/hip.py ``wgrad_overlap``): grads
+        were just set to None and G runs once in this backward; not with a DP reducer."""
+        if x.is_cuda and _native.get_backend() == "native":
+            from ..ops import hip
+            return hip.wgrad_overlap(x.device, enabled=reducer is None)
+        return contextlib.nullcontext()
+
     def _zero(self, opt, reducer):
         if reducer is not None:
             reducer.zero_grad()
@@ -156,7 +165,8 @@ class CompressGANStep:
         # ---- updates: G first (its backward also reaches D; those grads are dropped)
         with self._phase("G_bwd_opt"):
             self._zero(self.opt_g, self.reducer_g)
-            loss_g.backward()
+            with self._wgrad_overlap(real_a, self.reducer_g):
+                loss_g.backward()
             if self.reducer_g is not None:
                 self.reducer_g.finish()
             self._opt_step(self.opt_g, self.reducer_g, loss_g)

@@ -153,7 +153,8 @@ class Pix2PixStep:
             loss_D = (loss_D_fake + loss_D_real) * 0.5
         with self._phase("D_bwd_opt"):
             self._zero(self.opt_D, self.reducer_d)
-            loss_D.backward()
+            with hip.wgrad_overlap(real_A.device, enabled=self.reducer_d is None):
+                loss_D.backward()
             if self.reducer_d is not None:
                 self.reducer_d.finish()
             self._guarded_step(self.opt_D, self.reducer_d, loss_D)
@@ -167,7 +168,8 @@ class Pix2PixStep:
             loss_G = loss_G_GAN + hip.head_l1_tap(loss_G_L1)
         with self._phase("G_bwd_opt"):
             self._zero(self.opt_G, self.reducer_g)
-            loss_G.backward()
+            with hip.wgrad_overlap(real_A.device, enabled=self.reducer_g is None):
+                loss_G.backward()
             hip.assert_no_deferred()          # every parked U-Net skip gradient consumed
             if self.reducer_g is not None:
                 self.reducer_g.finish()

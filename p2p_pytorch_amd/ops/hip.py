@@ -24,6 +24,7 @@ see ``ops/reference.py`` for the fp32 oracle each kernel is tested against.
 """
 from __future__ import annotations
 
+import contextlib
 import itertools
 import os
 
@@ -36,6 +37,7 @@ ACT = {None: 0, "none": 0, "relu": 1, "lrelu": 2, "tanh": 3, "sigmoid": 4}
 # P2P_NB_FUSE=0: norm backward runs its own partial pass (A/B knob for the dgrad-epilogue fusion)
 _NB_FUSE = os.environ.get("P2P_NB_FUSE", "1") != "0"
 CL = torch.channels_last
+_NULLCTX = contextlib.nullcontext()
 
 _gen = [0]
 _seeds: dict = {}
@@ -130,6 +132,73 @@ def _take_nbp(g):
 def _take_colsum(gy):
     ent = _colsum_stash.pop((gy.data_ptr(), tuple(gy.shape)), None)
     return None if ent is None else ent[1]
+
+
+# ------------------------------------------------------------ weight-gradient side stream
+# A conv's weight gradient feeds nothing else in its backward: only the optimizer (and the
+# DP reducer) read it.  Inside ``wgrad_overlap`` every ConvFn weight gradient is launched on a
+# per-device side HIP stream (forked from the compute stream at that point), so the wgrad
+# GEMMs -- a quarter of the headline step -- run beside the dgrad / norm-backward chain that
+# the next layers wait on (LDS/MFMA-bound wgrads next to HBM-bound norm passes and the
+# small-grid deep U-Net levels).  The context's exit joins the side stream back (stream
+# order, no host sync; a hipGraph capture records the fork/join).  Tensors the side stream
+# reads are held until that join, so the allocator cannot recycle them under it (no
+# ``record_stream``: its deferred events under capture crashed a later capture).  Autograd
+# then hands each gradient to AccumulateGrad, which only STEALS it (grads set to None, one
+# gradient per weight); a weight that receives a second gradient in the same backward has
+# its earlier one joined first (autograd's add then runs on the compute stream).  Only used
+# without a DP reducer (its post-accumulate hooks copy the gradient on the compute stream).
+class _WgradSide:
+    on = False
+    streams: dict = {}
+    seen: set = set()
+    keep: list = []     # operands the side stream reads, held until the join
+
+
+def wgrad_overlap_enabled() -> bool:
+    return os.environ.get("P2P_WGRAD_STREAM", "1") != "0"
+
+
+class wgrad_overlap:
+    """``with wgrad_overlap(device): loss.backward()`` -- see the block comment above."""
+
+    def __init__(self, device, enabled=True):
+        self.dev = torch.device(device)
+        self.enabled = bool(enabled) and self.dev.type == "cuda" and wgrad_overlap_enabled()
+
+    def __enter__(self):
+        if self.enabled:
+            idx = self.dev.index if self.dev.index is not None else torch.cuda.current_device()
+            s = _WgradSide.streams.get(idx)
+            if s is None:
+                s = _WgradSide.streams[idx] = torch.cuda.Stream(device=idx)
+            self.stream = s
+            self.prev = _WgradSide.on
+            _WgradSide.on = s
+            _WgradSide.seen.clear()
+        return self
+
+    def __exit__(self, *exc):
+        if self.enabled:
+            _WgradSide.on = self.prev
+            _WgradSide.seen.clear()
+            torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+            _WgradSide.keep.clear()   # freed after the join: stream-ordered behind the side work
+        return False
+
+
+def _wgrad_side(weight):
+    """The side stream for this weight's gradient (None: compute stream)."""
+    s = _WgradSide.on
+    if not s:
+        return None
+    if weight.data_ptr() in _WgradSide.seen:
+        # second gradient of this weight: autograd will add it to the first on the compute
+        # stream, so the first must be complete before it
+        torch.cuda.current_stream(s.device).wait_stream(s)
+        return None
+    _WgradSide.seen.add(weight.data_ptr())
+    return s
 
 
 def _pad8(c: int) -> int:
@@ -472,13 +541,15 @@ class ConvFn(torch.autograd.Function):
             if ctx.needs_input_grad[2] or (ctx.has_bias and ctx.needs_input_grad[3]):
                 _, _, gw, gb = _conv_backward(ctx.cfg, ctx.geo, q1, q2, weight, y, gy, False, False,
                                               ctx.needs_input_grad[2],
-                                              ctx.has_bias and ctx.needs_input_grad[3])
+                                              ctx.has_bias and ctx.needs_input_grad[3],
+                                              side_ok=True)
                 return gx1, None, gw, gb, None
             return gx1, None, None, None, None
         gx1, gx2, gw, gb = _conv_backward(ctx.cfg, ctx.geo, q1, q2, weight, y, gy, need_x1,
                                           ctx.has_x2 and ctx.needs_input_grad[1],
                                           ctx.needs_input_grad[2],
-                                          ctx.has_bias and ctx.needs_input_grad[3], nb=ctx.nb)
+                                          ctx.has_bias and ctx.needs_input_grad[3], nb=ctx.nb,
+                                          side_ok=True)
         return gx1, gx2, gw, gb, None
 
 
@@ -556,21 +627,23 @@ def _nb_half(cfg, q2, nb, res_fused):
     return None
 
 
-def _wgrad_fp8(cfg, weight, q1, q2, gyp, act_in, gw) -> bool:
+def _wgrad_fp8(cfg, weight, q1, q2, gyp, act_in):
     """fp8 weight gradient (BASELINE config 5): dY e5m2 x X e4m3 on the scaled f8f6f4 MFMA,
     reading the fp8 copies the forward / dgrad of this conv already made (``_f8.quant`` caches
     them per step under the same site keys) -- the image-facing layers stay bf16.  Returns
-    False when the geometry is not the fp8 kernel's (the caller runs the bf16 wgrad)."""
+    None when the geometry is not the fp8 kernel's (the caller runs the bf16 wgrad), else
+    (launch(gw) -> bool, operand tensors): the quantisation runs here, on the compute stream,
+    the launch wherever the caller puts it (launch False: the caller runs the bf16 wgrad)."""
     if not _f8.enabled() or os.environ.get("P2P_FP8_WGRAD", "1") == "0":
-        return False
+        return None
     if cfg.reflect or cfg.up != 1 or act_in not in (0, 1):
-        return False
+        return None
     C1 = q1.shape[1]
     C2 = 0 if q2 is None else q2.shape[1]
     Cout = gyp.shape[1]
     if not (_f8.conv_ok(C1, C2, Cout, act_in) and C1 % 16 == 0 and C2 % 16 == 0 and Cout % 128 == 0
             and (C1 + C2) % 128 == 0 and C1 + C2 >= 128):
-        return False
+        return None
     k = id(weight)
     x1q, sx = _f8.quant(q1, (k, "x", 1), _f8.E4M3)
     x2q = sx2 = None
@@ -578,20 +651,24 @@ def _wgrad_fp8(cfg, weight, q1, q2, gyp, act_in, gw) -> bool:
         x2q, sx2 = _f8.quant(q2, (k, "x", 2), _f8.E4M3)
     gq, sg = _f8.quant(gyp, (k, "gy", 1), _f8.E5M2)
     KH, KW, s, p = cfg.KH, cfg.KW, cfg.stride, cfg.pad
-    if cfg.transposed:
-        return bool(P().conv_wgrad(x1q, x2q, act_in, gq, None, 0, KH, KW, s, p, 0, 1, gw, 1.0, 0, 0,
-                                   sx, sg, _f8.E4M3, _f8.E5M2, sx2, None))
-    return bool(P().conv_wgrad(gq, None, 0, x1q, x2q, act_in, KH, KW, s, p, 0, 1, gw, 1.0, 0, 0,
-                               sg, sx, _f8.E5M2, _f8.E4M3, None, sx2))
+
+    def launch(gw):
+        if cfg.transposed:
+            return bool(P().conv_wgrad(x1q, x2q, act_in, gq, None, 0, KH, KW, s, p, 0, 1, gw, 1.0, 0,
+                                       0, sx, sg, _f8.E4M3, _f8.E5M2, sx2, None))
+        return bool(P().conv_wgrad(gq, None, 0, x1q, x2q, act_in, KH, KW, s, p, 0, 1, gw, 1.0, 0, 0,
+                                   sg, sx, _f8.E5M2, _f8.E4M3, None, sx2))
+    return launch, (x1q, x2q, gq, sx, sx2, sg)
 
 
 def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, need_b, alpha=None,
-                   nb=None):
+                   nb=None, side_ok=False):
     """Input / weight / bias gradients of one fused conv (ConvFn's backward, shared with the
     image head): dgrad with the input-activation gate, concat split and skip-gradient
     hand-off in its epilogue; wgrad; bias = column sums (or the norm's exact zero).
     ``nb``: (x1, x2) norm-output infos (``_norm_lookup``) -- the dgrad epilogue emits the
-    norm-backward partials of a half that is a norm's output."""
+    norm-backward partials of a half that is a norm's output.  ``side_ok``: the weight gradient
+    is returned to autograd as is (not consumed here), so it may run on the wgrad side stream."""
     nbh = None
     nbp = None
     C1, C2, Cp, packed, Cout, Coutp, H, W = geo
@@ -675,20 +752,26 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
     if need_w:
         gw = torch.empty_like(weight, dtype=torch.float32, memory_format=torch.contiguous_format)
         act_in = _act_code(cfg.act_in)
-        if _wgrad_fp8(cfg, weight, q1, q2, gyp, act_in, gw):
-            pass
-        elif cfg.transposed:
-            P().conv_wgrad(q1, q2, act_in, gyp, None, 0, KH, KW, s, p, 0, 1, gw, 1.0, 0)
-        elif (s == 1 and Coutp <= 16 and Cp >= 128 and KH == KW and not cfg.reflect
-              and cfg.up == 1):
-            # tiny-Cout stride-1 conv (PatchGAN logits): the GEMM's R = Cout would waste
-            # the MFMA tile, so compute it in transposed-conv form -- rows = input
-            # channels, the dY gather with pad K-1-p, taps flipped by the reduce
-            P().conv_wgrad(q1, q2, act_in, gyp, None, 0, KH, KW, 1, KH - 1 - p, 0, 1, gw,
-                           1.0, 0, 1)
-        else:
-            P().conv_wgrad(gyp, None, 0, q1, q2, act_in, KH, KW, s, p, int(cfg.reflect),
-                           cfg.up, gw, 1.0, 0)
+        f8 = _wgrad_fp8(cfg, weight, q1, q2, gyp, act_in)
+        side = _wgrad_side(weight) if side_ok else None
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(side.device))
+            _WgradSide.keep.append((q1, q2, gyp, f8))
+        with (torch.cuda.stream(side) if side is not None else _NULLCTX):
+            if f8 is not None and f8[0](gw):
+                pass
+            elif cfg.transposed:
+                P().conv_wgrad(q1, q2, act_in, gyp, None, 0, KH, KW, s, p, 0, 1, gw, 1.0, 0)
+            elif (s == 1 and Coutp <= 16 and Cp >= 128 and KH == KW and not cfg.reflect
+                  and cfg.up == 1):
+                # tiny-Cout stride-1 conv (PatchGAN logits): the GEMM's R = Cout would waste
+                # the MFMA tile, so compute it in transposed-conv form -- rows = input
+                # channels, the dY gather with pad K-1-p, taps flipped by the reduce
+                P().conv_wgrad(q1, q2, act_in, gyp, None, 0, KH, KW, 1, KH - 1 - p, 0, 1, gw,
+                               1.0, 0, 1)
+            else:
+                P().conv_wgrad(gyp, None, 0, q1, q2, act_in, KH, KW, s, p, int(cfg.reflect),
+                               cfg.up, gw, 1.0, 0)
     if need_b:
         gb = _take_colsum(gy) if (cfg.act_out in (None, "none") or cfg.out_gated) else None
         if gb is None:
@@ -830,7 +913,8 @@ class ImageHeadFn(torch.autograd.Function):
         gx1, gx2, gw, gb = _conv_backward(cfg, ctx.geo, skip, u, weight, None, dz,
                                           ctx.needs_input_grad[0], ctx.needs_input_grad[1],
                                           ctx.needs_input_grad[2],
-                                          ctx.has_bias and ctx.needs_input_grad[3], nb=ctx.nb)
+                                          ctx.has_bias and ctx.needs_input_grad[3], nb=ctx.nb,
+                                          side_ok=True)
         if gb is not None:
             gb = gb[:3].contiguous()
         return gx1, gx2, gw, gb, None, None, None
