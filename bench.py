@@ -39,8 +39,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=256,
-                   help="images per GPU (sized for HBM; the eager baseline's best measured batch was 128)")
+    p.add_argument("--batch", type=int, default=1024,
+                   help="images per GPU, sized for the 288 GB HBM at the throughput knee: 256 / 512 / "
+                        "1024 measured 6841 / 7059 / 7116 img/s at 12.6 / 23.7 / 45.9 GiB "
+                        "(profiles/batch_sweep_r3.jsonl); the eager baseline's best batch was 128")
     p.add_argument("--size", type=int, default=256)
     p.add_argument("--family", default="pix2pix", choices=["pix2pix", "ref"],
                    help="pix2pix: the headline U-Net + PatchGAN step (BASELINE.json); ref: the reference "

@@ -379,9 +379,12 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   // stride-2 4x4 transposed convs onto 32x32 / 64x64 grids (U-Net decoder ConvT, every 4x4
   // s2 conv's input gradient): the class-shared halo kernel (csrc/conv_s2t.hip).  Its tiles
   // are BM = 128 rows of one class, which fixes the stats / partial chunk layout below.
+  // Only for 64-wide grids with K = 4 taps x C <= 1024 (census B = 256, profiles/
+  // kernel_experiments_r3.md): C = 512 (U-Net d3) and the 32-wide grids ran faster on the
+  // 256x128 implicit-GEMM tile.
   const bool s2t_ok = mode == 1 && !fp8 && splits == 1 && KH == 4 && KW == 4 && stride == 2 && pad == 1 &&
-                      !reflect && up == 1 && OH == 2 * H && OW == 2 * W && (W == 32 || W == 64) &&
-                      (H * W) % 128 == 0 && Cout % 64 == 0 && C1 % 64 == 0 && C2 % 64 == 0 &&
+                      !reflect && up == 1 && OH == 2 * H && OW == 2 * W && W == 64 &&
+                      (H * W) % 128 == 0 && Cout % 64 == 0 && C1 % 64 == 0 && C2 % 64 == 0 && C1 + C2 <= 256 &&
                       (act_in == 0 || (act_in == 1 && act_bwd == 0 && !res)) &&
                       std::getenv("P2P_NO_S2T") == nullptr;
   if (s2t_ok) bm = 128;

@@ -86,6 +86,7 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
                                                   PixF&& out_pix) {
   constexpr int CPR = BN / 8;
   static_assert(NT % CPR == 0, "a thread's 8-channel chunk is fixed across the store loop");
+  static_assert(64 % CPR == 0, "the lanes sharing a chunk lie in one wave");
   const int tid = threadIdx.x;
   const int co_t = n0 + (tid % CPR) * 8;
   const bool first_t = co_t < a.Csplit;
@@ -201,13 +202,25 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
     }
   }
   if (a.nb_ws) {
-    // per column: the NT / CPR threads sharing its chunk, summed in a fixed order
+    // per column: the NT / CPR threads sharing its chunk, summed in a fixed order -- first
+    // across the lanes of a wave that share it (lane % CPR), then across the waves in LDS
+    // (NT / 64 x CPR x 16 floats: fits in the staged tile it aliases)
+#pragma unroll
+    for (int off = CPR; off < 64; off <<= 1)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        s1[q] += __shfl_xor(s1[q], off);
+        s2[q] += __shfl_xor(s2[q], off);
+      }
     __syncthreads();   // every thread is done with the staged tile
     float* red = reinterpret_cast<float*>(smem);
+    const int lane = tid & 63, wid = tid >> 6;
+    if (lane < CPR) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      red[tid * 16 + q] = s1[q];
-      red[tid * 16 + 8 + q] = s2[q];
+      for (int q = 0; q < 8; ++q) {
+        red[(wid * CPR + lane) * 16 + q] = s1[q];
+        red[(wid * CPR + lane) * 16 + 8 + q] = s2[q];
+      }
     }
     __syncthreads();
     if (tid < BN) {
@@ -215,9 +228,9 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
       const int co = n0 + tid - a.nb_c0;
       if (co >= 0 && co < a.nb_C) {
         float S1 = 0.f, S2 = 0.f;
-        for (int k = 0; k < NT / CPR; ++k) {
-          S1 += red[(cc + CPR * k) * 16 + q];
-          S2 += red[(cc + CPR * k) * 16 + 8 + q];
+        for (int k = 0; k < NT / 64; ++k) {
+          S1 += red[(k * CPR + cc) * 16 + q];
+          S2 += red[(k * CPR + cc) * 16 + 8 + q];
         }
         const int img = m0 / HWq;
         const int cls = g.ry * s + g.rx;

@@ -10,15 +10,18 @@
 // one image) and 64 output channels of ALL four classes: per 64-channel chunk it stages
 // the (RH + 2) x (W + 2) input halo ONCE (global_load_lds, source-side swizzle, 2-stage
 // ring), and wave c (= class (ry, rx)) reads the A fragments of its 2 x 2 taps out of that
-// one LDS image at shifted pixel offsets.  A waves's B fragments (its class's 4 taps x 64
-// channels, the weights are L2-resident) go global -> VGPR one k-step ahead.  Per wave and
-// chunk: 64 ds_read_b128 + 32 global loads for 256 MFMAs (0.25 LDS reads per MFMA).
+// one LDS image at shifted pixel offsets.  8 waves: wave w computes class w & 3 for output
+// channels 32 (w >> 2) .. + 32 (128 x 32 per wave: 64 accumulator registers, so two blocks
+// fit a CU and one's epilogue overlaps the other's MFMAs).  A wave's B fragments (its
+// class's 4 taps x 32 channels; the weights are L2-resident) go global -> VGPR (buffer
+// loads) one k-step ahead.  Per wave and chunk: 64 ds_read_b128 + 16 buffer loads for 128
+// MFMAs.
 //
 // Tap geometry (conv_dev.h class_geom, s = 2, p = 1): class (ry, rx) reads input row
 // qy + dy - ty with kernel row ky = ky0 + 2 ty, ty in {0, 1}; ky0 = (ry + 1) % 2,
 // dy = (ry + 1 - ky0) / 2 (columns alike).  Halo pixel (hy, hx) = input (qy0 - 1 + hy, hx - 1).
 //
-// Epilogue: each wave stages its class's 128 x 64 bf16 tile into its own LDS region; then
+// Epilogue: each wave stages its 128 x 32 block into its class's LDS tile; then
 // the whole block runs the shared GEMM epilogue tail (conv_dev.h) class by class -- bias,
 // activation, statistics for a following norm, act' gate / skip gradient / norm-backward
 // partials of a dgrad, fp8 shadow -- with exactly the per-class BM = 128 tile conventions
@@ -33,13 +36,17 @@ __device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(lds_wave_base), 16, 0, 0);
 }
 
+// s_waitcnt vmcnt(N) through the builtin (not inline asm): the compiler's wait-count pass
+// sees it, so registers loaded before the wait are known complete after it (with an asm
+// wait it re-waits vmcnt(0) at the first use -- the chunk's fresh halo loads included)
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | 0x70 | 0xF00 | (((N >> 4) & 3) << 14));
 }
 
-constexpr int BM = 128, BN = 64, NT = 256;
-constexpr int TM = BM / 16, TN = BN / 16;   // one wave = one class: 8 x 4 fragments
+constexpr int BM = 128, BN = 64, NT = 512;
+constexpr int TM = BM / 16, TN = 2;         // one wave = one class x 32 channels: 8 x 2 fragments
 constexpr int LDC = BN + 8;
 
 template <int W>
@@ -52,12 +59,13 @@ struct S2TGeom {
   static constexpr int STAGE_BYTES = HLD * NT * 16;
   static constexpr int EPI_BYTES = 4 * BM * LDC * 2 + 2 * NT * 4;
   static constexpr int SMEM = 2 * STAGE_BYTES > EPI_BYTES ? 2 * STAGE_BYTES : EPI_BYTES;
+  static_assert(SMEM <= 80 * 1024, "two blocks per CU");
 };
 
 }  // namespace
 
 template <int W, bool RELU, bool EXT>
-__global__ void __launch_bounds__(256, 2) conv_s2t_kernel(ConvFwdArgs a) {
+__global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a) {
   using G = S2TGeom<W>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -82,22 +90,27 @@ __global__ void __launch_bounds__(256, 2) conv_s2t_kernel(ConvFwdArgs a) {
     const int cs = s1 ? a.C1 : a.C2;
     const int coff = s1 ? ch * 64 : ch * 64 - a.C1;
     char* dst = ring + stage * G::STAGE_BYTES;
+    // the per-lane unit geometry is loop-invariant: laundering tid keeps the compiler from
+    // hoisting it out of the chunk loop into (spilled) registers
+    int t = tid;
+    asm volatile("" : "+v"(t));
 #pragma unroll
     for (int j = 0; j < G::HLD; ++j) {
-      const int e = j * NT + tid;
+      const int e = j * NT + t;
       const int hp = e >> 3;
       const int hy = hp / G::HW, hx = hp - (hp / G::HW) * G::HW;
       const int iy = qy0 - 1 + hy, ix = hx - 1;
       const bool in = hp < G::HPIX && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
       const int kc = (e & 7) ^ ((hp >> 1) & 7);
-      const bf16* g = in ? src + (long)((img * a.H + iy) * a.W + ix) * cs + coff + kc * 8
-                         : static_cast<const bf16*>(a.zero);
-      glds16(g, dst + (j * NT + wid * 64) * 16);
+      const int pix = in ? (img * a.H + iy) * a.W + ix : 0;
+      const bf16* g = src + (long)pix * cs + coff + kc * 8;
+      glds16(in ? g : static_cast<const bf16*>(a.zero), dst + (j * NT + wid * 64) * 16);
     }
   };
 
   // ---- this wave's class and its tap geometry (wave-uniform: scalar registers)
-  const int cls_w = __builtin_amdgcn_readfirstlane(wid);
+  const int cls_w = __builtin_amdgcn_readfirstlane(wid & 3);
+  const int nh = __builtin_amdgcn_readfirstlane(wid >> 2);   // 32-channel half of the co tile
   const int ry = cls_w >> 1, rx = cls_w & 1;
   const int ky0 = (ry + 1) & 1, kx0 = (rx + 1) & 1;
   const int dy = (ry + 1 - ky0) >> 1, dx = (rx + 1 - kx0) >> 1;
@@ -105,15 +118,11 @@ __global__ void __launch_bounds__(256, 2) conv_s2t_kernel(ConvFwdArgs a) {
   // 8 * (lane >> 4)) in voffset, the (tap, k-step, 16-column block) offset in soffset
   const int wrow = 16 * C;   // bf16 elements per output channel of the [Cout][4][4][C] image
   const auto wsrd = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, a.Cout * wrow * 2, 0x00020000);
-  const int bvoff = ((n0 + (lane & 15)) * wrow + 8 * (lane >> 4)) * 2;
+  const int bvoff = ((n0 + 32 * nh + (lane & 15)) * wrow + 8 * (lane >> 4)) * 2;
   // A fragment rows: lane row r = lane & 15 of fragment i -> grid position p = 16 i + r
   //   (ly = p / W, qx = p % W); tap (ty, tx) reads halo pixel (ly + dy - ty + 1, qx + dx - tx + 1)
-  int apix[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int p = 16 * i + (lane & 15);
-    apix[i] = (p / W + dy + 1) * G::HW + (p % W) + dx + 1;
-  }
+  //   = abase + (i / (W / 16)) * HW + 16 * (i % (W / 16)): one register, the rest immediate
+  int abase = (dy + 1) * G::HW + (lane & 15) + dx + 1;
   const int kq = lane >> 4;
 
   f32x4 acc[TM][TN];
@@ -146,30 +155,51 @@ __global__ void __launch_bounds__(256, 2) conv_s2t_kernel(ConvFwdArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     const bf16* A = reinterpret_cast<const bf16*>(ring + stage * G::STAGE_BYTES);
     // the A addresses are loop-invariant per (tap, k-step, fragment): hoisted out of the chunk
-    // loop they would pin 64 registers (and spill); laundering apix keeps them per step
-#pragma unroll
-    for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(apix[i]));
+    // loop they would pin 64 registers (and spill); laundering abase keeps them per step
+    asm volatile("" : "+v"(abase));
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
       const int t = st >> 1, ks = st & 1;
-      // prefetch the next k-step's B (the next chunk's first after the last)
+      // prefetch the next k-step's B (the next chunk's first after the last) a whole k-step
+      // of MFMAs ahead of its use; then A fragment i + 1 is read while fragment i's 4 MFMAs
+      // run (sched_group_barrier pins that interleave: left alone the scheduler sinks the B
+      // loads below the MFMAs and the next step waits vmcnt(0) on a full L2 round trip)
       if (st < 7) loadB(ch, (st + 1) >> 1, (st + 1) & 1, bnxt);
       else if (ch + 1 < nch) loadB(ch + 1, 0, 0, bnxt);
       const int toff = -(t >> 1) * G::HW - (t & 1);
       const int kc = ks * 4 + kq;
-      bf16x8 af[TM];
+      // fragments of one grid row (i / FPR) differ by 16 pixels: the same swizzle key
+      // ((hp >> 1) & 7 moves by 8), so their addresses differ by an immediate 2 KiB
+      constexpr int FPR = W / 16;
+      int rowoff[TM / FPR];
+#pragma unroll
+      for (int g = 0; g < TM / FPR; ++g) {
+        const int hp = abase + g * G::HW + toff;
+        rowoff[g] = (hp * 8 + (kc ^ ((hp >> 1) & 7))) * 8;
+      }
+      auto rd = [&](int i) __attribute__((always_inline)) {
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(A + rowoff[i / FPR] + (i % FPR) * 16 * 64);
+        if constexpr (RELU) v = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, v)));
+        return v;
+      };
+      bf16x8 af[2];
+      af[0] = rd(0);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int hp = apix[i] + toff;
-        af[i] = *reinterpret_cast<const bf16x8*>(A + (hp * 8 + (kc ^ ((hp >> 1) & 7))) * 8);
-        if constexpr (RELU) af[i] = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, af[i])));
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
+        if (i + 1 < TM) af[(i + 1) & 1] = rd(i + 1);
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], __builtin_bit_cast(bf16x8, bcur[j]),
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i & 1], __builtin_bit_cast(bf16x8, bcur[j]),
                                                                acc[i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x020, TN, 0);   // the B prefetch (VMEM reads) first
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);    // A fragments 0 and 1
+#pragma unroll
+      for (int i = 0; i < TM - 2; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, TN, 0); // fragment i's MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // read fragment i + 2
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * TN, 0);
 #pragma unroll
       for (int j = 0; j < TN; ++j) bcur[j] = bnxt[j];
     }
@@ -180,7 +210,7 @@ __global__ void __launch_bounds__(256, 2) conv_s2t_kernel(ConvFwdArgs a) {
 
   // ---- epilogue: every wave stages its class tile, then the block stores class by class
   bf16* Cs0 = reinterpret_cast<bf16*>(smem);
-  conv_stage_tile<TM, TN, LDC>(a, acc, Cs0 + wid * BM * LDC, 0, 0, n0, lane);
+  conv_stage_tile<TM, TN, LDC>(a, acc, Cs0 + cls_w * BM * LDC, 0, 32 * nh, n0, lane);
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem + 4 * BM * LDC * 2);
   const FastDiv fd_hwq = make_fastdiv((uint32_t)HWq), fd_wq = make_fastdiv((uint32_t)a.W);
