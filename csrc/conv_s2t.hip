@@ -81,7 +81,11 @@ __global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a) {
 
   char* ring = smem;
   // halo chunk ch -> ring stage: unit e = j * NT + tid holds logical 16-B chunk
-  // (e & 7) ^ ((hp >> 1) & 7) of halo pixel hp = e >> 3 (source-side swizzle, conv_dev.h swz);
+  // (e & 7) ^ (hp & 6) of halo pixel hp = e >> 3 (source-side swizzle).  Unlike the im2col
+  // tiles' (row >> 1) & 7 key, hp & 6 keeps every ds_read_b128 lane group conflict-free for
+  // ANY fragment base pixel (the tap shifts move it by -1 / -HW): 16 consecutive pixels,
+  // 8 of each parity, with the group's two k chunks in the pattern 0,0,1,1,1,1,0,0 map to 16
+  // distinct bank quads (exhaustive check over bases and k steps; the old key: up to 4-way)
   // pixels outside the image (or beyond the halo) read the zero page.  Recomputed per issue
   // (a few VALU per unit, 2-4 issues per block) instead of holding 2 x HLD registers.
   auto issue = [&](int ch, int stage) {
@@ -101,7 +105,7 @@ __global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a) {
       const int hy = hp / G::HW, hx = hp - (hp / G::HW) * G::HW;
       const int iy = qy0 - 1 + hy, ix = hx - 1;
       const bool in = hp < G::HPIX && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-      const int kc = (e & 7) ^ ((hp >> 1) & 7);
+      const int kc = (e & 7) ^ (hp & 6);
       const int pix = in ? (img * a.H + iy) * a.W + ix : 0;
       const bf16* g = src + (long)pix * cs + coff + kc * 8;
       glds16(in ? g : static_cast<const bf16*>(a.zero), dst + (j * NT + wid * 64) * 16);
@@ -169,13 +173,13 @@ __global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a) {
       const int toff = -(t >> 1) * G::HW - (t & 1);
       const int kc = ks * 4 + kq;
       // fragments of one grid row (i / FPR) differ by 16 pixels: the same swizzle key
-      // ((hp >> 1) & 7 moves by 8), so their addresses differ by an immediate 2 KiB
+      // (hp & 6 is unchanged), so their addresses differ by an immediate 2 KiB
       constexpr int FPR = W / 16;
       int rowoff[TM / FPR];
 #pragma unroll
       for (int g = 0; g < TM / FPR; ++g) {
         const int hp = abase + g * G::HW + toff;
-        rowoff[g] = (hp * 8 + (kc ^ ((hp >> 1) & 7))) * 8;
+        rowoff[g] = (hp * 8 + (kc ^ (hp & 6))) * 8;
       }
       auto rd = [&](int i) __attribute__((always_inline)) {
         bf16x8 v = *reinterpret_cast<const bf16x8*>(A + rowoff[i / FPR] + (i % FPR) * 16 * 64);
