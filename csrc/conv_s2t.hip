@@ -52,7 +52,10 @@ constexpr int LDC = BN + 8;
 template <int W>
 struct S2TGeom {
   static constexpr int RH = BM / W;                 // grid rows per tile
-  static constexpr int HW = W + 2, HH = RH + 2;     // halo edge
+  // halo edge: W + 2 columns stored at a row pitch HW that is a multiple of 8 pixels, so
+  // the swizzle key hp & 6 is the same for every fragment of a k-step (only their -1 column
+  // shift changes it): a whole k-step's A reads are one base register + immediate offsets
+  static constexpr int HWV = W + 2, HW = (W + 2 + 7) / 8 * 8, HH = RH + 2;
   static constexpr int HPIX = HH * HW;
   static constexpr int UNITS = HPIX * 8;            // 16-B units per 64-channel chunk
   static constexpr int HLD = (UNITS + NT - 1) / NT; // glds per lane per stage
@@ -104,7 +107,7 @@ __global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a) {
       const int hp = e >> 3;
       const int hy = hp / G::HW, hx = hp - (hp / G::HW) * G::HW;
       const int iy = qy0 - 1 + hy, ix = hx - 1;
-      const bool in = hp < G::HPIX && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+      const bool in = hp < G::HPIX && hx < G::HWV && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
       const int kc = (e & 7) ^ (hp & 6);
       const int pix = in ? (img * a.H + iy) * a.W + ix : 0;
       const bf16* g = src + (long)pix * cs + coff + kc * 8;
@@ -172,17 +175,13 @@ __global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a) {
       else if (ch + 1 < nch) loadB(ch + 1, 0, 0, bnxt);
       const int toff = -(t >> 1) * G::HW - (t & 1);
       const int kc = ks * 4 + kq;
-      // fragments of one grid row (i / FPR) differ by 16 pixels: the same swizzle key
-      // (hp & 6 is unchanged), so their addresses differ by an immediate 2 KiB
+      // fragment i sits (i / FPR) rows and 16 (i % FPR) pixels from fragment 0: both multiples
+      // of 8 pixels, so the same swizzle key -- its address is an immediate offset
       constexpr int FPR = W / 16;
-      int rowoff[TM / FPR];
-#pragma unroll
-      for (int g = 0; g < TM / FPR; ++g) {
-        const int hp = abase + g * G::HW + toff;
-        rowoff[g] = (hp * 8 + (kc ^ (hp & 6))) * 8;
-      }
+      const int hp0 = abase + toff;
+      const int off0 = (hp0 * 8 + (kc ^ (hp0 & 6))) * 8;
       auto rd = [&](int i) __attribute__((always_inline)) {
-        bf16x8 v = *reinterpret_cast<const bf16x8*>(A + rowoff[i / FPR] + (i % FPR) * 16 * 64);
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(A + off0 + ((i / FPR) * G::HW + 16 * (i % FPR)) * 64);
         if constexpr (RELU) v = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, v)));
         return v;
       };
