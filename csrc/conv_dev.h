@@ -172,13 +172,17 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
   };
   constexpr int IT = (BM * CPR) / NT;   // rows per thread
   constexpr int RSTEP = NT / CPR;
+  // operand prefetch group: 2 rows in the small tiles (several blocks per CU: their registers
+  // would cost occupancy), up to 8 in the 256-row tiles, which run one block per CU anyway
+  // (their LDS ring) -- there each 2-row group was a serial HBM round trip per 256 x BN tile
+  constexpr int PG = (BM >= 256 && IT % 8 == 0) ? 8 : ((BM >= 256 && IT % 4 == 0) ? 4 : 2);
   if constexpr (IT >= 2 && (BM * CPR) % NT == 0 && IT % 2 == 0) {
     if (co_t < a.Cout) {
-      for (int g0 = 0; g0 < IT; g0 += 2) {
-        long pixv[2];
-        u32x4 xv[2], rv[2], nv[2];
+      for (int g0 = 0; g0 < IT; g0 += PG) {
+        long pixv[PG];
+        u32x4 xv[PG], rv[PG], nv[PG];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < PG; ++u) {
           const int m = m0 + tid / CPR + (g0 + u) * RSTEP;
           const bool ok = m < g.Mc;
           pixv[u] = ok ? out_pix(m) : -1;
@@ -187,7 +191,7 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
           nv[u] = (nb_x_on && ok) ? ld16(nbx_p + pixv[u] * a.nb_C + nb_co) : z4;
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+        for (int u = 0; u < PG; ++u)
           if (pixv[u] >= 0) finish(tid / CPR + (g0 + u) * RSTEP, pixv[u], xv[u], rv[u], nv[u]);
       }
     }
