@@ -32,6 +32,7 @@ path; spectral-norm 1/sigma on the weight image).  Losses stay on the device.
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 
@@ -113,6 +114,9 @@ class CompressGANStep:
     def _quant(self, x):
         return _STEQuantize.apply(x, self.bits) if self.train_c else ops.quantize(x, self.bits)
 
+    def _vgg(self, x, y, fy):
+        return self.criterionVGG(x, y) if fy is None else self.criterionVGG(x, y, fy=fy)
+
     @staticmethod
     def _wgrad_overlap(x, reducer):
         """G's conv weight gradients on the side stream (ops/hip.py ``wgrad_overlap``): grads
@@ -159,7 +163,11 @@ class CompressGANStep:
             for j in range(len(pred_fake_g[i]) - 1):
                 loss_feat = loss_feat + self.d_weights * self.feat_weights * ops.l1(
                     pred_fake_g[i][j], pred_real[i][j].detach(), gate_a=fgate) * self.lambda_feat
-        content = self.criterionVGG(fake_b, real_b) * self.lambda_vgg
+        # VGG(real_b): once per step for both perceptual losses against it (G and C phase)
+        fy_real = (self.criterionVGG.target_features(real_b)
+                   if hasattr(self.criterionVGG, "target_features")
+                   and os.environ.get("P2P_VGG_REUSE", "1") != "0" else None)
+        content = self._vgg(fake_b, real_b, fy_real) * self.lambda_vgg
         tv = calc_tv_Loss(fake_b)
         loss_g = loss_g_gan + loss_feat + content + tv * self.lambda_tv
         # ---- updates: G first (its backward also reaches D; those grads are dropped)
@@ -180,7 +188,7 @@ class CompressGANStep:
         need_graph = self.train_c or self.c_phase_backward
         with torch.set_grad_enabled(need_graph):
             fake_ac = G(compressed)     # also advances G's BN running stats, as the reference
-            loss_c = ops.mse(fake_ac, real_b) + self.criterionVGG(compressed, real_b) * \
+            loss_c = ops.mse(fake_ac, real_b) + self._vgg(compressed, real_b, fy_real) * \
                 self.lambda_vgg
         paused_g = (self.reducer_g.paused() if self.reducer_g is not None
                     else contextlib.nullcontext())

@@ -117,10 +117,17 @@ class VGGLoss(nn.Module):
         if device is not None:
             self.vgg = self.vgg.to(device)
 
-    def forward(self, x, y):
-        fx = self.vgg(x)
+    def target_features(self, y):
+        """phi(y) without a graph: pass it as ``fy`` to every loss against the same target
+        (the reference step evaluates VGG(real_b) twice, train.py:377 and :395 -- identical
+        frozen-network features, so the second forward is skipped)."""
         with torch.no_grad():
-            fy = self.vgg(y)
+            return self.vgg(y)
+
+    def forward(self, x, y, fy=None):
+        fx = self.vgg(x)
+        if fy is None:
+            fy = self.target_features(y)
         loss = 0
         for w, a, b in zip(self.weights, fx, fy):
             loss = loss + w * ops.l1(a, b.detach())
