@@ -252,7 +252,8 @@ __global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restri
 // ---------------------------------------------------------------- losses
 // kinds: 0 = mse vs const t, 1 = bce-with-logits vs const t, 2 = bce(prob) vs const t,
 //        3 = l1(a, b), 4 = mse(a, b), 5 = mean(a), 6 = l1(a, b) whose gradient also carries
-//        lrelu'(a) (a is a LeakyReLU output whose producer left its derivative to consumers)
+//        lrelu'(a) (a is a LeakyReLU output whose producer left its derivative to consumers),
+//        7 = the same with relu'(a) (a ReLU output)
 __device__ __forceinline__ float loss_elem(int kind, float a, float b, float t) {
   switch (kind) {
     case 0: { const float d = a - t; return d * d; }
@@ -262,7 +263,8 @@ __device__ __forceinline__ float loss_elem(int kind, float a, float b, float t) 
       return -(t * lp + (1.f - t) * lq);
     }
     case 3:
-    case 6: return fabsf(a - b);
+    case 6:
+    case 7: return fabsf(a - b);
     case 4: { const float d = a - b; return d * d; }
     default: return a;
   }
@@ -280,6 +282,10 @@ __device__ __forceinline__ float loss_grad(int kind, float a, float b, float t) 
     case 6: {
       const float d = a - b;
       return (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f)) * (a > 0.f ? 1.f : LRELU_SLOPE);
+    }
+    case 7: {   // a is a ReLU output: relu'(pre) = [a > 0]
+      const float d = a - b;
+      return a > 0.f ? (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f)) : 0.f;
     }
     case 4: return 2.f * (a - b);
     default: return 1.f;
@@ -428,6 +434,7 @@ static void with_loss(int is_f32, int kind, bool has_b, F&& f) {
       case 3: f(f32, std::integral_constant<int, 3>{}, std::true_type{}); break;
       case 4: f(f32, std::integral_constant<int, 4>{}, std::true_type{}); break;
       case 6: f(f32, std::integral_constant<int, 6>{}, std::true_type{}); break;
+      case 7: f(f32, std::integral_constant<int, 7>{}, std::true_type{}); break;
       default: f(f32, std::integral_constant<int, 5>{}, std::false_type{}); break;
     }
   };
@@ -617,7 +624,7 @@ int p2p_loss_fwd(const void* a, const void* b, int is_f32, long n, int kind, flo
                  float* ws, float* out, hipStream_t st) {
   using namespace p2p;
   const int nb = p2p_loss_blocks(n);
-  const bool pair = kind == 3 || kind == 4 || kind == 6;
+  const bool pair = kind == 3 || kind == 4 || kind == 6 || kind == 7;
   if (al16(a) && (!pair || (b && al16(b)))) {
     with_loss(is_f32, kind, pair, [&](auto f32, auto k, auto hb) {
       hipLaunchKernelGGL((loss_partial_vec_kernel<decltype(f32)::value, decltype(k)::value, decltype(hb)::value>),
@@ -650,7 +657,7 @@ int p2p_sum_partials(const float* ws, int nb, float scale, float* out, hipStream
 int p2p_loss_bwd(const void* a, const void* b, int is_f32, long n, int kind, float t, float scale,
                  const float* gout, void* ga, void* gb, hipStream_t st) {
   using namespace p2p;
-  const bool pair = kind == 3 || kind == 4 || kind == 6;
+  const bool pair = kind == 3 || kind == 4 || kind == 6 || kind == 7;
   if (al16(a) && (!pair || (b && al16(b))) && (!ga || al16(ga)) && (!gb || al16(gb))) {
     const long nv = n / (is_f32 ? 4 : 8);
     with_loss(is_f32, kind, pair, [&](auto f32, auto k, auto hb) {

@@ -114,6 +114,12 @@ class CompressGANStep:
     def _quant(self, x):
         return _STEQuantize.apply(x, self.bits) if self.train_c else ops.quantize(x, self.bits)
 
+    @staticmethod
+    def _no_deferred(x):
+        if x.is_cuda and _native.get_backend() == "native":
+            from ..ops import hip
+            hip.assert_no_deferred()
+
     def _vgg(self, x, y, fy):
         return self.criterionVGG(x, y) if fy is None else self.criterionVGG(x, y, fy=fy)
 
@@ -175,6 +181,7 @@ class CompressGANStep:
             self._zero(self.opt_g, self.reducer_g)
             with self._wgrad_overlap(real_a, self.reducer_g):
                 loss_g.backward()
+            self._no_deferred(real_a)   # every parked VGG-tap gradient was consumed
             if self.reducer_g is not None:
                 self.reducer_g.finish()
             self._opt_step(self.opt_g, self.reducer_g, loss_g)
@@ -196,12 +203,14 @@ class CompressGANStep:
             self._zero(self.opt_c, self.reducer_c)
             with paused_g:      # the G grads of this backward are discarded (zeroed next step)
                 loss_c.backward()
+            self._no_deferred(real_a)
             if self.reducer_c is not None:
                 self.reducer_c.finish()
             self._opt_step(self.opt_c, self.reducer_c, loss_c)
         elif self.c_phase_backward:
             with paused_g:      # reference: grads land on G (zeroed next step) -- no effect
                 loss_c.backward()
+            self._no_deferred(real_a)
         return {"D": loss_d.detach(), "G_GAN": loss_g_gan.detach(),
                 "C": loss_c.detach(), "G_GAN_Feat": torch.as_tensor(loss_feat).detach(),
                 "VGG": content.detach(), "TV": tv.detach(), "G": loss_g.detach()}

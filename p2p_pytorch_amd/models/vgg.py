@@ -10,7 +10,9 @@ is random-initialised (there is no network access) -- the loss is then a random-
 perceptual loss with identical cost.  Inputs are fed in [-1, 1] with no ImageNet
 normalisation, exactly like the reference (quirk A15).
 
-Every ReLU is fused into its conv's epilogue and each max-pool is a separate kernel.
+Every ReLU is fused into its conv's epilogue and each max-pool is a separate kernel.  In the
+perceptual loss the taps' gradients (relu' included) go straight into the next slice's first
+conv's dgrad epilogue (``Vgg19.set_tap_fusion``).
 """
 from __future__ import annotations
 
@@ -68,9 +70,28 @@ class Vgg19(nn.Module):
         for prod, cons in ((2, 5), (7, 10), (12, 14), (14, 16), (16, 19), (21, 23), (23, 25), (25, 28)):
             feats[prod].out_gated = True
             feats[cons].grad_gate = "relu"
+        self._feats = feats
+        self.tap_fusion = False
         if not requires_grad:
             for p in self.parameters():
                 p.requires_grad = False
+
+    # the loss taps (relu1_1 .. relu5_1 outputs) and the conv reading each of them
+    _TAPS = ((0, 2), (5, 7), (10, 12), (19, 21), (28, None))
+
+    def set_tap_fusion(self, on: bool = True):
+        """HIP path, for a loss whose gradient w.r.t. every tap carries the tap's relu' and
+        is parked for the tap's consumer conv (VGGLoss: ``ops.l1(gate_a="relu",
+        defer=True)``): the tap convs leave relu' to their consumers, which add the parked
+        loss gradient in their dgrad epilogue -- no accumulate or relu' pass per tap.  Off
+        (default), the taps are ordinary outputs."""
+        self.tap_fusion = bool(on)
+        for prod, cons in self._TAPS:
+            self._feats[prod].out_gated = self.tap_fusion
+            if cons is not None:
+                self._feats[cons].grad_gate = "relu" if self.tap_fusion else None
+                self._feats[cons].skip_grad = "take" if self.tap_fusion else None
+        return self
 
     def _init(self, path):
         for m in self.modules():
@@ -113,7 +134,7 @@ class VGGLoss(nn.Module):
 
     def __init__(self, device=None):
         super().__init__()
-        self.vgg = Vgg19()
+        self.vgg = Vgg19().set_tap_fusion(True)
         if device is not None:
             self.vgg = self.vgg.to(device)
 
@@ -129,6 +150,10 @@ class VGGLoss(nn.Module):
         if fy is None:
             fy = self.target_features(y)
         loss = 0
-        for w, a, b in zip(self.weights, fx, fy):
-            loss = loss + w * ops.l1(a, b.detach())
+        fused = self.vgg.tap_fusion
+        for i, (w, a, b) in enumerate(zip(self.weights, fx, fy)):
+            if fused:   # relu' of the tap in the L1 gradient, parked for the next slice's conv
+                loss = loss + w * ops.l1(a, b.detach(), gate_a="relu", defer=i < len(fx) - 1)
+            else:
+                loss = loss + w * ops.l1(a, b.detach())
         return loss

@@ -116,11 +116,13 @@ def bce_const(prob, target):
     return ref.bce_const(prob, target)
 
 
-def l1(a, b, gate_a=None):
+def l1(a, b, gate_a=None, defer=False):
     """``gate_a`` (HIP path): the gradient of ``a`` also carries that activation's derivative
-    (its producer is ``out_gated``); the oracle's producers apply their own activation."""
+    (its producer is ``out_gated``); the oracle's producers apply their own activation.
+    ``defer`` (HIP path): a's gradient goes to the conv reading ``a`` with
+    ``skip_grad="take"`` (added in its dgrad epilogue) instead of through autograd."""
     if _native.use_native(a):
-        return _hip().l1(a, b, gate_a)
+        return _hip().l1(a, b, gate_a, defer)
     return ref.l1(a, b)
 
 

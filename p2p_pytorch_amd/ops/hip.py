@@ -1252,7 +1252,8 @@ def dropout(x, p, salt=None):
 
 
 # ============================================================== losses
-LOSS = {"mse_const": 0, "bce_logits_const": 1, "bce_const": 2, "l1": 3, "mse": 4, "l1_glrelu": 6}
+LOSS = {"mse_const": 0, "bce_logits_const": 1, "bce_const": 2, "l1": 3, "mse": 4, "l1_glrelu": 6,
+        "l1_grelu": 7}
 
 
 def _dense(x):
@@ -1278,15 +1279,21 @@ class LossConstFn(torch.autograd.Function):
 
 
 class LossPairFn(torch.autograd.Function):
+    """``defer``: a's gradient is parked in ``_DEFERRED`` for the conv that also reads ``a``
+    (``skip_grad="take"``): its dgrad epilogue adds it, so no autograd accumulate pass runs
+    (the VGG loss taps, models/vgg.py).  Only when ``a`` is used as is (NHWC bf16)."""
+
     @staticmethod
-    def forward(ctx, a, b, kind):
+    def forward(ctx, a, b, kind, defer=False):
         if a.dtype != b.dtype:
             b = b.to(a.dtype)
+        a0 = a
         a = _dense(a)
         if b.stride() != a.stride():
             b = b.contiguous(memory_format=CL) if a.dim() == 4 and a.is_contiguous(
                 memory_format=CL) else b.contiguous()
         ctx.kind = kind
+        ctx.defer = bool(defer) and a is a0 and a.dtype == torch.bfloat16 and a.dim() == 4
         ctx.save_for_backward(a, b)
         return P().loss_fwd(a, b, kind, 0.0, 1.0 / a.numel())
 
@@ -1296,7 +1303,11 @@ class LossPairFn(torch.autograd.Function):
         na, nb = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         ga, gb = P().loss_bwd(a, b, ctx.kind, 0.0, 1.0 / a.numel(), gout.float().reshape(1),
                               na, nb)
-        return (ga if na else None), (gb if nb else None), None
+        if na and ctx.defer and a.data_ptr() not in _DEFERRED:
+            _DEFERRED[a.data_ptr()] = ga
+            ga = None
+            na = False
+        return (ga if na else None), (gb if nb else None), None, None
 
 
 def mse_const(pred, target):
@@ -1311,12 +1322,14 @@ def bce_const(prob, target):
     return LossConstFn.apply(prob, LOSS["bce_const"], float(target))
 
 
-def l1(a, b, gate_a=None):
-    """mean |a - b|; ``gate_a="lrelu"``: the gradient of a also carries lrelu'(a) -- a is a
-    LeakyReLU output whose producer conv left the derivative to its consumers (out_gated)."""
-    if gate_a not in (None, "lrelu"):
+def l1(a, b, gate_a=None, defer=False):
+    """mean |a - b|; ``gate_a="lrelu"`` / ``"relu"``: the gradient of a also carries that
+    activation's derivative -- a is its output and the producer conv left the derivative to
+    its consumers (out_gated).  ``defer``: see LossPairFn."""
+    kinds = {None: "l1", "lrelu": "l1_glrelu", "relu": "l1_grelu"}
+    if gate_a not in kinds:
         raise ValueError(f"l1: unsupported gate {gate_a!r}")
-    return LossPairFn.apply(a, b, LOSS["l1_glrelu" if gate_a else "l1"])
+    return LossPairFn.apply(a, b, LOSS[kinds[gate_a]], defer)
 
 
 def mse(a, b):
