@@ -460,6 +460,8 @@ __global__ void __launch_bounds__(256) norm_frozen_coef_kernel(int NC, int C, co
 }
 
 // d(gamma) = sum(dy_eff * xhat), d(beta) = sum(dy_eff) over every group of the channel
+// (stored, not accumulated: one launch per norm backward writes every channel once, so the
+// caller hands uninitialised buffers -- no zero fill per norm)
 template <int FIN_CT, int FIN_J>
 __global__ void __launch_bounds__(256) norm_param_grad_kernel(const float* __restrict__ ws, NormGeom g,
                                                               float* __restrict__ dgamma,
@@ -470,8 +472,8 @@ __global__ void __launch_bounds__(256) norm_param_grad_kernel(const float* __res
   float sdy, sdx;
   chunk_sums<FIN_CT, FIN_J>(ws, g, 0, g.N, c, j, sdy, sdx, ra, rb, cl);
   if (j != 0 || c >= g.C) return;
-  dgamma[c] += sdx;
-  dbeta[c] += sdy;
+  dgamma[c] = sdx;
+  dbeta[c] = sdy;
 }
 
 // dx = A*dy_eff + B + Cc*xhat.  (The column sums of dx -- the bias gradient of the conv

@@ -1056,8 +1056,8 @@ class NormFn(torch.autograd.Function):
         need_x = ctx.needs_input_grad[0]
         dg = db = None
         if gamma is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2]):
-            dg = torch.zeros_like(gamma, dtype=torch.float32)
-            db = torch.zeros_like(gamma, dtype=torch.float32)
+            dg = torch.empty_like(gamma, dtype=torch.float32)   # written whole by the kernel
+            db = torch.empty_like(gamma, dtype=torch.float32)
         g = gamma.detach().float().contiguous() if gamma is not None else None
         b = beta.detach().float().contiguous() if beta is not None else None
         if not training:
