@@ -641,8 +641,10 @@ def _wgrad_fp8(cfg, weight, q1, q2, gyp, act_in):
     C1 = q1.shape[1]
     C2 = 0 if q2 is None else q2.shape[1]
     Cout = gyp.shape[1]
-    if not (_f8.conv_ok(C1, C2, Cout, act_in) and C1 % 16 == 0 and C2 % 16 == 0 and Cout % 128 == 0
-            and (C1 + C2) % 128 == 0 and C1 + C2 >= 128):
+    # the kernel's own gate (conv_wgrad.hip p2p_conv_wgrad_f8_tile: R and taps x C multiples of
+    # 128) decides the rest; 64-channel sides (U-Net e2 / d2) are covered since round 3
+    if not (_f8.conv_ok(C1, C2, Cout, act_in) and C1 % 16 == 0 and C2 % 16 == 0 and Cout % 64 == 0
+            and (C1 + C2) % 64 == 0 and C1 + C2 >= 64):
         return None
     k = id(weight)
     x1q, sx = _f8.quant(q1, (k, "x", 1), _f8.E4M3)

@@ -251,7 +251,7 @@ def _deq(q, site):
     return q.float() * 2.0 ** (int(site[2].item()) - 127)
 
 
-@pytest.mark.parametrize("case", ["conv_s2_relu", "convT_concat", "conv_s1_wide"])
+@pytest.mark.parametrize("case", ["conv_s2_relu", "convT_concat", "conv_s1_wide", "conv_c64", "convT_c64out"])
 def test_fp8_wgrad_matches_dequantised_oracle(case):
     """fp8 weight gradient (e5m2 dY x e4m3 X on the scaled f8f6f4 MFMA, both operands read
     k-transposed with ds_read_b64_tr_b8) against an fp32 weight gradient of the DEQUANTISED
@@ -261,6 +261,10 @@ def test_fp8_wgrad_matches_dequantised_oracle(case):
         N, C1, C2, H, Cout, k, s, p, act, tr = 8, 128, 0, 32, 256, 4, 2, 1, 1, False
     elif case == "conv_s1_wide":    # PatchGAN c4-like: 256 -> 512, 4x4 s1 p1
         N, C1, C2, H, Cout, k, s, p, act, tr = 4, 256, 0, 17, 512, 4, 1, 1, 0, False
+    elif case == "conv_c64":        # U-Net e2-like: 64 -> 128 (a 64-channel im2col side)
+        N, C1, C2, H, Cout, k, s, p, act, tr = 4, 64, 0, 64, 128, 4, 2, 1, 0, False
+    elif case == "convT_c64out":    # U-Net d2-like ConvT: (128 | 128) -> 64 (64-channel dY side)
+        N, C1, C2, H, Cout, k, s, p, act, tr = 4, 128, 128, 32, 64, 4, 2, 1, 1, True
     else:                           # U-Net decoder ConvT on a skip concat: (128 | 128) -> 128
         N, C1, C2, H, Cout, k, s, p, act, tr = 8, 128, 128, 16, 128, 4, 2, 1, 1, True
     x1 = rand_img(N, C1, H, H, seed=61)
