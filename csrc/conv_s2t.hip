@@ -45,6 +45,9 @@ __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | 0x70 | 0xF00 | (((N >> 4) & 3) << 14));
 }
 
+#ifndef S2T_PD
+#define S2T_PD 1   // B prefetch distance in k-steps (2, 3: the register-ring experiment)
+#endif
 constexpr int BM = 128, BN = 64, NT = 512;
 constexpr int TM = BM / 16, TN = 2;         // one wave = one class x 32 channels: 8 x 2 fragments
 constexpr int LDC = BN + 8;
@@ -147,8 +150,17 @@ __global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a) {
       b[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wsrd, bvoff, so + j * 32 * wrow, 0));
   };
 
+#if S2T_PD > 1
+  // B ring: k-step st of a chunk uses bq[st & 3]; loads run PD k-steps ahead (8 k-steps per
+  // chunk keep the ring index static across chunks) -- experiment (kernel_experiments_r3.md)
+  constexpr int PD = S2T_PD;
+  u32x4 bq[4][TN];
+#pragma unroll
+  for (int st = 0; st < PD; ++st) loadB(0, st >> 1, st & 1, bq[st]);
+#else
   u32x4 bcur[TN], bnxt[TN];
   loadB(0, 0, 0, bcur);
+#endif
   issue(0, 0);
   for (int ch = 0; ch < nch; ++ch) {
     const int stage = ch & 1;
@@ -171,8 +183,14 @@ __global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a) {
       // of MFMAs ahead of its use; then A fragment i + 1 is read while fragment i's 4 MFMAs
       // run (sched_group_barrier pins that interleave: left alone the scheduler sinks the B
       // loads below the MFMAs and the next step waits vmcnt(0) on a full L2 round trip)
+#if S2T_PD > 1
+      if (st + PD < 8) loadB(ch, (st + PD) >> 1, (st + PD) & 1, bq[(st + PD) & 3]);
+      else if (ch + 1 < nch) loadB(ch + 1, (st + PD - 8) >> 1, (st + PD - 8) & 1, bq[(st + PD) & 3]);
+      u32x4 (&bcur)[TN] = bq[st & 3];
+#else
       if (st < 7) loadB(ch, (st + 1) >> 1, (st + 1) & 1, bnxt);
       else if (ch + 1 < nch) loadB(ch + 1, 0, 0, bnxt);
+#endif
       const int toff = -(t >> 1) * G::HW - (t & 1);
       const int kc = ks * 4 + kq;
       // fragment i sits (i / FPR) rows and 16 (i % FPR) pixels from fragment 0: both multiples
@@ -203,8 +221,10 @@ __global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a) {
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // read fragment i + 2
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 2 * TN, 0);
+#if S2T_PD <= 1
 #pragma unroll
       for (int j = 0; j < TN; ++j) bcur[j] = bnxt[j];
+#endif
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();   // every wave done reading this stage before it is re-filled

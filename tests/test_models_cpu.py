@@ -151,3 +151,34 @@ def test_dropout_levels():
     assert g.drop_levels == {4, 5, 6}
     g7 = UnetGenerator(3, 3, 7, 64, "instance", use_dropout=True)
     assert g7.drop_levels == {4, 5}
+
+
+def test_vgg_tap_fusion_flags_and_cpu_loss_unchanged():
+    """VGGLoss turns on tap fusion (HIP path: tap relu' + parked L1 gradient added in the next
+    slice's conv); on the CPU oracle the flags are inert, so the loss and its gradient equal
+    the plain VGG19 perceptual loss."""
+    import torch
+    from p2p_pytorch_amd.models.vgg import VGGLoss, Vgg19
+    torch.manual_seed(0)
+    loss_f = VGGLoss()
+    feats = loss_f.vgg._feats
+    assert loss_f.vgg.tap_fusion
+    for prod, cons in Vgg19._TAPS:
+        assert feats[prod].out_gated
+        if cons is not None:
+            assert feats[cons].skip_grad == "take" and feats[cons].grad_gate == "relu"
+    plain = Vgg19()
+    plain.load_state_dict(loss_f.vgg.state_dict())
+    assert not plain.tap_fusion and not plain._feats[0].out_gated
+    x = (torch.rand(1, 3, 32, 32) * 2 - 1).requires_grad_(True)
+    y = torch.rand(1, 3, 32, 32) * 2 - 1
+    l1 = loss_f(x, y)
+    g1, = torch.autograd.grad(l1, x)
+    fx, fy = plain(x), plain(y)
+    l2 = sum(w * (a - b.detach()).abs().mean() for w, a, b in zip(VGGLoss.weights, fx, fy))
+    g2, = torch.autograd.grad(l2, x)
+    assert torch.allclose(l1, l2, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(g1, g2, rtol=1e-4, atol=1e-7)
+    # the target features reused across losses give the same value
+    fyc = loss_f.target_features(y)
+    assert torch.allclose(loss_f(x, y, fy=fyc), l1)
