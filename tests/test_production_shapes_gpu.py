@@ -3,7 +3,8 @@
 ``bench.py`` runs U-Net-256 + 70x70 PatchGAN at 256x256; the kernels it selects there (the
 256x256 LATE-ring forward tile, the 256x128 3-stage tile, MODE-1 class-fastest order for the
 stride-2 transposed convs / dgrads, the EXT dgrad epilogue with fused norm partials, the
-packed image head) are chosen by layer shape, and several only engage at the real M of a
+packed image head, and since round 3 the class-shared halo kernel of the stride-2 transposed
+convs, csrc/conv_s2t.hip) are chosen by layer shape, and several only engage at the real M of a
 256x256 batch.  This test runs ONE packed native ``Pix2PixStep`` (lr = 0) at 256x256,
 B = 64 (the smallest batch at which the 256x256 tiles engage: they need >= 256 tiles per
 launch), and bounds every loss and every G / D gradient against the same step in fp32 on stock
@@ -91,7 +92,11 @@ def test_headline_step_at_production_shape_matches_fp32():
             "256x128 3-stage": "conv_fwd_glds_kernel<256, 128, 4, 2,",
             "EXT epilogue": "true>(p2p::ConvFwdArgs)",
             "wgrad 256x128": "conv_wgrad_glds_kernel<256, 128",
-            "image head": "halo_union_kernel"}
+            "image head": "halo_union_kernel",
+            # round 3: the class-shared halo kernel of the stride-2 transposed convs / dgrads
+            # onto 64x64 grids (d2 forward with input ReLU, the EXT dgrads)
+            "s2t halo ConvT": "conv_s2t_kernel<64, true, false>",
+            "s2t halo EXT dgrad": "conv_s2t_kernel<64, false, true>"}
     missing = [k for k, pat in want.items() if not any(pat in n for n in names)]
     rows, bad = [], []
     for k in lc:
