@@ -382,10 +382,16 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   // Only for 64-wide grids with K = 4 taps x C <= 1024 (census B = 256, profiles/
   // kernel_experiments_r3.md): C = 512 (U-Net d3) and the 32-wide grids ran faster on the
   // 256x128 implicit-GEMM tile.
-  const bool s2t_ok = mode == 1 && !fp8 && splits == 1 && KH == 4 && KW == 4 && stride == 2 && pad == 1 &&
+  // fp8 (e4m3 activations / e5m2 gradients): the same layers on 128-channel chunks (the
+  // 128-B halo pixel of the bf16 kernel); no input activation on gradients, no extended
+  // epilogue on activations (as the implicit-GEMM fp8 tiles)
+  const int64_t s2t_chc = fp8 ? 128 : 64;
+  const bool s2t_ok = mode == 1 && splits == 1 && KH == 4 && KW == 4 && stride == 2 && pad == 1 &&
                       !reflect && up == 1 && OH == 2 * H && OW == 2 * W && W == 64 &&
-                      (H * W) % 128 == 0 && Cout % 64 == 0 && C1 % 64 == 0 && C2 % 64 == 0 && C1 + C2 <= 256 &&
+                      (H * W) % 128 == 0 && Cout % 64 == 0 && C1 % s2t_chc == 0 && C2 % s2t_chc == 0 &&
+                      C1 + C2 >= s2t_chc && C1 + C2 <= 256 &&
                       (act_in == 0 || (act_in == 1 && act_bwd == 0 && !res)) &&
+                      (fp8 != 2 || act_in == 0) && (fp8 != 1 || (!act_bwd && !res)) &&
                       std::getenv("P2P_NO_S2T") == nullptr;
   if (s2t_ok) bm = 128;
   Tensor ws;

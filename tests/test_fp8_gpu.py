@@ -99,6 +99,10 @@ FP8_CASES = [
     ("convT_concat64_norelu", 2, 64, 64, 16, 64, 4, 2, 1, None, True),
     ("convT_concat64_cout128", 2, 64, 64, 16, 128, 4, 2, 1, "relu", True),
     ("enc_concat64_relu_cout64", 2, 64, 64, 16, 64, 3, 1, 1, "relu", False),
+    # 64-wide grids with 128-channel multiples: the class-shared halo kernel (conv_s2t.hip F8)
+    ("s2t_convT_concat_relu", 4, 128, 128, 64, 64, 4, 2, 1, "relu", True),
+    ("s2t_convT_c128_cout128", 4, 128, 0, 64, 128, 4, 2, 1, None, True),
+    ("s2t_dgrad_c64_cout128", 4, 64, 0, 128, 128, 4, 2, 1, None, False),
 ]
 
 
@@ -118,13 +122,20 @@ def test_fp8_conv_fwd_dgrad_match_dequantised_oracle(case):
     xin1 = x1.detach().clone().requires_grad_(True)
     xin2 = x2.detach().clone().requires_grad_(True) if x2 is not None else None
     xin = (xin1, xin2) if xin2 is not None else xin1
-    if transposed:
-        y = ops.conv_transpose2d(xin, w, None, s, p, act_in=act_in)
-    else:
-        y = ops.conv2d(xin, w, None, s, p, act_in=act_in)
-    gy = rand_img(*y.shape, scale=1e-3, seed=3)     # gradient-sized values: e5m2 + scaling
-    y.backward(gy)
-    torch.cuda.synchronize()
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        if transposed:
+            y = ops.conv_transpose2d(xin, w, None, s, p, act_in=act_in)
+        else:
+            y = ops.conv2d(xin, w, None, s, p, act_in=act_in)
+        gy = rand_img(*y.shape, scale=1e-3, seed=3)     # gradient-sized values: e5m2 + scaling
+        y.backward(gy)
+        torch.cuda.synchronize()
+    if name.startswith("s2t_"):
+        names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
+        want = "conv_s2t_kernel<64, true, false, 1>" if act_in == "relu" else (
+            "conv_s2t_kernel<64, false, false, 1>" if transposed else "conv_s2t_kernel<64, false, false, 2>")
+        assert any(want in k for k in names), (want, sorted(set(names)))
 
     # the fp8 operands exactly as the kernels saw them
     kk = id(w)
@@ -299,3 +310,38 @@ def test_fp8_wgrad_matches_dequantised_oracle(case):
                           sites[2], sites[0], 1, 0, None, sites[1] if x2q is not None else None)
     assert ok, "fp8 wgrad kernel did not take the geometry"
     assert rel_err(gw, w.grad) < 1e-4, rel_err(gw, w.grad)
+
+
+def test_fp8_s2t_ext_dgrad_chain_matches_implicit_gemm(monkeypatch):
+    """conv s2 -> IN + lrelu -> conv s2 (U-Net encoder / PatchGAN) in fp8: the second conv's
+    input gradient runs on the fp8 halo kernel with the act' gate and the norm-backward
+    partials in its extended epilogue (conv_s2t_kernel<64, false, true, 2>); the same chain
+    with P2P_NO_S2T=1 (the implicit-GEMM fp8 tile) must agree up to fp8 scale / summation
+    order noise -- an indexing error (tap, chunk, source scale) is an O(1) difference."""
+    from torch.profiler import ProfilerActivity, profile
+    x = rand_img(4, 64, 256, 256, seed=9)
+    g = torch.Generator(device=DEV).manual_seed(11)
+    w1 = torch.randn(64, 64, 4, 4, device=DEV, generator=g) * 0.03
+    w2 = torch.randn(128, 64, 4, 4, device=DEV, generator=g) * 0.03
+
+    def run():
+        hip.begin_step()
+        hx, hw1, hw2 = (t.detach().clone().requires_grad_(True) for t in (x, w1, w2))
+        h = ops.instance_norm(ops.conv2d(hx, hw1, None, 2, 1, stats=True), act="lrelu")
+        z = ops.conv2d(h, hw2, None, 2, 1)
+        loss = (z.float() * torch.linspace(-1, 1, z.numel(), device=DEV).view_as(z)).sum()
+        loss.backward()
+        torch.cuda.synchronize()
+        return hx.grad, hw1.grad, hw2.grad
+
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        run()
+    names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
+    assert any("conv_s2t_kernel<64, false, true, 2>" in k for k in names), sorted(set(names))
+    outs = [run() for _ in range(2)]          # the second with settled fp8 scales
+    monkeypatch.setenv("P2P_NO_S2T", "1")
+    outs0 = [run() for _ in range(2)]
+    monkeypatch.delenv("P2P_NO_S2T")
+    errs = [rel_err(a, b) for a, b in zip(outs[1], outs0[1])]
+    print("fp8 s2t vs implicit GEMM:", errs)
+    assert all(e < 0.05 for e in errs), errs
