@@ -95,8 +95,8 @@ def test_headline_step_at_production_shape_matches_fp32():
             "image head": "halo_union_kernel",
             # round 3: the class-shared halo kernel of the stride-2 transposed convs / dgrads
             # onto 64x64 grids (d2 forward with input ReLU, the EXT dgrads)
-            "s2t halo ConvT": "conv_s2t_kernel<64, true, false>",
-            "s2t halo EXT dgrad": "conv_s2t_kernel<64, false, true>"}
+            "s2t halo ConvT": "conv_s2t_kernel<64, true, false, 0>",
+            "s2t halo EXT dgrad": "conv_s2t_kernel<64, false, true, 0>"}
     missing = [k for k, pat in want.items() if not any(pat in n for n in names)]
     rows, bad = [], []
     for k in lc:
