@@ -83,6 +83,9 @@ int p2p_adam_max_tensors();
 int p2p_union_weight(const float* w, int CinT, int CoutT, int co_off, int nv, int Nrows, int Cpad,
                      const float* bias, void* out, float* bias_out, hipStream_t st);
 int p2p_sum_partials(const float* ws, int nb, float scale, float* out, hipStream_t st);
+int p2p_rowsum_f32(const float* ws, long R, int C, float* out, hipStream_t st);
+int p2p_lincomb(const float* a, const float* b, float wa, float wb, float c, long n, float* out, hipStream_t st);
+int p2p_i64_add(long long* t, long long v, long n, hipStream_t st);
 int p2p_guard_flag(const float* const* v, int n, float* flag, float* counter, hipStream_t st);
 int p2p_adam(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
              const long* n, const float* lr, const float* step, const float* skip, float b1, float b2,
@@ -288,7 +291,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     const int64_t T = KH * KW;
     const int64_t Cvp = Cv <= 2 ? Cv : (Cv <= 4 ? 4 : (Cv <= 8 ? 8 : 16));
     const int64_t Ncol = ((T * Cvp + 7) / 8) * 8;
-    Tensor wv = at::zeros({Ncol, C}, w.options());
+    Tensor wv = at::empty({Ncol, C}, w.options());
+    (void)hipMemsetAsync(wv.data_ptr(), 0, wv.numel() * wv.element_size(), st);   // pad taps / rows
     wv.narrow(0, 0, T * Cvp).view({T, Cvp, C}).narrow(1, 0, Cv).copy_(
         w.reshape({-1}).narrow(0, 0, Cout * T * C).view({Cout, T, C}).narrow(0, 0, Cv).transpose(0, 1));
     Tensor col = empty_nhwc(N, Ncol, H, W, obf);
@@ -676,8 +680,8 @@ Tensor conv_d2s(const Tensor& x1, const optional<Tensor>& x2, const Tensor& w, c
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int blocks = std::max(1, std::min(h.ntiles, cus));
     Tensor part;
-    if (mode == 1) {
-      part = at::zeros({blocks}, x1.options().dtype(at::kFloat));
+    if (mode == 1) {   // every block (each owns >= 1 tile) writes its partial
+      part = at::empty({blocks}, x1.options().dtype(at::kFloat));
       h.l1_part = part.data_ptr<float>();
     }
     const int rc = p2p_halo_union(&h, act_in == 1 ? 1 : 0, blocks, st);
@@ -1547,6 +1551,47 @@ std::vector<Tensor> loss_bwd(const Tensor& a, const optional<Tensor>& b, int64_t
   return {ga, gb};
 }
 
+// ------------------------------------------------------------------ small-tensor helpers
+// out = wa * a + wb * b + c over fp32 tensors of one shape (the step's scalar bookkeeping)
+Tensor lincomb(const Tensor& a, const optional<Tensor>& b, double wa, double wb, double c) {
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kFloat && a.is_contiguous(), "lincomb: a fp32 contiguous");
+  TORCH_CHECK(!b || (b->scalar_type() == at::kFloat && b->is_contiguous() && b->numel() == a.numel()),
+              "lincomb: b like a");
+  Tensor out = at::empty_like(a);
+  check_rc(p2p_lincomb(a.data_ptr<float>(), b ? b->data_ptr<float>() : nullptr, (float)wa, (float)wb, (float)c,
+                       a.numel(), out.data_ptr<float>(), cur_stream(a)),
+           "lincomb");
+  return out;
+}
+
+// in place: t = wa * t + wb * b + c
+void lincomb_(Tensor t, const optional<Tensor>& b, double wa, double wb, double c) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), "lincomb_: t fp32 contiguous");
+  TORCH_CHECK(!b || (b->scalar_type() == at::kFloat && b->is_contiguous() && b->numel() == t.numel()),
+              "lincomb_: b like t");
+  check_rc(p2p_lincomb(t.data_ptr<float>(), b ? b->data_ptr<float>() : nullptr, (float)wa, (float)wb, (float)c,
+                       t.numel(), t.data_ptr<float>(), cur_stream(t)),
+           "lincomb_");
+}
+
+void i64_add_(Tensor t, int64_t v) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kLong && t.is_contiguous(), "i64_add_: int64 contiguous");
+  check_rc(p2p_i64_add(reinterpret_cast<long long*>(t.data_ptr<int64_t>()), (long long)v, t.numel(), cur_stream(t)),
+           "i64_add_");
+}
+
+// column sums of an fp32 [..., C] partial-sum image (rows in fixed order)
+Tensor rowsum(const Tensor& ws) {
+  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.dim() >= 1,
+              "rowsum: fp32 contiguous");
+  const int64_t C = ws.size(-1);
+  Tensor out = at::empty({C}, ws.options());
+  check_rc(p2p_rowsum_f32(ws.data_ptr<float>(), ws.numel() / std::max<int64_t>(C, 1), (int)C,
+                          out.data_ptr<float>(), cur_stream(ws)),
+           "rowsum");
+  return out;
+}
+
 // ------------------------------------------------------------------ optimizer
 void adam(at::TensorList p, at::TensorList g, at::TensorList m, at::TensorList v, const Tensor& lr,
           const Tensor& step, double b1, double b2, double eps, double wd, const optional<Tensor>& skip) {
@@ -1656,6 +1701,10 @@ TORCH_LIBRARY(p2p, m) {
   m.def("pad_channels_into(Tensor a, Tensor? b, Tensor(a!) out) -> ()");
   m.def("slice_channels(Tensor x, int c0, int C) -> Tensor");
   m.def("colsum(Tensor x, Tensor(a!) out, float scale, bool accumulate) -> ()");
+  m.def("lincomb(Tensor a, Tensor? b, float wa, float wb, float c) -> Tensor");
+  m.def("lincomb_(Tensor(a!) t, Tensor? b, float wa, float wb, float c) -> ()");
+  m.def("i64_add_(Tensor(a!) t, int v) -> ()");
+  m.def("rowsum(Tensor ws) -> Tensor");
   m.def("guard_flag(Tensor[] losses, Tensor(a!)? counter) -> Tensor");
   m.def("loss_fwd(Tensor a, Tensor? b, int kind, float t, float scale) -> Tensor");
   m.def("loss_bwd(Tensor a, Tensor? b, int kind, float t, float scale, Tensor gout, bool need_a, "
@@ -1699,6 +1748,10 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("pixel_shuffle", pixel_shuffle);
   m.impl("slice_channels", slice_channels);
   m.impl("colsum", colsum);
+  m.impl("lincomb", lincomb);
+  m.impl("lincomb_", lincomb_);
+  m.impl("i64_add_", i64_add_);
+  m.impl("rowsum", rowsum);
   m.impl("loss_fwd", loss_fwd);
   m.impl("loss_bwd", loss_bwd);
   m.impl("adam", adam);

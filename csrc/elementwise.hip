@@ -538,6 +538,22 @@ __global__ void guard_flag_kernel(GuardArgs a, float* flag, float* counter) {
 }
 }  // namespace p2p
 
+// ---------------------------------------------------------------- small-tensor helpers
+// The step's scalar bookkeeping (loss composition, the optimizer's step counter, the dropout
+// seed) on HIP kernels instead of PyTorch elementwise ops: out = wa * a + wb * b + c.
+__global__ void __launch_bounds__(256) lincomb_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                      float wa, float wb, float c, long n, float* out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float v = wa * a[i] + (b ? wb * b[i] : 0.f) + c;
+  out[i] = v;
+}
+
+__global__ void __launch_bounds__(64) i64_add_kernel(long long* t, long long v, long n) {
+  const long i = (long)blockIdx.x * 64 + threadIdx.x;
+  if (i < n) t[i] += v;
+}
+
 extern "C" {
 
 int p2p_act(const void* a, const void* b, long n, int act, int mode, void* out, hipStream_t st) {
@@ -668,6 +684,27 @@ int p2p_loss_bwd(const void* a, const void* b, int is_f32, long n, int kind, flo
     hipLaunchKernelGGL(loss_grad_kernel, dim3(egrid(n)), dim3(256), 0, st, a, b, is_f32, n, kind, t, scale,
                        gout, ga, gb);
   }
+  return (int)hipGetLastError();
+}
+
+
+// out[c] = sum_r ws[r][c] for an fp32 [R][C] partial-sum image (fixed order)
+int p2p_rowsum_f32(const float* ws, long R, int C, float* out, hipStream_t st) {
+  using namespace p2p;
+  if (R <= 0 || R > 0x7fffffff) return -1;
+  hipLaunchKernelGGL(colsum_final_kernel<32>, dim3((C + 7) / 8), dim3(256), 0, st, ws, (int)R, C, 1.f, 0, out);
+  return (int)hipGetLastError();
+}
+
+int p2p_lincomb(const float* a, const float* b, float wa, float wb, float c, long n, float* out, hipStream_t st) {
+  using namespace p2p;
+  hipLaunchKernelGGL(lincomb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, b, wa, wb, c, n, out);
+  return (int)hipGetLastError();
+}
+
+int p2p_i64_add(long long* t, long long v, long n, hipStream_t st) {
+  using namespace p2p;
+  hipLaunchKernelGGL(i64_add_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, t, v, n);
   return (int)hipGetLastError();
 }
 

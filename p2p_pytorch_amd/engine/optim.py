@@ -70,12 +70,12 @@ class FusedAdam(torch.optim.Optimizer):
                 m2.append(st["exp_avg_sq"])
             if not params:
                 continue
-            if not capturing:
-                self._lr_t[gi].fill_(float(group["lr"]))
-            if skip is None:
-                self._step_t[gi].add_(1.0)
-            else:
-                self._step_t[gi].add_(1.0 - skip.reshape(1))
+            if not capturing:   # lr mirrored into the device tensor (HIP kernel: t = lr)
+                hip.P().lincomb_(self._lr_t[gi], None, 0.0, 0.0, float(group["lr"]))
+            # step += 1 - skip on the device (HIP kernel)
+            hip.P().lincomb_(self._step_t[gi],
+                             None if skip is None else skip.reshape(1).float().contiguous(),
+                             1.0, -1.0, 1.0)
             b1, b2 = group["betas"]
             hip.adam_(params, grads, m1, m2, self._lr_t[gi], self._step_t[gi], b1, b2,
                       group["eps"], group["weight_decay"],

@@ -88,6 +88,15 @@ class Pix2PixStep:
             return torch.autocast(device_type=device.type, dtype=self.autocast_dtype)
         return contextlib.nullcontext()
 
+    def _seed_grad(self, loss):
+        """d(loss)/d(loss) = 1 as a persistent device tensor (no fill kernel per backward)."""
+        seeds = self.__dict__.setdefault("_seeds", {})
+        key = (loss.device, loss.dtype, tuple(loss.shape))
+        s = seeds.get(key)
+        if s is None:
+            s = seeds[key] = torch.ones(loss.shape, device=loss.device, dtype=loss.dtype)
+        return s
+
     @staticmethod
     def _zero(opt, reducer):
         # with a reducer, grads are views into its flat buckets: zero in place
@@ -148,13 +157,14 @@ class Pix2PixStep:
         with self._phase("D_fwd"):
             set_requires_grad(netD, True)
             pred = netD(dd)                   # [D(A | fake.detach()); D(A | B)], one 2B pass
-            loss_D_fake = self.criterionGAN(pred[:B], False)
-            loss_D_real = self.criterionGAN(pred[B:], True)
-            loss_D = (loss_D_fake + loss_D_real) * 0.5
+            pred_fake, pred_real = hip.batch_halves(pred, B)
+            loss_D_fake = self.criterionGAN(pred_fake, False)
+            loss_D_real = self.criterionGAN(pred_real, True)
+            loss_D = hip.lincomb(loss_D_fake, loss_D_real, 0.5, 0.5)
         with self._phase("D_bwd_opt"):
             self._zero(self.opt_D, self.reducer_d)
             with hip.wgrad_overlap(real_A.device, enabled=self.reducer_d is None):
-                loss_D.backward()
+                loss_D.backward(self._seed_grad(loss_D))
             if self.reducer_d is not None:
                 self.reducer_d.finish()
             self._guarded_step(self.opt_D, self.reducer_d, loss_D)
@@ -165,11 +175,11 @@ class Pix2PixStep:
             loss_G_GAN = self.criterionGAN(pred_fake, True)
             # the L1 term's gradient is fused into D's first-conv dgrad; the tap hands that
             # kernel dL/d(L1) on the device (any weighting of the L1 term is honoured)
-            loss_G = loss_G_GAN + hip.head_l1_tap(loss_G_L1)
+            loss_G = hip.lincomb(loss_G_GAN, hip.head_l1_tap(loss_G_L1))
         with self._phase("G_bwd_opt"):
             self._zero(self.opt_G, self.reducer_g)
             with hip.wgrad_overlap(real_A.device, enabled=self.reducer_g is None):
-                loss_G.backward()
+                loss_G.backward(self._seed_grad(loss_G))
             hip.assert_no_deferred()          # every parked U-Net skip gradient consumed
             if self.reducer_g is not None:
                 self.reducer_g.finish()

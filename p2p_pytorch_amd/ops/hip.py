@@ -366,13 +366,24 @@ def prepare_weights(*modules):
         cache[key] = (w._version, _gen[0], img)
 
 
+_BIAS_PAD = {}
+
+
 def _bias_padded(b, coutp):
+    """fp32 bias padded to ``coutp`` columns: a persistent zero-tailed buffer per parameter,
+    refreshed by a device copy each call (stream-ordered, graph-capturable; no pad kernel)."""
     if b is None:
         return None
     b = b.detach().float()
     if b.numel() == coutp:
         return b.contiguous()
-    return torch.nn.functional.pad(b, (0, coutp - b.numel()))
+    key = (b.data_ptr(), coutp, b.device)
+    buf = _BIAS_PAD.get(key)
+    if buf is None:
+        buf = torch.zeros(coutp, device=b.device, dtype=torch.float32)
+        _BIAS_PAD[key] = buf
+    buf[: b.numel()].copy_(b)
+    return buf
 
 
 def _seed(device):
@@ -391,7 +402,7 @@ def advance_rng(device=None):
         _seed(device)
     for d, s in _seeds.items():
         if device is None or d == device:
-            s.add_(1)
+            P().i64_add_(s, 1)
 
 
 # ============================================================== convolution
@@ -734,7 +745,7 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
             g_half = gx1 if nbh[0] == 1 else gx2
             if g_half is not None:
                 if nbh[1] is _CS:
-                    _stash_colsum(g_half, nbp[0].sum((0, 1)))
+                    _stash_colsum(g_half, P().rowsum(nbp[0]))
                 else:
                     _stash_nbp(g_half, nbp)
         if not need_x1:
@@ -821,7 +832,9 @@ def _head_dgrad(head, af, weight, gy):
     ab, scale, state = head
     img, _ = P().union_weight(weight.detach().float().contiguous(), 3, 3, UNION_ROWS,
                               gy.shape[1], None)
-    zb = torch.zeros(UNION_ROWS, device=gy.device, dtype=torch.float32)
+    zb = _ZB.get(gy.device)
+    if zb is None:     # the dgrad's (absent) bias: a persistent zero vector, read only
+        zb = _ZB[gy.device] = torch.zeros(UNION_ROWS, device=gy.device, dtype=torch.float32)
     dz = torch.empty_like(af, memory_format=CL)
     tapped = state.tap_ran
     P().conv_d2s(gy, None, img, zb, 0, 0, 2, dz, ab, af, float(scale) if tapped else 0.0,
@@ -831,12 +844,16 @@ def _head_dgrad(head, af, weight, gy):
     return dz
 
 
+_ZB = {}
+
+
 class _HeadL1State:
-    """Per-forward hand-off between the L1 value's gradient tap and the head's fused dgrad."""
+    """Per-forward hand-off between the L1 value's gradient tap and the head's fused dgrad
+    (``weight`` is read only after the tap has written it)."""
     __slots__ = ("weight", "tap_ran")
 
     def __init__(self, device):
-        self.weight = torch.ones(1, device=device, dtype=torch.float32)
+        self.weight = torch.empty(1, device=device, dtype=torch.float32)
         self.tap_ran = False
 
 
@@ -1217,6 +1234,58 @@ class AddActFn(torch.autograd.Function):
 
 def add_act(a, b, name, defer_b=False):
     return AddActFn.apply(a, b, name, defer_b)
+
+
+class LinCombFn(torch.autograd.Function):
+    """wa * a + wb * b of fp32 loss scalars (the step's loss composition) on a HIP kernel."""
+
+    @staticmethod
+    def forward(ctx, a, b, wa, wb):
+        ctx.w = (wa, wb)
+        return P().lincomb(a.float().contiguous(), b.float().contiguous(), wa, wb, 0.0)
+
+    @staticmethod
+    def backward(ctx, g):
+        wa, wb = ctx.w
+        g = g.float().contiguous()
+        ga = P().lincomb(g, None, wa, 0.0, 0.0) if ctx.needs_input_grad[0] else None
+        gb = P().lincomb(g, None, wb, 0.0, 0.0) if ctx.needs_input_grad[1] else None
+        return ga, gb, None, None
+
+
+def lincomb(a, b, wa=1.0, wb=1.0):
+    """``wa * a + wb * b`` for same-shape fp32 tensors (loss scalars)."""
+    return LinCombFn.apply(a, b, float(wa), float(wb))
+
+
+class _BatchHalvesFn(torch.autograd.Function):
+    """(x[:n], x[n:]) whose gradients are written into one buffer by two device copies --
+    instead of two slice backwards (a zero fill each) and an accumulate."""
+
+    @staticmethod
+    def forward(ctx, x, n):
+        ctx.n = n
+        ctx.shape, ctx.dtype = x.shape, x.dtype
+        ctx.cl = x.dim() == 4 and x.is_contiguous(memory_format=CL)
+        return x.narrow(0, 0, n), x.narrow(0, n, x.shape[0] - n)
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        n = ctx.n
+        ref = g1 if g1 is not None else g2
+        mf = CL if ctx.cl else torch.contiguous_format
+        out = torch.empty(ctx.shape, device=ref.device, dtype=ctx.dtype, memory_format=mf)
+        for g, lo, ln in ((g1, 0, n), (g2, n, ctx.shape[0] - n)):
+            dst = out.narrow(0, lo, ln)
+            if g is None:
+                dst.zero_()
+            else:
+                dst.copy_(g)
+        return out, None
+
+
+def batch_halves(x, n):
+    return _BatchHalvesFn.apply(x, n)
 
 
 class DropoutFn(torch.autograd.Function):
