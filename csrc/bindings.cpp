@@ -86,6 +86,8 @@ int p2p_sum_partials(const float* ws, int nb, float scale, float* out, hipStream
 int p2p_rowsum_f32(const float* ws, long R, int C, float* out, hipStream_t st);
 int p2p_lincomb(const float* a, const float* b, float wa, float wb, float c, long n, float* out, hipStream_t st);
 int p2p_i64_add(long long* t, long long v, long n, hipStream_t st);
+int p2p_lincomb_n(const float* const* p, const float* w, int n, float* out, hipStream_t st);
+int p2p_scale_n(const float* g, const float* w, int n, float* out, hipStream_t st);
 int p2p_guard_flag(const float* const* v, int n, float* flag, float* counter, hipStream_t st);
 int p2p_adam(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
              const long* n, const float* lr, const float* step, const float* skip, float b1, float b2,
@@ -1580,6 +1582,33 @@ void i64_add_(Tensor t, int64_t v) {
            "i64_add_");
 }
 
+// sum_i w_i * t_i over up to 16 one-element fp32 tensors (a composed loss) -> 0-d tensor
+Tensor lincomb_n(at::TensorList ts, at::ArrayRef<double> ws) {
+  TORCH_CHECK(!ts.empty() && ts.size() <= 16 && ts.size() == ws.size(), "lincomb_n: 1..16 terms, one weight each");
+  std::vector<const float*> p;
+  std::vector<float> w;
+  for (size_t i = 0; i < ts.size(); ++i) {
+    TORCH_CHECK(ts[i].is_cuda() && ts[i].scalar_type() == at::kFloat && ts[i].numel() == 1, "lincomb_n: fp32 scalars");
+    p.push_back(ts[i].data_ptr<float>());
+    w.push_back((float)ws[i]);
+  }
+  Tensor out = at::empty({}, ts[0].options());
+  check_rc(p2p_lincomb_n(p.data(), w.data(), (int)p.size(), out.data_ptr<float>(), cur_stream(ts[0])), "lincomb_n");
+  return out;
+}
+
+// [n] = w_i * g (the n-term sum's backward)
+Tensor scale_n(const Tensor& g, at::ArrayRef<double> ws) {
+  TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kFloat && g.numel() == 1 && ws.size() >= 1 && ws.size() <= 16,
+              "scale_n: fp32 scalar, 1..16 weights");
+  std::vector<float> w(ws.begin(), ws.end());
+  Tensor gc = g.contiguous();
+  Tensor out = at::empty({(int64_t)w.size()}, g.options());
+  check_rc(p2p_scale_n(gc.data_ptr<float>(), w.data(), (int)w.size(), out.data_ptr<float>(), cur_stream(g)),
+           "scale_n");
+  return out;
+}
+
 // column sums of an fp32 [..., C] partial-sum image (rows in fixed order)
 Tensor rowsum(const Tensor& ws) {
   TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.dim() >= 1,
@@ -1705,6 +1734,8 @@ TORCH_LIBRARY(p2p, m) {
   m.def("lincomb_(Tensor(a!) t, Tensor? b, float wa, float wb, float c) -> ()");
   m.def("i64_add_(Tensor(a!) t, int v) -> ()");
   m.def("rowsum(Tensor ws) -> Tensor");
+  m.def("lincomb_n(Tensor[] ts, float[] ws) -> Tensor");
+  m.def("scale_n(Tensor g, float[] ws) -> Tensor");
   m.def("guard_flag(Tensor[] losses, Tensor(a!)? counter) -> Tensor");
   m.def("loss_fwd(Tensor a, Tensor? b, int kind, float t, float scale) -> Tensor");
   m.def("loss_bwd(Tensor a, Tensor? b, int kind, float t, float scale, Tensor gout, bool need_a, "
@@ -1752,6 +1783,8 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("lincomb_", lincomb_);
   m.impl("i64_add_", i64_add_);
   m.impl("rowsum", rowsum);
+  m.impl("lincomb_n", lincomb_n);
+  m.impl("scale_n", scale_n);
   m.impl("loss_fwd", loss_fwd);
   m.impl("loss_bwd", loss_bwd);
   m.impl("adam", adam);

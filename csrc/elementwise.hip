@@ -549,6 +549,26 @@ __global__ void __launch_bounds__(256) lincomb_kernel(const float* __restrict__ 
   out[i] = v;
 }
 
+// n-term weighted sum of fp32 scalars (a loss composed of up to 16 weighted terms) and its
+// backward (g * w_i into slot i): one launch each
+struct LinList {
+  const float* p[16];
+  float w[16];
+  int n;
+};
+
+__global__ void __launch_bounds__(64) lincomb_n_kernel(LinList l, float* out) {
+  if (threadIdx.x != 0) return;
+  float s = 0.f;
+  for (int i = 0; i < l.n; ++i) s += l.w[i] * l.p[i][0];
+  out[0] = s;
+}
+
+__global__ void __launch_bounds__(64) scale_n_kernel(const float* g, LinList l, float* out) {
+  const int i = threadIdx.x;
+  if (i < l.n) out[i] = l.w[i] * g[0];
+}
+
 __global__ void __launch_bounds__(64) i64_add_kernel(long long* t, long long v, long n) {
   const long i = (long)blockIdx.x * 64 + threadIdx.x;
   if (i < n) t[i] += v;
@@ -705,6 +725,29 @@ int p2p_lincomb(const float* a, const float* b, float wa, float wb, float c, lon
 int p2p_i64_add(long long* t, long long v, long n, hipStream_t st) {
   using namespace p2p;
   hipLaunchKernelGGL(i64_add_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, t, v, n);
+  return (int)hipGetLastError();
+}
+
+int p2p_lincomb_n(const float* const* p, const float* w, int n, float* out, hipStream_t st) {
+  using namespace p2p;
+  if (n < 1 || n > 16) return -1;
+  LinList l{};
+  for (int i = 0; i < n; ++i) {
+    l.p[i] = p[i];
+    l.w[i] = w[i];
+  }
+  l.n = n;
+  hipLaunchKernelGGL(lincomb_n_kernel, dim3(1), dim3(64), 0, st, l, out);
+  return (int)hipGetLastError();
+}
+
+int p2p_scale_n(const float* g, const float* w, int n, float* out, hipStream_t st) {
+  using namespace p2p;
+  if (n < 1 || n > 16) return -1;
+  LinList l{};
+  for (int i = 0; i < n; ++i) l.w[i] = w[i];
+  l.n = n;
+  hipLaunchKernelGGL(scale_n_kernel, dim3(1), dim3(64), 0, st, g, l, out);
   return (int)hipGetLastError();
 }
 

@@ -132,6 +132,15 @@ class CompressGANStep:
             return hip.wgrad_overlap(x.device, enabled=reducer is None)
         return contextlib.nullcontext()
 
+    def _seed_grad(self, loss):
+        """d(loss)/d(loss) = 1 as a persistent tensor (no fill kernel per backward)."""
+        seeds = self.__dict__.setdefault("_seeds", {})
+        key = (loss.device, loss.dtype, tuple(loss.shape))
+        s = seeds.get(key)
+        if s is None:
+            s = seeds[key] = torch.ones(loss.shape, device=loss.device, dtype=loss.dtype)
+        return s
+
     def _zero(self, opt, reducer):
         if reducer is not None:
             reducer.zero_grad()
@@ -155,7 +164,10 @@ class CompressGANStep:
         loss_d_fake = self.criterionGAN(pred_fake, False)
         pred_real = D(self._d_in(real_a, real_b.detach()))
         loss_d_real = self.criterionGAN(pred_real, True)
-        loss_d = (loss_d_fake + loss_d_real) * 0.5
+        if real_a.is_cuda and _native.get_backend() == "native":
+            loss_d = ops.lincomb_n([loss_d_fake, loss_d_real], [0.5, 0.5])
+        else:
+            loss_d = (loss_d_fake + loss_d_real) * 0.5
         # ---- G losses: D frozen (its G-loss gradients are discarded by the reference)
         set_requires_grad(self._d_trainable, False)
         pred_fake_g = D(self._d_in(real_a, fake_b))
@@ -163,31 +175,46 @@ class CompressGANStep:
         # requires grad, which would silently drop the D-loss gradients
         set_requires_grad(self._d_trainable, True)
         loss_g_gan = self.criterionGAN(pred_fake_g, True)
-        loss_feat = 0.0
         fgate = getattr(D, "feature_grad_gate", None)   # D's lrelu' rides in these gradients
-        for i in range(len(pred_fake_g)):
-            for j in range(len(pred_fake_g[i]) - 1):
-                loss_feat = loss_feat + self.d_weights * self.feat_weights * ops.l1(
-                    pred_fake_g[i][j], pred_real[i][j].detach(), gate_a=fgate) * self.lambda_feat
+        feat = [ops.l1(pred_fake_g[i][j], pred_real[i][j].detach(), gate_a=fgate)
+                for i in range(len(pred_fake_g)) for j in range(len(pred_fake_g[i]) - 1)]
+        # native: the loss compositions are one HIP launch each way (ops.lincomb_n); the torch
+        # path keeps the reference's expression order (bitwise parity on CPU)
+        native = real_a.is_cuda and _native.get_backend() == "native"
+        if native and feat:
+            fw = self.d_weights * self.feat_weights * self.lambda_feat
+            loss_feat = ops.lincomb_n(feat, [fw] * len(feat))
+        else:
+            loss_feat = 0.0
+            for f in feat:
+                loss_feat = loss_feat + self.d_weights * self.feat_weights * f * self.lambda_feat
         # VGG(real_b): once per step for both perceptual losses against it (G and C phase)
         fy_real = (self.criterionVGG.target_features(real_b)
                    if hasattr(self.criterionVGG, "target_features")
                    and os.environ.get("P2P_VGG_REUSE", "1") != "0" else None)
-        content = self._vgg(fake_b, real_b, fy_real) * self.lambda_vgg
+        vgg_g = self._vgg(fake_b, real_b, fy_real)
         tv = calc_tv_Loss(fake_b)
-        loss_g = loss_g_gan + loss_feat + content + tv * self.lambda_tv
+        if native:
+            terms = [loss_g_gan] + ([loss_feat] if feat else []) + [vgg_g, tv]
+            loss_g = ops.lincomb_n(terms, [1.0] + ([1.0] if feat else []) + [self.lambda_vgg,
+                                                                           self.lambda_tv])
+            with torch.no_grad():
+                content = ops.lincomb_n([vgg_g.detach()], [self.lambda_vgg])
+        else:
+            content = vgg_g * self.lambda_vgg
+            loss_g = loss_g_gan + loss_feat + content + tv * self.lambda_tv
         # ---- updates: G first (its backward also reaches D; those grads are dropped)
         with self._phase("G_bwd_opt"):
             self._zero(self.opt_g, self.reducer_g)
             with self._wgrad_overlap(real_a, self.reducer_g):
-                loss_g.backward()
+                loss_g.backward(self._seed_grad(loss_g))
             self._no_deferred(real_a)   # every parked VGG-tap gradient was consumed
             if self.reducer_g is not None:
                 self.reducer_g.finish()
             self._opt_step(self.opt_g, self.reducer_g, loss_g)
         with self._phase("D_bwd_opt"):
             self._zero(self.opt_d, self.reducer_d)
-            loss_d.backward()
+            loss_d.backward(self._seed_grad(loss_d))
             if self.reducer_d is not None:
                 self.reducer_d.finish()
             self._opt_step(self.opt_d, self.reducer_d, loss_d)
@@ -195,8 +222,9 @@ class CompressGANStep:
         need_graph = self.train_c or self.c_phase_backward
         with torch.set_grad_enabled(need_graph):
             fake_ac = G(compressed)     # also advances G's BN running stats, as the reference
-            loss_c = ops.mse(fake_ac, real_b) + self._vgg(compressed, real_b, fy_real) * \
-                self.lambda_vgg
+            mse_c, vgg_c = ops.mse(fake_ac, real_b), self._vgg(compressed, real_b, fy_real)
+            loss_c = (ops.lincomb_n([mse_c, vgg_c], [1.0, self.lambda_vgg]) if native
+                      else mse_c + vgg_c * self.lambda_vgg)
         paused_g = (self.reducer_g.paused() if self.reducer_g is not None
                     else contextlib.nullcontext())
         if self.train_c:

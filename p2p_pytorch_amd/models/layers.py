@@ -10,7 +10,7 @@ import os
 import torch
 import torch.nn as nn
 
-from .. import ops
+from .. import _native, ops
 
 
 class Conv2d(nn.Conv2d):
@@ -130,7 +130,10 @@ class BatchNorm2d(nn.BatchNorm2d):
         """``prelu``: slope Parameter of a following shared-slope PReLU, fused in."""
         training = self.training or not self.track_running_stats
         if self.training and self.track_running_stats:
-            self.num_batches_tracked.add_(1)
+            if self.num_batches_tracked.is_cuda and _native.use_native(x):
+                _native.ops().i64_add_(self.num_batches_tracked, 1)   # HIP kernel, not aten
+            else:
+                self.num_batches_tracked.add_(1)
         return ops.batch_norm(x, self.running_mean if self.track_running_stats else None,
                               self.running_var if self.track_running_stats else None,
                               self.weight, self.bias, training, self.momentum, self.eps, self.act,

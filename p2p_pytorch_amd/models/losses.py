@@ -46,10 +46,8 @@ class GANLoss(nn.Module):
     def forward(self, pred, target_is_real):
         if isinstance(pred, (list, tuple)):
             if isinstance(pred[0], (list, tuple)):
-                loss = 0
-                for p in pred:
-                    loss = loss + self._one(p[-1], target_is_real)
-                return loss
+                terms = [self._one(p[-1], target_is_real) for p in pred]
+                return ops.lincomb_n(terms, [1.0] * len(terms))
             return self._one(pred[-1], target_is_real)
         return self._one(pred, target_is_real)
 

@@ -149,11 +149,12 @@ class VGGLoss(nn.Module):
         fx = self.vgg(x)
         if fy is None:
             fy = self.target_features(y)
-        loss = 0
+        terms = []
         fused = self.vgg.tap_fusion
-        for i, (w, a, b) in enumerate(zip(self.weights, fx, fy)):
+        for i, (a, b) in enumerate(zip(fx, fy)):
             if fused:   # relu' of the tap in the L1 gradient, parked for the next slice's conv
-                loss = loss + w * ops.l1(a, b.detach(), gate_a="relu", defer=i < len(fx) - 1)
+                terms.append(ops.l1(a, b.detach(), gate_a="relu", defer=i < len(fx) - 1))
             else:
-                loss = loss + w * ops.l1(a, b.detach())
-        return loss
+                terms.append(ops.l1(a, b.detach()))
+        # the weighted sum in one launch each way on the native path (ops.lincomb_n)
+        return ops.lincomb_n(terms, self.weights[:len(terms)])

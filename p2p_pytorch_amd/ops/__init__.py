@@ -158,6 +158,19 @@ def l2_normalize_channels(x, eps=1e-12, residual=None):
     return y if residual is None else y + residual
 
 
+def lincomb_n(terms, weights):
+    """``sum(w * t)`` of loss scalars: one HIP launch each way for GPU tensors on the native
+    backend (python-float terms allowed only on the torch path)."""
+    ts = [t for t in terms if isinstance(t, torch.Tensor)]
+    if ts and len(ts) == len(terms) and _native.use_native(ts[0]) and all(
+            t.dtype == torch.float32 and t.numel() == 1 for t in ts):
+        return _hip().lincomb_n(terms, weights)
+    out = 0
+    for t, w in zip(terms, weights):
+        out = out + w * t
+    return out
+
+
 def pixel_shuffle(x, r):
     if _native.use_native(x):
         return _hip().pixel_shuffle(x, r)

@@ -1258,6 +1258,42 @@ def lincomb(a, b, wa=1.0, wb=1.0):
     return LinCombFn.apply(a, b, float(wa), float(wb))
 
 
+class LinCombNFn(torch.autograd.Function):
+    """sum_i w_i * t_i of up to 16 fp32 loss scalars: one HIP launch forward, one backward
+    (the composed losses of the reference step: GAN + feature matching + VGG + TV ...)."""
+
+    @staticmethod
+    def forward(ctx, ws, *ts):
+        ctx.ws = ws
+        return P().lincomb_n([t.float() for t in ts], list(ws))
+
+    @staticmethod
+    def backward(ctx, g):
+        gs = P().scale_n(g.float(), list(ctx.ws))
+        return (None,) + tuple(gs[i] for i in range(len(ctx.ws)))
+
+
+def lincomb_n(terms, weights):
+    """``sum(w * t)`` over fp32 scalar tensors (python-float terms are constants and are
+    dropped from the gradient; at most 16 tensor terms per launch)."""
+    ts, ws, const = [], [], 0.0
+    for t, w in zip(terms, weights):
+        if isinstance(t, torch.Tensor):
+            ts.append(t)
+            ws.append(float(w))
+        else:
+            const += float(w) * float(t)
+    if const != 0.0 or not ts:
+        raise ValueError("lincomb_n: tensor terms only")
+    out = None
+    for i in range(0, len(ts), 15):      # chains of 15 + the running total
+        chunk_t, chunk_w = ts[i:i + 15], ws[i:i + 15]
+        if out is not None:
+            chunk_t, chunk_w = [out] + chunk_t, [1.0] + chunk_w
+        out = LinCombNFn.apply(tuple(chunk_w), *chunk_t)
+    return out
+
+
 class _BatchHalvesFn(torch.autograd.Function):
     """(x[:n], x[n:]) whose gradients are written into one buffer by two device copies --
     instead of two slice backwards (a zero fill each) and an accumulate."""
