@@ -22,7 +22,10 @@
 extern "C" {
 long p2p_sn_ws_floats(int h, int wd);
 int p2p_sn_power_iter(const float* W, int h, int wd, float* u, float* v, float* sigma, float* ws,
-                      hipStream_t st);
+                      float* scale, hipStream_t st);
+int p2p_sn_wgrad_blocks(long n);
+int p2p_sn_wgrad(const float* G, const float* W, const float* u, const float* v, const float* scale, int h,
+                 int wd, float* part, float* out, hipStream_t st);
 long p2p_norm_ws_floats(int N, int HW, int C);
 int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, const float* partials,
                           float eps, const float* gamma, const float* beta, const float* prelu_w,
@@ -1422,9 +1425,43 @@ Tensor sn_power_iter(const Tensor& w, Tensor u, Tensor v) {
   Tensor ws = at::empty({p2p_sn_ws_floats((int)h, (int)wd)}, w.options());
   Tensor sigma = at::empty({}, w.options());
   check_rc(p2p_sn_power_iter(w.data_ptr<float>(), (int)h, (int)wd, u.data_ptr<float>(), v.data_ptr<float>(),
-                             sigma.data_ptr<float>(), ws.data_ptr<float>(), cur_stream(w)),
+                             sigma.data_ptr<float>(), ws.data_ptr<float>(), nullptr, cur_stream(w)),
            "sn_power_iter");
   return sigma;
+}
+
+// one power iteration, returning 1 / sigma (the conv epilogues' scale; no autograd here --
+// sn_wgrad carries the sigma path of the weight gradient)
+Tensor sn_scale(const Tensor& w, Tensor u, Tensor v) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.dim() == 2,
+              "sn_scale: fp32 contiguous [h][wd] weight");
+  const int64_t h = w.size(0), wd = w.size(1);
+  TORCH_CHECK(u.scalar_type() == at::kFloat && u.is_contiguous() && u.numel() == h, "sn_scale: u");
+  TORCH_CHECK(v.scalar_type() == at::kFloat && v.is_contiguous() && v.numel() == wd, "sn_scale: v");
+  Tensor ws = at::empty({p2p_sn_ws_floats((int)h, (int)wd) + 1}, w.options());
+  Tensor scale = at::empty({1}, w.options());
+  check_rc(p2p_sn_power_iter(w.data_ptr<float>(), (int)h, (int)wd, u.data_ptr<float>(), v.data_ptr<float>(),
+                             ws.data_ptr<float>() + p2p_sn_ws_floats((int)h, (int)wd), ws.data_ptr<float>(),
+                             scale.data_ptr<float>(), cur_stream(w)),
+           "sn_scale");
+  return scale;
+}
+
+// dL/dW_bar of a spectral-norm conv from its conv weight gradient G (see csrc/sn.hip)
+Tensor sn_wgrad(const Tensor& G, const Tensor& w, const Tensor& u, const Tensor& v, const Tensor& scale) {
+  TORCH_CHECK(G.is_cuda() && G.scalar_type() == at::kFloat && G.is_contiguous(), "sn_wgrad: G fp32 contiguous");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == G.numel(), "sn_wgrad: W like G");
+  const int64_t h = u.numel(), wd = v.numel();
+  TORCH_CHECK(h * wd == G.numel() && u.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat &&
+                  u.is_contiguous() && v.is_contiguous(), "sn_wgrad: u / v");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() == 1, "sn_wgrad: scale");
+  Tensor part = at::empty({p2p_sn_wgrad_blocks(h * wd)}, G.options());
+  Tensor out = at::empty_like(G);
+  check_rc(p2p_sn_wgrad(G.data_ptr<float>(), w.data_ptr<float>(), u.data_ptr<float>(), v.data_ptr<float>(),
+                        scale.data_ptr<float>(), (int)h, (int)wd, part.data_ptr<float>(), out.data_ptr<float>(),
+                        cur_stream(G)),
+           "sn_wgrad");
+  return out;
 }
 
 // ------------------------------------------------------------------ fp8 (csrc/fp8.hip)
@@ -1689,6 +1726,8 @@ TORCH_LIBRARY(p2p, m) {
         "-> Tensor[]");
   m.def("fp8_quant(Tensor x, Tensor(a!) site, int fmt, int use_cur=0) -> Tensor");
   m.def("sn_power_iter(Tensor w, Tensor(a!) u, Tensor(b!) v) -> Tensor");
+  m.def("sn_scale(Tensor w, Tensor(a!) u, Tensor(b!) v) -> Tensor");
+  m.def("sn_wgrad(Tensor G, Tensor w, Tensor u, Tensor v, Tensor scale) -> Tensor");
   m.def("fp8_amax(Tensor x, Tensor(a!) site, int slot) -> ()");
   m.def("fp8_roll(Tensor(a!) sites) -> ()");
   m.def("fp8_amax_multi(Tensor[] x, Tensor(a!) sites, int[] idx) -> ()");
@@ -1749,6 +1788,8 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("guard_flag", guard_flag);
   m.impl("fp8_quant", fp8_quant);
   m.impl("sn_power_iter", sn_power_iter);
+  m.impl("sn_scale", sn_scale);
+  m.impl("sn_wgrad", sn_wgrad);
   m.impl("fp8_amax", fp8_amax);
   m.impl("fp8_roll", fp8_roll);
   m.impl("fp8_amax_multi", fp8_amax_multi);

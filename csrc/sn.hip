@@ -75,7 +75,8 @@ __global__ void __launch_bounds__(256) sn_wv_kernel(const float* __restrict__ W,
 
 __global__ void __launch_bounds__(256) sn_finish_kernel(const float* __restrict__ s, int h,
                                                         const float* __restrict__ spart, int ns,
-                                                        float* __restrict__ u, float* __restrict__ sigma) {
+                                                        float* __restrict__ u, float* __restrict__ sigma,
+                                                        float* __restrict__ scale) {
   __shared__ float red[4];
   float n2 = 0.f;
   for (int i = 0; i < ns; ++i) n2 += spart[i];
@@ -87,7 +88,44 @@ __global__ void __launch_bounds__(256) sn_finish_kernel(const float* __restrict_
     dot += ur * s[r];
   }
   dot = block_sum256(dot, red);
-  if (threadIdx.x == 0) sigma[0] = dot;
+  if (threadIdx.x == 0) {
+    sigma[0] = dot;
+    if (scale) scale[0] = 1.f / dot;   // the conv epilogues' 1 / sigma
+  }
+}
+
+// Fused weight_bar gradient of a spectral-norm conv y = conv(x, s * W), s = 1 / sigma,
+// sigma = u^T W v (u, v constants): from the conv's weight gradient G = dL/d(sW),
+//   dL/dW = s G - <G, W> s^2 u v^T
+// (the direct term plus the one through sigma) -- one dot pass, one elementwise pass.
+__global__ void __launch_bounds__(256) sn_dot_kernel(const float* __restrict__ G, const float* __restrict__ W,
+                                                     long n, float* __restrict__ part) {
+  __shared__ float red[4];
+  float a = 0.f;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) a += G[i] * W[i];
+  a = block_sum256(a, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = a;
+}
+
+__global__ void __launch_bounds__(256) sn_grad_kernel(const float* __restrict__ G, const float* __restrict__ u,
+                                                      const float* __restrict__ v, const float* __restrict__ scale,
+                                                      const float* __restrict__ part, int np, int h, int wd,
+                                                      float* __restrict__ out) {
+  __shared__ float dsh;
+  if (threadIdx.x == 0) {
+    float d = 0.f;
+    for (int i = 0; i < np; ++i) d += part[i];   // fixed order: bitwise repeatable
+    dsh = d;
+  }
+  __syncthreads();
+  const float sc = scale[0];
+  const float k = dsh * sc * sc;
+  const long n = (long)h * wd;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int r = (int)(i / wd);
+    const int c = (int)(i - (long)r * wd);
+    out[i] = sc * G[i] - k * u[r] * v[c];
+  }
 }
 
 }  // namespace p2p
@@ -100,7 +138,7 @@ long p2p_sn_ws_floats(int h, int wd) {
 }
 
 int p2p_sn_power_iter(const float* W, int h, int wd, float* u, float* v, float* sigma, float* ws,
-                      hipStream_t st) {
+                      float* scale, hipStream_t st) {
   using namespace p2p;
   const int nt = (wd + 255) / 256, ns = (h + 3) / 4;
   float* tpart = ws;
@@ -111,7 +149,23 @@ int p2p_sn_power_iter(const float* W, int h, int wd, float* u, float* v, float* 
   hipLaunchKernelGGL(sn_wtu_kernel, dim3(nt, SN_RC), dim3(256), 0, st, W, h, wd, u, tpart);
   hipLaunchKernelGGL(sn_tsum_kernel, dim3(nt), dim3(256), 0, st, tpart, wd, t, tsq);
   hipLaunchKernelGGL(sn_wv_kernel, dim3(ns), dim3(256), 0, st, W, h, wd, t, tsq, nt, v, s, ssq);
-  hipLaunchKernelGGL(sn_finish_kernel, dim3(1), dim3(256), 0, st, s, h, ssq, ns, u, sigma);
+  hipLaunchKernelGGL(sn_finish_kernel, dim3(1), dim3(256), 0, st, s, h, ssq, ns, u, sigma, scale);
+  return (int)hipGetLastError();
+}
+
+int p2p_sn_wgrad_blocks(long n) {
+  long b = (n + 4095) / 4096;
+  return (int)(b < 1 ? 1 : (b > 256 ? 256 : b));
+}
+
+// part: p2p_sn_wgrad_blocks(h * wd) floats
+int p2p_sn_wgrad(const float* G, const float* W, const float* u, const float* v, const float* scale, int h,
+                 int wd, float* part, float* out, hipStream_t st) {
+  using namespace p2p;
+  const long n = (long)h * wd;
+  const int nb = p2p_sn_wgrad_blocks(n);
+  hipLaunchKernelGGL(sn_dot_kernel, dim3(nb), dim3(256), 0, st, G, W, n, part);
+  hipLaunchKernelGGL(sn_grad_kernel, dim3(nb), dim3(256), 0, st, G, u, v, scale, part, nb, h, wd, out);
   return (int)hipGetLastError();
 }
 }

@@ -231,12 +231,14 @@ class SpectralNorm(nn.Module):
             # 1 / sigma stays a device scalar applied in the conv epilogues (ops/hip.py SNConvFn)
             u = getattr(m, self.name + "_u")
             v = getattr(m, self.name + "_v")
+            # (the sigma path of the weight_bar gradient is fused into the conv's weight
+            # gradient: csrc/sn.hip sn_wgrad)
             with torch.autocast(device_type=w.device.type, enabled=False):
-                sigma = ops_hip().spectral_sigma(w.reshape(w.shape[0], -1), u, v, self.power_iterations)
-                scale = sigma.reciprocal()
+                scale = ops_hip().sn_scale(w.reshape(w.shape[0], -1), u, v, self.power_iterations)
             return ops_hip().sn_conv2d(x, w, m.bias, scale, m.stride, m.padding,
                                        getattr(m, "act_in", None), getattr(m, "act_out", None),
-                                       getattr(m, "grad_gate", None), getattr(m, "out_gated", False))
+                                       getattr(m, "grad_gate", None), getattr(m, "out_gated", False),
+                                       uv=(u, v))
         w = self.normalized_weight()
         return ops.conv2d(x, w, m.bias, m.stride, m.padding, pad_mode, 1,
                           getattr(m, "act_in", None), getattr(m, "act_out", None))

@@ -572,10 +572,13 @@ class SNConvFn(torch.autograd.Function):
 
     Backward: dx = dgrad(gy_eff, w_bar) * s (epilogue again); with G = wgrad(gy_eff, x),
     dL/dw_bar = s * G and dL/ds = <G, w_bar>, which autograd chains through s = 1 / sigma(w_bar)
-    -- the same gradient as the reference's ``w / sigma``."""
+    -- the same gradient as the reference's ``w / sigma``.  With ``uv`` = (u, v) (the power
+    iteration's vectors, held by reference like SigmaFn) and a detached ``scale``, the whole
+    w_bar gradient s G - <G, w_bar> s^2 u v^T is one fused pass (csrc/sn.hip sn_wgrad) instead
+    of the scale / reciprocal / sigma autograd chain."""
 
     @staticmethod
-    def forward(ctx, x, w_bar, bias, scale, cfg: _ConvCfg):
+    def forward(ctx, x, w_bar, bias, scale, cfg: _ConvCfg, uv=None):
         if cfg.transposed or cfg.reflect or cfg.up != 1:
             raise NotImplementedError("SNConvFn: plain zero-padded convs only")
         q1, _, C1, _, Cp, packed = _prep_inputs(x, None)
@@ -595,6 +598,7 @@ class SNConvFn(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.geo = (C1, 0, Cp, packed, Cout, Coutp, H, W)
         ctx.has_bias = bias is not None
+        ctx.uv = uv
         keep_y = cfg.act_out not in (None, "none") and not cfg.out_gated
         ctx.save_for_backward(q1, w_bar, sc, y if keep_y else None)
         return y
@@ -606,22 +610,39 @@ class SNConvFn(torch.autograd.Function):
         gx, _, G, gb = _conv_backward(ctx.cfg, ctx.geo, q1, None, w_bar, y, gy,
                                       ctx.needs_input_grad[0], False, need_w,
                                       ctx.has_bias and ctx.needs_input_grad[2], alpha=sc)
+        if ctx.uv is not None:
+            u, v = ctx.uv
+            wb = w_bar.detach()
+            wb = wb if (wb.dtype == torch.float32 and wb.is_contiguous()) else wb.float().contiguous()
+            gw = P().sn_wgrad(G, wb, u.detach(), v.detach(), sc) if ctx.needs_input_grad[1] else None
+            return gx, gw, gb, None, None, None
         gw = G * sc if ctx.needs_input_grad[1] else None
         gs = (G * w_bar.detach()).sum().reshape(1) if ctx.needs_input_grad[3] else None
-        return gx, gw, gb, gs, None
+        return gx, gw, gb, gs, None, None
+
+
+def sn_scale(w2, u, v, iters=1):
+    """1 / sigma of the power iteration (u, v updated in place) as a plain device scalar --
+    the sigma path of the gradient is SNConvFn's fused sn_wgrad (pass ``uv`` to sn_conv2d)."""
+    w = w2.detach()
+    w = w if (w.dtype == torch.float32 and w.is_contiguous()) else w.float().contiguous()
+    for _ in range(max(1, int(iters)) - 1):
+        P().sn_power_iter(w, u.data, v.data)
+    return P().sn_scale(w, u.data, v.data)
 
 
 def sn_conv2d(x, w_bar, bias, scale, stride=1, padding=0, act_in=None, act_out=None,
-              grad_gate=None, out_gated=False):
-    """Spectral-norm conv: ``conv2d(x, w_bar * scale)`` with ``scale`` (1 / sigma, a 1-element
-    tensor carrying its own gradient) applied in the conv epilogues."""
+              grad_gate=None, out_gated=False, uv=None):
+    """Spectral-norm conv: ``conv2d(x, w_bar * scale)`` with ``scale`` (1 / sigma) applied in
+    the conv epilogues -- either a 1-element tensor carrying its own gradient, or (``uv`` =
+    (u, v)) a detached ``sn_scale`` with the sigma path fused into the weight gradient."""
     s, s2 = _pair(stride)
     p, p2 = _pair(padding)
     if s != s2 or p != p2:
         raise NotImplementedError("anisotropic stride/padding")
     cfg = _ConvCfg(False, w_bar.shape[2], w_bar.shape[3], s, p, False, 1, act_in, act_out,
                    grad_gate=grad_gate, out_gated=out_gated)
-    return SNConvFn.apply(x, w_bar, bias, scale, cfg)
+    return SNConvFn.apply(x, w_bar, bias, scale, cfg, uv)
 
 
 def _nb_half(cfg, q2, nb, res_fused):
