@@ -86,7 +86,8 @@ int p2p_adam_max_tensors();
 int p2p_union_weight(const float* w, int CinT, int CoutT, int co_off, int nv, int Nrows, int Cpad,
                      const float* bias, void* out, float* bias_out, hipStream_t st);
 int p2p_sum_partials(const float* ws, int nb, float scale, float* out, hipStream_t st);
-int p2p_rowsum_f32(const float* ws, long R, int C, float* out, hipStream_t st);
+int p2p_rowsum_blocks(long R);
+int p2p_rowsum_f32(const float* ws, long R, int C, float* tmp, float* out, hipStream_t st);
 int p2p_lincomb(const float* a, const float* b, float wa, float wb, float c, long n, float* out, hipStream_t st);
 int p2p_i64_add(long long* t, long long v, long n, hipStream_t st);
 int p2p_lincomb_n(const float* const* p, const float* w, int n, float* out, hipStream_t st);
@@ -1651,9 +1652,11 @@ Tensor rowsum(const Tensor& ws) {
   TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.dim() >= 1,
               "rowsum: fp32 contiguous");
   const int64_t C = ws.size(-1);
+  const int64_t R = ws.numel() / std::max<int64_t>(C, 1);
   Tensor out = at::empty({C}, ws.options());
-  check_rc(p2p_rowsum_f32(ws.data_ptr<float>(), ws.numel() / std::max<int64_t>(C, 1), (int)C,
-                          out.data_ptr<float>(), cur_stream(ws)),
+  Tensor tmp = at::empty({(int64_t)p2p_rowsum_blocks(R) * C}, ws.options());
+  check_rc(p2p_rowsum_f32(ws.data_ptr<float>(), R, (int)C, tmp.data_ptr<float>(), out.data_ptr<float>(),
+                          cur_stream(ws)),
            "rowsum");
   return out;
 }

@@ -569,6 +569,18 @@ __global__ void __launch_bounds__(64) scale_n_kernel(const float* g, LinList l, 
   if (i < l.n) out[i] = l.w[i] * g[0];
 }
 
+// part[b][c] = sum of ws rows [b * rpb, (b + 1) * rpb) (column c per thread, rows in order)
+__global__ void __launch_bounds__(256) rowsum_partial_kernel(const float* __restrict__ ws, long R, int C, long rpb,
+                                                             float* __restrict__ part) {
+  const long r0 = (long)blockIdx.x * rpb;
+  const long r1 = r0 + rpb < R ? r0 + rpb : R;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a = 0.f;
+    for (long r = r0; r < r1; ++r) a += ws[r * C + c];
+    part[(long)blockIdx.x * C + c] = a;
+  }
+}
+
 __global__ void __launch_bounds__(64) i64_add_kernel(long long* t, long long v, long n) {
   const long i = (long)blockIdx.x * 64 + threadIdx.x;
   if (i < n) t[i] += v;
@@ -708,11 +720,24 @@ int p2p_loss_bwd(const void* a, const void* b, int is_f32, long n, int kind, flo
 }
 
 
-// out[c] = sum_r ws[r][c] for an fp32 [R][C] partial-sum image (fixed order)
-int p2p_rowsum_f32(const float* ws, long R, int C, float* out, hipStream_t st) {
+// out[c] = sum_r ws[r][c] for an fp32 [R][C] partial-sum image (fixed order): rows split over
+// up to 1024 blocks first (tmp: p2p_rowsum_tmp_floats(R, C)), then the partials combined
+int p2p_rowsum_blocks(long R) {
+  long b = (R + 31) / 32;
+  return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+}
+
+int p2p_rowsum_f32(const float* ws, long R, int C, float* tmp, float* out, hipStream_t st) {
   using namespace p2p;
   if (R <= 0 || R > 0x7fffffff) return -1;
-  hipLaunchKernelGGL(colsum_final_kernel<32>, dim3((C + 7) / 8), dim3(256), 0, st, ws, (int)R, C, 1.f, 0, out);
+  if (R <= 64) {
+    hipLaunchKernelGGL(colsum_final_kernel<32>, dim3((C + 7) / 8), dim3(256), 0, st, ws, (int)R, C, 1.f, 0, out);
+    return (int)hipGetLastError();
+  }
+  const int nb = p2p_rowsum_blocks(R);
+  const long rpb = (R + nb - 1) / nb;
+  hipLaunchKernelGGL(rowsum_partial_kernel, dim3(nb), dim3(256), 0, st, ws, R, C, rpb, tmp);
+  hipLaunchKernelGGL(colsum_final_kernel<32>, dim3((C + 7) / 8), dim3(256), 0, st, tmp, nb, C, 1.f, 0, out);
   return (int)hipGetLastError();
 }
 

@@ -921,3 +921,31 @@ def test_guard_flag_kernel():
     assert float(nonfinite(one, nan, counter=cnt)) == 1.0 and float(cnt) == 1.0
     assert float(nonfinite(inf, counter=cnt)) == 1.0 and float(cnt) == 2.0
     assert float(nonfinite(torch.tensor(3.0e38, device=DEV))) == 0.0
+
+
+@pytest.mark.parametrize("R,C", [(5, 64), (3000, 136), (40000, 64)])
+def test_rowsum_and_scalar_helpers(R, C):
+    """The step-bookkeeping kernels (csrc/elementwise.hip small-tensor helpers): rowsum (the
+    norm-partial column sums, both the one-pass and the split path) against an fp64 sum;
+    lincomb / lincomb_ / lincomb_n / scale_n / i64_add_ against the arithmetic they replace."""
+    P = _native.ops()
+    g = torch.Generator(device=DEV).manual_seed(3)
+    ws = torch.randn(R, C, device=DEV, generator=g)
+    out = P.rowsum(ws)
+    ref_ = ws.double().sum(0)
+    assert torch.allclose(out.double(), ref_, rtol=1e-5, atol=1e-3 * (R ** 0.5) * 1e-2)
+    assert torch.equal(out, P.rowsum(ws))        # fixed order: bitwise repeatable
+    a = torch.randn(7, device=DEV, generator=g)
+    b = torch.randn(7, device=DEV, generator=g)
+    assert torch.allclose(P.lincomb(a, b, 0.5, -2.0, 1.0), 0.5 * a - 2.0 * b + 1.0)
+    t = a.clone()
+    P.lincomb_(t, b, 1.0, -1.0, 1.0)
+    assert torch.allclose(t, a - b + 1.0)
+    ts = [torch.randn((), device=DEV, generator=g) for _ in range(5)]
+    ws5 = [0.5, 1.0, -3.0, 0.25, 2.0]
+    assert torch.allclose(P.lincomb_n(ts, ws5), sum(w * x for w, x in zip(ws5, ts)))
+    gs = P.scale_n(torch.tensor(1.5, device=DEV), ws5)
+    assert torch.allclose(gs, 1.5 * torch.tensor(ws5, device=DEV))
+    c = torch.tensor([41], dtype=torch.int64, device=DEV)
+    P.i64_add_(c, 1)
+    assert c.item() == 42
