@@ -182,3 +182,17 @@ def test_vgg_tap_fusion_flags_and_cpu_loss_unchanged():
     # the target features reused across losses give the same value
     fyc = loss_f.target_features(y)
     assert torch.allclose(loss_f(x, y, fy=fyc), l1)
+
+
+def test_lincomb_n_torch_path_matches_expression():
+    """ops.lincomb_n off the native path is the plain weighted sum in term order (the
+    reference's own expression order: bitwise on CPU) and differentiates like it."""
+    import torch
+    from p2p_pytorch_amd import ops
+    ts = [torch.tensor(v, requires_grad=True) for v in (0.3, -1.7, 2.5)]
+    ws = [1.0, 10.0, 0.25]
+    out = ops.lincomb_n(ts, ws)
+    ref_ = 0 + 1.0 * ts[0] + 10.0 * ts[1] + 0.25 * ts[2]
+    assert torch.equal(out, ref_)
+    out.backward()
+    assert [t.grad.item() for t in ts] == ws
