@@ -65,8 +65,8 @@ def parse():
     p.add_argument("--graph", action="store_true",
                    help="(native) hipGraph capture (the default for every N; kept for compatibility)")
     p.add_argument("--precision", default=os.environ.get("P2P_PRECISION", "bf16"), choices=["bf16", "fp8"],
-                   help="(native) conv GEMM operands: bf16, or fp8 (e4m3 fwd / e5m2 dgrad, bf16 wgrad; "
-                        "BASELINE config 5)")
+                   help="(native) conv GEMM operands: bf16, or fp8 (e4m3 fwd / e5m2 dgrad / e5m2 x e4m3 "
+                        "wgrad, image-facing layers bf16; BASELINE config 5)")
     p.add_argument("--c_phase_backward", type=int, default=1, choices=[0, 1],
                    help="(--family ref) run the reference's C-phase backward (locc.backward(),"
                         " train.py:400-402) even though with the reference's optimizer_c it updates"
@@ -249,8 +249,8 @@ def main():
                    "gan_mode": args.gan_mode, "lambda_L1": args.lamb,
                    "hipgraph": bool(use_graph),
                    **({"c_phase_backward": bool(args.c_phase_backward)} if ref else {}),
-                   "conv_precision": ("fp8 e4m3 fwd / e5m2 dgrad, bf16 wgrad + first/last layers"
-                                      if args.precision == "fp8" else "bf16")},
+                   "conv_precision": ("fp8: e4m3 fwd, e5m2 dgrad, e5m2 x e4m3 wgrad; image-facing first/last "
+                                      "layers bf16" if args.precision == "fp8" else "bf16")},
         "max_mem_gib": (round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)
                         if dev.type == "cuda" else None),
         "comm": comm,

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 namespace p2p {
 
 typedef __bf16 bf16;
@@ -127,6 +129,18 @@ __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+// Raise a kernel's dynamic-LDS limit once per DEVICE (the attribute is per device: a second
+// GPU driven by the same process needs its own call).  ``mask``: one static per kernel
+// instantiation at the call site, bit d = device d done.
+inline void smem_attr_once(const void* fn, int smem, std::atomic<uint64_t>& mask) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const uint64_t bit = 1ull << (dev & 63);
+  if (mask.load(std::memory_order_relaxed) & bit) return;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+  mask.fetch_or(bit, std::memory_order_relaxed);
 }
 
 }  // namespace p2p

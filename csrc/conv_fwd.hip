@@ -314,12 +314,8 @@ __global__ void __launch_bounds__(256) conv_finalize_kernel(ConvFwdArgs a, long 
 template <int BM, int BN, int WM, int WN, int MODE, bool FAST>
 static int launch_fwd(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = FwdSmem<BM, BN>::bytes;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_fwd_kernel<BM, BN, WM, WN, MODE, FAST>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> attr_mask{0};
+  smem_attr_once(reinterpret_cast<const void*>(&conv_fwd_kernel<BM, BN, WM, WN, MODE, FAST>), smem, attr_mask);
   int classes = MODE == 0 ? 1 : a.stride * a.stride;
   long mmax = 0;
   for (int c = 0; c < classes; ++c) {

@@ -502,13 +502,8 @@ static int launch_glds(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int pipe = STAGES * (BM + BN) * BK * 2;
   constexpr int epi = BM * (BN + 8) * 2 + 2 * (WM * WN * 64) * 4;  // + stats scratch
   constexpr int smem = pipe > epi ? pipe : epi;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU, F8, PK8, EXT>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> attr_mask{0};
+  smem_attr_once(reinterpret_cast<const void*>(&conv_fwd_glds_kernel<BM, BN, WM, WN, MODE, STAGES, FASTK, RELU, F8, PK8, EXT>), smem, attr_mask);
   const int classes = MODE == 0 ? 1 : a.stride * a.stride;
   long mmax = 0;
   for (int c = 0; c < classes; ++c) {

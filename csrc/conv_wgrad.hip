@@ -925,13 +925,8 @@ extern "C" int p2p_conv_wgrad_tile_rows(int R) { return R <= 16 ? 16 : (R <= 64 
 
 template <int TBR, int TBQ, int WM, int WN, int STG, int RM>
 static int wg_launch(const p2p::ConvWgradArgs& a, dim3 grid, int smem, hipStream_t st) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&p2p::conv_wgrad_glds_kernel<TBR, TBQ, WM, WN, STG, RM>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> attr_mask{0};
+  p2p::smem_attr_once(reinterpret_cast<const void*>(&p2p::conv_wgrad_glds_kernel<TBR, TBQ, WM, WN, STG, RM>), smem, attr_mask);
   hipLaunchKernelGGL((p2p::conv_wgrad_glds_kernel<TBR, TBQ, WM, WN, STG, RM>), grid, dim3(WM * WN * 64), smem,
                      st, a);
   return (int)hipGetLastError();
@@ -950,13 +945,8 @@ static int wg_launch_rm(int rm, const p2p::ConvWgradArgs& a, dim3 grid, int smem
 template <int TBR, int TBQ, int WM, int WN, int STG, int RM, int PF, int QF>
 static int wg8_launch(const p2p::ConvWgradArgs& a, hipStream_t st) {
   constexpr int smem = STG * (TBR + TBQ) * 128;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&p2p::conv_wgrad_f8_kernel<TBR, TBQ, WM, WN, STG, RM, PF, QF>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> attr_mask{0};
+  p2p::smem_attr_once(reinterpret_cast<const void*>(&p2p::conv_wgrad_f8_kernel<TBR, TBQ, WM, WN, STG, RM, PF, QF>), smem, attr_mask);
   dim3 grid(((a.R + TBR - 1) / TBR) * ((a.Kq + TBQ - 1) / TBQ), a.splits, 1);
   hipLaunchKernelGGL((p2p::conv_wgrad_f8_kernel<TBR, TBQ, WM, WN, STG, RM, PF, QF>), grid, dim3(WM * WN * 64), smem,
                      st, a);

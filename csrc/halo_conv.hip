@@ -217,12 +217,8 @@ __global__ void __launch_bounds__(256) halo_union_kernel(HaloArgs a) {
 template <int NCH, bool RELU>
 static int launch_halo(const HaloArgs& a, int blocks, hipStream_t st) {
   constexpr int smem = 2 * STAGE_BYTES + (9 * NCH * 16 * 8 + 255) / 256 * 256 * 16;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo_union_kernel<NCH, RELU>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr_mask{0};
+  smem_attr_once(reinterpret_cast<const void*>(&halo_union_kernel<NCH, RELU>), smem, attr_mask);
   hipLaunchKernelGGL((halo_union_kernel<NCH, RELU>), dim3(blocks), dim3(256), smem, st, a);
   return (int)hipGetLastError();
 }

@@ -244,12 +244,8 @@ static int launch_halo_kxk(const HaloKArgs& a, int blocks, hipStream_t st) {
   constexpr int EPI_BYTES = 256 * (NBLK * 16 + 8) * 2;
   constexpr int smem = 2 * G::STAGE_BYTES + BUNITS_PAD * 16 + (EPI_BYTES <= G::STAGE_BYTES ? 0 : EPI_BYTES);
   static_assert(smem <= 163840, "halo_kxk: LDS budget");
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo_kxk_kernel<KS, CIN, NBLK>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr_mask{0};
+  smem_attr_once(reinterpret_cast<const void*>(&halo_kxk_kernel<KS, CIN, NBLK>), smem, attr_mask);
   hipLaunchKernelGGL((halo_kxk_kernel<KS, CIN, NBLK>), dim3(blocks), dim3(256), smem, st, a);
   return (int)hipGetLastError();
 }

@@ -212,12 +212,8 @@ __global__ void __launch_bounds__(256, TN >= 8 ? 1 : 2) halo_pk8_kernel(HaloPk8A
 template <int TN, int ACT, bool GATE, bool QS = false>
 static int launch_pk8(const HaloPk8Args& a, int blocks, hipStream_t st) {
   constexpr int smem = (2 * SUNITS + TN * 16 * 16) * 16;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo_pk8_kernel<TN, ACT, GATE, QS>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr_mask{0};
+  smem_attr_once(reinterpret_cast<const void*>(&halo_pk8_kernel<TN, ACT, GATE, QS>), smem, attr_mask);
   hipLaunchKernelGGL((halo_pk8_kernel<TN, ACT, GATE, QS>), dim3(blocks), dim3(256), smem, st, a);
   return (int)hipGetLastError();
 }

@@ -241,12 +241,8 @@ static int launch_halo_wgrad(const HaloWArgs& a, int blocks, hipStream_t st) {
   using G = HaloW<KS, CIN, RL>;
   constexpr int smem = 2 * G::STAGE_BYTES;
   static_assert(smem <= 163840, "halo_wgrad: LDS budget");
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo_wgrad_kernel<KS, CIN, RL>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr_mask{0};
+  smem_attr_once(reinterpret_cast<const void*>(&halo_wgrad_kernel<KS, CIN, RL>), smem, attr_mask);
   hipLaunchKernelGGL((halo_wgrad_kernel<KS, CIN, RL>), dim3(blocks), dim3(256), smem, st, a);
   return (int)hipGetLastError();
 }

@@ -16,8 +16,10 @@ D's parameters (A1) and round() has no gradient (A2), so the C phase changes no
 parameter -- its loss is computed and logged, its backward is skipped because it is
 provably a no-op (``c_phase_backward=True`` runs it anyway for cost parity).
 ``train_c=True`` fixes both quirks: a straight-through quantiser and an Adam over C
-(``opt_c``, always built so train.py can schedule and checkpoint it like the reference's
-``optimizer_c`` / ``net_c_scheduler``, train.py:243-246, :441-443).
+(``opt_c``, scheduled and checkpointed by train.py like the reference's ``optimizer_c`` /
+``net_c_scheduler``, train.py:243-246, :441-443).  Without ``train_c`` no ``opt_c`` exists: the
+reference's optimizer_c steps nothing (A1), and a scheduler stepping an optimizer that never
+steps only produced PyTorch's order warning on every epoch.
 
 D's gradients from the G loss are discarded by the reference (``optimizer_d.zero_grad()``
 before ``loss_d.backward()``, train.py:384-389), so the third D forward (the one the G loss
@@ -77,7 +79,7 @@ class CompressGANStep:
         # D's trainable parameters (SN's weight_u / weight_v are Parameters that never train)
         self._d_trainable = [p for p in net_d.parameters() if p.requires_grad]
         self.train_c = train_c
-        self.opt_c = make_adam(net_c.parameters(), lr=lr, betas=(beta1, 0.999))
+        self.opt_c = make_adam(net_c.parameters(), lr=lr, betas=(beta1, 0.999)) if train_c else None
         self.c_phase_backward = c_phase_backward
         if hasattr(net_d, "set_feature_grad_gate"):
             net_d.set_feature_grad_gate(True)   # the feature-matching L1 below applies lrelu
@@ -88,7 +90,7 @@ class CompressGANStep:
         self.timer = None     # optional utils.PhaseTimer: per-phase HIP-event ms
 
     def optimizers(self):
-        return [self.opt_g, self.opt_d, self.opt_c]
+        return [o for o in (self.opt_g, self.opt_d, self.opt_c) if o is not None]
 
     def state_tensors(self):
         """Tensors one step mutates (CapturedStep snapshots them around its warmup)."""

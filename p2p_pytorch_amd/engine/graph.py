@@ -22,7 +22,20 @@ New input batches are copied into the static input buffers before each replay.
 """
 from __future__ import annotations
 
+import copy
+
 import torch
+
+
+class WarmupError(RuntimeError):
+    """A warmup (eager) step raised before capture: not a capture failure -- the trainer
+    itself is broken, and on a multi-rank job the other ranks are already blocked in that
+    step's collectives, so the process must exit (the launcher restarts the job)."""
+
+
+class CaptureError(RuntimeError):
+    """``torch.cuda.graph`` raised while recording; the pre-warmup state (tensors, optimizer
+    step counts, the dropout salt counter) has been restored, so eager can take over."""
 
 
 def trainer_state_tensors(modules, optimizers, extra=()):
@@ -91,17 +104,30 @@ class CapturedStep:
             snap = _Snapshot(trainer)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(max(1, warmup)):
-                step_fn(*self.static_inputs)
+        try:
+            with torch.cuda.stream(side):
+                for _ in range(max(1, warmup)):
+                    step_fn(*self.static_inputs)
+        except Exception as e:  # noqa: BLE001
+            raise WarmupError(f"warmup step failed: {type(e).__name__}: {e}") from e
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         if snap is not None:
             snap.restore()
             torch.cuda.synchronize()
+        from ..ops import hip as _hip
+        salt = copy.copy(_hip._salt)      # python-side state the capture advances
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.static_out = step_fn(*self.static_inputs)
+        try:
+            with torch.cuda.graph(self.graph):
+                self.static_out = step_fn(*self.static_inputs)
+        except Exception as e:  # noqa: BLE001
+            torch.cuda.synchronize()
+            if snap is not None:
+                snap.restore()
+                torch.cuda.synchronize()
+            _hip._salt = salt
+            raise CaptureError(f"{type(e).__name__}: {e}") from e
         torch.cuda.synchronize()
 
     def __call__(self, *inputs):
@@ -119,9 +145,15 @@ def capture_agreed(step_fn, *example_inputs, warmup: int = 2, log=None):
     * Only RCCL process groups are captured at world > 1: gloo (the CPU / one-GPU rehearsal
       backend) stages collectives through the host and cannot be captured, and a failed
       capture can leave the process in capture mode.
-    * A capture that raises on ANY rank makes every rank fall back to eager (``min_scalar``
-      consensus): collectives must match, so one rank replaying a graph while another runs
-      eager would hang until the watchdog.
+    * A failure DURING capture (``torch.cuda.graph`` raised, :class:`CaptureError`) on ANY
+      rank makes every rank fall back to eager (``min_scalar`` consensus): collectives must
+      match, so one rank replaying a graph while another runs eager would hang until the
+      watchdog.  The failing capture restored the pre-warmup state first, so the fallback
+      ranks and the ranks whose capture succeeded start eager from the same state.
+    * Only capture failures are agreed: a WARMUP step that raises (:class:`WarmupError`) is
+      re-raised -- the other ranks are blocked in that step's gradient all-reduces, a
+      min_scalar would be matched against a bucket collective, so the process exits non-zero
+      and the launcher (``torchrun --max-restarts``) / watchdog handles the restart.
     """
     from ..parallel import dist as pdist
     world = pdist.world_size()
@@ -131,7 +163,9 @@ def capture_agreed(step_fn, *example_inputs, warmup: int = 2, log=None):
     ok, step = 1.0, step_fn
     try:
         step = CapturedStep(step_fn, *example_inputs, warmup=warmup)
-    except Exception as e:  # noqa: BLE001 - any capture failure: eager on every rank
+    except WarmupError:
+        raise
+    except Exception as e:  # noqa: BLE001 - a capture failure: eager on every rank
         if log is not None:
             log(f"graph capture failed ({type(e).__name__}: {e}); running eager")
         ok = 0.0

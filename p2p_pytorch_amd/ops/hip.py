@@ -192,6 +192,14 @@ def _wgrad_side(weight):
     s = _WgradSide.on
     if not s:
         return None
+    # the side-stream gradient is only safe when AccumulateGrad STEALS it: a leaf weight with
+    # no gradient yet, fp32 and dense-contiguous like the returned gw (else autograd adds /
+    # clones it on the compute stream, racing the side-stream kernel that writes it)
+    if (not weight.is_leaf or weight.grad is not None or weight.dtype != torch.float32
+            or not weight.is_contiguous()):
+        if weight.data_ptr() in _WgradSide.seen:
+            torch.cuda.current_stream(s.device).wait_stream(s)
+        return None
     if weight.data_ptr() in _WgradSide.seen:
         # second gradient of this weight: autograd will add it to the first on the compute
         # stream, so the first must be complete before it
@@ -366,23 +374,23 @@ def prepare_weights(*modules):
         cache[key] = (w._version, _gen[0], img)
 
 
-_BIAS_PAD = {}
-
-
 def _bias_padded(b, coutp):
-    """fp32 bias padded to ``coutp`` columns: a persistent zero-tailed buffer per parameter,
-    refreshed by a device copy each call (stream-ordered, graph-capturable; no pad kernel)."""
+    """fp32 bias padded to ``coutp`` columns: a persistent zero-tailed buffer cached on the
+    bias tensor itself (dies with it), refreshed by a device copy each call (stream-ordered,
+    graph-capturable; no pad kernel)."""
     if b is None:
         return None
-    b = b.detach().float()
-    if b.numel() == coutp:
-        return b.contiguous()
-    key = (b.data_ptr(), coutp, b.device)
-    buf = _BIAS_PAD.get(key)
-    if buf is None:
-        buf = torch.zeros(coutp, device=b.device, dtype=torch.float32)
-        _BIAS_PAD[key] = buf
-    buf[: b.numel()].copy_(b)
+    src = b.detach()
+    if src.numel() == coutp:
+        return src.float().contiguous()
+    buf = getattr(b, "_p2p_bias_pad", None)
+    if buf is None or buf.numel() != coutp or buf.device != src.device:
+        buf = torch.zeros(coutp, device=src.device, dtype=torch.float32)
+        try:
+            b._p2p_bias_pad = buf
+        except AttributeError:   # plain tensor without __dict__: a per-call buffer
+            pass
+    buf[: src.numel()].copy_(src)
     return buf
 
 

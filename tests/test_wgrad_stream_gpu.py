@@ -92,3 +92,73 @@ def test_wgrad_side_stream_repeat_weight(monkeypatch):
         assert torch.equal(out[0], out[1])
     finally:
         p2p.set_deterministic(False)
+
+
+def _one_conv_grad(monkeypatch, flag, kind):
+    """conv weight gradient with the side stream on/off for a weight AccumulateGrad cannot
+    steal: ``nonleaf`` (weight = w * 0.5 feeds the conv, MulBackward reads gw), ``accum`` (the
+    leaf already has a gradient, autograd adds into it)."""
+    from p2p_pytorch_amd import ops
+    dev = torch.device("cuda")
+    monkeypatch.setenv("P2P_WGRAD_STREAM", flag)
+    torch.manual_seed(2)
+    conv = torch.nn.Conv2d(64, 128, 4, 2, 1).to(dev)
+    x = torch.randn(16, 64, 64, 64, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    if kind == "accum":
+        conv.weight.grad = torch.full_like(conv.weight, 0.25)
+    with hip.wgrad_overlap(dev):
+        w = conv.weight * 0.5 if kind == "nonleaf" else conv.weight
+        y = ops.conv2d(x, w, conv.bias, stride=2, padding=1)
+        y.float().square().mean().backward()
+    torch.cuda.synchronize()
+    return conv.weight.grad.clone()
+
+
+@pytest.mark.parametrize("kind", ["nonleaf", "accum"])
+def test_wgrad_side_stream_unstealable_grad(monkeypatch, kind):
+    """the side stream is bypassed when autograd would read gw on the compute stream
+    (non-leaf weight, existing gradient) -- bitwise the one-stream result."""
+    p2p.set_backend("native")
+    p2p.set_deterministic(True)
+    try:
+        g0 = _one_conv_grad(monkeypatch, "0", kind)
+        g1 = _one_conv_grad(monkeypatch, "1", kind)
+    finally:
+        p2p.set_deterministic(False)
+    assert torch.isfinite(g0).all()
+    assert torch.equal(g0, g1)
+
+
+def _run_ref_family(monkeypatch, flag):
+    from p2p_pytorch_amd.engine.compress_gan import CompressGANStep
+    from p2p_pytorch_amd.models import define_C, define_D, define_G
+    dev = torch.device("cuda")
+    monkeypatch.setenv("P2P_WGRAD_STREAM", flag)
+    hip.reset_rng(0)
+    torch.manual_seed(0)
+    G = define_G(netG="expand", gpu_id=dev, verbose=False)
+    D = define_D(6, 64, gpu_id=dev, netD="multiscale", verbose=False)
+    C = define_C(gpu_id=dev, verbose=False)
+    step = CompressGANStep(G, D, C)
+    g = torch.Generator(device=dev).manual_seed(5)
+    for _ in range(2):
+        a, b = [(torch.rand(2, 3, 128, 128, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+                .contiguous(memory_format=torch.channels_last) for _ in range(2)]
+        losses = step.step(a, b)
+    torch.cuda.synchronize()
+    return ({k: float(v) for k, v in losses.items()},
+            torch.cat([p.detach().reshape(-1) for p in list(G.parameters()) + list(D.parameters())]))
+
+
+def test_wgrad_side_stream_ref_family_bitwise(monkeypatch):
+    """The reference family's step (CompressGANStep) with its G weight gradients on the side
+    stream is bitwise the one-stream step."""
+    p2p.set_backend("native")
+    p2p.set_deterministic(True)
+    try:
+        l0, p0 = _run_ref_family(monkeypatch, "0")
+        l1, p1 = _run_ref_family(monkeypatch, "1")
+    finally:
+        p2p.set_deterministic(False)
+    assert l0 == l1
+    assert torch.equal(p0, p1)

@@ -102,8 +102,10 @@ def main():
             # ideal HBM bytes: every operand read once, the output written once
             byts = 2.0 * (x1.numel() + (x2.numel() if x2 is not None else 0) + w.numel()
                           + x1.shape[0] * OH * OW * Cout)
+            # EXT: a dgrad epilogue with an act' gate, a parked skip gradient or norm partials
+            ext = bool(xs[19]) or kw.get("res") is not None or kw.get("nb_half") is not None
             geo = f"fwd m{mode} N{x1.shape[0]} C{C} {x1.shape[2]}x{x1.shape[3]} -> {Cout} k{KH} s{s} p{pad}" \
-                  f"{' refl' if refl else ''}{' up2' if up == 2 else ''} -> {OH}x{OW}"
+                  f"{' refl' if refl else ''}{' up2' if up == 2 else ''} -> {OH}x{OW}{' EXT' if ext else ''}"
         else:
             p1, p2_, p_act, q1, q2, q_act, KH, KW, s, pad, refl, up, dw = xs[:13]
             R = p1.shape[1] + (p2_.shape[1] if p2_ is not None else 0)
