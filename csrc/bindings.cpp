@@ -19,6 +19,12 @@
 
 #include "conv.h"
 
+// boolean environment knob (A/B experiments): unset -> dflt, "0" -> false, else true
+static bool env_flag(const char* name, bool dflt) {
+  const char* v = std::getenv(name);
+  return v ? v[0] != '0' : dflt;
+}
+
 extern "C" {
 long p2p_sn_ws_floats(int h, int wd);
 int p2p_sn_power_iter(const float* W, int h, int wd, float* u, float* v, float* sigma, float* ws,
@@ -87,6 +93,8 @@ int p2p_union_weight(const float* w, int CinT, int CoutT, int co_off, int nv, in
                      const float* bias, void* out, float* bias_out, hipStream_t st);
 int p2p_sum_partials(const float* ws, int nb, float scale, float* out, hipStream_t st);
 int p2p_rowsum_blocks(long R);
+long p2p_s2t_dbg_bytes();
+int p2p_s2t_dbg_read(void* dst, long bytes);
 int p2p_rowsum_f32(const float* ws, long R, int C, float* tmp, float* out, hipStream_t st);
 int p2p_lincomb(const float* a, const float* b, float wa, float wb, float c, long n, float* out, hipStream_t st);
 int p2p_i64_add(long long* t, long long v, long n, hipStream_t st);
@@ -389,18 +397,18 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   // stride-2 4x4 transposed convs onto 32x32 / 64x64 grids (U-Net decoder ConvT, every 4x4
   // s2 conv's input gradient): the class-shared halo kernel (csrc/conv_s2t.hip).  Its tiles
   // are BM = 128 rows of one class, which fixes the stats / partial chunk layout below.
-  // Only for 64-wide grids with K = 4 taps x C <= 1024 (census B = 256, profiles/
-  // kernel_experiments_r3.md): C = 512 (U-Net d3) and the 32-wide grids ran faster on the
-  // 256x128 implicit-GEMM tile.
+  // 32- and 64-wide grids with K = 4 taps x C <= 1024 (C = 512, U-Net d3 / d6 ConvT, runs
+  // at 830+ TF/s on the 256x128 implicit-GEMM tile; profiles/kernel_experiments_r4.md).
   // fp8 (e4m3 activations / e5m2 gradients): the same layers on 128-channel chunks (the
   // 128-B halo pixel of the bf16 kernel); no input activation on gradients, no extended
   // epilogue on activations (as the implicit-GEMM fp8 tiles)
   const int64_t s2t_chc = fp8 ? 128 : 64;
   const bool s2t_ok = mode == 1 && splits == 1 && KH == 4 && KW == 4 && stride == 2 && pad == 1 &&
-                      !reflect && up == 1 && OH == 2 * H && OW == 2 * W && W == 64 &&
+                      !reflect && up == 1 && OH == 2 * H && OW == 2 * W &&
+                      (W == 64 || (W == 32 && !fp8 && env_flag("P2P_S2T_W32", true))) &&
                       (H * W) % 128 == 0 && Cout % 64 == 0 && C1 % s2t_chc == 0 && C2 % s2t_chc == 0 &&
                       C1 + C2 >= s2t_chc && C1 + C2 <= 256 &&
-                      (act_in == 0 || (act_in == 1 && act_bwd == 0 && !res)) &&
+                      (act_in == 0 || (act_in == 1 && act_bwd == 0 && !res)) && act_out <= 2 &&
                       (fp8 != 2 || act_in == 0) && (fp8 != 1 || (!act_bwd && !res)) &&
                       std::getenv("P2P_NO_S2T") == nullptr;
   if (s2t_ok) bm = 128;
@@ -1648,6 +1656,15 @@ Tensor scale_n(const Tensor& g, at::ArrayRef<double> ws) {
 }
 
 // column sums of an fp32 [..., C] partial-sum image (rows in fixed order)
+// timeline probe of the s2t kernel (P2P_S2T_DEBUG=1): int64 [blocks][tiles][4] on the host
+Tensor s2t_debug() {
+  (void)hipDeviceSynchronize();
+  const long n = p2p_s2t_dbg_bytes() / 8;
+  Tensor out = at::empty({n}, at::TensorOptions().dtype(at::kLong));
+  check_rc(p2p_s2t_dbg_read(out.data_ptr(), n * 8), "s2t_debug");
+  return out;
+}
+
 Tensor rowsum(const Tensor& ws) {
   TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.dim() >= 1,
               "rowsum: fp32 contiguous");
@@ -1776,6 +1793,7 @@ TORCH_LIBRARY(p2p, m) {
   m.def("lincomb_(Tensor(a!) t, Tensor? b, float wa, float wb, float c) -> ()");
   m.def("i64_add_(Tensor(a!) t, int v) -> ()");
   m.def("rowsum(Tensor ws) -> Tensor");
+  m.def("s2t_debug() -> Tensor", &s2t_debug);
   m.def("lincomb_n(Tensor[] ts, float[] ws) -> Tensor");
   m.def("scale_n(Tensor g, float[] ws) -> Tensor");
   m.def("guard_flag(Tensor[] losses, Tensor(a!)? counter) -> Tensor");

@@ -1,31 +1,35 @@
 // Stride-2 transposed conv (4x4, pad 1, OH = 2H) -- the U-Net decoder's ConvTranspose2d and
 // the input gradient of every 4x4 stride-2 conv -- on a halo tile shared by the 4 parity
-// classes (VERDICT r2 #1a).
+// classes, for 32- and 64-wide input grids.
 //
 // The implicit GEMM (conv_fwd_glds.hip MODE 1) runs one GEMM per output parity class: every
 // class tile gathers its own im2col rows, so each input pixel is staged from L2 into LDS
-// 16 times (4 classes x 4 taps) for a 64-column output -- these layers ran at 390-540 TF/s,
-// bound by the L2 -> LDS staging rate (profiles/kernel_experiments_r3.md).  Here a block
-// owns BM = 128 consecutive grid positions q (RH = 128 / W whole rows of the input grid,
-// one image) and 64 output channels of ALL four classes: per 64-channel chunk it stages
-// the (RH + 2) x (W + 2) input halo ONCE (global_load_lds, source-side swizzle, 2-stage
-// ring), and wave c (= class (ry, rx)) reads the A fragments of its 2 x 2 taps out of that
-// one LDS image at shifted pixel offsets.  8 waves: wave w computes class w & 3 for output
-// channels 32 (w >> 2) .. + 32 (128 x 32 per wave: 64 accumulator registers, so two blocks
-// fit a CU and one's epilogue overlaps the other's MFMAs).  A wave's B fragments (its
-// class's 4 taps x 32 channels; the weights are L2-resident) go global -> VGPR (buffer
-// loads) one k-step ahead.  Per wave and chunk: 64 ds_read_b128 + 16 buffer loads for 128
-// MFMAs.
+// 16 times (4 classes x 4 taps) -- these layers ran at 390-580 TF/s, bound by the L2 -> LDS
+// staging rate (profiles/kernel_experiments_r3.md).  Here a tile is BM = 128 consecutive grid
+// positions q (RH = 128 / W whole rows of the input grid, one image) x 64 output channels of
+// ALL four classes: per 64-channel chunk the (RH + 2) x (W + 2) input halo is staged ONCE
+// (global_load_lds, source-side swizzle, 2-stage ring) and wave c (= class (ry, rx)) reads the
+// fragments of its 2 x 2 taps out of that one LDS image at shifted pixel offsets.  8 waves:
+// wave w computes class w & 3 for output channels 32 (w >> 2) .. + 32.  A wave's weight
+// fragments (its class's 4 taps x 32 channels; L2-resident) go global -> VGPR (buffer loads)
+// one k-step ahead.
+//
+// Round 4 (VERDICT r3 M1 / "next round" 1a-b): the kernel was latency-bound (SQ_WAIT_ANY
+// 50-64 %, 16 % MFMA busy on the extended dgrads): every tile staged its accumulators through
+// LDS and ran four class-serial store tails, each one HBM round trip for the act' gate /
+// skip gradient / norm operands, with block-wide barriers in between.  Now:
+//  * the MFMA operands are swapped (weights = src A, halo pixels = src B), so a lane's
+//    accumulator holds 4 CONSECUTIVE output channels of one output pixel: the epilogue runs
+//    from registers -- each wave stores its own (class, 32-channel) block with 8-byte stores
+//    and loads the epilogue operands at the same addresses, half a tile in flight at once;
+//    the norm statistics / norm-backward partials of a (class, channel) column are reduced
+//    with lane shuffles inside the one wave that owns it (no LDS, no barrier);
+//  * the grid is persistent (2 blocks per CU, tiles k * grid + slot): the next tile's first
+//    halo chunk and weight fragments are in flight while this tile's epilogue runs.
 //
 // Tap geometry (conv_dev.h class_geom, s = 2, p = 1): class (ry, rx) reads input row
 // qy + dy - ty with kernel row ky = ky0 + 2 ty, ty in {0, 1}; ky0 = (ry + 1) % 2,
 // dy = (ry + 1 - ky0) / 2 (columns alike).  Halo pixel (hy, hx) = input (qy0 - 1 + hy, hx - 1).
-//
-// Epilogue: each wave stages its 128 x 32 block into its class's LDS tile; then
-// the whole block runs the shared GEMM epilogue tail (conv_dev.h) class by class -- bias,
-// activation, statistics for a following norm, act' gate / skip gradient / norm-backward
-// partials of a dgrad, fp8 shadow -- with exactly the per-class BM = 128 tile conventions
-// of the implicit GEMM (stats / partial chunk index), so the host's buffers are the same.
 //
 // F8 = 1 / 2 (fp8 precision: x e4m3 / gradients e5m2, weights e4m3): the same kernel on a
 // 128-channel chunk -- byte for byte the bf16 64-channel halo (128 B per pixel, same units,
@@ -33,6 +37,8 @@
 // 16x16x32 MFMAs: its lane group q takes K [16q, 16q + 16) from LDS chunk q and
 // [64 + 16q, ...) from chunk q + 4 -- the same two reads the two bf16 k-steps make -- and the
 // per-source E8M0 exponents are its scale operands (csrc/fp8.hip sites).
+#include <cstdlib>
+
 #include "conv_dev.h"
 
 namespace p2p {
@@ -43,9 +49,6 @@ __device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(lds_wave_base), 16, 0, 0);
 }
 
-// s_waitcnt vmcnt(N) through the builtin (not inline asm): the compiler's wait-count pass
-// sees it, so registers loaded before the wait are known complete after it (with an asm
-// wait it re-waits vmcnt(0) at the first use -- the chunk's fresh halo loads included)
 typedef int s2t_i32x8 __attribute__((ext_vector_type(8)));
 typedef int s2t_i32x4 __attribute__((ext_vector_type(4)));
 
@@ -61,71 +64,510 @@ __device__ __forceinline__ u32x4 s2t_relu_fp8x16(u32x4 v) {
   return v;
 }
 
+// s_waitcnt vmcnt(N) through the builtin (not inline asm): the compiler's wait-count pass
+// sees it, so registers loaded before the wait are known complete after it
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   __builtin_amdgcn_s_waitcnt((N & 15) | 0x70 | 0xF00 | (((N >> 4) & 3) << 14));
 }
 
-#ifndef S2T_F8PF
-#define S2T_F8PF 0   // fp8: B one tap ahead (1 spills the accumulators at 128 VGPRs)
-#endif
-#ifndef S2T_PD
-#define S2T_PD 1   // B prefetch distance in k-steps (2, 3: the register-ring experiment)
-#endif
+// two bf16 (round to nearest even, NaN kept) packed in one word / unpacked
+__device__ __forceinline__ uint32_t pk2(float lo, float hi) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, (bf16)lo) | ((uint32_t)__builtin_bit_cast(uint16_t, (bf16)hi) << 16);
+}
+__device__ __forceinline__ float bfw(const uint2& v, int r) {
+  const uint32_t w = r < 2 ? v.x : v.y;
+  return __uint_as_float((r & 1) ? (w & 0xffff0000u) : (w << 16));
+}
+
 constexpr int BM = 128, BN = 64, NT = 512;
 constexpr int TM = BM / 16, TN = 2;         // one wave = one class x 32 channels: 8 x 2 fragments
-constexpr int LDC = BN + 8;
+#ifndef S2T_PG
+#define S2T_PG 4
+#endif
+constexpr int PG = S2T_PG;
+#ifndef S2T_CASES
+#define S2T_CASES 127
+#endif                        // epilogue fragment group (operand loads in flight)
 
 template <int W>
 struct S2TGeom {
   static constexpr int RH = BM / W;                 // grid rows per tile
   // halo edge: W + 2 columns stored at a row pitch HW that is a multiple of 8 pixels, so
   // the swizzle key hp & 6 is the same for every fragment of a k-step (only their -1 column
-  // shift changes it): a whole k-step's A reads are one base register + immediate offsets
+  // shift changes it): a whole k-step's fragment reads are one base register + immediates
   static constexpr int HWV = W + 2, HW = (W + 2 + 7) / 8 * 8, HH = RH + 2;
   static constexpr int HPIX = HH * HW;
   static constexpr int UNITS = HPIX * 8;            // 16-B units per 128-B chunk (64 bf16 / 128 fp8)
   static constexpr int HLD = (UNITS + NT - 1) / NT; // glds per lane per stage
   static constexpr int STAGE_BYTES = HLD * NT * 16;
-  static constexpr int EPI_BYTES = 4 * BM * LDC * 2 + 2 * NT * 4;
-  static constexpr int SMEM = 2 * STAGE_BYTES > EPI_BYTES ? 2 * STAGE_BYTES : EPI_BYTES;
+  static constexpr int SMEM = 2 * STAGE_BYTES;
   static_assert(SMEM <= 80 * 1024, "two blocks per CU");
 };
 
+// EXT (dgrad) epilogue with the tile's operand loads issued up front -- every act' gate /
+// skip-gradient / norm-input load of both 16-channel columns in flight at once (one HBM
+// round trip per tile instead of four: the round-4 timeline probe, tools/s2t_timeline.py,
+// measured the grouped version's epilogue at 15 us per tile against a 20 us MFMA loop).
+// HX / HR / HN: the loaded gate, skip gradient and norm input (compile-time, uniform over the
+// wave; with two operand streams the columns go one at a time: registers).  Unsplit outputs
+// only: every tensor is addressed through a buffer resource based at the tile's first output
+// row, so a lane keeps ONE 32-bit offset (+ scalar per-fragment offsets, + an immediate per
+// column) instead of 16 64-bit addresses per stream.
+typedef unsigned int s2t_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 s2t_bld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  const s2t_u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+  return uint2{v.x, v.y};
+}
+
+template <int W, bool HX, bool HR, bool HN>
+__device__ __forceinline__ void s2t_ext_all(const ConvFwdArgs& a, const uint2 (&vv)[TM][TN], int img, int qy0,
+                                            int chunk, int nc0, int cls, int lane, bool nb_on) {
+  constexpr int FPR = W / 16;
+  constexpr bool ALL = (int)HX + (int)HR + (int)HN <= 1;
+  const int g = lane >> 4, pl = lane & 15;
+  const int ry = cls >> 1, rx = cls & 1;
+  const long P0 = (long)(img * a.OH + 2 * qy0) * a.OW;     // the tile's first output pixel row
+  const int lpix = ry * a.OW + 2 * pl + rx;                 // this lane's fragment-0 pixel, from P0
+  const int ld = a.Cout;
+  const int nbC = a.nb_C, nbc0 = nc0 - a.nb_c0;
+  auto rsrc = [&](const void* base, long off_elems) __attribute__((always_inline)) {
+    return __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16*>(static_cast<const bf16*>(base) + off_elems), 0, 0x7fffffff, 0x00020000);
+  };
+  const auto ry_ = rsrc(a.y1, P0 * ld);
+  const auto rx_ = rsrc(HX ? a.xb1 : a.y1, P0 * ld);
+  const auto rr_ = rsrc(HR ? a.res1 : a.y1, P0 * ld);
+  const auto rn_ = rsrc(HN ? a.nb_x : a.y1, P0 * nbC);
+  const int voff = (lpix * ld + nc0 + 4 * g) * 2;           // + 32 B per column (immediate)
+  const int voffn = (lpix * nbC + nbc0 + 4 * g) * 2;
+  auto soff = [&](int i, int l) __attribute__((always_inline)) {   // fragment i's pixel offset, bytes
+    return ((i / FPR) * 2 * a.OW + 32 * (i % FPR)) * l * 2;
+  };
+  const bool gate_nb = a.act_bwd && HN && a.nb_gate;
+  const float nb_slope = (a.nb_act && !a.nb_colsum) ? neg_slope(a.nb_act) : 1.f;
+  const float gate_slope = neg_slope(a.act_bwd);
+  uint2 xv[TM][ALL ? TN : 1], rv[TM][ALL ? TN : 1], nv[TM][ALL ? TN : 1];
+  auto load = [&](int j, int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      if constexpr (HX) xv[i][slot] = s2t_bld(rx_, voff + 32 * j, soff(i, ld));
+      if constexpr (HR) rv[i][slot] = s2t_bld(rr_, voff + 32 * j, soff(i, ld));
+      if constexpr (HN) nv[i][slot] = s2t_bld(rn_, voffn + 32 * j, soff(i, nbC));
+    }
+  };
+  if constexpr (ALL) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) load(j, j);
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int slot = ALL ? j : 0;
+    if constexpr (!ALL) load(j, 0);
+    float rs[4], c1[4], s1[4], s2[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      rs[r] = c1[r] = s1[r] = s2[r] = 0.f;
+      if constexpr (HN) {
+        const long si = (a.nb_batch ? 0L : (long)img * nbC) + nbc0 + 16 * j + 4 * g + r;
+        rs[r] = a.nb_rstd[si];
+        c1[r] = -a.nb_mean[si] * rs[r];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      uint2 w = vv[i][j];
+      if constexpr (HX) {
+        if (a.act_bwd == ACT_RELU) {
+          // zero the gradient where x <= 0 (bf16 sign / zero test on the int pipe)
+          const uint32_t x0 = xv[i][slot].x, x1 = xv[i][slot].y;
+          w.x &= (((int16_t)(x0 & 0xffffu) > 0) ? 0xffffu : 0u) | (((int16_t)(x0 >> 16) > 0) ? 0xffff0000u : 0u);
+          w.y &= (((int16_t)(x1 & 0xffffu) > 0) ? 0xffffu : 0u) | (((int16_t)(x1 >> 16) > 0) ? 0xffff0000u : 0u);
+        } else {
+          float f[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) f[r] = bfw(w, r) * act_grad_from_input(bfw(xv[i][slot], r), a.act_bwd);
+          w = uint2{pk2(f[0], f[1]), pk2(f[2], f[3])};
+        }
+      }
+      float xh[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xh[r] = HN ? bfw(nv[i][slot], r) * rs[r] + c1[r] : 0.f;
+      if (gate_nb) {
+        float f[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) f[r] = bfw(w, r) * (xh[r] > 0.f ? 1.f : gate_slope);
+        w = uint2{pk2(f[0], f[1]), pk2(f[2], f[3])};
+      }
+      if constexpr (HR) {
+        float f[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) f[r] = bfw(w, r) + bfw(rv[i][slot], r);
+        w = uint2{pk2(f[0], f[1]), pk2(f[2], f[3])};
+      }
+      __builtin_amdgcn_raw_buffer_store_b64(s2t_u32x2{w.x, w.y}, ry_, voff + 32 * j, soff(i, ld), 0);
+      if (nb_on) {   // from the stored bf16 dz, as the unfused partial pass reads it
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = bfw(w, r) * (xh[r] > 0.f ? 1.f : nb_slope);
+          s1[r] += d;
+          s2[r] += d * xh[r];
+        }
+      }
+    }
+    if (nb_on) {
+      // the column's 128 rows live in the 16 lanes of this lane's group: fixed-order xor tree
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s1[r] += __shfl_xor(s1[r], o);
+          s2[r] += __shfl_xor(s2[r], o);
+        }
+      if (pl == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const long o = ((long)img * a.nb_nchunks + chunk) * nbC + nbc0 + 16 * j + 4 * g + r;
+          a.nb_ws[o] = s1[r];
+          a.nb_ws[(long)a.N * a.nb_nchunks * nbC + o] = s2[r];
+        }
+      }
+    }
+  }
+}
+
+// One wave's register epilogue.  acc[i][j][r] = output channel nc0 + 16 j + 4 g + r (g = lane
+// >> 4) at tile position p = 16 i + (lane & 15) of class cls (grid row qy0 + p / W, column
+// p % W).  bias / alpha / output activation, the norm statistics of a following norm and the
+// fp8 shadow (plain path), or -- EXT, a dgrad -- the act' gate (loaded, or from the norm's
+// xhat), the parked skip gradient and the norm-backward partials.  Same bf16 rounding points
+// and the same stats / partials layout as the implicit-GEMM epilogue (conv_dev.h): chunk =
+// class * (H*W / BM) + tile-in-image.  One 16-channel fragment column j at a time (its 4
+// channels per lane, 8 positions): the live set stays within the 128-register budget.
+template <int W, bool EXT>
+__device__ __forceinline__ void s2t_epilogue(const ConvFwdArgs& a, f32x4 (&acc)[TM][TN], int m0, int img, int qy0,
+                                             int nc0, int cls, int lane) {
+  constexpr int FPR = W / 16;
+  const int g = lane >> 4, pl = lane & 15;
+  const int ry = cls >> 1, rx = cls & 1;
+  const int HWq = a.H * W;
+  const int chunk = cls * (HWq / BM) + (m0 - img * HWq) / BM;
+  const int pix0 = (img * a.OH + 2 * qy0 + ry) * a.OW + 2 * pl + rx;
+  auto pix = [&](int i) __attribute__((always_inline)) { return pix0 + (i / FPR) * 2 * a.OW + 32 * (i % FPR); };
+  const float al = a.alpha ? a.alpha[0] : 1.f;
+  const uint2 z2 = {0u, 0u};
+  const Fp8Shadow qsh{static_cast<uint8_t*>(a.q_out), a.q_site, a.q_fmt};
+  const float qsc = (!EXT && qsh.q) ? fp8_shadow_scale(qsh) : 0.f;
+  float qmax = 0.f;
+
+  // ---- accumulators -> bf16 (bias, alpha, output activation): 32 registers instead of 64
+  uint2 vv[TM][TN];
+  auto cvt = [&](auto act_tag) __attribute__((always_inline)) {
+    constexpr int ACT = decltype(act_tag)::value;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float bj[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bj[r] = a.bias ? a.bias[nc0 + 16 * j + 4 * g + r] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        float f[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) f[r] = act_fwd(acc[i][j][r] * al + bj[r], ACT);
+        vv[i][j] = uint2{pk2(f[0], f[1]), pk2(f[2], f[3])};
+      }
+    }
+  };
+  switch (a.act_out) {   // tanh / sigmoid outputs are refused by the gate (image layers only)
+    case ACT_RELU: cvt(std::integral_constant<int, ACT_RELU>{}); break;
+    case ACT_LRELU: cvt(std::integral_constant<int, ACT_LRELU>{}); break;
+    default: cvt(std::integral_constant<int, ACT_NONE>{}); break;
+  }
+
+  if constexpr (EXT) {
+    // the operand set per column: uniform over the wave's two columns -> one up-front path
+    bool fx[TN], fr[TN], fn[TN], fo[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int co = nc0 + 16 * j + 4 * g;
+      const bool first = co < a.Csplit;
+      const int nbco = co - a.nb_c0;
+      fo[j] = a.nb_ws != nullptr && nbco >= 0 && nbco < a.nb_C;
+      fn[j] = fo[j] && !a.nb_colsum;
+      const bool xbj = (first ? a.xb1 : a.xb2) != nullptr;
+      fx[j] = a.act_bwd && xbj && !(fn[j] && a.nb_gate);
+      fr[j] = a.res1 && first;
+    }
+    const bool uni = fx[0] == fx[1] && fr[0] == fr[1] && fn[0] == fn[1] && fo[0] == fo[1] &&
+                     __builtin_amdgcn_readfirstlane(fx[0] | (fr[0] << 1) | (fn[0] << 2) | (fo[0] << 3)) ==
+                         (fx[0] | (fr[0] << 1) | (fn[0] << 2) | (fo[0] << 3));
+    // unsplit output, the nb channel range whole 32-channel wave columns (host-typical)
+    const bool plain = a.Csplit == a.Cout && (!a.nb_ws || (a.nb_c0 % 32 == 0 && a.nb_C % 32 == 0));
+    if (plain && __builtin_amdgcn_readfirstlane(uni) && !(a.act_bwd && fn[0] && a.nb_gate && !a.xb1)) {
+      const int code = fx[0] | (fr[0] << 1) | (fn[0] << 2);
+      switch (code) {
+        case 1: if (S2T_CASES >> 1 & 1) s2t_ext_all<W, true, false, false>(a, vv, img, qy0, chunk, nc0, cls, lane, fo[0]); return;
+        case 2: if (S2T_CASES >> 2 & 1) s2t_ext_all<W, false, true, false>(a, vv, img, qy0, chunk, nc0, cls, lane, fo[0]); return;
+        case 3: if (S2T_CASES >> 3 & 1) s2t_ext_all<W, true, true, false>(a, vv, img, qy0, chunk, nc0, cls, lane, fo[0]); return;
+        case 4: if (S2T_CASES >> 4 & 1) s2t_ext_all<W, false, false, true>(a, vv, img, qy0, chunk, nc0, cls, lane, fo[0]); return;
+        case 5: if (S2T_CASES >> 5 & 1) s2t_ext_all<W, true, false, true>(a, vv, img, qy0, chunk, nc0, cls, lane, fo[0]); return;
+        case 6: if (S2T_CASES >> 6 & 1) s2t_ext_all<W, false, true, true>(a, vv, img, qy0, chunk, nc0, cls, lane, fo[0]); return;
+        case 0: if (S2T_CASES >> 0 & 1) s2t_ext_all<W, false, false, false>(a, vv, img, qy0, chunk, nc0, cls, lane, fo[0]); return;
+        default: break;
+      }
+    }
+  }
+
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int co = nc0 + 16 * j + 4 * g;
+    uint2 v[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) v[i] = vv[i][j];
+    // ---- output half (virtual concat split of a dgrad into a concat input)
+    const bool first = co < a.Csplit;
+    bf16* y = static_cast<bf16*>(first ? a.y1 : a.y2);
+    const int ld = first ? a.Csplit : a.Cout - a.Csplit;
+    const int cof = first ? co : co - a.Csplit;
+
+    if constexpr (!EXT) {
+      // ---- norm statistics: (mean, M2) per column, shifted by the tile's first row
+      if (a.stats) {
+        const uint2 p0 = {(uint32_t)__shfl((int)v[0].x, lane & 48), (uint32_t)__shfl((int)v[0].y, lane & 48)};
+        float s1[4], s2[4], piv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          piv[r] = bfw(p0, r);
+          s1[r] = s2[r] = 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float d = bfw(v[i], r) - piv[r];
+            s1[r] += d;
+            s2[r] += d * d;
+          }
+        // the column's 128 rows live in the 16 lanes of this lane's group: fixed-order xor tree
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            s1[r] += __shfl_xor(s1[r], o);
+            s2[r] += __shfl_xor(s2[r], o);
+          }
+        if (pl == 0) {
+          const float inv = 1.f / (float)BM;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const long o = ((long)img * a.stats_nchunks + chunk) * a.Cout + co + r;
+            a.stats[o] = piv[r] + s1[r] * inv;
+            a.stats[(long)a.N * a.stats_nchunks * a.Cout + o] = fmaxf(s2[r] - s1[r] * s1[r] * inv, 0.f);
+          }
+        }
+      }
+      // ---- stores (+ fp8 shadow: host only with an unsplit output, no act' gate)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const long p = pix(i);
+        *reinterpret_cast<uint2*>(y + p * ld + cof) = v[i];
+        if (qsh.q) {
+          const float fm = fp8_max(qsh.fmt);
+          float f[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            f[r] = bfw(v[i], r);
+            qmax = fmaxf(qmax, fabsf(f[r]));
+            f[r] = fminf(fmaxf(f[r] * qsc, -fm), fm);
+          }
+          *reinterpret_cast<uint32_t*>(qsh.q + p * ld + cof) = cvt4(f[0], f[1], f[2], f[3], qsh.fmt);
+        }
+      }
+    } else {
+      // ---- dgrad: act' gate, skip gradient, norm-backward partials
+      const bf16* xb = static_cast<const bf16*>(first ? a.xb1 : a.xb2);
+      const bool res_t = a.res1 && first;   // host: res1 only with Csplit == Cout
+      const int nbco = co - a.nb_c0;
+      const bool nb_on = a.nb_ws != nullptr && nbco >= 0 && nbco < a.nb_C;
+      const bool nbx_on = nb_on && !a.nb_colsum;
+      const bool gate_nb = a.act_bwd && xb && nbx_on && a.nb_gate;
+      const bool gate_t = a.act_bwd && xb && !gate_nb;
+      const float nb_slope = (a.nb_act && !a.nb_colsum) ? neg_slope(a.nb_act) : 1.f;
+      const float gate_slope = neg_slope(a.act_bwd);
+      const bf16* res_p = static_cast<const bf16*>(a.res1);
+      const bf16* nbx_p = static_cast<const bf16*>(a.nb_x);
+      float rs[4], c1[4], s1[4], s2[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        rs[r] = c1[r] = s1[r] = s2[r] = 0.f;
+        if (nbx_on) {
+          const long si = a.nb_batch ? nbco + r : (long)img * a.nb_C + nbco + r;
+          rs[r] = a.nb_rstd[si];
+          c1[r] = -a.nb_mean[si] * rs[r];
+        }
+      }
+#pragma unroll
+      for (int i0 = 0; i0 < TM; i0 += PG) {
+        uint2 xv[PG], rv[PG], nv[PG];
+#pragma unroll
+        for (int u = 0; u < PG; ++u) {
+          const long p = pix(i0 + u);
+          xv[u] = gate_t ? *reinterpret_cast<const uint2*>(xb + p * ld + cof) : z2;
+          rv[u] = res_t ? *reinterpret_cast<const uint2*>(res_p + p * ld + cof) : z2;
+          nv[u] = nbx_on ? *reinterpret_cast<const uint2*>(nbx_p + p * a.nb_C + nbco) : z2;
+        }
+#pragma unroll
+        for (int u = 0; u < PG; ++u) {
+          const long p = pix(i0 + u);
+          uint2 w = v[i0 + u];
+          if (gate_t) {
+            if (a.act_bwd == ACT_RELU) {
+              // zero the gradient where x <= 0 (bf16 sign / zero test on the int pipe)
+              const uint32_t x0 = xv[u].x, x1 = xv[u].y;
+              w.x &= (((int16_t)(x0 & 0xffffu) > 0) ? 0xffffu : 0u) | (((int16_t)(x0 >> 16) > 0) ? 0xffff0000u : 0u);
+              w.y &= (((int16_t)(x1 & 0xffffu) > 0) ? 0xffffu : 0u) | (((int16_t)(x1 >> 16) > 0) ? 0xffff0000u : 0u);
+            } else {
+              float f[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) f[r] = bfw(w, r) * act_grad_from_input(bfw(xv[u], r), a.act_bwd);
+              w = uint2{pk2(f[0], f[1]), pk2(f[2], f[3])};
+            }
+          }
+          float xh[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xh[r] = bfw(nv[u], r) * rs[r] + c1[r];
+          if (gate_nb) {
+            float f[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) f[r] = bfw(w, r) * (xh[r] > 0.f ? 1.f : gate_slope);
+            w = uint2{pk2(f[0], f[1]), pk2(f[2], f[3])};
+          }
+          if (res_t) {
+            float f[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) f[r] = bfw(w, r) + bfw(rv[u], r);
+            w = uint2{pk2(f[0], f[1]), pk2(f[2], f[3])};
+          }
+          *reinterpret_cast<uint2*>(y + p * ld + cof) = w;
+          if (nb_on) {   // from the stored bf16 dz, as the unfused partial pass reads it
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float d = bfw(w, r) * (xh[r] > 0.f ? 1.f : nb_slope);
+              s1[r] += d;
+              s2[r] += d * xh[r];
+            }
+          }
+        }
+      }
+      if (a.nb_ws) {
+        // the column's 128 rows live in the 16 lanes of this lane's group: fixed-order xor tree
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            s1[r] += __shfl_xor(s1[r], o);
+            s2[r] += __shfl_xor(s2[r], o);
+          }
+        if (pl == 0 && nb_on) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const long o = ((long)img * a.nb_nchunks + chunk) * a.nb_C + nbco + r;
+            a.nb_ws[o] = s1[r];
+            a.nb_ws[(long)a.N * a.nb_nchunks * a.nb_C + o] = s2[r];
+          }
+        }
+      }
+    }
+  }
+  if (!EXT && qsh.q) fp8_amax_commit(qmax, qsh.site);
+}
+
 }  // namespace
 
+// arrival counters of the persistent blocks per CU (key: XCC, SE, SH, CU of the hardware id)
+__device__ unsigned s2t_cu_arrivals[8 * 512];
+
+// timeline probe (P2P_S2T_DEBUG=1, tools/s2t_timeline.py): per block and tile, wave 0's
+// s_memrealtime (100 MHz) at the tile's loop start, epilogue start, epilogue end, and the
+// block's hardware id (XCC << 16 | HW_ID >> 8) -- diagnostics only, never in a timed run
+constexpr int S2T_DBG_BLOCKS = 1024, S2T_DBG_TILES = 96;
+__device__ unsigned long long s2t_dbg[S2T_DBG_BLOCKS * S2T_DBG_TILES * 4];
+__device__ __forceinline__ void s2t_stamp(int dbg, int k, int field) {
+  if (dbg && threadIdx.x == 0 && blockIdx.x < S2T_DBG_BLOCKS && k < S2T_DBG_TILES)
+    s2t_dbg[((size_t)blockIdx.x * S2T_DBG_TILES + k) * 4 + field] = __builtin_amdgcn_s_memrealtime();
+}
+
 template <int W, bool RELU, bool EXT, int F8 = 0>
-__global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a) {
+__global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a, int ntiles, int stagger_ns, int stagger_mode, int dbg) {
   using G = S2TGeom<W>;
   constexpr int ES = F8 ? 1 : 2;      // bytes per operand element
   constexpr int CHC = 128 / ES;       // channels per 128-B halo chunk
+  constexpr int FPR = W / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int ntiles_n = a.Cout / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int mt = bid / ntiles_n, nt = bid - mt * ntiles_n;
-  const int m0 = mt * BM, n0 = nt * BN;
   const int HWq = a.H * a.W;
-  const int img = m0 / HWq;
-  const int qy0 = (m0 - img * HWq) / W;
   const int C = a.C1 + a.C2;
   const int nch = C / CHC;
   // fp8: E8M0 dequant exponents of the two sources and of the weight image
   const int ex1 = (F8 && a.qs_x1) ? a.qs_x1[2] : 127;
   const int ex2 = (F8 && a.qs_x2) ? a.qs_x2[2] : 127;
   const int ew = (F8 && a.qs_w) ? a.qs_w[2] : 127;
-
   char* ring = smem;
-  // halo chunk ch -> ring stage: unit e = j * NT + tid holds logical 16-B chunk
-  // (e & 7) ^ (hp & 6) of halo pixel hp = e >> 3 (source-side swizzle).  Unlike the im2col
-  // tiles' (row >> 1) & 7 key, hp & 6 keeps every ds_read_b128 lane group conflict-free for
-  // ANY fragment base pixel (the tap shifts move it by -1 / -HW): 16 consecutive pixels,
-  // 8 of each parity, with the group's two k chunks in the pattern 0,0,1,1,1,1,0,0 map to 16
-  // distinct bank quads (exhaustive check over bases and k steps; the old key: up to 4-way)
-  // pixels outside the image (or beyond the halo) read the zero page.  Recomputed per issue
-  // (a few VALU per unit, 2-4 issues per block) instead of holding 2 x HLD registers.
-  auto issue = [&](int ch, int stage) {
+
+  // persistent tile sequence of this block: k * gridDim.x + slot (XCD-contiguous slots: the
+  // tiles running at once on one XCD are neighbours -- shared halo rows and weights in its L2)
+  const int grid = gridDim.x;
+  int L = xcd_remap(blockIdx.x, grid);
+  if (L >= ntiles) return;
+  // two persistent blocks share a CU and run identical tiles: started together they stay in
+  // lockstep, both in their MFMA loops, then both in their memory-bound epilogues.  The
+  // second block to arrive on a CU starts stagger_ns later, so one block's epilogue runs
+  // beside the other's MFMAs (a speed heuristic only: any placement computes the same tiles)
+  if (dbg && tid == 0 && blockIdx.x < S2T_DBG_BLOCKS) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    s2t_dbg[(size_t)blockIdx.x * S2T_DBG_TILES * 4 + 3] = ((unsigned long long)xcc << 16) | (hw >> 8);
+  }
+  if (stagger_ns > 0 && stagger_mode == 1) {
+    // blocks 0 .. grid/2 - 1 fill one slot per CU first, the second half pairs with them
+    if (blockIdx.x >= grid / 2) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) * 10 < stagger_ns) __builtin_amdgcn_s_sleep(32);
+    }
+  } else if (stagger_ns > 0) {
+    if (tid == 0) {
+      unsigned hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      const unsigned key = ((xcc & 7u) << 9) | ((hw >> 8) & 511u);
+      *reinterpret_cast<volatile int*>(ring) = (int)(atomicAdd(&s2t_cu_arrivals[key], 1u) & 1u);
+    }
+    __syncthreads();
+    const int late = *reinterpret_cast<volatile int*>(ring);
+    __syncthreads();
+    if (late) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) * 10 < stagger_ns) __builtin_amdgcn_s_sleep(32);
+    }
+  }
+  auto tile_geo = [&](int Lt, int& m0, int& n0, int& img, int& qy0) __attribute__((always_inline)) {
+    const int mt = Lt / ntiles_n;
+    const int nt = Lt - mt * ntiles_n;
+    m0 = mt * BM;
+    n0 = nt * BN;
+    img = m0 / HWq;
+    qy0 = (m0 - img * HWq) / W;
+  };
+
+  // halo chunk ch of a tile -> ring stage: unit e = j * NT + tid holds logical 16-B chunk
+  // (e & 7) ^ (hp & 6) of halo pixel hp = e >> 3 (source-side swizzle: every ds_read_b128
+  // lane group conflict-free for ANY fragment base pixel -- the tap shifts move it by -1 /
+  // -HW; kernel_experiments_r3.md); pixels outside the image (or beyond the halo) read the
+  // zero page
+  auto issue = [&](int img, int qy0, int ch, int stage) __attribute__((always_inline)) {
     const bool s1 = ch * CHC < a.C1;
     const char* src = static_cast<const char*>(s1 ? a.x1 : a.x2);
     const int cs = s1 ? a.C1 : a.C2;
@@ -144,8 +586,8 @@ __global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a) {
       const bool in = hp < G::HPIX && hx < G::HWV && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
       const int kc = (e & 7) ^ (hp & 6);
       const int pix = in ? (img * a.H + iy) * a.W + ix : 0;
-      const char* g = src + ((long)pix * cs + coff) * ES + kc * 16;
-      glds16(in ? g : static_cast<const char*>(a.zero), dst + (j * NT + wid * 64) * 16);
+      const char* gp = src + ((long)pix * cs + coff) * ES + kc * 16;
+      glds16(in ? gp : static_cast<const char*>(a.zero), dst + (j * NT + wid * 64) * 16);
     }
   };
 
@@ -155,26 +597,22 @@ __global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a) {
   const int ry = cls_w >> 1, rx = cls_w & 1;
   const int ky0 = (ry + 1) & 1, kx0 = (rx + 1) & 1;
   const int dy = (ry + 1 - ky0) >> 1, dx = (rx + 1 - kx0) >> 1;
-  // B fragments by buffer loads: per-lane row offset (output channel n0 + (lane & 15), k block
-  // 8 * (lane >> 4)) in voffset, the (tap, k-step, 16-column block) offset in soffset
+  // weight fragments by buffer loads: per-lane row offset (output channel n0 + 32 nh + (lane
+  // & 15), k block 8 (lane >> 4)) in voffset, the (tap, k-step, 16-column block) in soffset
   const int wrow = 16 * C * ES;   // bytes per output channel of the [Cout][4][4][C] image
   const auto wsrd = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, a.Cout * wrow, 0x00020000);
-  const int bvoff = (n0 + 32 * nh + (lane & 15)) * wrow + 16 * (lane >> 4);
-  // A fragment rows: lane row r = lane & 15 of fragment i -> grid position p = 16 i + r
+  auto bv_of = [&](int n0) __attribute__((always_inline)) {
+    return (n0 + 32 * nh + (lane & 15)) * wrow + 16 * (lane >> 4);
+  };
+  // halo fragment rows: lane row r = lane & 15 of fragment i -> grid position p = 16 i + r
   //   (ly = p / W, qx = p % W); tap (ty, tx) reads halo pixel (ly + dy - ty + 1, qx + dx - tx + 1)
-  //   = abase + (i / (W / 16)) * HW + 16 * (i % (W / 16)): one register, the rest immediate
+  //   = abase + (i / FPR) * HW + 16 * (i % FPR): one register, the rest immediate
   int abase = (dy + 1) * G::HW + (lane & 15) + dx + 1;
   const int kq = lane >> 4;
 
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // B operand of k-step (ch, t, ks): t = ty * 2 + tx, ks = 64-B half of the chunk (bf16: the
-  // 32-deep half; fp8: the high 16 bytes of each lane's 32-deep operand)
-  auto loadB = [&](int ch, int t, int ks, u32x4 (&b)[TN]) __attribute__((always_inline)) {
+  // weight operand of k-step (ch, t, ks): t = ty * 2 + tx, ks = 64-B half of the chunk (bf16:
+  // the 32-deep half; fp8: the high 16 bytes of each lane's 32-deep operand)
+  auto loadB = [&](int bvoff, int ch, int t, int ks, u32x4 (&b)[TN]) __attribute__((always_inline)) {
     const int ky = ky0 + 2 * (t >> 1), kx = kx0 + 2 * (t & 1);
     const int so = ((ky * 4 + kx) * C + ch * CHC) * ES + ks * 64;
 #pragma unroll
@@ -182,25 +620,40 @@ __global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a) {
       b[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wsrd, bvoff, so + j * 16 * wrow, 0));
   };
 
-  if constexpr (F8 != 0) {
-    // fp8: one k-step per tap (128 deep); both 64-B halves of its B operand one tap ahead
-    // both halves land in one 8-register operand per fragment (no concatenation copies)
-    auto loadB8 = [&](int ch, int t, s2t_i32x8 (&b)[TN]) __attribute__((always_inline)) {
-      u32x4 lo[TN], hi[TN];
-      loadB(ch, t, 0, lo);
-      loadB(ch, t, 1, hi);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = s2t_cat8(lo[j], hi[j]);
-    };
-#if S2T_F8PF
-    s2t_i32x8 bc[TN], bn[TN];
-    loadB8(0, 0, bc);
+  int m0, n0, img, qy0;
+  tile_geo(L, m0, n0, img, qy0);
+  int bvoff = bv_of(n0);
+  f32x4 acc[TM][TN];
+  int stage = 0;
+  u32x4 bcur[TN], bnxt[TN];
+  issue(img, qy0, 0, 0);
+  int kt = 0;   // tile count of this block (timeline probe)
+  for (;;) {
+    s2t_stamp(dbg, kt, 0);
+    const int Ln = L + grid;
+#ifdef S2T_ONE
+    const bool has_next = false;
+#else
+    const bool has_next = Ln < ntiles;
 #endif
-    issue(0, 0);
+    int m0n = m0, n0n = n0, imgn = img, qy0n = qy0;
+    if (has_next) tile_geo(Ln, m0n, n0n, imgn, qy0n);
+    const int bvoffn = bv_of(n0n);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if constexpr (F8 == 0) loadB(bvoff, 0, 0, 0, bcur);
     for (int ch = 0; ch < nch; ++ch) {
-      const int stage = ch & 1;
-      if (ch + 1 < nch) {
-        issue(ch + 1, stage ^ 1);
+      const bool last = ch + 1 == nch;
+      // the next halo chunk of the flat (tile, chunk) stream into the other stage: the next
+      // tile's first chunk lands while this tile's last chunk and epilogue run
+      if (!last) {
+        issue(img, qy0, ch + 1, stage ^ 1);
+        wait_vm<G::HLD>();
+      } else if (has_next) {
+        issue(imgn, qy0n, 0, stage ^ 1);
         wait_vm<G::HLD>();
       } else {
         wait_vm<0>();
@@ -208,184 +661,183 @@ __global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a) {
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       const char* A = ring + stage * G::STAGE_BYTES;
+      // the fragment addresses are loop-invariant per (tap, k-step, fragment): hoisted out of
+      // the chunk loop they would pin 64 registers (and spill); laundering abase keeps them per step
       asm volatile("" : "+v"(abase));
-      const int sa = ch * CHC < a.C1 ? ex1 : ex2;   // a chunk never straddles the sources
+      if constexpr (F8 != 0) {
+        // fp8: one k-step per tap (128 deep); both 64-B halves of its weight operand at the top
+        // of the tap (4 waves per SIMD hide the L2 round trip; one tap ahead spilled)
+        const int sa = ch * CHC < a.C1 ? ex1 : ex2;   // a chunk never straddles the sources
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-#if S2T_F8PF
-        if (t < 3) loadB8(ch, t + 1, bn);
-        else if (ch + 1 < nch) loadB8(ch + 1, 0, bn);
-#else
-        s2t_i32x8 bc[TN];
-        loadB8(ch, t, bc);
-#endif
-        const int toff = -(t >> 1) * G::HW - (t & 1);
-        constexpr int FPR = W / 16;
-        const int hp0 = abase + toff;
-        const int offlo = (hp0 * 8 + (kq ^ (hp0 & 6))) * 16;
-        const int offhi = (hp0 * 8 + ((kq + 4) ^ (hp0 & 6))) * 16;
-        auto rd = [&](int i) __attribute__((always_inline)) {
-          const int fo = ((i / FPR) * G::HW + 16 * (i % FPR)) * 128;
-          u32x4 lo = *reinterpret_cast<const u32x4*>(A + offlo + fo);
-          u32x4 hi = *reinterpret_cast<const u32x4*>(A + offhi + fo);
-          if constexpr (RELU) {
-            lo = s2t_relu_fp8x16(lo);
-            hi = s2t_relu_fp8x16(hi);
+        for (int t = 0; t < 4; ++t) {
+          s2t_i32x8 bc[TN];
+          {
+            u32x4 lo[TN], hi[TN];
+            loadB(bvoff, ch, t, 0, lo);
+            loadB(bvoff, ch, t, 1, hi);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bc[j] = s2t_cat8(lo[j], hi[j]);
           }
-          return s2t_cat8(lo, hi);
-        };
-        s2t_i32x8 af[2];
-        af[0] = rd(0);
+          const int toff = -(t >> 1) * G::HW - (t & 1);
+          const int hp0 = abase + toff;
+          const int offlo = (hp0 * 8 + (kq ^ (hp0 & 6))) * 16;
+          const int offhi = (hp0 * 8 + ((kq + 4) ^ (hp0 & 6))) * 16;
+          auto rd = [&](int i) __attribute__((always_inline)) {
+            const int fo = ((i / FPR) * G::HW + 16 * (i % FPR)) * 128;
+            u32x4 lo = *reinterpret_cast<const u32x4*>(A + offlo + fo);
+            u32x4 hi = *reinterpret_cast<const u32x4*>(A + offhi + fo);
+            if constexpr (RELU) {
+              lo = s2t_relu_fp8x16(lo);
+              hi = s2t_relu_fp8x16(hi);
+            }
+            return s2t_cat8(lo, hi);
+          };
+          s2t_i32x8 af[2];
+          af[0] = rd(0);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          if (i + 1 < TM) af[(i + 1) & 1] = rd(i + 1);
+          for (int i = 0; i < TM; ++i) {
+            if (i + 1 < TM) af[(i + 1) & 1] = rd(i + 1);
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i & 1], bc[j], acc[i][j], F8 - 1, 0, 0,
-                                                                         sa, 0, ew);
+            for (int j = 0; j < TN; ++j)   // weights = src A (rows = channels), pixels = src B
+              acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bc[j], af[i & 1], acc[i][j], 0, F8 - 1,
+                                                                           0, ew, 0, sa);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x020, 2 * TN, 0);   // the weight loads first
+          __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);        // fragments 0 and 1
+#pragma unroll
+          for (int i = 0; i < TM - 2; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, TN, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 2 * TN, 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x020, 2 * TN, 0);   // the B prefetch first
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);        // A fragments 0 and 1
-#pragma unroll
-        for (int i = 0; i < TM - 2; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, TN, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 2 * TN, 0);
-#if S2T_F8PF
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bc[j] = bn[j];
-#endif
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-  } else {
-#if S2T_PD > 1
-    // B ring: k-step st of a chunk uses bq[st & 3]; loads run PD k-steps ahead (8 k-steps per
-    // chunk keep the ring index static across chunks) -- experiment (kernel_experiments_r3.md)
-    constexpr int PD = S2T_PD;
-    u32x4 bq[4][TN];
-#pragma unroll
-    for (int st = 0; st < PD; ++st) loadB(0, st >> 1, st & 1, bq[st]);
-#else
-    u32x4 bcur[TN], bnxt[TN];
-    loadB(0, 0, 0, bcur);
-#endif
-    issue(0, 0);
-    for (int ch = 0; ch < nch; ++ch) {
-      const int stage = ch & 1;
-      if (ch + 1 < nch) {
-        issue(ch + 1, stage ^ 1);
-        wait_vm<G::HLD>();
       } else {
-        wait_vm<0>();
-      }
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      const bf16* A = reinterpret_cast<const bf16*>(ring + stage * G::STAGE_BYTES);
-      // the A addresses are loop-invariant per (tap, k-step, fragment): hoisted out of the chunk
-      // loop they would pin 64 registers (and spill); laundering abase keeps them per step
-      asm volatile("" : "+v"(abase));
+        const bf16* Ab = reinterpret_cast<const bf16*>(A);
 #pragma unroll
-      for (int st = 0; st < 8; ++st) {
-        const int t = st >> 1, ks = st & 1;
-        // prefetch the next k-step's B (the next chunk's first after the last) a whole k-step
-        // of MFMAs ahead of its use; then A fragment i + 1 is read while fragment i's 4 MFMAs
-        // run (sched_group_barrier pins that interleave: left alone the scheduler sinks the B
-        // loads below the MFMAs and the next step waits vmcnt(0) on a full L2 round trip)
-#if S2T_PD > 1
-        if (st + PD < 8) loadB(ch, (st + PD) >> 1, (st + PD) & 1, bq[(st + PD) & 3]);
-        else if (ch + 1 < nch) loadB(ch + 1, (st + PD - 8) >> 1, (st + PD - 8) & 1, bq[(st + PD) & 3]);
-        u32x4 (&bcur)[TN] = bq[st & 3];
-#else
-        if (st < 7) loadB(ch, (st + 1) >> 1, (st + 1) & 1, bnxt);
-        else if (ch + 1 < nch) loadB(ch + 1, 0, 0, bnxt);
-#endif
-        const int toff = -(t >> 1) * G::HW - (t & 1);
-        const int kc = ks * 4 + kq;
-        // fragment i sits (i / FPR) rows and 16 (i % FPR) pixels from fragment 0: both multiples
-        // of 8 pixels, so the same swizzle key -- its address is an immediate offset
-        constexpr int FPR = W / 16;
-        const int hp0 = abase + toff;
-        const int off0 = (hp0 * 8 + (kc ^ (hp0 & 6))) * 8;
-        auto rd = [&](int i) __attribute__((always_inline)) {
-          bf16x8 v = *reinterpret_cast<const bf16x8*>(A + off0 + ((i / FPR) * G::HW + 16 * (i % FPR)) * 64);
-          if constexpr (RELU) v = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, v)));
-          return v;
-        };
-        bf16x8 af[2];
-        af[0] = rd(0);
+        for (int st = 0; st < 8; ++st) {
+          const int t = st >> 1, ks = st & 1;
+          // prefetch the next k-step's weights (the next chunk's -- or the next tile's -- first
+          // after the last) a whole k-step of MFMAs ahead of use, unconditionally (selects, no
+          // branch: the schedule pins below need one basic block); then fragment i + 1 is read
+          // while fragment i's MFMAs run
+          {
+            // (after the tile's last k-step: a dummy reload of the current k-step -- the
+            // next tile loads its first weights itself, so no operand is live across the
+            // epilogue: its registers are the epilogue's)
+            int nchk = ch, nst = st + 1;
+            if (st == 7) {
+              nst = last ? 7 : 0;
+              nchk = last ? ch : ch + 1;
+            }
+            loadB(bvoff, nchk, nst >> 1, nst & 1, bnxt);
+          }
+          const int toff = -(t >> 1) * G::HW - (t & 1);
+          const int kc = ks * 4 + kq;
+          // fragment i sits (i / FPR) rows and 16 (i % FPR) pixels from fragment 0: both multiples
+          // of 8 pixels, so the same swizzle key -- its address is an immediate offset
+          const int hp0 = abase + toff;
+          const int off0 = (hp0 * 8 + (kc ^ (hp0 & 6))) * 8;
+          auto rd = [&](int i) __attribute__((always_inline)) {
+            bf16x8 x = *reinterpret_cast<const bf16x8*>(Ab + off0 + ((i / FPR) * G::HW + 16 * (i % FPR)) * 64);
+            if constexpr (RELU) x = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, x)));
+            return x;
+          };
+          bf16x8 af[2];
+          af[0] = rd(0);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          if (i + 1 < TM) af[(i + 1) & 1] = rd(i + 1);
+          for (int i = 0; i < TM; ++i) {
+            if (i + 1 < TM) af[(i + 1) & 1] = rd(i + 1);
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i & 1], __builtin_bit_cast(bf16x8, bcur[j]),
-                                                                 acc[i][j], 0, 0, 0);
+            for (int j = 0; j < TN; ++j)   // weights = src A (rows = channels), pixels = src B
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bcur[j]), af[i & 1],
+                                                                   acc[i][j], 0, 0, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x020, TN, 0);   // the weight prefetch (VMEM reads) first
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);    // fragments 0 and 1
+#pragma unroll
+          for (int i = 0; i < TM - 2; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, TN, 0); // fragment i's MFMAs
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // read fragment i + 2
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 2 * TN, 0);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) bcur[j] = bnxt[j];
         }
-        __builtin_amdgcn_sched_group_barrier(0x020, TN, 0);   // the B prefetch (VMEM reads) first
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);    // A fragments 0 and 1
-#pragma unroll
-        for (int i = 0; i < TM - 2; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, TN, 0); // fragment i's MFMAs
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // read fragment i + 2
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 2 * TN, 0);
-#if S2T_PD <= 1
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bcur[j] = bnxt[j];
-#endif
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();   // every wave done reading this stage before it is re-filled
+      stage ^= 1;
     }
-  }
-  __syncthreads();
 
-  // ---- epilogue: every wave stages its class tile, then the block stores class by class
-  bf16* Cs0 = reinterpret_cast<bf16*>(smem);
-  conv_stage_tile<TM, TN, LDC>(a, acc, Cs0 + cls_w * BM * LDC, 0, 32 * nh, n0, lane);
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(smem + 4 * BM * LDC * 2);
-  const FastDiv fd_hwq = make_fastdiv((uint32_t)HWq), fd_wq = make_fastdiv((uint32_t)a.W);
-#pragma unroll 1
-  for (int cls = 0; cls < 4; ++cls) {
-    const ClassGeom g = class_geom<1>(a, cls);
-    bf16* Cs = Cs0 + cls * BM * LDC;
-    conv_epilogue_tail<BM, BN, 1, NT, EXT>(a, g, m0, n0, Cs, red, reinterpret_cast<char*>(Cs), fd_hwq, fd_wq);
-    __syncthreads();
+#ifndef S2T_NOEPI
+    s2t_stamp(dbg, kt, 1);
+    s2t_epilogue<W, EXT>(a, acc, m0, img, qy0, n0 + 32 * nh, cls_w, lane);
+    s2t_stamp(dbg, kt, 2);
+    ++kt;
+#else
+    { float s = 0; for (int i = 0; i < TM; ++i) for (int j = 0; j < TN; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3]; static_cast<float*>(a.y1)[threadIdx.x] = s; }
+#endif
+    if (!has_next) break;
+    L = Ln;
+    m0 = m0n;
+    n0 = n0n;
+    img = imgn;
+    qy0 = qy0n;
+    bvoff = bvoffn;
   }
+}
+
+// blocks of the grid: P2P_S2T_GRID = 0 (default) one tile per block; N = a persistent grid of
+// N blocks per CU (the LDS ring and 128 VGPRs admit two 8-wave blocks).  Measured at the U-Net
+// e2 / e3 input-gradient shapes, B = 1024: one tile per block 2.34 / 1.78 ms, persistent
+// 2.49 / 1.82 ms -- the dispatcher's refill desynchronises the two blocks of a CU, the
+// persistent pair runs its MFMA loops and its epilogues in lockstep (timeline probe).
+static int s2t_grid(long tiles) {
+  static int cus[64] = {0};
+  const char* e = std::getenv("P2P_S2T_GRID");   // read per launch: tests toggle it
+  const int per_cu = e ? std::atoi(e) : 0;
+  if (per_cu <= 0) return (int)tiles;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int& n = cus[dev & 63];
+  if (n == 0) {
+    int c = 256;
+    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    n = c;
+  }
+  return (int)std::min<long>(tiles, (long)per_cu * n);
 }
 
 template <int W, bool RELU, bool EXT, int F8 = 0>
 static int launch_s2t(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = S2TGeom<W>::SMEM;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_s2t_kernel<W, RELU, EXT, F8>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
-  }
-  const long mtiles = (long)a.N * a.H * a.W / BM;
-  const long blocks = mtiles * (a.Cout / BN);
-  hipLaunchKernelGGL((conv_s2t_kernel<W, RELU, EXT, F8>), dim3((unsigned)blocks), dim3(NT), smem, st, a);
+  static std::atomic<uint64_t> attr_mask{0};
+  smem_attr_once(reinterpret_cast<const void*>(&conv_s2t_kernel<W, RELU, EXT, F8>), smem, attr_mask);
+  const long tiles = (long)a.N * a.H * a.W / BM * (a.Cout / BN);
+  const char* e = std::getenv("P2P_S2T_STAGGER");   // ns (A/B knob)
+  const int stagger = e ? std::atoi(e) : 0;
+  const char* em = std::getenv("P2P_S2T_STAGGER_MODE");   // 0: per-CU arrival order, 1: grid halves
+  const int smode = em ? std::atoi(em) : 0;
+  const char* ed = std::getenv("P2P_S2T_DEBUG");
+  const int dbg = (ed && ed[0] == '1') ? 1 : 0;
+  hipLaunchKernelGGL((conv_s2t_kernel<W, RELU, EXT, F8>), dim3((unsigned)s2t_grid(tiles)), dim3(NT), smem, st, a,
+                     (int)tiles, stagger, smode, dbg);
   return (int)hipGetLastError();
 }
 
-template <int W>
+template <int W, int F8>
 static int dispatch_s2t_w(const ConvFwdArgs& a, bool ext, hipStream_t st) {
   const bool relu = a.act_in == ACT_RELU;
-  if (ext) return relu ? -2 : launch_s2t<W, false, true>(a, st);
-  return relu ? launch_s2t<W, true, false>(a, st) : launch_s2t<W, false, false>(a, st);
+  if (ext) return relu ? -2 : launch_s2t<W, false, true, F8>(a, st);
+  return relu ? launch_s2t<W, true, false, F8>(a, st) : launch_s2t<W, false, false, F8>(a, st);
 }
 
 }  // namespace p2p
 
 // Geometry gate (the host checks the same before choosing this path, see s2t_ok in
-// bindings.cpp): returns -2 when not covered.  fp8: 64-wide grids, 128-channel chunks;
-// activations (e4m3) as the ConvT forward with or without its input ReLU, gradients (e5m2)
-// as input gradients with or without the extended epilogue.
+// bindings.cpp): returns -2 when not covered.  fp8: 128-channel chunks; activations (e4m3) as
+// the ConvT forward with or without its input ReLU, gradients (e5m2) as input gradients with
+// or without the extended epilogue.
 extern "C" int p2p_conv_s2t(const p2p::ConvFwdArgs* a, hipStream_t st) {
   using namespace p2p;
   if (a->splits != 1 || a->d2s || a->KH != 4 || a->KW != 4 || a->stride != 2 || a->pad != 1 || a->up != 1 ||
@@ -394,22 +846,30 @@ extern "C" int p2p_conv_s2t(const p2p::ConvFwdArgs* a, hipStream_t st) {
   const int chc = a->fp8 ? 128 : 64;
   if (a->OH != 2 * a->H || a->OW != 2 * a->W || a->Cout % 64 || a->C1 % chc || a->C2 % chc || a->C1 + a->C2 < chc)
     return -2;
-  if ((long)a->H * a->W % 128) return -2;
+  if ((long)a->H * a->W % 128 || (long)a->N * a->OH * a->OW >= (1l << 31)) return -2;
   if (a->act_in != ACT_NONE && a->act_in != ACT_RELU) return -2;
-  const bool ext = a->nb_ws || ((a->act_bwd || a->res1) && !a->epi_serial);
-  if (ext && a->act_in) return -2;
+  if (a->act_out != ACT_NONE && a->act_out != ACT_RELU && a->act_out != ACT_LRELU) return -2;
+  if (a->Csplit % 8 || (a->nb_ws && (a->nb_c0 % 8 || a->nb_C % 8))) return -2;
+  const bool ext = a->nb_ws || a->act_bwd || a->res1;
+  if (ext && (a->act_in || a->stats || a->q_out)) return -2;
   if (a->fp8) {
-    if (a->W != 64 || !a->qs_x1 || !a->qs_w || (a->C2 && !a->qs_x2)) return -2;
-    if (a->fp8 == 1) {
-      if (ext) return -2;
-      return a->act_in == ACT_RELU ? launch_s2t<64, true, false, 1>(*a, st) : launch_s2t<64, false, false, 1>(*a, st);
-    }
-    if (a->act_in) return -2;
-    return ext ? launch_s2t<64, false, true, 2>(*a, st) : launch_s2t<64, false, false, 2>(*a, st);
+    if (!a->qs_x1 || !a->qs_w || (a->C2 && !a->qs_x2)) return -2;
+    if (a->fp8 == 1 && ext) return -2;
+    if (a->fp8 == 2 && a->act_in) return -2;
+    // 64-wide grids only: the fp8 32-wide variants spill inside the k loop (the 128-channel
+    // chunk's two-half operands); those layers stay on the implicit-GEMM fp8 tile
+    if (a->W != 64) return -2;
+    return a->fp8 == 1 ? dispatch_s2t_w<64, 1>(*a, ext, st) : dispatch_s2t_w<64, 2>(*a, ext, st);
   }
   switch (a->W) {
-    case 32: return dispatch_s2t_w<32>(*a, ext, st);
-    case 64: return dispatch_s2t_w<64>(*a, ext, st);
+    case 32: return dispatch_s2t_w<32, 0>(*a, ext, st);
+    case 64: return dispatch_s2t_w<64, 0>(*a, ext, st);
     default: return -2;
   }
+}
+
+// timeline probe read-out (tools/s2t_timeline.py through torch.ops.p2p.s2t_debug)
+extern "C" long p2p_s2t_dbg_bytes() { return (long)sizeof(p2p::s2t_dbg); }
+extern "C" int p2p_s2t_dbg_read(void* dst, long bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(p2p::s2t_dbg), (size_t)bytes, 0, hipMemcpyDeviceToHost);
 }

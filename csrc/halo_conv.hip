@@ -25,8 +25,13 @@ constexpr int HT = 16;                  // q tile edge
 constexpr int HP = HT + 2;              // halo edge
 constexpr int HPIX = HP * HP;           // 324 halo pixels
 constexpr int HUNITS = HPIX * 8;        // 16-B units per 64-channel chunk
-constexpr int HLD = (HUNITS + 255) / 256;  // glds per lane per stage (11)
-constexpr int STAGE_UNITS = HLD * 256;
+constexpr int NTH = 512;                // 8 waves: 2 per SIMD at one block per CU (round 4:
+                                        // 4 waves left a single wave per SIMD to hide every
+                                        // halo and epilogue round trip of this memory-bound layer)
+constexpr int NW = NTH / 64;
+constexpr int RPW = HT / NW;            // q rows (16-pixel fragments) per wave
+constexpr int HLD = (HUNITS + NTH - 1) / NTH;  // glds per lane per stage (6)
+constexpr int STAGE_UNITS = HLD * NTH;
 constexpr int STAGE_BYTES = STAGE_UNITS * 16;
 constexpr int LDC = 24;                 // epilogue staging row (16 columns + pad)
 
@@ -43,7 +48,7 @@ __device__ __forceinline__ void wait_vm() {
 
 
 template <int NCH, bool RELU>
-__global__ void __launch_bounds__(256) halo_union_kernel(HaloArgs a) {
+__global__ void __launch_bounds__(NTH) halo_union_kernel(HaloArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* As = reinterpret_cast<bf16*>(smem);                       // 2 stages
   bf16* Bs = reinterpret_cast<bf16*>(smem + 2 * STAGE_BYTES);     // [9][NCH][16][64]
@@ -55,9 +60,9 @@ __global__ void __launch_bounds__(256) halo_union_kernel(HaloArgs a) {
 
   // ---- resident B operand (waited together with the first stage)
   constexpr int BUNITS = 9 * NCH * 16 * 8;
-  constexpr int BUNITS_PAD = (BUNITS + 255) / 256 * 256;   // whole wave instructions
+  constexpr int BUNITS_PAD = (BUNITS + NTH - 1) / NTH * NTH;   // whole wave instructions
 #pragma unroll
-  for (int e0 = wid * 64; e0 < BUNITS_PAD; e0 += 256) {
+  for (int e0 = wid * 64; e0 < BUNITS_PAD; e0 += NTH) {
     const int e = e0 + lane;
     const int n = (e >> 3) & 15, tc = e >> 7;
     const int tap = tc / NCH, ch = tc - tap * NCH;
@@ -69,7 +74,7 @@ __global__ void __launch_bounds__(256) halo_union_kernel(HaloArgs a) {
   int hy[HLD], hx[HLD], kcs[HLD];
 #pragma unroll
   for (int j = 0; j < HLD; ++j) {
-    const int e = (j * 4 + wid) * 64 + lane;
+    const int e = (j * NW + wid) * 64 + lane;
     const int hp = e >> 3;
     hy[j] = hp < HPIX ? hp / HP : -4096;   // beyond the halo: out of image -> zero page
     hx[j] = hp - (hp / HP) * HP;
@@ -97,13 +102,13 @@ __global__ void __launch_bounds__(256) halo_union_kernel(HaloArgs a) {
       const int iy = qy0 - 1 + hy[j], ix = qx0 - 1 + hx[j];
       const bool inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
       const bf16* g = inb ? src + ((long)(n * a.H + iy) * a.W + ix) * cs + coff + kcs[j] * 8 : a.zero;
-      glds16(g, dst + (j * 4 + wid) * 64 * 8);
+      glds16(g, dst + (j * NW + wid) * 64 * 8);
     }
   };
 
-  f32x4 acc[4];
+  f32x4 acc[RPW];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < RPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float l1 = 0.f;
   // mode 2: the L1 sign term's weight = scale x dL/dl1 (a device scalar written by autograd)
   const float l1w = a.scale * (a.mode == 2 && a.wscale ? *a.wscale : 1.f);
@@ -131,8 +136,8 @@ __global__ void __launch_bounds__(256) halo_union_kernel(HaloArgs a) {
         const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(
             Bs + (((tap * NCH + ch) * 16 + px) * 8 + (kc ^ ((px >> 1) & 7))) * 8);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int hp = (wid * 4 + i + uy) * HP + px + ux;
+        for (int i = 0; i < RPW; ++i) {
+          const int hp = (wid * RPW + i + uy) * HP + px + ux;
           bf16x8 af = *reinterpret_cast<const bf16x8*>(A + (hp * 8 + (kc ^ ((hp >> 1) & 7))) * 8);
           if constexpr (RELU) af = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, af)));
           acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[i], 0, 0, 0);
@@ -148,8 +153,8 @@ __global__ void __launch_bounds__(256) halo_union_kernel(HaloArgs a) {
       bf16* Cs = As + stage * (STAGE_UNITS * 8);
       const float bj = a.bias[px];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rowb = wid * 64 + i * 16 + kq * 4;
+      for (int i = 0; i < RPW; ++i) {
+        const int rowb = (wid * RPW + i) * 16 + kq * 4;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float v = acc[i][r] + bj;
@@ -162,12 +167,13 @@ __global__ void __launch_bounds__(256) halo_union_kernel(HaloArgs a) {
       // depth-to-space stores: 4 output pixels per thread, their packed-image operands
       // loaded before any is used (one HBM round trip per tile, not four)
       const int Ho = 2 * a.H, Wo = 2 * a.W;
-      long P[4];
-      bool ok[4];
-      bf16x8 ab[4], af[4];
+      constexpr int PQ = 1024 / NTH;   // output pixels per thread (256 q x 4 classes)
+      long P[PQ];
+      bool ok[PQ];
+      bf16x8 ab[PQ], af[PQ];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int item = tid + q * 256, row = item >> 2, cls = item & 3;
+      for (int q = 0; q < PQ; ++q) {
+        const int item = tid + q * NTH, row = item >> 2, cls = item & 3;
         const int qy = qy0 + (row >> 4), qx = qx0 + (row & 15);
         ok[q] = qy < a.H && qx < a.W;
         P[q] = ((long)n * Ho + 2 * (ok[q] ? qy : 0) + (cls >> 1)) * Wo + 2 * (ok[q] ? qx : 0) + (cls & 1);
@@ -175,8 +181,8 @@ __global__ void __launch_bounds__(256) halo_union_kernel(HaloArgs a) {
         if (a.mode == 2) af[q] = *reinterpret_cast<const bf16x8*>(a.pk_f + P[q] * 8);
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int item = tid + q * 256, row = item >> 2, cls = item & 3;
+      for (int q = 0; q < PQ; ++q) {
+        const int item = tid + q * NTH, row = item >> 2, cls = item & 3;
         if (!ok[q]) continue;
         const bf16* c = Cs + row * LDC + cls * 4;
         bf16x8 o;
@@ -210,7 +216,11 @@ __global__ void __launch_bounds__(256) halo_union_kernel(HaloArgs a) {
     __syncthreads();
     if (lane == 0) red[wid] = l1;
     __syncthreads();
-    if (tid == 0) a.l1_part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+    if (tid == 0) {
+      float t = 0.f;
+      for (int w = 0; w < NW; ++w) t += red[w];
+      a.l1_part[blockIdx.x] = t;
+    }
   }
 }
 
@@ -219,7 +229,7 @@ static int launch_halo(const HaloArgs& a, int blocks, hipStream_t st) {
   constexpr int smem = 2 * STAGE_BYTES + (9 * NCH * 16 * 8 + 255) / 256 * 256 * 16;
   static std::atomic<uint64_t> attr_mask{0};
   smem_attr_once(reinterpret_cast<const void*>(&halo_union_kernel<NCH, RELU>), smem, attr_mask);
-  hipLaunchKernelGGL((halo_union_kernel<NCH, RELU>), dim3(blocks), dim3(256), smem, st, a);
+  hipLaunchKernelGGL((halo_union_kernel<NCH, RELU>), dim3(blocks), dim3(NTH), smem, st, a);
   return (int)hipGetLastError();
 }
 

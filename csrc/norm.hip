@@ -494,18 +494,23 @@ __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
   const int p0 = cb * g.chunk;
   const int p1 = min(g.HW, p0 + g.chunk);
   const long NC = (long)g.N * g.C;
-  float mu[8], rs[8], ga[8], be[8], ca[8], cx[8], c0[8];
+  // per channel, folded once: z = x * zs + zb (the fused activation's input), and
+  // dx = ca * dy_eff + k0 + k1 * x (= ca * dy_eff + c0 + cx * xhat): five registers per
+  // channel instead of seven, two fewer VALU per element
+  float ca[8], k0[8], k1[8], zs[8], zb[8];
   const float pw = ACT == ACT_PRELU_T ? prelu_w[0] : 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const long ci = (long)n * g.C + cg * 8 + j;
-    mu[j] = mean[ci];
-    rs[j] = rstd[ci];
-    ga[j] = gamma ? gamma[cg * 8 + j] : 1.f;
-    be[j] = gamma ? beta[cg * 8 + j] : 0.f;
+    const float mu = mean[ci], rs = rstd[ci];
+    const float ga = gamma ? gamma[cg * 8 + j] : 1.f;
+    const float be = gamma ? beta[cg * 8 + j] : 0.f;
+    const float cx = coef[2 * NC + ci];
     ca[j] = coef[ci];
-    cx[j] = coef[2 * NC + ci];
-    c0[j] = coef[NC + ci];
+    k1[j] = cx * rs;
+    k0[j] = coef[NC + ci] - k1[j] * mu;
+    zs[j] = rs * ga;
+    zb[j] = be - mu * zs[j];
   }
   const long base = (long)n * g.HW * g.C + cg * 8;
   // optional fp8 (e5m2) shadow of dx: the producing conv's dgrad operand
@@ -517,9 +522,8 @@ __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
     unpack8(vd, fd);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float xh = (fx[j] - mu[j]) * rs[j];
-      const float d = ACT ? fd[j] * act_gate(xh * ga[j] + be[j], ACT, pw) : fd[j];
-      fd[j] = ca[j] * d + c0[j] + cx[j] * xh;
+      const float d = ACT ? fd[j] * act_gate(fmaf(fx[j], zs[j], zb[j]), ACT, pw) : fd[j];
+      fd[j] = fmaf(ca[j], d, fmaf(k1[j], fx[j], k0[j]));
     }
     const u32x4 o = pack8(fd);
     *reinterpret_cast<u32x4*>(dx + off) = o;

@@ -128,10 +128,12 @@ class CompressGANStep:
     @staticmethod
     def _wgrad_overlap(x, reducer):
         """G's conv weight gradients on the side stream (ops/hip.py ``wgrad_overlap``): grads
-        were just set to None and G runs once in this backward; not with a DP reducer."""
+        were just set to None and G runs once in this backward; with a DP reducer the conv
+        weight gradients are written straight into its buckets (parallel/ddp.py direct
+        gradients), everything else stays on the compute stream."""
         if x.is_cuda and _native.get_backend() == "native":
             from ..ops import hip
-            return hip.wgrad_overlap(x.device, enabled=reducer is None)
+            return hip.wgrad_overlap(x.device)
         return contextlib.nullcontext()
 
     def _seed_grad(self, loss):

@@ -163,7 +163,7 @@ class Pix2PixStep:
             loss_D = hip.lincomb(loss_D_fake, loss_D_real, 0.5, 0.5)
         with self._phase("D_bwd_opt"):
             self._zero(self.opt_D, self.reducer_d)
-            with hip.wgrad_overlap(real_A.device, enabled=self.reducer_d is None):
+            with hip.wgrad_overlap(real_A.device):
                 loss_D.backward(self._seed_grad(loss_D))
             if self.reducer_d is not None:
                 self.reducer_d.finish()
@@ -178,7 +178,7 @@ class Pix2PixStep:
             loss_G = hip.lincomb(loss_G_GAN, hip.head_l1_tap(loss_G_L1))
         with self._phase("G_bwd_opt"):
             self._zero(self.opt_G, self.reducer_g)
-            with hip.wgrad_overlap(real_A.device, enabled=self.reducer_g is None):
+            with hip.wgrad_overlap(real_A.device):
                 loss_G.backward(self._seed_grad(loss_G))
             hip.assert_no_deferred()          # every parked U-Net skip gradient consumed
             if self.reducer_g is not None:

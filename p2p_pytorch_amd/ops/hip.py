@@ -27,6 +27,7 @@ from __future__ import annotations
 import contextlib
 import itertools
 import os
+import sys
 
 import torch
 
@@ -36,6 +37,7 @@ from . import fp8 as _f8
 ACT = {None: 0, "none": 0, "relu": 1, "lrelu": 2, "tanh": 3, "sigmoid": 4}
 # P2P_NB_FUSE=0: norm backward runs its own partial pass (A/B knob for the dgrad-epilogue fusion)
 _NB_FUSE = os.environ.get("P2P_NB_FUSE", "1") != "0"
+_NB_LOG = os.environ.get("P2P_NB_LOG", "0") == "1"
 CL = torch.channels_last
 _NULLCTX = contextlib.nullcontext()
 
@@ -146,8 +148,10 @@ def _take_colsum(gy):
 # ``record_stream``: its deferred events under capture crashed a later capture).  Autograd
 # then hands each gradient to AccumulateGrad, which only STEALS it (grads set to None, one
 # gradient per weight); a weight that receives a second gradient in the same backward has
-# its earlier one joined first (autograd's add then runs on the compute stream).  Only used
-# without a DP reducer (its post-accumulate hooks copy the gradient on the compute stream).
+# its earlier one joined first (autograd's add then runs on the compute stream).  Under a DP
+# reducer (parallel/ddp.py) a conv weight's gradient is written straight into its bucket by
+# the kernel (accumulate mode, pre-scaled), so it may run on the side stream too; the
+# reducer's collective for that bucket waits on a side-stream event.
 class _WgradSide:
     on = False
     streams: dict = {}
@@ -538,6 +542,9 @@ class ConvFn(torch.autograd.Function):
             _stash_stats(y, outs[1])
         if Coutp != Cout:
             y = P().slice_channels(y, 0, Cout)
+        red = getattr(weight, "_p2p_direct", None)
+        if red is not None and ctx.needs_input_grad[2]:
+            red.count_use(weight)   # one direct backward contribution to expect
         ctx.cfg = cfg
         ctx.geo = (C1, C2, Cp, packed, Cout, Coutp, H, W)
         ctx.has_x2 = x2 is not None
@@ -694,11 +701,11 @@ def _wgrad_fp8(cfg, weight, q1, q2, gyp, act_in):
     gq, sg = _f8.quant(gyp, (k, "gy", 1), _f8.E5M2)
     KH, KW, s, p = cfg.KH, cfg.KW, cfg.stride, cfg.pad
 
-    def launch(gw):
+    def launch(gw, scale=1.0, acc=0):
         if cfg.transposed:
-            return bool(P().conv_wgrad(x1q, x2q, act_in, gq, None, 0, KH, KW, s, p, 0, 1, gw, 1.0, 0,
+            return bool(P().conv_wgrad(x1q, x2q, act_in, gq, None, 0, KH, KW, s, p, 0, 1, gw, scale, acc,
                                        0, sx, sg, _f8.E4M3, _f8.E5M2, sx2, None))
-        return bool(P().conv_wgrad(gq, None, 0, x1q, x2q, act_in, KH, KW, s, p, 0, 1, gw, 1.0, 0, 0,
+        return bool(P().conv_wgrad(gq, None, 0, x1q, x2q, act_in, KH, KW, s, p, 0, 1, gw, scale, acc, 0,
                                    sg, sx, _f8.E5M2, _f8.E4M3, None, sx2))
     return launch, (x1q, x2q, gq, sx, sx2, sg)
 
@@ -792,28 +799,45 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
             _DEFERRED[key] = gx1
             gx1 = None
     if need_w:
-        gw = torch.empty_like(weight, dtype=torch.float32, memory_format=torch.contiguous_format)
+        # data-parallel direct gradient (parallel/ddp.py): the kernel accumulates straight
+        # into the weight's bucket view, pre-scaled by 1/world, and the reducer is told --
+        # autograd gets no gradient for the weight (no AccumulateGrad add, no rescale pass),
+        # so the kernel may also run on the side stream
+        red = getattr(weight, "_p2p_direct", None) if alpha is None else None
+        direct = red is not None and red.direct_ok(weight)
+        if direct:
+            gw, wscale, wacc = weight.grad, red.scale, 1
+        else:
+            gw = torch.empty_like(weight, dtype=torch.float32, memory_format=torch.contiguous_format)
+            wscale, wacc = 1.0, 0
         act_in = _act_code(cfg.act_in)
         f8 = _wgrad_fp8(cfg, weight, q1, q2, gyp, act_in)
-        side = _wgrad_side(weight) if side_ok else None
+        if direct:
+            side = _WgradSide.on if side_ok else None
+            side = side or None
+        else:
+            side = _wgrad_side(weight) if side_ok else None
         if side is not None:
             side.wait_stream(torch.cuda.current_stream(side.device))
             _WgradSide.keep.append((q1, q2, gyp, f8))
         with (torch.cuda.stream(side) if side is not None else _NULLCTX):
-            if f8 is not None and f8[0](gw):
+            if f8 is not None and f8[0](gw, wscale, wacc):
                 pass
             elif cfg.transposed:
-                P().conv_wgrad(q1, q2, act_in, gyp, None, 0, KH, KW, s, p, 0, 1, gw, 1.0, 0)
+                P().conv_wgrad(q1, q2, act_in, gyp, None, 0, KH, KW, s, p, 0, 1, gw, wscale, wacc)
             elif (s == 1 and Coutp <= 16 and Cp >= 128 and KH == KW and not cfg.reflect
                   and cfg.up == 1):
                 # tiny-Cout stride-1 conv (PatchGAN logits): the GEMM's R = Cout would waste
                 # the MFMA tile, so compute it in transposed-conv form -- rows = input
                 # channels, the dY gather with pad K-1-p, taps flipped by the reduce
                 P().conv_wgrad(q1, q2, act_in, gyp, None, 0, KH, KW, 1, KH - 1 - p, 0, 1, gw,
-                               1.0, 0, 1)
+                               wscale, wacc, 1)
             else:
                 P().conv_wgrad(gyp, None, 0, q1, q2, act_in, KH, KW, s, p, int(cfg.reflect),
-                               cfg.up, gw, 1.0, 0)
+                               cfg.up, gw, wscale, wacc)
+        if direct:
+            red.direct_done(weight, side)
+            gw = None
     if need_b:
         gb = _take_colsum(gy) if (cfg.act_out in (None, "none") or cfg.out_gated) else None
         if gb is None:
@@ -1122,6 +1146,9 @@ class NormFn(torch.autograd.Function):
                 qd = _f8.shadow_buffer(x, _f8.E5M2)
                 qargs = (dsite, qd, _f8.E5M2)
         parts = _take_nbp(gy) if pw is None else None
+        if _NB_LOG:   # which norm backwards still run the partial-sum pass (tools/diag)
+            print(f"[nb] {'fused' if parts is not None else 'PARTIAL PASS'} x{tuple(x.shape)} "
+                  f"act={act} batch={bool(batch)}", file=sys.stderr)
         if parts is not None:
             dx = P().norm_bwd(x, gy, mean, rstd, g, b, fused_act, dg, db, need_x, batch, dsum,
                               *(qargs or (None, None, 0)), partials=parts)

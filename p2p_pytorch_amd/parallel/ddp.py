@@ -39,6 +39,16 @@ Mechanism
     completion callback), and ``comm_stats()`` reports the last backward's collective
     busy time, the part of it left exposed after backward's last kernel, and the overlap
     fraction -- the JSONL "comm ms / overlap %" of SURVEY.md section 5.5.
+  * Direct gradients (``direct=True``, round 4): the native conv backward writes a weight's
+    (and bias's) gradient straight into its bucket view, pre-scaled by 1/world, with the
+    wgrad kernel's own accumulate mode -- no AccumulateGrad add, no 1/world pass -- and may
+    run it on the weight-gradient side stream (ops/hip.py ``wgrad_overlap``).  Readiness:
+    each conv forward with grad enabled counts a use of its weight (``count_use``), each
+    backward contribution retires one (``direct_done``, with the stream it was enqueued on);
+    the last one marks the param ready, and a bucket whose params were written on the side
+    stream launches its all-reduce from a comm stream that waits on both streams' events.
+    Gradients that still arrive through autograd are scaled by 1/world in their hook, so
+    ``finish`` never rescales.
   * Bucket size: xGMI is point-to-point (7 links x ~153 GB/s per GPU); RCCL's ring /
     direct algorithms are per-link bound, so few large buckets (tens of MB) amortise the
     per-collective latency while still leaving >= 2-4 buckets per network to overlap.
@@ -54,7 +64,7 @@ import torch.distributed as dist
 
 
 class _Bucket:
-    __slots__ = ("params", "flat", "cbuf", "pending", "work", "index", "events")
+    __slots__ = ("params", "flat", "cbuf", "pending", "work", "index", "events", "side")
 
     def __init__(self, params, device, dtype, index, comm_dtype):
         self.params = params
@@ -66,6 +76,7 @@ class _Bucket:
         self.work = None
         self.index = index
         self.events = None
+        self.side = []        # events of direct gradient writes enqueued on other streams
 
 
 class _StreamJoin:
@@ -105,7 +116,7 @@ class _HostEvent:
 class GradReducer:
     def __init__(self, module: torch.nn.Module, bucket_mb: float = 64.0, process_group=None,
                  comm_dtype: torch.dtype | None = None, tail_mb: float = 8.0, rebucket: bool = True,
-                 force_comm: bool = False):
+                 force_comm: bool = False, direct: bool = True):
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.backend = dist.get_backend(process_group) if dist.is_initialized() else None
@@ -126,6 +137,13 @@ class GradReducer:
         self._timing = False
         self._comm_stream = None
         self._last = None        # (bucket events, end-of-backward event) of the last finish()
+        # every gradient lands pre-scaled by 1/world (direct writes and autograd hooks alike)
+        self.scale = 1.0 / self.world if (self.comm and self.world > 1) else 1.0
+        self.direct = bool(direct)
+        self._uses: dict = {}
+        if self.direct:
+            for p in params:
+                p._p2p_direct = self
 
     def _build(self, order):
         self.buckets: list[_Bucket] = []
@@ -198,6 +216,42 @@ class GradReducer:
         lo = b.flat.data_ptr()
         if not (lo <= p.grad.data_ptr() < lo + b.flat.numel() * b.flat.element_size()):
             self._rebind(p, b, copy=True)
+        if self.scale != 1.0:
+            p.grad.mul_(self.scale)          # this backward's gradient alone (bucket zeroed)
+        b.pending -= 1
+        if b.pending == 0:
+            self._launch(b)
+
+    # ------------------------------------------------------------------ direct gradients
+    def count_use(self, p):
+        """A forward read ``p`` with grad enabled: one more backward contribution to expect."""
+        self._uses[id(p)] = self._uses.get(id(p), 0) + 1
+
+    def direct_ok(self, p) -> bool:
+        """The backward may write ``p``'s gradient into its bucket view itself."""
+        if not (self.direct and self.active) or p.grad is None:
+            return False
+        b = self._param_bucket.get(p)
+        if b is None or b.work is not None:
+            return False
+        lo = b.flat.data_ptr()
+        return lo <= p.grad.data_ptr() < lo + b.flat.numel() * b.flat.element_size()
+
+    def direct_done(self, p, stream=None):
+        """One direct contribution to ``p.grad`` has been enqueued (on ``stream``, default the
+        current one); the last expected one marks ``p`` ready."""
+        b = self._param_bucket[p]
+        if stream is not None and stream != torch.cuda.current_stream(stream.device):
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            b.side.append(ev)
+        n = self._uses.get(id(p), 1) - 1
+        if n > 0:
+            self._uses[id(p)] = n
+            return
+        self._uses.pop(id(p), None)
+        if self._ready_order is not None:
+            self._ready_order.append(p)
         b.pending -= 1
         if b.pending == 0:
             self._launch(b)
@@ -220,7 +274,7 @@ class GradReducer:
             # callback (gloo completes it on its own thread while backward continues)
             buf = b.flat
             if b.cbuf is not None:
-                torch.mul(b.flat, 1.0 / self.world, out=b.cbuf)
+                b.cbuf.copy_(b.flat)
                 buf = b.cbuf
             e0, e1 = _HostEvent().record(), _HostEvent()
             b.work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
@@ -229,19 +283,25 @@ class GradReducer:
             return
         timed = self._timing and not torch.cuda.is_current_stream_capturing() and b.flat.is_cuda
         cur = torch.cuda.current_stream(b.flat.device) if b.flat.is_cuda else None
-        if timed:
+        side = b.flat.is_cuda and bool(b.side)
+        if timed or side:
+            # a comm stream ordered after the compute stream AND the side-stream gradient
+            # writes of this bucket (their events), so the compute stream itself never waits
             if self._comm_stream is None:
                 self._comm_stream = torch.cuda.Stream(device=b.flat.device)
             cs = self._comm_stream
             cs.wait_stream(cur)
+            for ev in b.side:
+                cs.wait_event(ev)
             ctx = torch.cuda.stream(cs)
         else:
             ctx = contextlib.nullcontext()
         with ctx:
             buf = b.flat
             if b.cbuf is not None:
-                # pre-scale into the narrow comm buffer: sum of world terms of x/world
-                torch.mul(b.flat, 1.0 / self.world, out=b.cbuf)
+                # the narrow comm buffer (gradients arrive pre-scaled by 1/world: the bf16 sum
+                # of world terms x/world is exact in scale for power-of-two worlds)
+                b.cbuf.copy_(b.flat)
                 buf = b.cbuf
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -254,6 +314,10 @@ class GradReducer:
                     b.cbuf.record_stream(cs)
                 b.events = (e0, e1)
                 b.work = _StreamJoin(cs)
+            elif side:
+                work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                work.wait()                     # cs waits for RCCL's stream (no host sync)
+                b.work = _StreamJoin(cs)
             else:
                 b.work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
@@ -261,7 +325,9 @@ class GradReducer:
         for b in self.buckets:
             b.work = None
             b.events = None
+            b.side = []
             b.pending = len(b.params)
+        self._uses = {}
 
     def _join_inflight(self):
         # collectives launched but never finished (e.g. a backward abandoned by an
@@ -296,14 +362,15 @@ class GradReducer:
                 self._launch(b)
         if end_bwd is not None:
             self._last = ([b.events for b in self.buckets if b.events is not None], end_bwd)
-        inv = 1.0 / self.world
         for b in self.buckets:
             if b.work is not True and b.work is not None:
                 b.work.wait()
+            elif b.side:
+                # no collective (world 1): order the compute stream after the side writes
+                for ev in b.side:
+                    torch.cuda.current_stream(b.flat.device).wait_event(ev)
             if b.cbuf is not None:
                 b.flat.copy_(b.cbuf)            # already averaged (pre-scaled)
-            elif self.world > 1:
-                b.flat.mul_(inv)
         self._reset()
 
     def enable_timing(self, on: bool = True):
@@ -363,3 +430,6 @@ class GradReducer:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        for p in self.params:
+            if getattr(p, "_p2p_direct", None) is self:
+                del p._p2p_direct

@@ -1,0 +1,122 @@
+"""Training-convergence evidence for the native paths.
+
+Every other numerics test compares ONE step.  Here the same pix2pix model (U-Net-128 + 70x70
+PatchGAN, GAN + 100 * L1, Adam 2e-4 / 0.5, batch 16 at 128x128) is trained from the same
+initial weights for ``STEPS`` steps on a learnable synthetic task -- B is a fixed 3x3 colour
+mix + blur of A, with A smooth random images -- three ways:
+
+  * stock PyTorch fp32 eager (``set_backend('torch')``, no autocast): the reference numerics;
+  * the native HIP path in bf16 (the headline path);
+  * the native HIP path with fp8 convs (BASELINE config 5).
+
+Asserted per native path: the train L1 (mean of the last 20 steps) fell to <= 50 % of the
+first 10 steps'; it ends within 15 % of the fp32 run's; no update was skipped by the NaN
+guard; and the held-out PSNR (the reference's per-epoch validation metric, train.py:450-502,
+computed on the device by engine/metrics.py) is at most 1 dB below the fp32 run's and 3 dB
+above the untrained generator's (first MI355X run: L1 0.197 -> 0.0304 / 0.0287 / 0.0294 and
+PSNR 14.5 -> 33.6 / 35.4 / 35.0 dB for fp32 / bf16 / fp8).  Dropout is off (``use_dropout=False``) so the three runs see the same
+network function (their dropout RNG streams differ by backend).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import p2p_pytorch_amd as p2p
+from p2p_pytorch_amd.ops import fp8 as _fp8
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 300
+BATCH = 16
+SIZE = 128
+NTRAIN = 64
+NTEST = 16
+
+
+def _task(seed=0):
+    """Smooth random A in [-1, 1] (bilinear-upsampled 16x16 noise) and B = clamp(mix(A))."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(seed)
+    n = NTRAIN + NTEST
+    low = torch.rand(n, 3, 16, 16, device=dev, generator=g) * 2 - 1
+    a = F.interpolate(low, size=(SIZE, SIZE), mode="bilinear", align_corners=False).clamp(-1, 1)
+    mix = torch.tensor([[0.2, 0.7, 0.1], [0.6, -0.3, 0.5], [-0.4, 0.3, 0.8]], device=dev)
+    w = torch.zeros(3, 3, 3, 3, device=dev)
+    blur = torch.tensor([[1., 2., 1.], [2., 4., 2.], [1., 2., 1.]], device=dev) / 16.0
+    for o in range(3):
+        for i in range(3):
+            w[o, i] = mix[o, i] * blur
+    b = F.conv2d(a, w, padding=1).clamp(-1, 1)
+    return a[:NTRAIN], b[:NTRAIN], a[NTRAIN:], b[NTRAIN:]
+
+
+def _init_state():
+    from p2p_pytorch_amd.models import define_D, define_G
+    torch.manual_seed(1234)
+    G = define_G(netG="unet_128", gpu_id="cuda", use_dropout=False, verbose=False)
+    D = define_D(6, 64, norm="instance", netD="basic", gpu_id="cuda", verbose=False)
+    return ({k: v.detach().clone() for k, v in G.state_dict().items()},
+            {k: v.detach().clone() for k, v in D.state_dict().items()})
+
+
+def _train(backend, precision, init, task):
+    from p2p_pytorch_amd.engine.metrics import psnr
+    from p2p_pytorch_amd.engine.pix2pix import Pix2PixStep
+    from p2p_pytorch_amd.models import define_D, define_G
+    p2p.set_backend(backend)
+    _fp8.set_precision(precision)
+    try:
+        G = define_G(netG="unet_128", gpu_id="cuda", use_dropout=False, verbose=False)
+        D = define_D(6, 64, norm="instance", netD="basic", gpu_id="cuda", verbose=False)
+        G.load_state_dict(init[0])
+        D.load_state_dict(init[1])
+        step = Pix2PixStep(G, D, lr=2e-4, beta1=0.5, lambda_L1=100.0)
+        a_tr, b_tr, a_te, b_te = task
+        dt = torch.float32 if backend == "torch" else torch.bfloat16
+
+        def prep(x):
+            return x.to(dt).contiguous(memory_format=torch.channels_last)
+
+        def held_out_psnr():
+            with torch.no_grad():
+                out = G(prep(a_te)).float()
+            # per-image PSNR on [-1, 1] -> [0, 1] levels, averaged like the reference's epoch mean
+            return float(psnr(b_te.float(), out, ref_compat=False).float().mean())
+
+        p0 = held_out_psnr()
+        l1 = []
+        for s in range(STEPS):
+            i = (s * BATCH) % NTRAIN
+            losses = step.step(prep(a_tr[i:i + BATCH]), prep(b_tr[i:i + BATCH]))
+            l1.append(losses["G_L1"])
+        l1 = [float(v) / 100.0 for v in l1]
+        p1 = held_out_psnr()
+        skipped = float(step.skipped) if step.skipped is not None else 0.0
+        return {"l1_first": sum(l1[:10]) / 10, "l1_last": sum(l1[-20:]) / 20, "psnr0": p0, "psnr": p1,
+                "skipped": skipped, "finite": all(v == v for v in l1)}
+    finally:
+        _fp8.set_precision("bf16")
+        p2p.set_backend("native")
+
+
+@pytest.fixture(scope="module")
+def runs():
+    task = _task()
+    init = _init_state()
+    out = {"fp32": _train("torch", "bf16", init, task),
+           "bf16": _train("native", "bf16", init, task),
+           "fp8": _train("native", "fp8", init, task)}
+    print("convergence:", out)
+    return out
+
+
+@pytest.mark.parametrize("path", ["bf16", "fp8"])
+def test_native_training_converges_like_fp32(runs, path):
+    ref, r = runs["fp32"], runs[path]
+    assert ref["finite"] and r["finite"]
+    assert ref["l1_last"] <= 0.5 * ref["l1_first"], ref          # the task is learnable
+    assert r["skipped"] == 0.0, r
+    assert r["l1_last"] <= 0.5 * r["l1_first"], r
+    assert abs(r["l1_last"] - ref["l1_last"]) <= 0.15 * ref["l1_last"], (r, ref)
+    assert r["psnr"] > r["psnr0"] + 3.0, r
+    assert r["psnr"] >= ref["psnr"] - 1.0, (r, ref)   # (GAN runs land a dB or two apart either way)

@@ -52,7 +52,7 @@ def _worker(rank, world, port, q):
 
         def spy(b):
             launches.append(b.index)
-            local[b.index] = b.flat.detach().clone()
+            local[b.index] = b.flat.detach().clone() / red_d.scale   # grads arrive pre-scaled
             orig(b)
 
         red_d._launch = spy

@@ -1,7 +1,7 @@
 """Data-parallel hardening on CPU (gloo): the paths a multi-GPU run takes that the basic
 reducer tests do not.
 
-  * ``comm_dtype=torch.bfloat16``: buckets pre-scaled by 1/world into a bf16 wire buffer,
+  * ``comm_dtype=torch.bfloat16``: buckets (gradients pre-scaled by 1/world) cast into a bf16 wire buffer,
     all-reduced, widened back -- the reduced gradient is within a bf16 bound of the fp32
     mean of the rank-local gradients, and parameters stay bitwise identical across ranks.
   * ``enable_timing()`` + ``comm_stats()``: every bucket is counted, busy / exposed times
@@ -72,7 +72,8 @@ def _bf16_worker(rank, world, port, q):
         orig = red._launch
 
         def spy(b):
-            local[b.index] = b.flat.detach().clone()   # the rank-local fp32 gradient
+            # the rank-local fp32 gradient (buckets hold it pre-scaled by 1/world since round 4)
+            local[b.index] = b.flat.detach().clone() / red.scale
             orig(b)
 
         red._launch = spy

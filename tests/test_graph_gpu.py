@@ -9,7 +9,9 @@ step.  With ``set_deterministic(True)`` (ordered split-K reductions):
       weight images) advances on the device;
   (b) the same with the data-parallel reducers attached on a world-size-1 RCCL process
       group and ``force_comm=True``: the bucket all-reduces are real RCCL collectives,
-      captured into the graph, and the result is still bitwise the plain eager step.
+      captured into the graph, and the result is still bitwise the plain eager step --
+      with the conv weight gradients written straight into the buckets by the kernels
+      (direct gradients, on the side stream; counted) and with them through autograd.
 """
 import pytest
 import torch
@@ -23,7 +25,7 @@ pytestmark = pytest.mark.gpu
 STEPS = 3
 
 
-def _build(reducers=False):
+def _build(reducers=False, direct=True):
     from p2p_pytorch_amd.engine.pix2pix import Pix2PixStep
     from p2p_pytorch_amd.models import define_D, define_G
     from p2p_pytorch_amd.parallel import GradReducer
@@ -34,8 +36,8 @@ def _build(reducers=False):
     D = define_D(6, 64, norm="instance", netD="basic", gpu_id=dev, verbose=False)
     rg = rd = None
     if reducers:
-        rg = GradReducer(G, bucket_mb=4.0, force_comm=True)
-        rd = GradReducer(D, bucket_mb=4.0, force_comm=True)
+        rg = GradReducer(G, bucket_mb=4.0, force_comm=True, direct=direct)
+        rd = GradReducer(D, bucket_mb=4.0, force_comm=True, direct=direct)
         assert len(rg.buckets) > 1
     return Pix2PixStep(G, D, reducer_g=rg, reducer_d=rd), G, D
 
@@ -55,8 +57,8 @@ def _params(G, D):
     return torch.cat([p.detach().reshape(-1) for p in list(G.parameters()) + list(D.parameters())])
 
 
-def _eager(reducers=False):
-    step, G, D = _build(reducers)
+def _eager(reducers=False, direct=True):
+    step, G, D = _build(reducers, direct)
     for a, b in _data():
         losses = step.step(a, b)
     torch.cuda.synchronize()
@@ -92,13 +94,27 @@ def test_graph_replay_equals_eager_steps(deterministic):
 def test_rccl_reducers_under_capture_equal_eager(deterministic):
     from p2p_pytorch_amd.parallel import dist as pdist
     pdist.init_single(torch.device("cuda", torch.cuda.current_device()))
+    from p2p_pytorch_amd.parallel import GradReducer
+    ndirect = [0]
+    orig = GradReducer.direct_done
+
+    def counted(self, p, stream=None):
+        ndirect[0] += 1
+        return orig(self, p, stream)
+
+    GradReducer.direct_done = counted
     try:
         assert dist.get_backend() == "nccl"
         pe, le = _eager(reducers=False)
         pr, lr = _eager(reducers=True)          # eager with real RCCL collectives
+        n_eager = ndirect[0]
+        pa, la = _eager(reducers=True, direct=False)   # gradients through autograd
         pg, lg = _graph(reducers=True)          # the same, captured into one hipGraph
     finally:
+        GradReducer.direct_done = orig
         dist.destroy_process_group()
-    assert le == lr == lg
+    assert n_eager > 0, "no conv weight gradient took the direct path"
+    assert le == lr == la == lg
     assert torch.equal(pe, pr), (pe - pr).abs().max().item()
+    assert torch.equal(pe, pa), (pe - pa).abs().max().item()
     assert torch.equal(pe, pg), (pe - pg).abs().max().item()

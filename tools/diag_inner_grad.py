@@ -1,0 +1,104 @@
+"""Where does the native gradient of the innermost normalised encoder conv (U-Net e7,
+``G.downs.6``, IN over a 2x2 plane) lose accuracy?  
+
+One production-shape step (tests/test_production_shapes_gpu.py: U-Net-256 + PatchGAN,
+256x256, B = 64, lr = 0) in fp32 (stock PyTorch), eager bf16 autocast and native; tensor
+hooks capture the gradients of the innermost levels' activations:
+  e6_z  skip 5 (e6 IN+lrelu output, 4x4)       e7_x  e7 conv output (pre-norm, 2x2)
+  e7_z  skip 6 (e7 IN+lrelu output, 2x2)       e8    e8 conv output (relu, 1x1)
+and the parameter gradients of downs.5 / 6 / 7.  Printed: max |err| / max |ref| per tensor.
+Also an fp64 run of the same step: how far fp32 itself is from fp64 (conditioning).
+
+    python tools/diag_inner_grad.py [--B 64]
+"""
+import argparse
+import copy
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import p2p_pytorch_amd as p2p  # noqa: E402
+
+
+def nets():
+    from p2p_pytorch_amd.models import define_D, define_G
+    torch.manual_seed(11)
+    G = define_G(netG="unet_256", gpu_id="cpu", verbose=False, use_dropout=False)
+    D = define_D(6, 64, norm="instance", netD="basic", gpu_id="cpu", verbose=False)
+    return G, D
+
+
+def run(kind, G0, D0, a, b):
+    from p2p_pytorch_amd.engine.pix2pix import Pix2PixStep
+    G, D = copy.deepcopy(G0).cuda(), copy.deepcopy(D0).cuda()
+    grads = {}
+
+    def cap(name):
+        def fwd_hook(mod, inp, out):
+            if out.requires_grad:
+                out.register_hook(lambda g, n=name: grads.__setitem__(n, g.detach().float().cpu()))
+        return fwd_hook
+
+    hs = [G.down_norms[5].register_forward_hook(cap("e6_z")),
+          G.downs[6].register_forward_hook(cap("e7_x")),
+          G.down_norms[6].register_forward_hook(cap("e7_z")),
+          G.downs[7].register_forward_hook(cap("e8"))]
+    if kind in ("fp32", "eager", "fp64"):
+        p2p.set_backend("torch")
+        if kind == "fp64":
+            G, D = G.double(), D.double()
+        try:
+            step = Pix2PixStep(G, D, lr=0.0, autocast_dtype=torch.bfloat16 if kind == "eager" else None)
+            dt = torch.float64 if kind == "fp64" else torch.float32
+            step.step(a.cuda().to(dt), b.cuda().to(dt))
+        finally:
+            p2p.set_backend("native")
+    else:
+        p2p.set_backend("native")
+        step = Pix2PixStep(G, D, lr=0.0, packed=(kind == "native"))
+
+        def dev(x):
+            return x.cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        step.step(dev(a), dev(b))
+    torch.cuda.synchronize()
+    for h in hs:
+        h.remove()
+    for i in (5, 6, 7):
+        grads[f"downs.{i}.weight"] = G.downs[i].weight.grad.detach().double().cpu()
+    return grads
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=64)
+    args = ap.parse_args()
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    G0, D0 = nets()
+    g = torch.Generator().manual_seed(13)
+    a = torch.rand(args.B, 3, 256, 256, generator=g) * 2 - 1
+    b = torch.rand(args.B, 3, 256, 256, generator=g) * 2 - 1
+    res = {k: run(k, G0, D0, a, b) for k in ("fp64", "fp32", "eager", "native", "native_unpacked")}
+    ref = res["fp64"]
+    print(f"{'tensor':18s} {'|ref|max':>10s} " + " ".join(f"{k:>16s}" for k in res if k != "fp64"))
+    for name in ref:
+        r = ref[name].double()
+        m = r.abs().max().item()
+        row = []
+        for k, gr in res.items():
+            if k == "fp64":
+                continue
+            if name not in gr:
+                row.append(f"{'-':>16s}")
+                continue
+            x = gr[name].double()
+            if x.shape != r.shape:   # channels_last / layout differences: compare as NCHW
+                x = x.reshape(r.shape)
+            row.append(f"{(x - r).abs().max().item() / max(m, 1e-30):16.3e}")
+        print(f"{name:18s} {m:10.3e} " + " ".join(row))
+
+
+if __name__ == "__main__":
+    main()

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--H", type=int, default=64, help="input grid of the transposed conv")
     ap.add_argument("--Cout", type=int, default=64)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--act", default="lrelu", choices=["lrelu", "none"],
+                    help="dgrad: input activation of the conv (lrelu: the act' gate in the epilogue)")
     a = ap.parse_args()
     p2p.set_backend("native")
     dev = torch.device("cuda")
@@ -39,7 +41,7 @@ def main():
         x = torch.randn(a.N, a.Cout, 2 * a.H, 2 * a.H, device=dev).to(torch.bfloat16).contiguous(
             memory_format=torch.channels_last).requires_grad_(True)
         w = (torch.randn(a.C, a.Cout, 4, 4, device=dev) * 0.02).requires_grad_(False)
-        y = ops.conv2d(x, w, None, 2, 1, act_in="lrelu")
+        y = ops.conv2d(x, w, None, 2, 1, act_in=None if a.act == "none" else a.act)
         gy = torch.randn_like(y)
 
         def fn():
@@ -47,12 +49,17 @@ def main():
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
-    t = time.perf_counter()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
     for _ in range(a.iters):
         fn()
+    e1.record()
     torch.cuda.synchronize()
-    ms = (time.perf_counter() - t) / a.iters * 1e3
-    print(f"{a.mode} N{a.N} C{a.C} H{a.H} Cout{a.Cout} s2t={os.environ.get('P2P_NO_S2T') is None}: {ms:.3f} ms")
+    ms = e0.elapsed_time(e1) / a.iters
+    flop = 2.0 * a.N * (2 * a.H) ** 2 * a.Cout * a.C * 4
+    print(f"{a.mode} act={a.act} N{a.N} C{a.C} H{a.H} Cout{a.Cout} s2t={os.environ.get('P2P_NO_S2T') is None} "
+          f"lib={os.path.basename(os.environ.get('P2P_LIB', 'default'))} grid={os.environ.get('P2P_S2T_GRID', '2')}: "
+          f"{ms:.3f} ms {flop / ms / 1e9:.0f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
