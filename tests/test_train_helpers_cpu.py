@@ -69,3 +69,49 @@ def test_resume_follows_uninterrupted_lr_schedule(tmp_path, monkeypatch):
     for e in full:
         assert part[e] == pytest.approx(full[e]), (e, full, part)
     assert full[4] < full[1]          # the schedule really decays inside this window
+
+
+def _rewrite(path, keep=None, drop=()):
+    """Rewrite a checkpoint written by this test (own file: safe loader, tensors only)."""
+    st = torch.load(path, map_location="cpu", weights_only=True)
+    if keep is not None:
+        st = {k: v for k, v in st.items() if k in keep}
+    for k in drop:
+        st.pop(k, None)
+    torch.save(st, path)
+
+
+@pytest.mark.parametrize("variant", ["offset_chain", "no_offset_key", "reference_file"])
+def test_resume_keeps_scheduler_offset(tmp_path, monkeypatch, variant):
+    """the saved scheduler offset (sched_epoch_count) survives a chain of resumes.
+
+    * offset_chain: 1-2, then ``--epoch_count 3`` to 4 (its file records offset 1, not 3),
+      then ``--resume`` to 6 -- the LR of every epoch equals the uninterrupted 1-6 run's;
+    * no_offset_key: the epoch-2 file loses ``sched_epoch_count`` (a file from before the
+      key existed): the restored scheduler defaults to offset 1;
+    * reference_file: the epoch-2 file keeps only the reference's keys (epoch, G, C): a
+      fresh scheduler offset by ``--epoch_count`` (the reference's rule) lands on the same LRs.
+    """
+    monkeypatch.chdir(tmp_path)
+    import train
+    common = ["--synthetic", "--image_size", "32", "--netG", "unet_4", "--netD", "pixel",
+              "--ngf", "8", "--ndf", "8", "--steps_per_epoch", "1", "--epochsave", "1",
+              "--niter", "1", "--niter_decay", "6", "--no_eval", "--log_every", "1"]
+    train.main(common + ["--name", "full", "--nepoch", "6", "--log_json", "full.jsonl"])
+    train.main(common + ["--name", "part", "--nepoch", "2", "--log_json", "part.jsonl"])
+    ck2 = os.path.join("checkpoint", "synthetic", "net_part_epoch_2.pth")
+    if variant == "no_offset_key":
+        _rewrite(ck2, drop=("sched_epoch_count",))
+    elif variant == "reference_file":
+        _rewrite(ck2, keep=("epoch", "state_dict_g", "state_dict_c"))
+    train.main(common + ["--name", "part", "--nepoch", "4", "--epoch_count", "3",
+                         "--log_json", "part.jsonl"])
+    from p2p_pytorch_amd.engine.checkpoint import scheduler_offset
+    assert scheduler_offset(os.path.join("checkpoint", "synthetic", "net_part_epoch_4.pth")) == \
+        (3 if variant == "reference_file" else 1)
+    train.main(common + ["--name", "part", "--nepoch", "6", "--resume", "--log_json", "part.jsonl"])
+    full, part = _lrs("full.jsonl"), _lrs("part.jsonl")
+    assert sorted(full) == sorted(part) == [1, 2, 3, 4, 5, 6]
+    for e in full:
+        assert part[e] == pytest.approx(full[e]), (variant, e, full, part)
+    assert full[6] < full[3] < full[1]
