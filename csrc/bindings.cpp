@@ -77,6 +77,8 @@ int p2p_weight_prep_pairs(int count, const float* const* w, void* const* out0, v
                           int* const* site, hipStream_t st);
 int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, int reflect,
                  const void* xb, int act, const void* res, void* dx, hipStream_t st);
+int p2p_fold_band(const void* fb, int N, int H, int W, int C, int pad, const void* xb, int act, void* dx,
+                  hipStream_t st);
 int p2p_pad_channels(const void* a, int Ca, const void* b, int Cb, long P, int Co, void* out,
                      hipStream_t st);
 int p2p_slice_channels(const void* in, int Ci, int c0, long P, int C, void* out, hipStream_t st);
@@ -190,7 +192,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                              const optional<Tensor>& nb_x, const optional<Tensor>& nb_mean,
                              const optional<Tensor>& nb_rstd, const optional<Tensor>& nb_gamma,
                              const optional<Tensor>& nb_beta, int64_t nb_act, int64_t nb_half, bool nb_batch,
-                             bool nb_colsum, bool nb_gate) {
+                             bool nb_colsum, bool nb_gate, int64_t fold_H, int64_t fold_W, int64_t fold_p) {
   check_act(x1, "conv_fwd x1", true);
   // fp8 operands: x e4m3 (activations) or e5m2 (gradients), weight image e4m3, each with
   // an fp8 scale site (csrc/fp8.hip); outputs stay bf16
@@ -220,16 +222,26 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   TORCH_CHECK(mode == 0 || (up == 1 && reflect == 0), "conv_fwd: CONVT mode has no pad/upsample folds");
   if (reflect) TORCH_CHECK(pad < H * up && pad < W * up, "conv_fwd: reflect pad too large");
   if (bias) TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= Cout, "conv_fwd: bias");
+  // reflect-pad fold of a dgrad onto the virtual padded grid (conv.h fold_buf): y1, xb1 and
+  // res are real-grid (fold_H x fold_W) tensors
+  const bool fold = fold_p > 0;
+  if (fold)
+    TORCH_CHECK(mode == 1 && up == 1 && !reflect && pad == 0 && !x2 && Csplit == Cout && !want_stats &&
+                    !y_qsite && !nb_x && !nb_colsum && OH == fold_H + 2 * fold_p && OW == fold_W + 2 * fold_p,
+                "conv_fwd: reflect fold geometry");
+  const int64_t RH = fold ? fold_H : OH, RW = fold ? fold_W : OW;
   if (act_bwd) {
     TORCH_CHECK(xb1.has_value(), "conv_fwd: act_bwd needs xb1");
     check_act(*xb1, "xb1");
-    TORCH_CHECK(xb1->size(1) == Csplit && xb1->size(2) == OH && xb1->size(3) == OW, "xb1 shape");
+    TORCH_CHECK(xb1->size(1) == Csplit && xb1->size(2) == RH && xb1->size(3) == RW, "xb1 shape");
     if (Csplit < Cout && xb2.has_value()) {   // no xb2: the second half is not gated
       check_act(*xb2, "xb2");
       TORCH_CHECK(xb2->size(1) == Cout - Csplit, "xb2 shape");
     }
   }
-  Tensor y1 = empty_nhwc(N, Csplit, OH, OW, obf);
+  Tensor y1 = empty_nhwc(N, Csplit, RH, RW, obf);
+  Tensor fbuf;   // fold: the padded-grid gradient (only its frame is written in the epilogue route)
+  if (fold) fbuf = empty_nhwc(N, Cout, OH, OW, obf);
   Tensor y2;
   if (Csplit < Cout) y2 = empty_nhwc(N, Cout - Csplit, OH, OW, obf);
 
@@ -268,8 +280,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   a.res1 = nullptr;
   if (res) {
     check_act(*res, "conv_fwd res");
-    TORCH_CHECK(Csplit == Cout && res->size(0) == N && res->size(1) == Cout && res->size(2) == OH &&
-                    res->size(3) == OW,
+    TORCH_CHECK(Csplit == Cout && res->size(0) == N && res->size(1) == Cout && res->size(2) == RH &&
+                    res->size(3) == RW,
                 "conv_fwd: res must match the (unsplit) output");
     a.res1 = res->data_ptr();
   }
@@ -296,7 +308,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   // ---- tiny-Cout "col" path: dense GEMM over the input pixels (N = taps x Cvalid) + col2im
   const int64_t Cv = Cvalid > 0 ? Cvalid : Cout;
   if (Cout <= 16 && Cv <= 16 && Csplit == Cout && !reflect && up == 1 && C1 % 64 == 0 &&
-      C2 % 64 == 0) {
+      C2 % 64 == 0 && !fold) {
     TORCH_CHECK(!fp8, "conv_fwd: fp8 is not supported on the tiny-Cout col path");
     TORCH_CHECK(!res, "conv_fwd: no residual on the tiny-Cout col path");
     TORCH_CHECK(!alpha, "conv_fwd: no alpha on the tiny-Cout col path");
@@ -497,6 +509,33 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     a.q_site = y_qsite->data_ptr<int>();
     a.q_fmt = (int)y_qfmt;
   }
+  // stride-1 9x9 convs with 8-32 input channels and <= 32 outputs (family R's full-res
+  // layers): the halo-tile direct conv (csrc/halo_kxk.hip); MODE 1 stride 1 = flipped taps
+  const bool halo_geo = (KH == 9 && KW == 9 && (C1 == 8 || C1 == 16 || C1 == 32) && Cout <= 32) ||
+                        (KH == 3 && KW == 3 && C1 == 64 && Cout <= 32);
+  const bool halo_cond = !fp8 && C2 == 0 && halo_geo && stride == 1 && Csplit == Cout && act_in == 0 &&
+                         act_bwd == 0 && !a.res1 && !a.q_out && !a.stats && !a.nb_ws && !a.alpha &&
+                         (mode == 0 || (up == 1 && !reflect && pad <= KH - 1)) &&
+                         std::getenv("P2P_NO_HALO") == nullptr;
+  // reflect fold: in the implicit-GEMM epilogue (interior pixels straight into y1, the frame
+  // folded by fold_band); the split-K / halo routes write the whole padded grid and pad_fold
+  // folds it afterwards (gate and skip gradient applied there)
+  bool fold_late = false;
+  if (fold) {
+    fold_late = splits > 1 || halo_cond || fold_H < 2 * fold_p + 2 || fold_W < 2 * fold_p + 2 ||
+                std::getenv("P2P_FOLD_LATE") != nullptr;
+    if (fold_late) {
+      a.y1 = fbuf.data_ptr();
+      a.xb1 = nullptr;
+      a.act_bwd = 0;
+      a.res1 = nullptr;
+    } else {
+      a.fold_buf = fbuf.data_ptr();
+      a.fold_H = (int)fold_H;
+      a.fold_W = (int)fold_W;
+      a.fold_p = (int)fold_p;
+    }
+  }
   int rc = -2;
   // packed 8-channel image convs (4x4 s2 p1): the halo-tile kernel (csrc/halo_pk8.hip)
   if (mode == 0 && !fp8 && C1 == 8 && C2 == 0 && KH == 4 && KW == 4 && stride == 2 && pad == 1 && !reflect &&
@@ -534,13 +573,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       rc = p2p_halo_pk8(&h, std::max(1, std::min(h.ntiles, per_cu * cus)), st);
     }
   }
-  // stride-1 9x9 convs with 8-32 input channels and <= 32 outputs (family R's full-res
-  // layers): the halo-tile direct conv (csrc/halo_kxk.hip); MODE 1 stride 1 = flipped taps
-  const bool halo_geo = (KH == 9 && KW == 9 && (C1 == 8 || C1 == 16 || C1 == 32) && Cout <= 32) ||
-                        (KH == 3 && KW == 3 && C1 == 64 && Cout <= 32);
-  if (rc == -2 && !fp8 && C2 == 0 && halo_geo && stride == 1 && Csplit == Cout && act_in == 0 && act_bwd == 0 &&
-      !a.res1 && !a.q_out && !a.stats && !a.nb_ws && !a.alpha && (mode == 0 || (up == 1 && !reflect && pad <= KH - 1)) &&
-      std::getenv("P2P_NO_HALO") == nullptr) {
+  if (rc == -2 && halo_cond) {
     p2p::HaloKArgs h{};
     h.x = static_cast<const __bf16*>(x1.data_ptr());
     h.C = (int)C1;
@@ -596,6 +629,17 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   }
   check_rc(rc, "conv_fwd");
   if (splits > 1) check_rc(p2p_conv_finalize(&a, st), "conv_finalize");
+  if (fold) {
+    const void* xg = act_bwd ? xb1->data_ptr() : nullptr;
+    if (fold_late)
+      check_rc(p2p_pad_fold(fbuf.data_ptr(), (int)N, (int)fold_H, (int)fold_W, (int)Cout, (int)fold_p, 1, 1, xg,
+                            (int)act_bwd, res ? res->data_ptr() : nullptr, y1.data_ptr(), st),
+               "conv_fwd(pad_fold)");
+    else
+      check_rc(p2p_fold_band(fbuf.data_ptr(), (int)N, (int)fold_H, (int)fold_W, (int)Cout, (int)fold_p, xg,
+                             (int)act_bwd, y1.data_ptr(), st),
+               "conv_fwd(fold_band)");
+  }
   std::vector<Tensor> out{y1};
   if (y2.defined()) out.push_back(y2);
   if (stats.defined()) out.push_back(stats);
@@ -1742,7 +1786,7 @@ TORCH_LIBRARY(p2p, m) {
         "Tensor? qs_x2=None, Tensor? qs_w=None, Tensor(a!)? y_qsite=None, int y_qfmt=0, Tensor? res=None, "
         "Tensor? alpha=None, Tensor? nb_x=None, Tensor? nb_mean=None, Tensor? nb_rstd=None, "
         "Tensor? nb_gamma=None, Tensor? nb_beta=None, int nb_act=0, int nb_half=0, bool nb_batch=False, "
-        "bool nb_colsum=False, bool nb_gate=False) "
+        "bool nb_colsum=False, bool nb_gate=False, int fold_H=0, int fold_W=0, int fold_p=0) "
         "-> Tensor[]");
   m.def("fp8_quant(Tensor x, Tensor(a!) site, int fmt, int use_cur=0) -> Tensor");
   m.def("sn_power_iter(Tensor w, Tensor(a!) u, Tensor(b!) v) -> Tensor");

@@ -121,6 +121,10 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
   auto ld16 = [](const bf16* p) __attribute__((always_inline)) { return *reinterpret_cast<const u32x4*>(p); };
   auto finish = [&](int row, long pix, u32x4 xv, u32x4 rv, u32x4 nv) __attribute__((always_inline)) {
     u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * LDC + (tid % CPR) * 8);
+    if (MODE == 1 && pix < 0) {   // reflect-fold frame pixel (no nb partials with a fold: host)
+      *reinterpret_cast<u32x4*>(static_cast<bf16*>(a.fold_buf) + (-pix - 2) * a.Cout + co_t) = v;
+      return;
+    }
     if (gate_t) {
       if (a.act_bwd == ACT_RELU) {
 #pragma unroll
@@ -184,15 +188,15 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
 #pragma unroll
         for (int u = 0; u < PG; ++u) {
           const int m = m0 + tid / CPR + (g0 + u) * RSTEP;
-          const bool ok = m < g.Mc;
-          pixv[u] = ok ? out_pix(m) : -1;
+          pixv[u] = m < g.Mc ? out_pix(m) : -1;
+          const bool ok = pixv[u] >= 0;
           xv[u] = (gate_t && ok) ? ld16(xb_t + pixv[u] * ld_t + cof_t) : z4;
           rv[u] = (res_t && ok) ? ld16(res_p + pixv[u] * ld_t + cof_t) : z4;
           nv[u] = (nb_x_on && ok) ? ld16(nbx_p + pixv[u] * a.nb_C + nb_co) : z4;
         }
 #pragma unroll
         for (int u = 0; u < PG; ++u)
-          if (pixv[u] >= 0) finish(tid / CPR + (g0 + u) * RSTEP, pixv[u], xv[u], rv[u], nv[u]);
+          if (pixv[u] != -1) finish(tid / CPR + (g0 + u) * RSTEP, pixv[u], xv[u], rv[u], nv[u]);
       }
     }
   } else {
@@ -201,8 +205,10 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
       const int m = m0 + row;
       if (m >= g.Mc || co_t >= a.Cout) continue;
       const long pix = out_pix(m);
-      finish(row, pix, gate_t ? ld16(xb_t + pix * ld_t + cof_t) : z4, res_t ? ld16(res_p + pix * ld_t + cof_t) : z4,
-             nb_x_on ? ld16(nbx_p + pix * a.nb_C + nb_co) : z4);
+      const bool ok = pix >= 0;
+      finish(row, pix, (gate_t && ok) ? ld16(xb_t + pix * ld_t + cof_t) : z4,
+             (res_t && ok) ? ld16(res_p + pix * ld_t + cof_t) : z4,
+             (nb_x_on && ok) ? ld16(nbx_p + pix * a.nb_C + nb_co) : z4);
     }
   }
   if (a.nb_ws) {
@@ -292,13 +298,22 @@ __device__ __forceinline__ void conv_epilogue_tail(const ConvFwdArgs& a, const C
   const int HWq = g.Hq * g.Wq;
   const int s = a.stride;
   constexpr int LDC = BN + 8;
+  // output pixel of GEMM row m; with the reflect fold (MODE 1): the real-grid pixel of an
+  // interior row, or -(padded pixel) - 2 for a frame row (-1 stays "no row")
   auto out_pix = [&](int m) __attribute__((always_inline)) -> long {
     if (MODE == 0) return m;
     const int n = (int)fdiv((uint32_t)m, fd_hwq);
     const int r = m - n * HWq;
     const int qy = (int)fdiv((uint32_t)r, fd_wq);
     const int qx = r - qy * g.Wq;
-    return ((long)n * a.OH + qy * s + g.ry) * a.OW + qx * s + g.rx;
+    const int oy = qy * s + g.ry, ox = qx * s + g.rx;
+    if (a.fold_buf) {
+      const int iy = oy - a.fold_p, ix = ox - a.fold_p;
+      if ((unsigned)iy < (unsigned)a.fold_H && (unsigned)ix < (unsigned)a.fold_W)
+        return ((long)n * a.fold_H + iy) * a.fold_W + ix;
+      return -(((long)n * a.OH + oy) * a.OW + ox) - 2;
+    }
+    return ((long)n * a.OH + oy) * a.OW + ox;
   };
 
   if (a.d2s) {  // depth-to-space packed image (d1 forward / its head gradient)
@@ -378,6 +393,10 @@ __device__ __forceinline__ void conv_epilogue_tail(const ConvFwdArgs& a, const C
     if (m >= g.Mc || co >= a.Cout) continue;
     const long pix = out_pix(m);
     u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * LDC + cc * 8);
+    if (MODE == 1 && pix < 0) {   // reflect-fold frame pixel: raw, folded by fold_band (host: Csplit == Cout)
+      *reinterpret_cast<u32x4*>(static_cast<bf16*>(a.fold_buf) + (-pix - 2) * a.Cout + co) = v;
+      continue;
+    }
     const bool first = co < a.Csplit;
     const int ld = first ? a.Csplit : a.Cout - a.Csplit;
     const int cof = first ? co : co - a.Csplit;

@@ -516,6 +516,66 @@ __global__ void __launch_bounds__(256) pad_fold_s1_kernel(const bf16* __restrict
     for (int k = 0; k < 4; ++k) *reinterpret_cast<u32x4*>(dx + o + k * 8) = pack8e(acc[k]);
   }
 }
+
+// Frame half of the reflect-pad fold (conv.h fold_buf): the dgrad's epilogue already stored
+// every interior pixel of the padded grid -- gated, + the parked skip gradient -- into dx; here
+// each real pixel with a mirror image in the p-wide frame (rows / columns 1..p and
+// H-1-p..H-2) adds the frame values that reflect onto it, times the same act' gate.  Band
+// pixels only: 2p rows x W + (H - 2p) rows x 2p columns per image (host: H, W >= 2p + 2).
+__global__ void __launch_bounds__(256) fold_band_kernel(const bf16* __restrict__ fb, int N, int H, int W, int C,
+                                                        int pad, const bf16* __restrict__ xb, int act,
+                                                        bf16* __restrict__ dx) {
+  const int CP = C >> 3;
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+  const int nrow = 2 * pad * W, per_img = nrow + (H - 2 * pad) * 2 * pad;
+  const long total = (long)N * per_img * CP;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int cg = (int)(e % CP);
+    const long t = e / CP;
+    const int n = (int)(t / per_img);
+    int k = (int)(t - (long)n * per_img), y, x;
+    if (k < nrow) {   // a band row, every column
+      const int r = k / W;
+      x = k - r * W;
+      y = r < pad ? 1 + r : H - 1 - pad + (r - pad);
+    } else {          // another row, a band column
+      k -= nrow;
+      const int r = k / (2 * pad), c = k - r * 2 * pad;
+      y = r == 0 ? 0 : (r == H - 2 * pad - 1 ? H - 1 : pad + r);
+      x = c < pad ? 1 + c : W - 1 - pad + (c - pad);
+    }
+    int qy[3], qx[3], ny = 0, nx = 0;
+    qy[ny++] = y + pad;
+    qx[nx++] = x + pad;
+    if (y >= 1 && y <= pad) qy[ny++] = pad - y;
+    if (y >= H - 1 - pad && y <= H - 2) qy[ny++] = 2 * (H - 1) + pad - y;
+    if (x >= 1 && x <= pad) qx[nx++] = pad - x;
+    if (x >= W - 1 - pad && x <= W - 2) qx[nx++] = 2 * (W - 1) + pad - x;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int i = 0; i < ny; ++i)
+      for (int k2 = 0; k2 < nx; ++k2) {
+        if (i == 0 && k2 == 0) continue;   // the interior pixel itself: already in dx
+        float f[8];
+        unpack8e(*reinterpret_cast<const u32x4*>(fb + (((long)n * Hp + qy[i]) * Wp + qx[k2]) * C + cg * 8), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += f[j];
+      }
+    const long o = (((long)n * H + y) * W + x) * C + cg * 8;
+    if (act) {
+      float xf[8];
+      unpack8e(*reinterpret_cast<const u32x4*>(xb + o), xf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] *= act_grad_from_input(xf[j], act);
+    }
+    float d[8];
+    unpack8e(*reinterpret_cast<const u32x4*>(dx + o), d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += d[j];
+    *reinterpret_cast<u32x4*>(dx + o) = pack8e(acc);
+  }
+}
 }  // namespace p2p
 
 namespace p2p {
@@ -629,6 +689,16 @@ int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, i
   hipLaunchKernelGGL(pad_fold_kernel, dim3(egrid(total)), dim3(256), 0, st, static_cast<const bf16*>(dxp), N,
                      H, W, C, pad, up, reflect, static_cast<const bf16*>(xb), act, static_cast<const bf16*>(res),
                      static_cast<bf16*>(dx));
+  return (int)hipGetLastError();
+}
+
+int p2p_fold_band(const void* fb, int N, int H, int W, int C, int pad, const void* xb, int act, void* dx,
+                  hipStream_t st) {
+  using namespace p2p;
+  if (C % 8 || pad < 1 || H < 2 * pad + 2 || W < 2 * pad + 2) return -2;
+  const long total = (long)N * (2 * pad * W + (H - 2 * pad) * 2 * pad) * (C / 8);
+  hipLaunchKernelGGL(fold_band_kernel, dim3(egrid(total)), dim3(256), 0, st, static_cast<const bf16*>(fb), N, H, W,
+                     C, pad, static_cast<const bf16*>(xb), act, static_cast<bf16*>(dx));
   return (int)hipGetLastError();
 }
 

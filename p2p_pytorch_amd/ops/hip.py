@@ -38,6 +38,8 @@ ACT = {None: 0, "none": 0, "relu": 1, "lrelu": 2, "tanh": 3, "sigmoid": 4}
 # P2P_NB_FUSE=0: norm backward runs its own partial pass (A/B knob for the dgrad-epilogue fusion)
 _NB_FUSE = os.environ.get("P2P_NB_FUSE", "1") != "0"
 _NB_LOG = os.environ.get("P2P_NB_LOG", "0") == "1"
+# reflect-pad dgrads fold in the conv epilogue (P2P_FOLD_EPI=0: padded grid + pad_fold, A/B)
+_FOLD_EPI = os.environ.get("P2P_FOLD_EPI", "1") != "0"
 CL = torch.channels_last
 _NULLCTX = contextlib.nullcontext()
 
@@ -267,7 +269,7 @@ def _weight_image_fp8(w: torch.Tensor, swap: int, xp: int, yp: int):
 
 def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout, act_out,
                Csplit, xb1, xb2, act_bwd, Cvalid, want, weight=None, swap=0, xp=0, yp=0, role="x",
-               y_qkey=None, res=None, alpha=None, nb=None):
+               y_qkey=None, res=None, alpha=None, nb=None, fold=None):
     """conv_fwd on bf16 operands, or -- fp8 precision and a geometry the fp8 kernel takes --
     on fp8 ones: x (role 'x': activations, e4m3; 'gy': gradients, e5m2) quantised with
     delayed scaling (or taken from the producer's fused shadow), the weight image with
@@ -276,7 +278,11 @@ def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, 
     ``wimg`` may be None (built on demand for the bf16 path).  ``res``: bf16 tensor added to
     the (unsplit) output in the epilogue, after the act' gate.  ``nb`` = (half, norm info): the
     dgrad epilogue also emits that half's norm-backward partials (bf16 path only), appended
-    as the last output."""
+    as the last output.  ``fold`` = (H, W, p): a MODE-1 dgrad onto the reflect-padded grid
+    (OH, OW) = (H + 2p, W + 2p) returns the real input's gradient (H, W): interior pixels
+    stored by the epilogue, the frame folded by elementwise.hip fold_band (xb1 / res are
+    real-grid tensors)."""
+    fk = {} if fold is None else dict(fold_H=int(fold[0]), fold_W=int(fold[1]), fold_p=int(fold[2]))
     C1 = x1.shape[1]
     C2 = 0 if x2 is None else x2.shape[1]
     if weight is not None and _f8.enabled() and _f8.conv_ok(C1, C2, Cout, act_in):
@@ -291,7 +297,7 @@ def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, 
         a2, s2 = _f8.quant(x2, (k, role, 2), fmt) if x2 is not None else (None, None)
         return P().conv_fwd(a1, a2, w8, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout,
                             act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, s1, s2, sw, *yq, res=res,
-                            alpha=alpha, **_nb_kwargs(nb if not yq else None))
+                            alpha=alpha, **_nb_kwargs(nb if not yq else None), **fk)
     if wimg is None:
         wimg = _weight_image(weight, swap, xp, yp)
     yq = ()
@@ -300,7 +306,7 @@ def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, 
         yq = (None, None, None, None, 0) if fresh else (None, None, None, ysite, _f8.E4M3)
     return P().conv_fwd(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout,
                         act_out, Csplit, xb1, xb2, act_bwd, Cvalid, want, *yq, res=res, alpha=alpha,
-                        **_nb_kwargs(nb if not yq else None))
+                        **_nb_kwargs(nb if not yq else None), **fk)
 
 
 def _nb_kwargs(nb):
@@ -737,16 +743,23 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
             if q2 is not None:
                 raise NotImplementedError("virtual concat with reflect/upsample gather")
             Hp, Wp = H * cfg.up + 2 * p, W * cfg.up + 2 * p
-            dxp = _conv_call(gyp, None, None, None, 1, KH, KW, s, 0, 0, 1, 0, Hp, Wp, Cp,
-                             0, Cp, None, None, 0, C1, False, weight, 1, Cp, Coutp, "gy")[0]
             res = None
             if cfg.skip_grad == "take" and q2 is None and need_x1 and Cp == C1:
                 res = _DEFERRED.pop(q1.data_ptr(), None)   # the residual add's gradient
                 if res is not None and res.shape != (q1.shape[0], Cp, H, W):
                     _DEFERRED[q1.data_ptr()] = res   # not fusable: added below instead
                     res = None
-            outs = [P().pad_fold(dxp, H, W, p, cfg.up, int(cfg.reflect),
-                                 q1 if act_in else None, act_in, res)]
+            if cfg.up == 1 and cfg.reflect and p > 0 and _FOLD_EPI:
+                # reflect pad only: the fold happens in the dgrad's epilogue (interior pixels
+                # gated + skip gradient straight into dx) plus a frame-band pass
+                outs = _conv_call(gyp, None, None, None, 1, KH, KW, s, 0, 0, 1, 0, Hp, Wp, Cp,
+                                  0, Cp, q1 if act_in else None, None, act_in, C1, False, weight,
+                                  1, Cp, Coutp, "gy", res=res, fold=(H, W, p))[:1]
+            else:
+                dxp = _conv_call(gyp, None, None, None, 1, KH, KW, s, 0, 0, 1, 0, Hp, Wp, Cp,
+                                 0, Cp, None, None, 0, C1, False, weight, 1, Cp, Coutp, "gy")[0]
+                outs = [P().pad_fold(dxp, H, W, p, cfg.up, int(cfg.reflect),
+                                     q1 if act_in else None, act_in, res)]
         elif cfg.transposed:
             nbh = _nb_half(cfg, q2, nb, False) if not packed else None
             outs = _conv_call(gyp, None, None, None, 0, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,

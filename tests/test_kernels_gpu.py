@@ -178,6 +178,51 @@ def test_conv_reflect_upsample_fwd_bwd(case):
     assert rel_err(hb.grad, rb.grad) < 3e-2, name
 
 
+FOLD_CASES = [
+    # (N, Cin, H, W, k, s, act_in): the reflect-pad dgrad folded in the conv epilogue + frame band
+    (2, 128, 16, 16, 3, 1, "relu"),      # residual-block conv (256x128 EXT tile, ReLU gate)
+    (2, 64, 20, 18, 3, 2, "lrelu"),      # G.conv2 / conv3 (stride 2: four parity classes)
+    (2, 64, 12, 14, 5, 1, None),         # pad 2: two-pixel frame and bands
+    (2, 12, 24, 20, 9, 1, None),         # pad 4, 16-channel gradient (register-staged tile)
+    (1, 32, 6, 6, 3, 1, "relu"),         # smallest band geometry H = W = 2p + 4
+]
+
+
+@pytest.mark.parametrize("case", FOLD_CASES, ids=[f"c{c[1]}_h{c[2]}_k{c[4]}_s{c[5]}" for c in FOLD_CASES])
+def test_reflect_dgrad_epilogue_fold_matches_pad_fold(case, monkeypatch):
+    """The epilogue fold (interior pixels stored gated by the dgrad, frame mirrored by fold_band)
+    equals the padded-grid dgrad + pad_fold pass: bitwise off the bands, within one bf16
+    rounding on them (there the interior value is rounded before the frame adds in)."""
+    from p2p_pytorch_amd.ops import hip
+    N, Cin, H, W, k, s, act_in = case
+    x = rand_img(N, Cin, H, W, seed=21)
+    w = torch.randn(Cin * 2, Cin, k, k, device=DEV) * (1.0 / (Cin * k * k) ** 0.5)
+
+    p = k // 2
+    gy = rand_img(N, 2 * Cin, (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1, seed=22)
+
+    def dgrad(fold_epi):
+        monkeypatch.setattr(hip, "_FOLD_EPI", fold_epi)
+        hx = _leaf(x)
+        ops.conv2d(hx, w, None, s, p, pad_mode="reflect", act_in=act_in).backward(gy)
+        return hx.grad.float()
+
+    ge, gl = dgrad(True), dgrad(False)
+    band = torch.zeros(H, W, dtype=torch.bool, device=DEV)
+    for r in list(range(1, p + 1)) + list(range(H - 1 - p, H - 1)):
+        band[r, :] = True
+    for c in list(range(1, p + 1)) + list(range(W - 1 - p, W - 1)):
+        band[:, c] = True
+    off = ~band
+    assert torch.equal(ge[:, :, off], gl[:, :, off])
+    tol = 2.0 ** -7 * gl.abs().max().item()
+    assert (ge - gl).abs().max().item() <= tol
+    rx = _leaf(x.float())
+    ref.conv2d(rx, w.to(torch.bfloat16).float(), None, s, p, pad_mode="reflect",
+               act_in=act_in).backward(gy.float())
+    assert rel_err(ge, rx.grad) < 3e-2
+
+
 def test_conv_wgrad_large_m():
     # many pixels per weight -> many split-K slabs; checks the deterministic slab reduce
     x = rand_img(8, 64, 64, 64, seed=8)

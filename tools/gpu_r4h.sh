@@ -1,17 +1,19 @@
 #!/bin/bash
-# Round-4 pass h: full GPU suite on the s2t register-epilogue / direct-gradient / halo-epilogue
-# build, headline A/B (W32 s2t on / off), DP force_comm line, inner-gradient diagnosis.
+# Round-4 pass h: headline A/B (W32 s2t on / off), DP force_comm line, family-R bench (reflect
+# fold in the dgrad epilogue), then the full GPU suite and the inner-gradient diagnosis.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r4h
 mkdir -p $O
-timeout -k 10 780 python -u -m pytest tests -m gpu -x -q -s --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { grep -E "passed|failed|Error|error" $O/tests.log | tail -30; exit 1; }
-tail -1 $O/tests.log
-grep "convergence:" $O/tests.log
 j() { python -c "import json;d=json.load(open('$1'));print(d['value'], d['ms_per_step'], d.get('max_mem_gib'), d.get('comm'))"; }
 run() { local tag=$1; shift; timeout -k 10 300 python bench.py "$@" > $O/$tag.json 2>> $O/err.log || exit $?; echo "$tag $(j $O/$tag.json)"; cat $O/$tag.json >> $O/all.jsonl; }
 run headline
 P2P_S2T_W32=0 run w32off
 run force_comm --force_comm
+run famR --family ref --batch 64
+P2P_FOLD_EPI=0 run famR_nofold --family ref --batch 64
+timeout -k 10 840 python -u -m pytest tests -m gpu -x -q -s --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { grep -E "passed|failed|Error|error" $O/tests.log | tail -30; exit 1; }
+tail -1 $O/tests.log
+grep "convergence:" $O/tests.log
 timeout -k 10 200 python tools/diag_inner_grad.py > $O/diag_inner.txt 2>&1; echo "diag rc=$?"; tail -12 $O/diag_inner.txt
