@@ -13,6 +13,7 @@ P2P_S2T_W32=0 run w32off
 run force_comm --force_comm
 run famR --family ref --batch 64
 P2P_FOLD_EPI=0 run famR_nofold --family ref --batch 64
+for nt in 0 1 3; do P2P_NORM_NT=$nt timeout -k 10 120 python tools/norm_bw.py > $O/norm_bw_nt$nt.txt 2>&1 || exit $?; tail -1 $O/norm_bw_nt$nt.txt; done
 timeout -k 10 840 python -u -m pytest tests -m gpu -x -q -s --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { grep -E "passed|failed|Error|error" $O/tests.log | tail -30; exit 1; }
 tail -1 $O/tests.log
 grep "convergence:" $O/tests.log
