@@ -23,7 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native, ops
-from .layers import BatchNorm2d, Conv2d
+from .layers import BatchNorm2d, Conv2d, link_norm
 
 
 def ops_hip():
@@ -99,6 +99,9 @@ class ResidualBlock(nn.Module):
         # x is read by conv1 and by the residual add: the add's gradient for x is folded into
         # conv1's input-gradient pass (HIP path) instead of an autograd accumulate
         self.conv1.conv2d.skip_grad = "take"
+        # the BN statistics come from the conv epilogues (no separate statistics pass)
+        link_norm(self.conv1.conv2d, self.in1)
+        link_norm(self.conv2.conv2d, self.in2)
 
     def forward(self, x):
         out = self.in2(self.conv2(self.in1(self.conv1(x))))
@@ -129,6 +132,9 @@ class ExpandNetwork(nn.Module):
         self.in2_d = BatchNorm2d(32, affine=True)
         self.deconv1 = UpsampleConvLayer(32, 3, kernel_size=9, stride=1)
         self.in1_d = BatchNorm2d(3, affine=True, act="tanh")
+        for conv, bn in ((self.conv2, self.in2_e), (self.conv3, self.in3_e), (self.deconv3, self.in3_d),
+                         (self.deconv2, self.in2_d), (self.deconv1, self.in1_d)):
+            link_norm(conv.conv2d, bn)
 
     def forward(self, x):
         if x.shape[-1] % 4 or x.shape[-2] % 4:
@@ -136,7 +142,8 @@ class ExpandNetwork(nn.Module):
                              " (quirk A16: the reference silently returns a wrong-size image)")
         # pixel-unshuffle(2) followed by nearest x2: the conv sees 12 channels at full res.
         y = self.inversePixel(x)
-        y = ops.conv2d(y, self.conv1.conv2d.weight, self.conv1.conv2d.bias, 1, 4, "reflect", 2)
+        y = ops.conv2d(y, self.conv1.conv2d.weight, self.conv1.conv2d.bias, 1, 4, "reflect", 2,
+                       stats=self.training)
         pw = self.relu.weight            # PReLU fused into the BN passes (fwd and bwd)
         y = self.in1_e(y, prelu=pw)
         y = self.in2_e(self.conv2(y), prelu=pw)
@@ -160,6 +167,7 @@ class CompressionNetwork(nn.Module):
                                          BatchNorm2d(64), PReLU())
         self.conv_block2 = nn.Sequential(ConvLayer(64, 12, kernel_size=3, stride=2),
                                          PixelShuffle(2))
+        link_norm(self.conv_block1[0].conv2d, self.conv_block1[1])
 
     def forward(self, x):
         conv, bn, act = self.conv_block1
