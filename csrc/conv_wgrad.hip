@@ -877,6 +877,61 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   dw[o] = accumulate ? dw[o] + s : s;
 }
 
+// The same reduction with coalesced stores: a block owns one GEMM row r and 32 consecutive
+// input channels of every tap -- it sums the slabs into an LDS tile read as 128-B rows per
+// (split, tap), then writes dw in its [r][ci][kh][kw] order (T contiguous floats per channel,
+// 32 x T per block) instead of one 4-B store every T floats.  Same fixed split order per
+// element as wgrad_reduce_kernel, so bitwise identical to it.
+template <int G>
+__global__ void __launch_bounds__(256) wgrad_reduce_t_kernel(const float* __restrict__ ws, int splits,
+                                                             int R, int T, int C, int KW, int Rr, int Cr,
+                                                             float* __restrict__ dw, float scale,
+                                                             int accumulate, int flip) {
+  constexpr int CB = 32, LDT = CB + 1;
+  constexpr int EPB = 256 / G;
+  __shared__ float tile[81 * LDT];
+  __shared__ float red[256];
+  const int r = blockIdx.y, c0 = blockIdx.x * CB;
+  const int Kq = T * C;
+  const long total = (long)R * Kq;
+  const int E = T * CB;
+  const int le = threadIdx.x % EPB, sg = threadIdx.x / EPB;
+  for (int b0 = 0; b0 < E; b0 += EPB) {
+    const int idx = b0 + le;
+    const int tap = idx / CB, cc = idx - tap * CB;
+    const bool ok = idx < E && c0 + cc < C;
+    float s = 0.f;
+    if (ok) {
+      const float* src = ws + (long)r * Kq + tap * C + c0 + cc;
+      for (int k = sg; k < splits; k += G) s += src[(long)k * total];
+    }
+    if (G > 1) {
+      red[threadIdx.x] = s;
+      __syncthreads();
+      if (sg == 0)
+        for (int q = 1; q < G; ++q) s += red[q * EPB + le];
+    }
+    if (sg == 0 && idx < E) tile[tap * LDT + cc] = s * scale;
+    if (G > 1) __syncthreads();
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < E; j += 256) {
+    const int cl = j / T, t = j - cl * T;
+    const int ci = c0 + cl;
+    long o;
+    if (!flip) {
+      if (r >= Rr || ci >= Cr) continue;
+      o = ((long)r * Cr + ci) * T + t;
+    } else {
+      if (ci >= Rr || r >= Cr) continue;
+      const int kh = t / KW, kw = t - kh * KW;
+      o = ((long)ci * Cr + r) * T + (T / KW - 1 - kh) * KW + (KW - 1 - kw);
+    }
+    const float v = tile[t * LDT + cl];
+    dw[o] = accumulate ? dw[o] + v : v;
+  }
+}
+
 }  // namespace p2p
 
 // glds variant geometry: 0 = none (fall back), 1 = 256(R) x 128(Kq), 2 = 128(R) x 256(Kq),
@@ -1033,6 +1088,25 @@ extern "C" int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int 
   const long total = (long)R * KH * KW * C;
   int G = 1;
   while (G < 32 && splits > 8 * G) G *= 2;   // <= ~8 slab reads per thread
+  static const bool old_red = std::getenv("P2P_WRED_OLD") != nullptr;   // A/B: 4-B scattered stores
+  if (!old_red && KH * KW <= 81) {
+    const dim3 grid((unsigned)((C + 31) / 32), (unsigned)R);
+#define P2P_REDT(g)                                                                                       \
+  case g:                                                                                                  \
+    hipLaunchKernelGGL(p2p::wgrad_reduce_t_kernel<g>, grid, dim3(256), 0, st, ws, splits, R, KH * KW, C, KW, \
+                       Rr, Cr, dw, scale, accumulate, flip);                                               \
+    break;
+    switch (G) {
+      P2P_REDT(1)
+      P2P_REDT(2)
+      P2P_REDT(4)
+      P2P_REDT(8)
+      P2P_REDT(16)
+      P2P_REDT(32)
+    }
+#undef P2P_REDT
+    return (int)hipGetLastError();
+  }
   const int EPB = 256 / G;
   const unsigned blocks = (unsigned)((total + EPB - 1) / EPB);
 #define P2P_RED(g)                                                                              \
