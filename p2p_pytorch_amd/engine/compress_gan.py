@@ -180,11 +180,14 @@ class CompressGANStep:
         set_requires_grad(self._d_trainable, True)
         loss_g_gan = self.criterionGAN(pred_fake_g, True)
         fgate = getattr(D, "feature_grad_gate", None)   # D's lrelu' rides in these gradients
-        feat = [ops.l1(pred_fake_g[i][j], pred_real[i][j].detach(), gate_a=fgate)
-                for i in range(len(pred_fake_g)) for j in range(len(pred_fake_g[i]) - 1)]
         # native: the loss compositions are one HIP launch each way (ops.lincomb_n); the torch
         # path keeps the reference's expression order (bitwise parity on CPU)
         native = real_a.is_cuda and _native.get_backend() == "native"
+        # each feature's L1 gradient is parked for the next D conv (skip_grad="take"), which
+        # adds it in its dgrad epilogue: no accumulate of the feature's two gradients
+        feat = [ops.l1(pred_fake_g[i][j], pred_real[i][j].detach(), gate_a=fgate,
+                       defer=native and fgate is not None)
+                for i in range(len(pred_fake_g)) for j in range(len(pred_fake_g[i]) - 1)]
         if native and feat:
             fw = self.d_weights * self.feat_weights * self.lambda_feat
             loss_feat = ops.lincomb_n(feat, [fw] * len(feat))

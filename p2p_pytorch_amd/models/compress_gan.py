@@ -246,7 +246,7 @@ class SpectralNorm(nn.Module):
             return ops_hip().sn_conv2d(x, w, m.bias, scale, m.stride, m.padding,
                                        getattr(m, "act_in", None), getattr(m, "act_out", None),
                                        getattr(m, "grad_gate", None), getattr(m, "out_gated", False),
-                                       uv=(u, v))
+                                       uv=(u, v), skip_grad=getattr(m, "skip_grad", None))
         w = self.normalized_weight()
         return ops.conv2d(x, w, m.bias, m.stride, m.padding, pad_mode, 1,
                           getattr(m, "act_in", None), getattr(m, "act_out", None))
@@ -285,11 +285,15 @@ class NLayerDiscriminatorSN(nn.Module):
         into the next conv's dgrad epilogue (HIP path) -- no separate gate pass per layer.
         Only valid when every OTHER consumer of the intermediate features applies lrelu' to
         its own gradient, as the step's feature-matching L1 does (``ops.l1(..., gate_a=
-        self.feature_grad_gate)``).  The oracle path ignores the flags."""
+        self.feature_grad_gate)``).  The next conv also takes a feature gradient the L1 parked
+        for it (``ops.l1(defer=True)``, ``skip_grad="take"``): added in its dgrad epilogue
+        instead of an autograd accumulate of the two consumers' gradients.  The oracle path
+        ignores the flags."""
         for prod, cons in zip(self._chain[:-1], self._chain[1:]):
             if getattr(prod, "act_out", None) == "lrelu":
                 prod.out_gated = bool(on)
                 cons.grad_gate = "lrelu" if on else None
+                cons.skip_grad = "take" if on else None
         self.feature_grad_gate = "lrelu" if on else None
 
     def forward(self, x):

@@ -653,7 +653,7 @@ def sn_scale(w2, u, v, iters=1):
 
 
 def sn_conv2d(x, w_bar, bias, scale, stride=1, padding=0, act_in=None, act_out=None,
-              grad_gate=None, out_gated=False, uv=None):
+              grad_gate=None, out_gated=False, uv=None, skip_grad=None):
     """Spectral-norm conv: ``conv2d(x, w_bar * scale)`` with ``scale`` (1 / sigma) applied in
     the conv epilogues -- either a 1-element tensor carrying its own gradient, or (``uv`` =
     (u, v)) a detached ``sn_scale`` with the sigma path fused into the weight gradient."""
@@ -662,7 +662,7 @@ def sn_conv2d(x, w_bar, bias, scale, stride=1, padding=0, act_in=None, act_out=N
     if s != s2 or p != p2:
         raise NotImplementedError("anisotropic stride/padding")
     cfg = _ConvCfg(False, w_bar.shape[2], w_bar.shape[3], s, p, False, 1, act_in, act_out,
-                   grad_gate=grad_gate, out_gated=out_gated)
+                   grad_gate=grad_gate, out_gated=out_gated, skip_grad=skip_grad)
     return SNConvFn.apply(x, w_bar, bias, scale, cfg, uv)
 
 

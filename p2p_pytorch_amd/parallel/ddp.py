@@ -56,6 +56,7 @@ Mechanism
 from __future__ import annotations
 
 import contextlib
+import os
 import threading
 import time
 
@@ -116,7 +117,7 @@ class _HostEvent:
 class GradReducer:
     def __init__(self, module: torch.nn.Module, bucket_mb: float = 64.0, process_group=None,
                  comm_dtype: torch.dtype | None = None, tail_mb: float = 8.0, rebucket: bool = True,
-                 force_comm: bool = False, direct: bool = True):
+                 force_comm: bool = False, direct: bool | None = None):
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.backend = dist.get_backend(process_group) if dist.is_initialized() else None
@@ -139,8 +140,11 @@ class GradReducer:
         self._last = None        # (bucket events, end-of-backward event) of the last finish()
         # every gradient lands pre-scaled by 1/world (direct writes and autograd hooks alike)
         self.scale = 1.0 / self.world if (self.comm and self.world > 1) else 1.0
+        if direct is None:   # opt-in until the native path's use counting is hardware-verified
+            direct = os.environ.get("P2P_DIRECT_GRAD", "0") == "1"
         self.direct = bool(direct)
         self._uses: dict = {}
+        self._names = {id(p): n for n, p in module.named_parameters()}
         if self.direct:
             for p in params:
                 p._p2p_direct = self
@@ -209,7 +213,9 @@ class GradReducer:
             raise RuntimeError(
                 "GradReducer: a gradient arrived for a bucket whose all-reduce was already "
                 "launched (a second backward without zero_grad()/finish(); wrap backwards whose "
-                "gradients are discarded in reducer.paused())")
+                f"gradients are discarded in reducer.paused()): parameter "
+                f"{self._names.get(id(p), '?')} {tuple(p.shape)}, bucket {b.index} of "
+                f"{len(self.buckets)} ({len(b.params)} params)")
         if self._ready_order is not None:
             self._ready_order.append(p)
         # autograd may have replaced the view (e.g. after set_to_none): copy back in.

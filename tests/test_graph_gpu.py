@@ -65,9 +65,9 @@ def _eager(reducers=False, direct=True):
     return _params(G, D), {k: v.item() for k, v in losses.items()}
 
 
-def _graph(reducers=False):
+def _graph(reducers=False, direct=True):
     from p2p_pytorch_amd.engine.graph import CapturedStep
-    step, G, D = _build(reducers)
+    step, G, D = _build(reducers, direct)
     data = _data()
     cap = CapturedStep(step.step, *data[0], warmup=2)
     for a, b in data:
