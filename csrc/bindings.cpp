@@ -77,7 +77,7 @@ int p2p_weight_prep_pairs(int count, const float* const* w, void* const* out0, v
                           int* const* site, hipStream_t st);
 int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, int reflect,
                  const void* xb, int act, const void* res, void* dx, hipStream_t st);
-int p2p_fold_band(const void* fb, int N, int H, int W, int C, int pad, const void* xb, int act, void* dx,
+int p2p_fold_band(const void* fb, int N, int H, int W, int C, int pad, int edge, const void* xb, int act, void* dx,
                   hipStream_t st);
 int p2p_pad_channels(const void* a, int Ca, const void* b, int Cb, long P, int Co, void* out,
                      hipStream_t st);
@@ -192,7 +192,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                              const optional<Tensor>& nb_x, const optional<Tensor>& nb_mean,
                              const optional<Tensor>& nb_rstd, const optional<Tensor>& nb_gamma,
                              const optional<Tensor>& nb_beta, int64_t nb_act, int64_t nb_half, bool nb_batch,
-                             bool nb_colsum, bool nb_gate, int64_t fold_H, int64_t fold_W, int64_t fold_p) {
+                             bool nb_colsum, bool nb_gate, int64_t fold_H, int64_t fold_W, int64_t fold_p,
+                             int64_t fold_edge) {
   check_act(x1, "conv_fwd x1", true);
   // fp8 operands: x e4m3 (activations) or e5m2 (gradients), weight image e4m3, each with
   // an fp8 scale site (csrc/fp8.hip); outputs stay bf16
@@ -222,13 +223,15 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   TORCH_CHECK(mode == 0 || (up == 1 && reflect == 0), "conv_fwd: CONVT mode has no pad/upsample folds");
   if (reflect) TORCH_CHECK(pad < H * up && pad < W * up, "conv_fwd: reflect pad too large");
   if (bias) TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= Cout, "conv_fwd: bias");
-  // reflect-pad fold of a dgrad onto the virtual padded grid (conv.h fold_buf): y1, xb1 and
-  // res are real-grid (fold_H x fold_W) tensors
+  // pad fold of an input gradient computed on a padded grid (conv.h fold_buf): y1, xb1 and
+  // res are real-grid (fold_H x fold_W) tensors.  Reflect: a MODE-1 dgrad onto the reflect-
+  // padded grid; edge: the MODE-0 4x4 stride-2 dgrad of nearest-x2 + reflect-1 (ops/hip.py)
   const bool fold = fold_p > 0;
   if (fold)
-    TORCH_CHECK(mode == 1 && up == 1 && !reflect && pad == 0 && !x2 && Csplit == Cout && !want_stats &&
-                    !y_qsite && !nb_x && !nb_colsum && OH == fold_H + 2 * fold_p && OW == fold_W + 2 * fold_p,
-                "conv_fwd: reflect fold geometry");
+    TORCH_CHECK(((mode == 1 && pad == 0 && !fold_edge) || (mode == 0 && fold_edge && fold_p <= 2)) && up == 1 &&
+                    !reflect && !x2 && Csplit == Cout && !want_stats && !y_qsite && !nb_x && !nb_colsum &&
+                    OH == fold_H + 2 * fold_p && OW == fold_W + 2 * fold_p,
+                "conv_fwd: fold geometry");
   const int64_t RH = fold ? fold_H : OH, RW = fold ? fold_W : OW;
   if (act_bwd) {
     TORCH_CHECK(xb1.has_value(), "conv_fwd: act_bwd needs xb1");
@@ -522,7 +525,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   // folds it afterwards (gate and skip gradient applied there)
   bool fold_late = false;
   if (fold) {
-    fold_late = splits > 1 || halo_cond || fold_H < 2 * fold_p + 2 || fold_W < 2 * fold_p + 2 ||
+    const int64_t bw = fold_edge ? 1 : fold_p;   // band rows / columns per side (elementwise.hip fold_band)
+    fold_late = splits > 1 || halo_cond || fold_H < 2 * bw + 2 || fold_W < 2 * bw + 2 ||
                 std::getenv("P2P_FOLD_LATE") != nullptr;
     if (fold_late) {
       a.y1 = fbuf.data_ptr();
@@ -632,11 +636,13 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   if (fold) {
     const void* xg = act_bwd ? xb1->data_ptr() : nullptr;
     if (fold_late)
-      check_rc(p2p_pad_fold(fbuf.data_ptr(), (int)N, (int)fold_H, (int)fold_W, (int)Cout, (int)fold_p, 1, 1, xg,
+      check_rc(p2p_pad_fold(fbuf.data_ptr(), (int)N, (int)fold_H, (int)fold_W, (int)Cout, (int)fold_p, 1,
+                            fold_edge ? 2 : 1, xg,
                             (int)act_bwd, res ? res->data_ptr() : nullptr, y1.data_ptr(), st),
                "conv_fwd(pad_fold)");
     else
-      check_rc(p2p_fold_band(fbuf.data_ptr(), (int)N, (int)fold_H, (int)fold_W, (int)Cout, (int)fold_p, xg,
+      check_rc(p2p_fold_band(fbuf.data_ptr(), (int)N, (int)fold_H, (int)fold_W, (int)Cout, (int)fold_p,
+                             (int)fold_edge, xg,
                              (int)act_bwd, y1.data_ptr(), st),
                "conv_fwd(fold_band)");
   }
@@ -1786,7 +1792,7 @@ TORCH_LIBRARY(p2p, m) {
         "Tensor? qs_x2=None, Tensor? qs_w=None, Tensor(a!)? y_qsite=None, int y_qfmt=0, Tensor? res=None, "
         "Tensor? alpha=None, Tensor? nb_x=None, Tensor? nb_mean=None, Tensor? nb_rstd=None, "
         "Tensor? nb_gamma=None, Tensor? nb_beta=None, int nb_act=0, int nb_half=0, bool nb_batch=False, "
-        "bool nb_colsum=False, bool nb_gate=False, int fold_H=0, int fold_W=0, int fold_p=0) "
+        "bool nb_colsum=False, bool nb_gate=False, int fold_H=0, int fold_W=0, int fold_p=0, int fold_edge=0) "
         "-> Tensor[]");
   m.def("fp8_quant(Tensor x, Tensor(a!) site, int fmt, int use_cur=0) -> Tensor");
   m.def("sn_power_iter(Tensor w, Tensor(a!) u, Tensor(b!) v) -> Tensor");

@@ -89,12 +89,14 @@ struct ConvFwdArgs {
   int nb_gate;      // the act' gate of the nb half reads the norm's output, which IS xhat (non-affine,
                     // no fused act): compute the gate from the xhat the partials already form,
                     // instead of loading that output again (one operand stream fewer)
-  // Reflect-pad fold (MODE 1 dgrad onto the virtual padded grid OH x OW = (fold_H + 2p) x
-  // (fold_W + 2p), fold_buf null = off): an interior output pixel is stored straight into the
+  // Pad fold of an input gradient computed on a padded grid OH x OW = (fold_H + 2p) x
+  // (fold_W + 2p) (fold_buf null = off): an interior output pixel is stored straight into the
   // real input's gradient y1 [N][fold_H][fold_W] (act' gate and parked skip gradient as
   // usual); a pixel of the p-wide frame goes, raw, to fold_buf [N][OH][OW] -- only the frame
-  // of which is ever written -- and elementwise.hip fold_band adds it (gated) onto the
-  // reflected band pixels afterwards.  Unsplit single-output GEMMs only (host-checked).
+  // of which is ever written -- and elementwise.hip fold_band adds it (gated) onto the band
+  // pixels it pads (reflect: the mirrored ones; edge: the replicated border) afterwards.
+  // Reflect-pad dgrads (MODE 1 onto the padded grid) and the nearest-x2 + reflect-1 dgrad
+  // (MODE 0, 4x4 stride 2 over dY onto the edge-padded grid).  Unsplit single-output GEMMs.
   void* fold_buf;
   int fold_H, fold_W, fold_p;
 };

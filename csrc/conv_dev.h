@@ -121,7 +121,7 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
   auto ld16 = [](const bf16* p) __attribute__((always_inline)) { return *reinterpret_cast<const u32x4*>(p); };
   auto finish = [&](int row, long pix, u32x4 xv, u32x4 rv, u32x4 nv) __attribute__((always_inline)) {
     u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * LDC + (tid % CPR) * 8);
-    if (MODE == 1 && pix < 0) {   // reflect-fold frame pixel (no nb partials with a fold: host)
+    if (pix < 0) {   // fold frame pixel (no nb partials with a fold: host)
       *reinterpret_cast<u32x4*>(static_cast<bf16*>(a.fold_buf) + (-pix - 2) * a.Cout + co_t) = v;
       return;
     }
@@ -298,15 +298,15 @@ __device__ __forceinline__ void conv_epilogue_tail(const ConvFwdArgs& a, const C
   const int HWq = g.Hq * g.Wq;
   const int s = a.stride;
   constexpr int LDC = BN + 8;
-  // output pixel of GEMM row m; with the reflect fold (MODE 1): the real-grid pixel of an
+  // output pixel of GEMM row m; with a fold (conv.h fold_buf): the real-grid pixel of an
   // interior row, or -(padded pixel) - 2 for a frame row (-1 stays "no row")
   auto out_pix = [&](int m) __attribute__((always_inline)) -> long {
-    if (MODE == 0) return m;
+    if (MODE == 0 && !a.fold_buf) return m;
     const int n = (int)fdiv((uint32_t)m, fd_hwq);
     const int r = m - n * HWq;
     const int qy = (int)fdiv((uint32_t)r, fd_wq);
     const int qx = r - qy * g.Wq;
-    const int oy = qy * s + g.ry, ox = qx * s + g.rx;
+    const int oy = MODE == 0 ? qy : qy * s + g.ry, ox = MODE == 0 ? qx : qx * s + g.rx;
     if (a.fold_buf) {
       const int iy = oy - a.fold_p, ix = ox - a.fold_p;
       if ((unsigned)iy < (unsigned)a.fold_H && (unsigned)ix < (unsigned)a.fold_W)
@@ -393,7 +393,7 @@ __device__ __forceinline__ void conv_epilogue_tail(const ConvFwdArgs& a, const C
     if (m >= g.Mc || co >= a.Cout) continue;
     const long pix = out_pix(m);
     u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * LDC + cc * 8);
-    if (MODE == 1 && pix < 0) {   // reflect-fold frame pixel: raw, folded by fold_band (host: Csplit == Cout)
+    if (pix < 0) {   // fold frame pixel: raw, folded by fold_band (host: Csplit == Cout)
       *reinterpret_cast<u32x4*>(static_cast<bf16*>(a.fold_buf) + (-pix - 2) * a.Cout + co) = v;
       continue;
     }

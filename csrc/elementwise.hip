@@ -117,8 +117,16 @@ __global__ void __launch_bounds__(256) pad_channels_kernel(const bf16* __restric
 // to 3 padded rows onto one, the upsample 2x2 up-pixels onto one), then the input
 // activation's derivative is applied (act_bwd with the saved input xb).
 // One thread per (pixel, 8-channel chunk).
-__device__ __forceinline__ int fold_taps(int u, int pad, int Hu, bool reflect, int* q) {
+__device__ __forceinline__ int fold_taps(int u, int pad, int Hu, int reflect, int* q) {
   int n = 0;
+  if (reflect == 2) {   // replicate (edge) padding: the border pixel collects the whole frame side
+    q[n++] = u + pad;
+    if (u == 0)
+      for (int j = 0; j < pad && n < 5; ++j) q[n++] = j;
+    if (u == Hu - 1)
+      for (int j = 0; j < pad && n < 5; ++j) q[n++] = Hu + pad + j;
+    return n;
+  }
   const int c[3] = {u + pad, pad - u, 2 * (Hu - 1) + pad - u};
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -152,8 +160,8 @@ __global__ void __launch_bounds__(256) pad_fold_kernel(const bf16* __restrict__ 
     int qy[6], qx[6];
     int ny = 0, nx = 0;
     for (int k = 0; k < up; ++k) {
-      ny += fold_taps(y * up + k, pad, Hu, reflect != 0, qy + ny);
-      nx += fold_taps(x * up + k, pad, Wu, reflect != 0, qx + nx);
+      ny += fold_taps(y * up + k, pad, Hu, reflect, qy + ny);
+      nx += fold_taps(x * up + k, pad, Wu, reflect, qx + nx);
     }
     float acc[8];
 #pragma unroll
@@ -522,35 +530,48 @@ __global__ void __launch_bounds__(256) pad_fold_s1_kernel(const bf16* __restrict
 // each real pixel with a mirror image in the p-wide frame (rows / columns 1..p and
 // H-1-p..H-2) adds the frame values that reflect onto it, times the same act' gate.  Band
 // pixels only: 2p rows x W + (H - 2p) rows x 2p columns per image (host: H, W >= 2p + 2).
+// edge = 1 (replicate pad, the nearest-x2 + reflect-1 dgrad): the band is the outermost row /
+// column on each side, which collects all p frame rows / columns beyond it (host: p <= 4).
 __global__ void __launch_bounds__(256) fold_band_kernel(const bf16* __restrict__ fb, int N, int H, int W, int C,
-                                                        int pad, const bf16* __restrict__ xb, int act,
+                                                        int pad, int edge, const bf16* __restrict__ xb, int act,
                                                         bf16* __restrict__ dx) {
   const int CP = C >> 3;
   const int Hp = H + 2 * pad, Wp = W + 2 * pad;
-  const int nrow = 2 * pad * W, per_img = nrow + (H - 2 * pad) * 2 * pad;
+  const int bw = edge ? 1 : pad;   // band rows / columns per side
+  const int nrow = 2 * bw * W, per_img = nrow + (H - 2 * bw) * 2 * bw;
   const long total = (long)N * per_img * CP;
   for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
     const int cg = (int)(e % CP);
     const long t = e / CP;
     const int n = (int)(t / per_img);
     int k = (int)(t - (long)n * per_img), y, x;
+    // band of a side: reflect -> indices 1..p / H-1-p..H-2, edge -> 0 / H-1
+    const int b0 = edge ? 0 : 1;
     if (k < nrow) {   // a band row, every column
       const int r = k / W;
       x = k - r * W;
-      y = r < pad ? 1 + r : H - 1 - pad + (r - pad);
+      y = r < bw ? b0 + r : H - b0 - bw + (r - bw);
     } else {          // another row, a band column
       k -= nrow;
-      const int r = k / (2 * pad), c = k - r * 2 * pad;
-      y = r == 0 ? 0 : (r == H - 2 * pad - 1 ? H - 1 : pad + r);
-      x = c < pad ? 1 + c : W - 1 - pad + (c - pad);
+      const int r = k / (2 * bw), c = k - r * 2 * bw;
+      // the rows outside the bands, in order: reflect 0, p+1 .. H-2-p, H-1; edge 1 .. H-2
+      y = edge ? 1 + r : (r == 0 ? 0 : (r == H - 2 * bw - 1 ? H - 1 : pad + r));
+      x = c < bw ? b0 + c : W - b0 - bw + (c - bw);
     }
-    int qy[3], qx[3], ny = 0, nx = 0;
+    int qy[9], qx[9], ny = 0, nx = 0;
     qy[ny++] = y + pad;
     qx[nx++] = x + pad;
-    if (y >= 1 && y <= pad) qy[ny++] = pad - y;
-    if (y >= H - 1 - pad && y <= H - 2) qy[ny++] = 2 * (H - 1) + pad - y;
-    if (x >= 1 && x <= pad) qx[nx++] = pad - x;
-    if (x >= W - 1 - pad && x <= W - 2) qx[nx++] = 2 * (W - 1) + pad - x;
+    if (edge) {
+      if (y == 0) for (int j = 0; j < pad; ++j) qy[ny++] = j;
+      if (y == H - 1) for (int j = 0; j < pad; ++j) qy[ny++] = H + pad + j;
+      if (x == 0) for (int j = 0; j < pad; ++j) qx[nx++] = j;
+      if (x == W - 1) for (int j = 0; j < pad; ++j) qx[nx++] = W + pad + j;
+    } else {
+      if (y >= 1 && y <= pad) qy[ny++] = pad - y;
+      if (y >= H - 1 - pad && y <= H - 2) qy[ny++] = 2 * (H - 1) + pad - y;
+      if (x >= 1 && x <= pad) qx[nx++] = pad - x;
+      if (x >= W - 1 - pad && x <= W - 2) qx[nx++] = 2 * (W - 1) + pad - x;
+    }
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
@@ -676,7 +697,8 @@ int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, i
                  const void* xb, int act, const void* res, void* dx, hipStream_t st) {
   using namespace p2p;
   const long padded = (long)N * (H + 2 * pad) * (W + 2 * pad) * C;
-  if (up == 1 && C % 32 == 0 && pad < H - 1 && pad < W - 1 && padded < (1L << 31)) {
+  if (reflect == 2 && (up != 1 || pad > 2)) return -2;   // replicate: the edge dgrad's own frame only
+  if (up == 1 && reflect != 2 && C % 32 == 0 && pad < H - 1 && pad < W - 1 && padded < (1L << 31)) {
     const long work = (long)N * H * W * (C / 32);
     long b = (work + 255) / 256;
     b = b > 8192 ? 8192 : (b < 1 ? 1 : b);
@@ -692,13 +714,14 @@ int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, i
   return (int)hipGetLastError();
 }
 
-int p2p_fold_band(const void* fb, int N, int H, int W, int C, int pad, const void* xb, int act, void* dx,
+int p2p_fold_band(const void* fb, int N, int H, int W, int C, int pad, int edge, const void* xb, int act, void* dx,
                   hipStream_t st) {
   using namespace p2p;
-  if (C % 8 || pad < 1 || H < 2 * pad + 2 || W < 2 * pad + 2) return -2;
-  const long total = (long)N * (2 * pad * W + (H - 2 * pad) * 2 * pad) * (C / 8);
+  const int bw = edge ? 1 : pad;
+  if (C % 8 || pad < 1 || (edge && pad > 4) || H < 2 * bw + 2 || W < 2 * bw + 2) return -2;
+  const long total = (long)N * (2 * bw * W + (H - 2 * bw) * 2 * bw) * (C / 8);
   hipLaunchKernelGGL(fold_band_kernel, dim3(egrid(total)), dim3(256), 0, st, static_cast<const bf16*>(fb), N, H, W,
-                     C, pad, static_cast<const bf16*>(xb), act, static_cast<bf16*>(dx));
+                     C, pad, edge, static_cast<const bf16*>(xb), act, static_cast<bf16*>(dx));
   return (int)hipGetLastError();
 }
 

@@ -185,8 +185,8 @@ class CompressGANStep:
         native = real_a.is_cuda and _native.get_backend() == "native"
         # each feature's L1 gradient is parked for the next D conv (skip_grad="take"), which
         # adds it in its dgrad epilogue: no accumulate of the feature's two gradients
-        feat = [ops.l1(pred_fake_g[i][j], pred_real[i][j].detach(), gate_a=fgate,
-                       defer=native and fgate is not None)
+        defer = native and fgate is not None and os.environ.get("P2P_FEAT_DEFER", "1") != "0"
+        feat = [ops.l1(pred_fake_g[i][j], pred_real[i][j].detach(), gate_a=fgate, defer=defer)
                 for i in range(len(pred_fake_g)) for j in range(len(pred_fake_g[i]) - 1)]
         if native and feat:
             fw = self.d_weights * self.feat_weights * self.lambda_feat

@@ -18,12 +18,20 @@ keep PyTorch's default init, full-res input -> ``scale{num_D-1}_*``).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native, ops
 from .layers import BatchNorm2d, Conv2d, link_norm
+
+
+# P2P_FEAT_DEFER=0: D's feature-matching gradients accumulate through autograd (A/B knob)
+_FEAT_DEFER = os.environ.get("P2P_FEAT_DEFER", "1") != "0"
+# P2P_FAMR_STATS=0: the BNs compute their own statistics (A/B knob for the conv-epilogue stats)
+_FUSED_STATS = os.environ.get("P2P_FAMR_STATS", "1") != "0"
 
 
 def ops_hip():
@@ -100,8 +108,9 @@ class ResidualBlock(nn.Module):
         # conv1's input-gradient pass (HIP path) instead of an autograd accumulate
         self.conv1.conv2d.skip_grad = "take"
         # the BN statistics come from the conv epilogues (no separate statistics pass)
-        link_norm(self.conv1.conv2d, self.in1)
-        link_norm(self.conv2.conv2d, self.in2)
+        if _FUSED_STATS:
+            link_norm(self.conv1.conv2d, self.in1)
+            link_norm(self.conv2.conv2d, self.in2)
 
     def forward(self, x):
         out = self.in2(self.conv2(self.in1(self.conv1(x))))
@@ -134,7 +143,8 @@ class ExpandNetwork(nn.Module):
         self.in1_d = BatchNorm2d(3, affine=True, act="tanh")
         for conv, bn in ((self.conv2, self.in2_e), (self.conv3, self.in3_e), (self.deconv3, self.in3_d),
                          (self.deconv2, self.in2_d), (self.deconv1, self.in1_d)):
-            link_norm(conv.conv2d, bn)
+            if _FUSED_STATS:
+                link_norm(conv.conv2d, bn)
 
     def forward(self, x):
         if x.shape[-1] % 4 or x.shape[-2] % 4:
@@ -143,7 +153,7 @@ class ExpandNetwork(nn.Module):
         # pixel-unshuffle(2) followed by nearest x2: the conv sees 12 channels at full res.
         y = self.inversePixel(x)
         y = ops.conv2d(y, self.conv1.conv2d.weight, self.conv1.conv2d.bias, 1, 4, "reflect", 2,
-                       stats=self.training)
+                       stats=self.training and _FUSED_STATS)
         pw = self.relu.weight            # PReLU fused into the BN passes (fwd and bwd)
         y = self.in1_e(y, prelu=pw)
         y = self.in2_e(self.conv2(y), prelu=pw)
@@ -167,7 +177,8 @@ class CompressionNetwork(nn.Module):
                                          BatchNorm2d(64), PReLU())
         self.conv_block2 = nn.Sequential(ConvLayer(64, 12, kernel_size=3, stride=2),
                                          PixelShuffle(2))
-        link_norm(self.conv_block1[0].conv2d, self.conv_block1[1])
+        if _FUSED_STATS:
+            link_norm(self.conv_block1[0].conv2d, self.conv_block1[1])
 
     def forward(self, x):
         conv, bn, act = self.conv_block1
@@ -293,7 +304,7 @@ class NLayerDiscriminatorSN(nn.Module):
             if getattr(prod, "act_out", None) == "lrelu":
                 prod.out_gated = bool(on)
                 cons.grad_gate = "lrelu" if on else None
-                cons.skip_grad = "take" if on else None
+                cons.skip_grad = "take" if (on and _FEAT_DEFER) else None
         self.feature_grad_gate = "lrelu" if on else None
 
     def forward(self, x):

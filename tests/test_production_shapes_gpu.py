@@ -12,9 +12,10 @@ PyTorch (MIOpen fp32, no autocast), with the rule of tests/test_pix2pix_step_gpu
 
     |native - fp32| <= 2 |eager bf16 autocast - fp32| + 1 % of the quantity's scale
 
-(gradients: absolute floor 1e-3 of the network's largest gradient -- biases of convs feeding
-an instance norm have an exactly-zero true gradient).  It also checks which kernels ran, so
-the bound is known to cover the production tiles.
+per tensor, with no network-wide floor: only the structurally-zero gradients (biases of convs
+feeding an instance norm, ZERO_REL below) get an absolute bound.  It also checks which kernels
+ran, so the bound is known to cover the production tiles.  The same step in fp8 (BASELINE
+config 5) has its own, fp8-derived bound (F8_REL / F8_COS below).
 """
 import copy
 import json
@@ -73,35 +74,57 @@ def _run(kind, G0, D0, a, b):
     return res
 
 
-def test_headline_step_at_production_shape_matches_fp32():
+@pytest.fixture(scope="module")
+def refs():
+    """The fp32 oracle and the eager bf16 autocast step, shared by the bf16 and fp8 tests."""
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
     G0, D0 = _nets()
     g = torch.Generator().manual_seed(13)
     a = torch.rand(B, 3, S, S, generator=g) * 2 - 1
     b = torch.rand(B, 3, S, S, generator=g) * 2 - 1
+    lc, gc = _run("fp32", G0, D0, a, b)
+    le, ge = _run("eager", G0, D0, a, b)
+    return G0, D0, a, b, lc, gc, le, ge
+
+
+# A gradient whose fp32 magnitude is below ZERO_REL of the network's largest is structurally
+# zero (the bias of a conv feeding an instance norm: the norm removes any per-channel shift, so
+# its true gradient is exactly 0 and fp32 shows rounding noise); the native step returns exact
+# zeros there (the norm backward's column sums), bounded by the same absolute ZERO_REL.
+ZERO_REL = 1e-5
+
+
+def _log(test, rows, extra):
+    if os.path.isdir("gpurun_out"):
+        with open("gpurun_out/bounds.jsonl", "a") as f:
+            f.write(json.dumps({"test": test, "rows": rows, **extra}) + "\n")
+
+
+def test_headline_step_at_production_shape_matches_fp32(refs):
+    """Per tensor: |native - fp32|_max <= 2 |eager - fp32|_max + 1 % of that tensor's own
+    scale (no network-wide floor), or the structurally-zero class above."""
+    G0, D0, a, b, lc, gc, le, ge = refs
     # the native run under the profiler's kernel list: the production tiles must be among them
     from torch.profiler import ProfilerActivity, profile
     with profile(activities=[ProfilerActivity.CUDA]) as prof:
         ln, gn = _run("native", G0, D0, a, b)
     names = {e.name for e in prof.events()}
-    lc, gc = _run("fp32", G0, D0, a, b)
-    le, ge = _run("eager", G0, D0, a, b)
     want = {"256x256 LATE fwd": "conv_fwd_glds_kernel<256, 256, 2, 4, 0, 2",
             "256x256 MODE-1": "conv_fwd_glds_kernel<256, 256, 2, 4, 1, 2",
             "256x128 3-stage": "conv_fwd_glds_kernel<256, 128, 4, 2,",
             "EXT epilogue": "true>(p2p::ConvFwdArgs)",
             "wgrad 256x128": "conv_wgrad_glds_kernel<256, 128",
             "image head": "halo_union_kernel",
-            # round 3: the class-shared halo kernel of the stride-2 transposed convs / dgrads
-            # onto 64x64 grids (d2 forward with input ReLU, the EXT dgrads)
+            # the class-shared halo kernel of the stride-2 transposed convs / dgrads onto
+            # 64x64 grids (d2 forward with input ReLU, the EXT dgrads)
             "s2t halo ConvT": "conv_s2t_kernel<64, true, false, 0>",
             "s2t halo EXT dgrad": "conv_s2t_kernel<64, false, true, 0>"}
     missing = [k for k, pat in want.items() if not any(pat in n for n in names)]
     rows, bad = [], []
     for k in lc:
         err, erre = abs(ln[k] - lc[k]), abs(le[k] - lc[k])
-        rows.append(("loss:" + k, err, erre, abs(lc[k])))
+        rows.append(("loss:" + k, err, erre, abs(lc[k]), "loss"))
         if err > 2 * erre + 1e-2 * abs(lc[k]) + 1e-5:
             bad.append(("loss", k, ln[k], lc[k], le[k]))
     assert set(gn) == set(gc), set(gn) ^ set(gc)
@@ -113,12 +136,71 @@ def test_headline_step_at_production_shape_matches_fp32():
             err = (gn[n] - gc[n]).abs().max().item()
             erre = (ge[n] - gc[n]).abs().max().item()
             scale = gc[n].abs().max().item()
-            rows.append((n, err, erre, scale))
-            if err > 2 * erre + 1e-2 * scale and err > 1e-3 * gscale:
-                bad.append((n, err, erre, scale))
-    if os.path.isdir("gpurun_out"):
-        with open("gpurun_out/bounds.jsonl", "a") as f:
-            f.write(json.dumps({"test": "headline_step_production_shape", "rows": rows,
-                                "missing_kernels": missing}) + "\n")
+            if scale <= ZERO_REL * gscale:
+                cls, ok = "zero", err <= ZERO_REL * gscale
+            else:
+                cls, ok = "bound", err <= 2 * erre + 1e-2 * scale
+            rows.append((n, err, erre, scale, cls))
+            if not ok:
+                bad.append((n, cls, err, erre, scale))
+    _log("headline_step_production_shape", rows, {"missing_kernels": missing})
     assert not missing, f"production tiles not exercised: {missing}"
+    assert not bad, bad
+
+
+# fp8 (BASELINE config 5): e4m3 activations / weights (3 mantissa bits) and e5m2 gradients
+# (2 bits) against bf16's 7 -- per-element rounding 2^4 - 2^5 times bf16's, so the max-error
+# rule above does not transfer.  Bounded instead per tensor by the relative L2 error
+# ||native - fp32|| / ||fp32|| <= F8_REL (structurally-zero tensors as above), the whole
+# network's gradient direction (cosine >= F8_COS) and the losses within 5 % + 0.02.
+F8_REL = 0.25
+F8_COS = 0.98
+
+
+def test_fp8_step_at_production_shape_close_to_fp32(refs):
+    from p2p_pytorch_amd.ops import fp8 as _f8
+    G0, D0, a, b, lc, gc, le, ge = refs
+    _f8.set_precision("fp8")
+    try:
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            ln, gn = _run("native", G0, D0, a, b)
+    finally:
+        _f8.set_precision("bf16")
+    names = {e.name for e in prof.events()}
+    assert any("conv_wgrad_f8_kernel" in n for n in names), "fp8 weight gradient not exercised"
+    rows, bad = [], []
+    for k in lc:
+        err = abs(ln[k] - lc[k])
+        rows.append(("loss:" + k, err, abs(le[k] - lc[k]), abs(lc[k]), "loss"))
+        if err > 0.05 * abs(lc[k]) + 0.02:
+            bad.append(("loss", k, ln[k], lc[k]))
+    for tag in "GD":
+        names_t = [n for n in gc if n.startswith(tag)]
+        gscale = max(gc[n].abs().max().item() for n in names_t)
+        vn = torch.cat([gn[n].reshape(-1) for n in names_t])
+        vc = torch.cat([gc[n].reshape(-1) for n in names_t])
+        cos = (vn @ vc / (vn.norm() * vc.norm()).clamp_min(1e-30)).item()
+        rows.append((tag + ":cosine", cos, None, None, "cosine"))
+        if cos < F8_COS:
+            bad.append((tag, "cosine", cos))
+        for n in names_t:
+            assert torch.isfinite(gn[n]).all(), n
+            d = gn[n] - gc[n]
+            scale = gc[n].abs().max().item()
+            if scale <= ZERO_REL * gscale:
+                err = d.abs().max().item()
+                cls, ok = "zero", err <= ZERO_REL * gscale
+            else:
+                err = (d.norm() / gc[n].norm()).item()
+                erre = ((ge[n] - gc[n]).norm() / gc[n].norm()).item()
+                cls, ok = "rel_l2", err <= F8_REL
+                rows.append((n, err, erre, scale, cls))
+                if not ok:
+                    bad.append((n, cls, err, erre))
+                continue
+            rows.append((n, err, None, scale, cls))
+            if not ok:
+                bad.append((n, cls, err))
+    _log("fp8_step_production_shape", rows, {})
     assert not bad, bad
