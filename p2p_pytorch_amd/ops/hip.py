@@ -40,6 +40,9 @@ _NB_FUSE = os.environ.get("P2P_NB_FUSE", "1") != "0"
 _NB_LOG = os.environ.get("P2P_NB_LOG", "0") == "1"
 # reflect-pad dgrads fold in the conv epilogue (P2P_FOLD_EPI=0: padded grid + pad_fold, A/B)
 _FOLD_EPI = os.environ.get("P2P_FOLD_EPI", "1") != "0"
+# nearest-x2 + reflect-1 3x3 dgrads as one 4x4 stride-2 conv over dY (P2P_UP_FOLD=1; opt-in
+# until measured on hardware)
+_UP_FOLD = os.environ.get("P2P_UP_FOLD", "0") == "1"
 CL = torch.channels_last
 _NULLCTX = contextlib.nullcontext()
 
@@ -252,6 +255,32 @@ def _weight_image(w: torch.Tensor, swap: int, xp: int, yp: int, scale=None) -> t
     return img
 
 
+# phase sums of a 3x3 kernel seen through nearest x2 + edge pad 1 (ops/hip.py up-fold dgrad):
+# tap a of the 4-tap stride-2 input-gradient kernel collects the 3x3 taps k with
+# o + k + 1 in {2q, 2q + 1} for o = 2q + a - 3
+_UP2_M = ((0, 0, 1), (0, 1, 1), (1, 1, 0), (1, 0, 0))
+
+
+def _up2_dgrad_image(w: torch.Tensor, cp: int, coutp: int) -> torch.Tensor:
+    """bf16 [Cp][4][4][Coutp] GEMM image of the nearest-x2 + reflect-1 3x3 conv's input
+    gradient as a 4x4 stride-2 conv over dY: W''[ci][co][a][b] = sum_kl M[a][k] M[b][l]
+    w[co][ci][k][l].  Cached per step like the plain weight images."""
+    cache = getattr(w, "_p2p_cache", None)
+    if cache is None:
+        cache = {}
+        w._p2p_cache = cache
+    key = ("up2d", cp, coutp)
+    ver = w._version
+    ent = cache.get(key)
+    if ent is not None and ent[0] == ver and ent[1] == _gen[0]:
+        return ent[2]
+    m = torch.tensor(_UP2_M, dtype=torch.float32, device=w.device)
+    wd = torch.einsum("ak,oikl,bl->ioab", m, w.detach().float(), m).contiguous()
+    img = P().weight_prep(wd, 0, cp, coutp, None)
+    cache[key] = (ver, _gen[0], img)
+    return img
+
+
 def _weight_image_fp8(w: torch.Tensor, swap: int, xp: int, yp: int):
     """e4m3 copy (current scaling) of the bf16 GEMM-operand image, cached like the bf16 one;
     returns (image, scale site)."""
@@ -282,7 +311,8 @@ def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, 
     (OH, OW) = (H + 2p, W + 2p) returns the real input's gradient (H, W): interior pixels
     stored by the epilogue, the frame folded by elementwise.hip fold_band (xb1 / res are
     real-grid tensors)."""
-    fk = {} if fold is None else dict(fold_H=int(fold[0]), fold_W=int(fold[1]), fold_p=int(fold[2]))
+    fk = {} if fold is None else dict(fold_H=int(fold[0]), fold_W=int(fold[1]), fold_p=int(fold[2]),
+                                      fold_edge=int(fold[3]) if len(fold) > 3 else 0)
     C1 = x1.shape[1]
     C2 = 0 if x2 is None else x2.shape[1]
     if weight is not None and _f8.enabled() and _f8.conv_ok(C1, C2, Cout, act_in):
@@ -749,7 +779,16 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
                 if res is not None and res.shape != (q1.shape[0], Cp, H, W):
                     _DEFERRED[q1.data_ptr()] = res   # not fusable: added below instead
                     res = None
-            if cfg.up == 1 and cfg.reflect and p > 0 and _FOLD_EPI:
+            if (cfg.up == 2 and cfg.reflect and p == 1 and KH == 3 and KW == 3 and s == 1
+                    and _UP_FOLD):
+                # nearest x2 then reflect pad 1 == edge-replicate pad 1 of the upsample: the
+                # dgrad is a 4x4 stride-2 pad-3 conv over dY with phase-summed taps onto the
+                # edge-padded (H+2) x (W+2) grid, folded in the epilogue -- no 4x up-grid, 16
+                # instead of 36 taps per input pixel (_up2_dgrad_image)
+                outs = _conv_call(gyp, None, _up2_dgrad_image(weight, Cp, Coutp), None, 0, 4, 4, 2, 3,
+                                  0, 1, 0, H + 2, W + 2, Cp, 0, Cp, q1 if act_in else None, None, act_in,
+                                  C1, False, role="gy", res=res, fold=(H, W, 1, 1))[:1]
+            elif cfg.up == 1 and cfg.reflect and p > 0 and _FOLD_EPI:
                 # reflect pad only: the fold happens in the dgrad's epilogue (interior pixels
                 # gated + skip gradient straight into dx) plus a frame-band pass
                 outs = _conv_call(gyp, None, None, None, 1, KH, KW, s, 0, 0, 1, 0, Hp, Wp, Cp,

@@ -328,12 +328,13 @@ class GradReducer:
                 b.work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     def _reset(self):
+        # (the forward use counts survive: zero_grad() runs between the forward that counted
+        # them and the backward that retires them; finish() clears them)
         for b in self.buckets:
             b.work = None
             b.events = None
             b.side = []
             b.pending = len(b.params)
-        self._uses = {}
 
     def _join_inflight(self):
         # collectives launched but never finished (e.g. a backward abandoned by an
@@ -378,6 +379,7 @@ class GradReducer:
             if b.cbuf is not None:
                 b.flat.copy_(b.cbuf)            # already averaged (pre-scaled)
         self._reset()
+        self._uses = {}   # uses counted by forwards whose backward is done (or never ran)
 
     def enable_timing(self, on: bool = True):
         self._timing = bool(on)

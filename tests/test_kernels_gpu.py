@@ -223,6 +223,39 @@ def test_reflect_dgrad_epilogue_fold_matches_pad_fold(case, monkeypatch):
     assert rel_err(ge, rx.grad) < 3e-2
 
 
+UPFOLD_CASES = [
+    # (N, Cin, Cout, H, W, act_in): G.deconv3 / deconv2 (nearest x2 + reflect 1 + 3x3)
+    (2, 128, 64, 16, 16, None),
+    (2, 64, 32, 12, 20, "relu"),
+    (1, 32, 64, 5, 7, None),
+]
+
+
+@pytest.mark.parametrize("case", UPFOLD_CASES, ids=[f"c{c[1]}o{c[2]}_h{c[3]}w{c[4]}" for c in UPFOLD_CASES])
+def test_up2_reflect_dgrad_as_strided_conv(case, monkeypatch):
+    """The nearest-x2 + reflect-1 3x3 conv's input gradient as ONE 4x4 stride-2 conv over dY
+    (phase-summed taps, edge-replicate fold in the epilogue) against the fp32 oracle and the
+    upsampled-grid dgrad + pad_fold path."""
+    from p2p_pytorch_amd.ops import hip
+    N, Cin, Cout, H, W, act_in = case
+    x = rand_img(N, Cin, H, W, seed=31)
+    w = torch.randn(Cout, Cin, 3, 3, device=DEV) * (1.0 / (Cin * 9) ** 0.5)
+    gy = rand_img(N, Cout, 2 * H, 2 * W, seed=32)
+
+    def dgrad(up_fold):
+        monkeypatch.setattr(hip, "_UP_FOLD", up_fold)
+        hx = _leaf(x)
+        ops.conv2d(hx, w, None, 1, 1, pad_mode="reflect", upsample=2, act_in=act_in).backward(gy)
+        return hx.grad.float()
+
+    gf, gp = dgrad(True), dgrad(False)
+    rx = _leaf(x.float())
+    ref.conv2d(rx, w.to(torch.bfloat16).float(), None, 1, 1, pad_mode="reflect", upsample=2,
+               act_in=act_in).backward(gy.float())
+    assert rel_err(gf, rx.grad) < 3e-2
+    assert rel_err(gf, gp) < 3e-2
+
+
 def test_conv_wgrad_large_m():
     # many pixels per weight -> many split-K slabs; checks the deterministic slab reduce
     x = rand_img(8, 64, 64, 64, seed=8)

@@ -30,7 +30,7 @@ def main():
     from p2p_pytorch_amd.models import define_D, define_G
     from p2p_pytorch_amd.parallel import GradReducer
     from p2p_pytorch_amd.parallel import dist as pdist
-    dev = torch.device("cuda")
+    dev = torch.device("cuda", torch.cuda.current_device())
     p2p.set_backend("native")
     pdist.init_single(dev)
     torch.manual_seed(0)
