@@ -99,7 +99,10 @@ def family_r_phase(world, rank, dev, steps=3):
         for bk in red_d.buckets:
             gl = [torch.zeros_like(local[bk.index]) for _ in range(world)]
             dist.all_gather(gl, local[bk.index])
-            mean = torch.stack(gl).float().mean(0)
+            # the buckets hold gradients pre-scaled by red_d.scale (1/world): the reduced bucket
+            # is the SUM of the ranks' local buckets (= the mean of their raw gradients)
+            stk = torch.stack(gl).float()
+            mean = stk.sum(0) if red_d.scale != 1.0 else stk.mean(0)
             worst = max(worst, float((bk.flat.float() - mean).abs().max() / mean.abs().max().clamp_min(1e-12)))
         for m in (G, D, C):
             f = torch.cat([p.detach().reshape(-1) for p in m.parameters()])

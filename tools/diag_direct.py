@@ -44,17 +44,27 @@ def main():
         for n, p in (G if tag == "G" else D).named_parameters():
             names[id(p)] = f"{tag}.{n}"
 
-    orig = {k: getattr(GradReducer, k) for k in ("count_use", "direct_done", "_on_grad", "zero_grad", "finish")}
+    orig = {k: getattr(GradReducer, k) for k in ("count_use", "direct_done", "_on_grad", "zero_grad", "finish",
+                                                  "_launch")}
+    history = []   # (reducer, kind, param name, bucket index, pending before)
 
     def wrap(kind):
         f = orig[kind]
 
         def g(self, *a, **k):
+            tag = "G" if self is rg else "D"
             if kind in ("count_use", "direct_done", "_on_grad"):
-                log[names.get(id(a[0]), "?")][kind] += 1
+                nm = names.get(id(a[0]), "?%x" % id(a[0]))
+                log[nm][kind] += 1
+                b = self._param_bucket.get(a[0])
+                history.append((tag, kind, nm, None if b is None else b.index,
+                                None if b is None else b.pending, self._uses.get(id(a[0]))))
+            elif kind == "_launch":
+                history.append((tag, "LAUNCH", "-", a[0].index, a[0].pending, None))
+                return f(self, *a, **k)
             else:
-                tag = "G" if self is rg else "D"
                 print(f"-- {tag}.{kind}", flush=True)
+                history.append((tag, kind.upper(), "-", None, None, None))
                 if kind == "finish":
                     bad = {n: dict(c) for n, c in log.items() if n.startswith(tag) and
                            (c["direct_done"] + c["_on_grad"] != 1 or c["direct_done"] > max(c["count_use"], 1))}
@@ -82,6 +92,9 @@ def main():
     except Exception:
         traceback.print_exc()
         snap = {n: dict(c) for n, c in log.items()}
+        print("reducer history (tag, event, param, bucket, pending before, uses):", flush=True)
+        for h in history[-60:]:
+            print("   ", h)
         print("arrivals at the error:", flush=True)
         for n, c in snap.items():
             if c.get("direct_done", 0) + c.get("_on_grad", 0) != 1:
