@@ -9,18 +9,18 @@ mix + blur of A, with A smooth random images -- three ways:
   * the native HIP path in bf16 (the headline path);
   * the native HIP path with fp8 convs (BASELINE config 5).
 
-Asserted per native path: the train L1 (mean of the last 20 steps) fell to <= 20 % of the
-first 10 steps'; it ends within 25 % of the fp32 run's; no update was skipped by the NaN
-guard; and the held-out PSNR (the reference's per-epoch validation metric, train.py:450-502,
-computed on the device by engine/metrics.py) is at most 2.5 dB below the fp32 run's and 15 dB
-above the untrained generator's.  Dropout is off (``use_dropout=False``) so the three runs see
-the same network function (their dropout RNG streams differ by backend).
-
-The bounds are set by the spread of the fp32 run itself: a 300-step GAN run amplifies any
-numeric difference, and two MI355X runs of the identical fp32 configuration (MIOpen picks its
-algorithms per run) ended at L1 0.0298 / 0.0267 and PSNR 33.2 / 34.6 dB (gpurun_out/r4l,
-r4m); the native runs are deterministic (bf16 0.0306 / 33.5 dB, fp8 0.0294 / 32.5 dB on the
-round-4 build; L1 0.197 -> ~0.03 and PSNR 14.5 -> 32.5-35.4 dB for all three paths).
+Each path is trained from three initialisations (SEEDS) and compared by its mean over them:
+a 300-step GAN run amplifies any numeric difference, and single runs of the identical fp32
+configuration ended at L1 0.0219 / 0.0267 / 0.0298 and PSNR 35.6 / 34.6 / 33.2 dB on three
+MI355X runs (MIOpen picks its algorithms per run; gpurun_out/r4l, r4m, r4m2 -- the fp32 runs
+here use cudnn.deterministic), while one native bf16 / fp8 run gave 0.0306 / 33.5 dB and
+0.0294 / 32.5 dB.  Asserted per native path (seed means): the train L1 (mean of the last 20
+steps) fell to <= 20 % of the first 10 steps'; it ends within 20 % of the fp32 mean; no update
+was skipped by the NaN guard; and the held-out PSNR (the reference's per-epoch validation
+metric, train.py:450-502, computed on the device by engine/metrics.py) is at most 1.5 dB below
+the fp32 mean and 15 dB above the untrained generator's.  Dropout is off
+(``use_dropout=False``) so the runs see the same network function (their dropout RNG streams
+differ by backend).
 """
 import pytest
 import torch
@@ -55,9 +55,9 @@ def _task(seed=0):
     return a[:NTRAIN], b[:NTRAIN], a[NTRAIN:], b[NTRAIN:]
 
 
-def _init_state():
+def _init_state(seed=1234):
     from p2p_pytorch_amd.models import define_D, define_G
-    torch.manual_seed(1234)
+    torch.manual_seed(seed)
     G = define_G(netG="unet_128", gpu_id="cuda", use_dropout=False, verbose=False)
     D = define_D(6, 64, norm="instance", netD="basic", gpu_id="cuda", verbose=False)
     return ({k: v.detach().clone() for k, v in G.state_dict().items()},
@@ -104,13 +104,27 @@ def _train(backend, precision, init, task):
         p2p.set_backend("native")
 
 
+SEEDS = (1234, 1235, 1236)
+
+
 @pytest.fixture(scope="module")
 def runs():
+    """Every path trained from the same SEEDS initialisations; per path the mean over seeds."""
     task = _task()
-    init = _init_state()
-    out = {"fp32": _train("torch", "bf16", init, task),
-           "bf16": _train("native", "bf16", init, task),
-           "fp8": _train("native", "fp8", init, task)}
+    inits = [_init_state(sd) for sd in SEEDS]
+    cudnn = (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark)
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        per = {"fp32": [_train("torch", "bf16", i, task) for i in inits]}
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = cudnn
+    per["bf16"] = [_train("native", "bf16", i, task) for i in inits]
+    per["fp8"] = [_train("native", "fp8", i, task) for i in inits]
+    out = {}
+    for k, rs in per.items():
+        out[k] = {f: sum(r[f] for r in rs) / len(rs) for f in ("l1_first", "l1_last", "psnr0", "psnr", "skipped")}
+        out[k]["finite"] = all(r["finite"] for r in rs)
+        out[k]["per_seed"] = [(round(r["l1_last"], 5), round(r["psnr"], 2)) for r in rs]
     print("convergence:", out)
     return out
 
@@ -122,6 +136,6 @@ def test_native_training_converges_like_fp32(runs, path):
     assert ref["l1_last"] <= 0.2 * ref["l1_first"], ref          # the task is learnable
     assert r["skipped"] == 0.0, r
     assert r["l1_last"] <= 0.2 * r["l1_first"], r
-    assert abs(r["l1_last"] - ref["l1_last"]) <= 0.25 * ref["l1_last"], (r, ref)
+    assert abs(r["l1_last"] - ref["l1_last"]) <= 0.2 * ref["l1_last"], (r, ref)
     assert r["psnr"] > r["psnr0"] + 15.0, r
-    assert r["psnr"] >= ref["psnr"] - 2.5, (r, ref)   # (GAN runs land a dB or two apart either way)
+    assert r["psnr"] >= ref["psnr"] - 1.5, (r, ref)   # (GAN runs land a dB or two apart either way)
