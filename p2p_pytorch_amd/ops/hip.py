@@ -578,9 +578,6 @@ class ConvFn(torch.autograd.Function):
             _stash_stats(y, outs[1])
         if Coutp != Cout:
             y = P().slice_channels(y, 0, Cout)
-        red = getattr(weight, "_p2p_direct", None)
-        if red is not None and ctx.needs_input_grad[2]:
-            red.count_use(weight)   # one direct backward contribution to expect
         ctx.cfg = cfg
         ctx.geo = (C1, C2, Cp, packed, Cout, Coutp, H, W)
         ctx.has_x2 = x2 is not None

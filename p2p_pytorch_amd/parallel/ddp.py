@@ -39,16 +39,17 @@ Mechanism
     completion callback), and ``comm_stats()`` reports the last backward's collective
     busy time, the part of it left exposed after backward's last kernel, and the overlap
     fraction -- the JSONL "comm ms / overlap %" of SURVEY.md section 5.5.
-  * Direct gradients (``direct=True``, round 4): the native conv backward writes a weight's
-    (and bias's) gradient straight into its bucket view, pre-scaled by 1/world, with the
+  * Direct gradients (``direct=True``, round 4): the native conv backward writes a conv
+    weight's gradient straight into its bucket view, pre-scaled by 1/world, with the
     wgrad kernel's own accumulate mode -- no AccumulateGrad add, no 1/world pass -- and may
-    run it on the weight-gradient side stream (ops/hip.py ``wgrad_overlap``).  Readiness:
-    each conv forward with grad enabled counts a use of its weight (``count_use``), each
-    backward contribution retires one (``direct_done``, with the stream it was enqueued on);
-    the last one marks the param ready, and a bucket whose params were written on the side
-    stream launches its all-reduce from a comm stream that waits on both streams' events.
-    Gradients that still arrive through autograd are scaled by 1/world in their hook, so
-    ``finish`` never rescales.
+    run it on the weight-gradient side stream (ops/hip.py ``wgrad_overlap``).  Readiness
+    still comes from autograd: a leaf's post-accumulate hook fires once per backward after all
+    of its producers ran, also when they all returned None because they wrote the bucket
+    themselves; ``direct_done`` only records the side-stream event the bucket's all-reduce
+    must wait on (it is issued from a comm stream that waits on both streams) and marks the
+    param as already scaled.  Gradients that arrive through autograd are scaled by 1/world in
+    their hook, so ``finish`` never rescales.  Opt-in (``P2P_DIRECT_GRAD=1``) until the
+    hardware A/B is in.
   * Bucket size: xGMI is point-to-point (7 links x ~153 GB/s per GPU); RCCL's ring /
     direct algorithms are per-link bound, so few large buckets (tens of MB) amortise the
     per-collective latency while still leaving >= 2-4 buckets per network to overlap.
@@ -143,7 +144,7 @@ class GradReducer:
         if direct is None:   # opt-in until the native path's use counting is hardware-verified
             direct = os.environ.get("P2P_DIRECT_GRAD", "0") == "1"
         self.direct = bool(direct)
-        self._uses: dict = {}
+        self._direct_seen: set = set()   # params written directly in the current backward
         self._names = {id(p): n for n, p in module.named_parameters()}
         if self.direct:
             for p in params:
@@ -222,17 +223,13 @@ class GradReducer:
         lo = b.flat.data_ptr()
         if not (lo <= p.grad.data_ptr() < lo + b.flat.numel() * b.flat.element_size()):
             self._rebind(p, b, copy=True)
-        if self.scale != 1.0:
+        if self.scale != 1.0 and id(p) not in self._direct_seen:
             p.grad.mul_(self.scale)          # this backward's gradient alone (bucket zeroed)
         b.pending -= 1
         if b.pending == 0:
             self._launch(b)
 
     # ------------------------------------------------------------------ direct gradients
-    def count_use(self, p):
-        """A forward read ``p`` with grad enabled: one more backward contribution to expect."""
-        self._uses[id(p)] = self._uses.get(id(p), 0) + 1
-
     def direct_ok(self, p) -> bool:
         """The backward may write ``p``'s gradient into its bucket view itself."""
         if not (self.direct and self.active) or p.grad is None:
@@ -244,23 +241,16 @@ class GradReducer:
         return lo <= p.grad.data_ptr() < lo + b.flat.numel() * b.flat.element_size()
 
     def direct_done(self, p, stream=None):
-        """One direct contribution to ``p.grad`` has been enqueued (on ``stream``, default the
-        current one); the last expected one marks ``p`` ready."""
+        """A direct contribution to ``p.grad`` has been enqueued (on ``stream``, default the
+        current one).  Readiness still comes from autograd: its post-accumulate hook fires once
+        per backward for every leaf the backward reached -- also when every contribution was
+        None (written here) -- after all of that leaf's producers ran."""
         b = self._param_bucket[p]
         if stream is not None and stream != torch.cuda.current_stream(stream.device):
             ev = torch.cuda.Event()
             ev.record(stream)
             b.side.append(ev)
-        n = self._uses.get(id(p), 1) - 1
-        if n > 0:
-            self._uses[id(p)] = n
-            return
-        self._uses.pop(id(p), None)
-        if self._ready_order is not None:
-            self._ready_order.append(p)
-        b.pending -= 1
-        if b.pending == 0:
-            self._launch(b)
+        self._direct_seen.add(id(p))
 
     def _rebind(self, p, b, copy):
         off = self._offset[p]
@@ -328,13 +318,12 @@ class GradReducer:
                 b.work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     def _reset(self):
-        # (the forward use counts survive: zero_grad() runs between the forward that counted
-        # them and the backward that retires them; finish() clears them)
         for b in self.buckets:
             b.work = None
             b.events = None
             b.side = []
             b.pending = len(b.params)
+        self._direct_seen = set()
 
     def _join_inflight(self):
         # collectives launched but never finished (e.g. a backward abandoned by an
@@ -379,7 +368,6 @@ class GradReducer:
             if b.cbuf is not None:
                 b.flat.copy_(b.cbuf)            # already averaged (pre-scaled)
         self._reset()
-        self._uses = {}   # uses counted by forwards whose backward is done (or never ran)
 
     def enable_timing(self, on: bool = True):
         self._timing = bool(on)

@@ -36,16 +36,14 @@ def main():
     torch.manual_seed(0)
     G = define_G(netG="unet_256", gpu_id=dev, verbose=False)
     D = define_D(6, 64, norm="instance", netD="basic", gpu_id=dev, verbose=False)
-    rg = GradReducer(G, bucket_mb=16.0, force_comm=True, direct=True)
-    rd = GradReducer(D, bucket_mb=16.0, force_comm=True, direct=True)
+    rg = rd = None
     log = collections.defaultdict(lambda: collections.Counter())
     names = {}
-    for tag, r in (("G", rg), ("D", rd)):
-        for n, p in (G if tag == "G" else D).named_parameters():
+    for tag, net in (("G", G), ("D", D)):
+        for n, p in net.named_parameters():
             names[id(p)] = f"{tag}.{n}"
 
-    orig = {k: getattr(GradReducer, k) for k in ("count_use", "direct_done", "_on_grad", "zero_grad", "finish",
-                                                  "_launch")}
+    orig = {k: getattr(GradReducer, k) for k in ("direct_done", "_on_grad", "zero_grad", "finish", "_launch")}
     history = []   # (reducer, kind, param name, bucket index, pending before)
 
     def wrap(kind):
@@ -53,12 +51,12 @@ def main():
 
         def g(self, *a, **k):
             tag = "G" if self is rg else "D"
-            if kind in ("count_use", "direct_done", "_on_grad"):
+            if kind in ("direct_done", "_on_grad"):
                 nm = names.get(id(a[0]), "?%x" % id(a[0]))
                 log[nm][kind] += 1
                 b = self._param_bucket.get(a[0])
                 history.append((tag, kind, nm, None if b is None else b.index,
-                                None if b is None else b.pending, self._uses.get(id(a[0]))))
+                                None if b is None else b.pending, id(a[0]) in self._direct_seen))
             elif kind == "_launch":
                 history.append((tag, "LAUNCH", "-", a[0].index, a[0].pending, None))
                 return f(self, *a, **k)
@@ -66,8 +64,7 @@ def main():
                 print(f"-- {tag}.{kind}", flush=True)
                 history.append((tag, kind.upper(), "-", None, None, None))
                 if kind == "finish":
-                    bad = {n: dict(c) for n, c in log.items() if n.startswith(tag) and
-                           (c["direct_done"] + c["_on_grad"] != 1 or c["direct_done"] > max(c["count_use"], 1))}
+                    bad = {n: dict(c) for n, c in log.items() if n.startswith(tag) and c["_on_grad"] != 1}
                     print(f"   {tag} params with anomalous arrivals: {len(bad)}", flush=True)
                     for n, c in list(bad.items())[:20]:
                         print(f"     {n}: {c}", flush=True)
@@ -78,6 +75,9 @@ def main():
 
     for k in orig:
         setattr(GradReducer, k, wrap(k))
+    # built after the patch: the grad hooks bind _on_grad at construction
+    rg = GradReducer(G, bucket_mb=16.0, force_comm=True, direct=True)
+    rd = GradReducer(D, bucket_mb=16.0, force_comm=True, direct=True)
     step = Pix2PixStep(G, D, reducer_g=rg, reducer_d=rd)
     a = (torch.rand(args.batch, 3, args.size, args.size, device=dev) * 2 - 1).to(torch.bfloat16).contiguous(
         memory_format=torch.channels_last)
@@ -97,7 +97,7 @@ def main():
             print("   ", h)
         print("arrivals at the error:", flush=True)
         for n, c in snap.items():
-            if c.get("direct_done", 0) + c.get("_on_grad", 0) != 1:
+            if c.get("_on_grad", 0) != 1:
                 print(f"   {n}: {c}")
     finally:
         for k, f in orig.items():
