@@ -420,7 +420,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   const int64_t s2t_chc = fp8 ? 128 : 64;
   const bool s2t_ok = mode == 1 && splits == 1 && KH == 4 && KW == 4 && stride == 2 && pad == 1 &&
                       !reflect && up == 1 && OH == 2 * H && OW == 2 * W &&
-                      (W == 64 || (W == 32 && !fp8 && env_flag("P2P_S2T_W32", true))) &&
+                      (W == 64 || (W == 32 && !fp8 && env_flag("P2P_S2T_W32", false))) &&
                       (H * W) % 128 == 0 && Cout % 64 == 0 && C1 % s2t_chc == 0 && C2 % s2t_chc == 0 &&
                       C1 + C2 >= s2t_chc && C1 + C2 <= 256 &&
                       (act_in == 0 || (act_in == 1 && act_bwd == 0 && !res)) && act_out <= 2 &&

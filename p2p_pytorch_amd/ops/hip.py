@@ -40,9 +40,9 @@ _NB_FUSE = os.environ.get("P2P_NB_FUSE", "1") != "0"
 _NB_LOG = os.environ.get("P2P_NB_LOG", "0") == "1"
 # reflect-pad dgrads fold in the conv epilogue (P2P_FOLD_EPI=0: padded grid + pad_fold, A/B)
 _FOLD_EPI = os.environ.get("P2P_FOLD_EPI", "1") != "0"
-# nearest-x2 + reflect-1 3x3 dgrads as one 4x4 stride-2 conv over dY (P2P_UP_FOLD=1; opt-in
-# until measured on hardware)
-_UP_FOLD = os.environ.get("P2P_UP_FOLD", "0") == "1"
+# nearest-x2 + reflect-1 3x3 dgrads as one 4x4 stride-2 conv over dY (P2P_UP_FOLD=0: the
+# upsampled-grid dgrad + pad_fold, A/B; family R B = 64 835.5 vs 808.9 img/s, gpurun_out/r4n)
+_UP_FOLD = os.environ.get("P2P_UP_FOLD", "1") != "0"
 CL = torch.channels_last
 _NULLCTX = contextlib.nullcontext()
 

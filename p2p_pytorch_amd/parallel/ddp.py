@@ -277,9 +277,16 @@ class GradReducer:
             b.work.get_future().then(lambda _f, e=e1: e.record())
             b.events = (e0, e1)
             return
-        timed = self._timing and not torch.cuda.is_current_stream_capturing() and b.flat.is_cuda
+        capturing = b.flat.is_cuda and torch.cuda.is_current_stream_capturing()
+        timed = self._timing and not capturing and b.flat.is_cuda
         cur = torch.cuda.current_stream(b.flat.device) if b.flat.is_cuda else None
-        side = b.flat.is_cuda and bool(b.side)
+        side = b.flat.is_cuda and bool(b.side) and not capturing
+        if capturing and b.side:
+            # under hipGraph capture the collective stays on the capturing stream (RCCL work
+            # issued from a joined side stream trips the process-group watchdog's event
+            # queries): that stream waits on the side-stream gradient writes instead
+            for ev in b.side:
+                cur.wait_event(ev)
         if timed or side:
             # a comm stream ordered after the compute stream AND the side-stream gradient
             # writes of this bucket (their events), so the compute stream itself never waits
