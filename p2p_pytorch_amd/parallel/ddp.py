@@ -65,6 +65,9 @@ import torch
 import torch.distributed as dist
 
 
+_DEBUG = os.environ.get("P2P_DDP_DEBUG", "0") == "1"
+
+
 class _Bucket:
     __slots__ = ("params", "flat", "cbuf", "pending", "work", "index", "events", "side")
 
@@ -138,6 +141,11 @@ class GradReducer:
         self.active = True
         self._timing = False
         self._comm_stream = None
+        # the stream the step's backward runs on, taken at zero_grad() on the step's thread:
+        # autograd may run a leaf's post-accumulate hook on ANOTHER stream (a leaf whose
+        # producers all returned None -- direct gradients -- gets no stream sync), so the
+        # collectives are ordered and capture-checked against this one, not the hook's
+        self._compute_stream = None
         self._last = None        # (bucket events, end-of-backward event) of the last finish()
         # every gradient lands pre-scaled by 1/world (direct writes and autograd hooks alike)
         self.scale = 1.0 / self.world if (self.comm and self.world > 1) else 1.0
@@ -223,8 +231,16 @@ class GradReducer:
         lo = b.flat.data_ptr()
         if not (lo <= p.grad.data_ptr() < lo + b.flat.numel() * b.flat.element_size()):
             self._rebind(p, b, copy=True)
-        if self.scale != 1.0 and id(p) not in self._direct_seen:
-            p.grad.mul_(self.scale)          # this backward's gradient alone (bucket zeroed)
+        if id(p) not in self._direct_seen:
+            if self.scale != 1.0:
+                p.grad.mul_(self.scale)      # this backward's gradient alone (bucket zeroed)
+            if p.grad.is_cuda:
+                hs = torch.cuda.current_stream(p.grad.device)
+                if hs != self._stream(p.grad.device):
+                    # accumulated on the leaf's own stream: the collective waits on it
+                    ev = torch.cuda.Event()
+                    ev.record(hs)
+                    b.side.append(ev)
         b.pending -= 1
         if b.pending == 0:
             self._launch(b)
@@ -246,11 +262,17 @@ class GradReducer:
         per backward for every leaf the backward reached -- also when every contribution was
         None (written here) -- after all of that leaf's producers ran."""
         b = self._param_bucket[p]
-        if stream is not None and stream != torch.cuda.current_stream(stream.device):
+        if stream is not None and stream != self._stream(stream.device):
             ev = torch.cuda.Event()
             ev.record(stream)
             b.side.append(ev)
         self._direct_seen.add(id(p))
+
+    def _stream(self, device):
+        """The step's compute stream (see ``_compute_stream``)."""
+        if self._compute_stream is None or self._compute_stream.device != device:
+            return torch.cuda.current_stream(device)
+        return self._compute_stream
 
     def _rebind(self, p, b, copy):
         off = self._offset[p]
@@ -277,9 +299,18 @@ class GradReducer:
             b.work.get_future().then(lambda _f, e=e1: e.record())
             b.events = (e0, e1)
             return
-        capturing = b.flat.is_cuda and torch.cuda.is_current_stream_capturing()
+        cur = self._stream(b.flat.device) if b.flat.is_cuda else None
+        capturing = False
+        if cur is not None:
+            with torch.cuda.stream(cur):
+                capturing = torch.cuda.is_current_stream_capturing()
         timed = self._timing and not capturing and b.flat.is_cuda
-        cur = torch.cuda.current_stream(b.flat.device) if b.flat.is_cuda else None
+        if _DEBUG and cur is not None:
+            hs = torch.cuda.current_stream(b.flat.device)
+            print(f"[reducer] bucket {b.index}: thread {threading.get_ident()} hook stream "
+                  f"{hs.stream_id} compute stream {cur.stream_id} capturing {capturing} "
+                  f"hook-stream capturing {torch.cuda.is_current_stream_capturing()} "
+                  f"side events {len(b.side)}", flush=True)
         side = b.flat.is_cuda and bool(b.side) and not capturing
         if capturing and b.side:
             # under hipGraph capture the collective stays on the capturing stream (RCCL work
@@ -298,7 +329,7 @@ class GradReducer:
                 cs.wait_event(ev)
             ctx = torch.cuda.stream(cs)
         else:
-            ctx = contextlib.nullcontext()
+            ctx = torch.cuda.stream(cur) if cur is not None else contextlib.nullcontext()
         with ctx:
             buf = b.flat
             if b.cbuf is not None:
@@ -371,7 +402,7 @@ class GradReducer:
             elif b.side:
                 # no collective (world 1): order the compute stream after the side writes
                 for ev in b.side:
-                    torch.cuda.current_stream(b.flat.device).wait_event(ev)
+                    self._stream(b.flat.device).wait_event(ev)
             if b.cbuf is not None:
                 b.flat.copy_(b.cbuf)            # already averaged (pre-scaled)
         self._reset()
@@ -418,6 +449,8 @@ class GradReducer:
         """Start a backward: join stale collectives, (re-bucket once), zero the buckets and
         reset the per-backward bookkeeping."""
         self._join_inflight()
+        if self.buckets and self.buckets[0].flat.is_cuda:
+            self._compute_stream = torch.cuda.current_stream(self.buckets[0].flat.device)
         if self._ready_order:
             self._rebucket()
         for b in self.buckets:

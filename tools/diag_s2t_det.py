@@ -7,6 +7,9 @@ nondeterministic reduction (repeats differ) from a route difference (repeats equ
 differ).
 """
 import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch
 

@@ -1,0 +1,118 @@
+"""Where do the s2t and implicit-GEMM routes of the norm chain differ?
+(tests/test_s2t_gpu.py::test_s2t_norm_chain_fused_partials_and_stats)
+
+Runs the chain on both routes and on the fp32 oracle, keeps the gradient of every
+intermediate (h = lrelu(IN(conv1 x)), c1 = conv1 x, z = conv2 h, t = convT z) and prints per
+tensor: max-norm relative error of each route vs the oracle, the route-to-route difference,
+and the location (n, y, x, c) of the worst elements -- with whether they sit on the image
+border -- so a wrong-pixel epilogue shows as a spatial pattern rather than noise.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+import torch.nn.functional as F
+
+from p2p_pytorch_amd import _native, ops
+from p2p_pytorch_amd.ops import reference as ref
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def worst(a, b, k=5):
+    """top-k |a-b| locations of NCHW tensors, as (n, y, x, c, a, b)."""
+    a, b = a.float(), b.float()
+    d = (a - b).abs()
+    N, C, H, W = d.shape
+    v, idx = d.flatten().topk(k)
+    out = []
+    for i in idx.tolist():
+        n, r = divmod(i, C * H * W)
+        c, r = divmod(r, H * W)
+        y, x = divmod(r, W)
+        out.append((n, y, x, c, round(a.flatten()[i].item(), 5), round(b.flatten()[i].item(), 5)))
+    return out, (H, W)
+
+
+def border_profile(a, b):
+    """mean |a-b| on the outer 1-pixel frame vs the interior, normalised by max|b|."""
+    d = (a.float() - b.float()).abs()
+    s = b.float().abs().max().clamp_min(1e-6)
+    fr = torch.ones_like(d[0, 0], dtype=torch.bool)
+    fr[1:-1, 1:-1] = False
+    return (d[..., fr].mean() / s).item(), (d[..., ~fr].mean() / s).item()
+
+
+def main():
+    _native.set_backend("native")
+    assert _native.load(), _native.load_error()
+    g = torch.Generator(device=DEV).manual_seed(9)
+    x = (torch.randn(4, 64, 256, 256, device=DEV, generator=g)
+         .to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+    torch.manual_seed(0)
+    w1 = torch.randn(64, 64, 4, 4, device=DEV) * 0.03
+    b1 = torch.randn(64, device=DEV) * 0.1
+    w2 = torch.randn(128, 64, 4, 4, device=DEV) * 0.03
+    wt = torch.randn(128, 64, 4, 4, device=DEV) * 0.03
+    lin = None
+
+    def native():
+        nonlocal lin
+        hx, hw1, hb1, hw2, hwt = [t.detach().clone().requires_grad_(True) for t in (x, w1, b1, w2, wt)]
+        c1 = ops.conv2d(hx, hw1, hb1, 2, 1, stats=True)
+        h = ops.instance_norm(c1, act="lrelu")
+        z = ops.conv2d(h, hw2, None, 2, 1)
+        t = ops.conv_transpose2d(z, hwt, None, 2, 1, act_in="relu", stats=True)
+        u = ops.instance_norm(t, act="relu")
+        for v in (c1, h, z, t):
+            v.retain_grad()
+        if lin is None:
+            lin = torch.linspace(-1, 1, u.numel(), device=DEV).view_as(u)
+        (u.float() * lin).sum().backward()
+        torch.cuda.synchronize()
+        return {"u": u.detach(), "g_t": t.grad, "g_z": z.grad, "g_h": h.grad, "g_c1": c1.grad,
+                "dx": hx.grad, "dw1": hw1.grad, "dw2": hw2.grad, "dwt": hwt.grad}
+
+    s2t = native()
+    os.environ["P2P_NO_S2T"] = "1"
+    gemm = native()
+    os.environ.pop("P2P_NO_S2T")
+
+    rx, rw1, rb1, rw2, rwt = [t.detach().clone().float().requires_grad_(True) for t in (x, w1, b1, w2, wt)]
+    bfw = lambda w: w.to(torch.bfloat16).float()  # noqa: E731
+    c1 = ref.conv2d(rx, bfw(rw1), rb1, 2, 1)
+    c1 = c1 + (c1.to(torch.bfloat16).float() - c1).detach()
+    h = F.leaky_relu(F.instance_norm(c1), 0.2)
+    z = ref.conv2d(h, bfw(rw2), None, 2, 1)
+    z = z + (z.to(torch.bfloat16).float() - z).detach()
+    t = ref.conv_transpose2d(z, bfw(rwt), None, 2, 1, "relu", None)
+    t = t + (t.to(torch.bfloat16).float() - t).detach()
+    u = F.relu(F.instance_norm(t))
+    for v in (c1, h, z, t):
+        v.retain_grad()
+    (u * lin).sum().backward()
+    oracle = {"u": u.detach(), "g_t": t.grad, "g_z": z.grad, "g_h": h.grad, "g_c1": c1.grad,
+              "dx": rx.grad, "dw1": rw1.grad, "dw2": rw2.grad, "dwt": rwt.grad}
+
+    for k in oracle:
+        a, b, r = s2t[k], gemm[k], oracle[k]
+        print(f"{k:5s} s2t-vs-oracle {rel(a, r):.5f}  gemm-vs-oracle {rel(b, r):.5f}  "
+              f"s2t-vs-gemm {rel(a, b):.5f}")
+        if a.dim() == 4:
+            fa, ia = border_profile(a, r)
+            fb, ib = border_profile(b, r)
+            print(f"      mean err frame/interior: s2t {fa:.2e}/{ia:.2e}  gemm {fb:.2e}/{ib:.2e}")
+            for name, q in (("s2t", a), ("gemm", b)):
+                w, hw = worst(q, r)
+                print(f"      worst {name} vs oracle (n,y,x,c,native,oracle) on {hw}: {w}")
+
+
+if __name__ == "__main__":
+    main()
