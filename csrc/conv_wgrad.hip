@@ -878,41 +878,49 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 }
 
 // The same reduction with coalesced stores: a block owns one GEMM row r and 32 consecutive
-// input channels of every tap -- it sums the slabs into an LDS tile read as 128-B rows per
-// (split, tap), then writes dw in its [r][ci][kh][kw] order (T contiguous floats per channel,
-// 32 x T per block) instead of one 4-B store every T floats.  Same fixed split order per
-// element as wgrad_reduce_kernel, so bitwise identical to it.
+// input channels of every tap -- it sums the slabs into an LDS tile (each tap's 32 channels
+// are one 128-B row per split), then writes dw in its [r][ci][kh][kw] order (T contiguous
+// floats per channel, 32 x T per block) instead of one 4-B store every T floats.  Every thread
+// owns whole elements and walks ALL splits itself, G independent loads in flight per step
+// into G partial sums (split k -> partial k % G, each in increasing k, then partial 0 + 1 +
+// ... in order): exactly wgrad_reduce_kernel's summation order, so bitwise identical to it,
+// with no block barrier inside the split loop (a split-group-per-thread layout serialised
+// T*32/EPB barrier rounds per block: 4x slower on the 57-split family-R wgrads).
 template <int G>
 __global__ void __launch_bounds__(256) wgrad_reduce_t_kernel(const float* __restrict__ ws, int splits,
                                                              int R, int T, int C, int KW, int Rr, int Cr,
                                                              float* __restrict__ dw, float scale,
                                                              int accumulate, int flip) {
   constexpr int CB = 32, LDT = CB + 1;
-  constexpr int EPB = 256 / G;
   __shared__ float tile[81 * LDT];
-  __shared__ float red[256];
   const int r = blockIdx.y, c0 = blockIdx.x * CB;
   const int Kq = T * C;
   const long total = (long)R * Kq;
   const int E = T * CB;
-  const int le = threadIdx.x % EPB, sg = threadIdx.x / EPB;
-  for (int b0 = 0; b0 < E; b0 += EPB) {
-    const int idx = b0 + le;
+  for (int idx = threadIdx.x; idx < E; idx += 256) {
     const int tap = idx / CB, cc = idx - tap * CB;
-    const bool ok = idx < E && c0 + cc < C;
     float s = 0.f;
-    if (ok) {
+    if (c0 + cc < C) {
       const float* src = ws + (long)r * Kq + tap * C + c0 + cc;
-      for (int k = sg; k < splits; k += G) s += src[(long)k * total];
+      float acc[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) acc[g] = 0.f;
+      int k0 = 0;
+      for (; k0 + G <= splits; k0 += G) {
+        float v[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) v[g] = src[(long)(k0 + g) * total];
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[g] += v[g];
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (k0 + g < splits) acc[g] += src[(long)(k0 + g) * total];
+      s = acc[0];
+#pragma unroll
+      for (int g = 1; g < G; ++g) s += acc[g];
     }
-    if (G > 1) {
-      red[threadIdx.x] = s;
-      __syncthreads();
-      if (sg == 0)
-        for (int q = 1; q < G; ++q) s += red[q * EPB + le];
-    }
-    if (sg == 0 && idx < E) tile[tap * LDT + cc] = s * scale;
-    if (G > 1) __syncthreads();
+    tile[tap * LDT + cc] = s * scale;
   }
   __syncthreads();
   for (int j = threadIdx.x; j < E; j += 256) {
@@ -1088,7 +1096,7 @@ extern "C" int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int 
   const long total = (long)R * KH * KW * C;
   int G = 1;
   while (G < 32 && splits > 8 * G) G *= 2;   // <= ~8 slab reads per thread
-  static const bool old_red = std::getenv("P2P_WRED_OLD") != nullptr;   // A/B: 4-B scattered stores
+  const bool old_red = std::getenv("P2P_WRED_OLD") != nullptr;   // A/B: 4-B scattered stores (per call)
   if (!old_red && KH * KW <= 81) {
     const dim3 grid((unsigned)((C + 31) / 32), (unsigned)R);
 #define P2P_REDT(g)                                                                                       \

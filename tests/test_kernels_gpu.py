@@ -275,6 +275,41 @@ def test_conv_wgrad_large_m():
     assert rel_err(hw.grad, rw.grad) < 2e-2
 
 
+# (N, Cin, Cout, H, k, pad_mode): family-R residual 3x3 (reflect, tens of splits), the U-Net
+# 4x4 s1-equivalent shape, a 9x9 head (T = 81 taps, the LDS tile's limit), odd channel count
+@pytest.mark.parametrize("N,Cin,Cout,H,k,pad_mode", [(16, 128, 128, 64, 3, "reflect"),
+                                                     (8, 64, 128, 64, 4, "zeros"),
+                                                     (4, 32, 32, 128, 9, "reflect"),
+                                                     (16, 40, 24, 32, 3, "zeros")])
+def test_wgrad_split_reduce_kernels_bitwise(N, Cin, Cout, H, k, pad_mode, monkeypatch):
+    """The coalesced split-K reduce (per-thread split walk, G partial sums) sums in exactly the
+    scattered-store kernel's order (P2P_WRED_OLD=1, read per call): bitwise equal weight
+    gradients, and both within bf16 tolerance of the fp32 oracle."""
+    x = rand_img(N, Cin, H, H, seed=21)
+    w = torch.randn(Cout, Cin, k, k, device=DEV) * (1.0 / (Cin * k * k) ** 0.5)
+    stride, pad = (1, k // 2) if k % 2 else (2, 1)
+
+    def run():
+        hw = _leaf(w)
+        y = ops.conv2d(x, hw, None, stride, pad, pad_mode)
+        y.backward(gy)
+        return hw.grad
+
+    with torch.no_grad():
+        shape = ops.conv2d(x, w, None, stride, pad, pad_mode).shape
+    gy = rand_img(*shape, seed=22)
+    g_new = run()
+    monkeypatch.setenv("P2P_WRED_OLD", "1")
+    g_old = run()
+    monkeypatch.delenv("P2P_WRED_OLD")
+    assert torch.equal(g_new, g_old), (g_new - g_old).abs().max().item()
+    rw = _leaf(w)
+    xr = F.pad(x.float(), (pad,) * 4, mode="reflect") if pad_mode == "reflect" else x.float()
+    F.conv2d(xr, rw.to(torch.bfloat16).float(), None, stride,
+             0 if pad_mode == "reflect" else pad).backward(gy.float())
+    assert rel_err(g_new, rw.grad) < 2e-2
+
+
 @pytest.mark.parametrize("N,C,H", [(2, 64, 32), (4, 512, 2), (2, 128, 64), (3, 256, 5)])
 def test_instance_norm(N, C, H):
     x = rand_img(N, C, H, H, scale=3.0, seed=10)

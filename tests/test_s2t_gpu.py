@@ -54,6 +54,14 @@ def _leaf(x):
     return x.detach().clone().requires_grad_(True)
 
 
+def _loss_weights(u):
+    """Fixed random per-element loss weights.  (A global linspace ramp varies by less than one
+    bf16 step inside an instance-norm plane, so the norm backward's dy - mean(dy) cancels to
+    rounding noise -- 50-80 % max-norm errors on either route, `tools/diag_s2t_route.py`.)"""
+    g = torch.Generator(device=DEV).manual_seed(17)
+    return torch.randn(u.shape, device=DEV, generator=g)
+
+
 def _kernels(fn):
     """Names of the kernels ``fn`` launched (torch profiler, HIP activity)."""
     from torch.profiler import ProfilerActivity, profile
@@ -160,7 +168,7 @@ def test_s2t_norm_chain_fused_partials_and_stats(monkeypatch):
         z = ops.conv2d(h, hw2, None, 2, 1)                           # 128 -> 64, dgrad: s2t
         u = ops.instance_norm(ops.conv_transpose2d(z, hwt, None, 2, 1, act_in="relu", stats=True),
                               act="relu")                              # ConvT 64 -> 128: s2t + stats
-        loss = (u.float() * torch.linspace(-1, 1, u.numel(), device=DEV).view_as(u)).sum()
+        loss = (u.float() * _loss_weights(u)).sum()
         loss.backward()
         return u, hx.grad, hw1.grad, hw2.grad, hwt.grad
 
@@ -182,9 +190,8 @@ def test_s2t_norm_chain_fused_partials_and_stats(monkeypatch):
     t = ref.conv_transpose2d(z, rwt.to(torch.bfloat16).float(), None, 2, 1, "relu", None)
     t = t + (t.to(torch.bfloat16).float() - t).detach()
     u = F.relu(F.instance_norm(t))
-    (u * torch.linspace(-1, 1, u.numel(), device=DEV).view_as(u)).sum().backward()
-    # two norms deep, the bf16 gradients of either native path sit 10-20 % (max-norm) from the
-    # fp32 oracle: bound the s2t path by the implicit-GEMM path it replaces, against the oracle
+    (u * _loss_weights(u)).sum().backward()
+    # bound the s2t path by the implicit-GEMM path it replaces, against the oracle
     refs = (u, rx.grad, rw1.grad, rw2.grad, rwt.grad)
     errs = [(rel_err(a, r), rel_err(b, r)) for a, b, r in zip(out, out0, refs)]
     print("s2t / glds errors vs fp32 oracle:", errs)
@@ -232,7 +239,7 @@ def test_s2t_w32_norm_chain_fused_partials_and_stats(monkeypatch):
         z = ops.conv2d(h, hw2, None, 2, 1)
         u = ops.instance_norm(ops.conv_transpose2d(z, hwt, None, 2, 1, act_in="relu", stats=True),
                               act="relu")
-        loss = (u.float() * torch.linspace(-1, 1, u.numel(), device=DEV).view_as(u)).sum()
+        loss = (u.float() * _loss_weights(u)).sum()
         loss.backward()
         return u, hx.grad, hw1.grad, hw2.grad, hwt.grad
 
@@ -251,7 +258,7 @@ def test_s2t_w32_norm_chain_fused_partials_and_stats(monkeypatch):
     t = ref.conv_transpose2d(z, rwt.to(torch.bfloat16).float(), None, 2, 1, "relu", None)
     t = t + (t.to(torch.bfloat16).float() - t).detach()
     u = F.relu(F.instance_norm(t))
-    (u * torch.linspace(-1, 1, u.numel(), device=DEV).view_as(u)).sum().backward()
+    (u * _loss_weights(u)).sum().backward()
     refs = (u, rx.grad, rw1.grad, rw2.grad, rwt.grad)
     errs = [(rel_err(a, r), rel_err(b, r)) for a, b, r in zip(out, out0, refs)]
     print("s2t / glds errors vs fp32 oracle (W=32):", errs)

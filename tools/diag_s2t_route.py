@@ -6,6 +6,7 @@ intermediate (h = lrelu(IN(conv1 x)), c1 = conv1 x, z = conv2 h, t = convT z) an
 tensor: max-norm relative error of each route vs the oracle, the route-to-route difference,
 and the location (n, y, x, c) of the worst elements -- with whether they sit on the image
 border -- so a wrong-pixel epilogue shows as a spatial pattern rather than noise.
+``randn``: per-element random loss weights instead of one global linspace ramp.
 """
 import os
 import sys
@@ -74,7 +75,11 @@ def main():
         for v in (c1, h, z, t):
             v.retain_grad()
         if lin is None:
-            lin = torch.linspace(-1, 1, u.numel(), device=DEV).view_as(u)
+            if "randn" in sys.argv[1:]:   # well-conditioned weights (tests/test_s2t_gpu.py)
+                gw = torch.Generator(device=DEV).manual_seed(17)
+                lin = torch.randn(u.shape, device=DEV, generator=gw)
+            else:                         # the global ramp: ill-conditioned through each norm
+                lin = torch.linspace(-1, 1, u.numel(), device=DEV).view_as(u)
         (u.float() * lin).sum().backward()
         torch.cuda.synchronize()
         return {"u": u.detach(), "g_t": t.grad, "g_z": z.grad, "g_h": h.grad, "g_c1": c1.grad,
