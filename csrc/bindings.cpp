@@ -36,14 +36,15 @@ long p2p_norm_ws_floats(int N, int HW, int C);
 int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, const float* partials,
                           float eps, const float* gamma, const float* beta, const float* prelu_w,
                           int act, float* mean, float* rstd, float* run_mean, float* run_var,
-                          float momentum, void* y, void* q, int* qsite, int qfmt, hipStream_t st);
+                          float momentum, void* y, void* q, int* qsite, int qfmt, const void* res,
+                          hipStream_t st);
 int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* gamma,
                  const float* beta, const float* prelu_w, int act, float* mean, float* rstd,
                  float* run_mean, float* run_var, float momentum, float* ws, void* y,
-                 void* q, int* qsite, int qfmt, hipStream_t st);
+                 void* q, int* qsite, int qfmt, const void* res, hipStream_t st);
 int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const float* rstd,
                    const float* gamma, const float* beta, const float* prelu_w, int act, void* y,
-                   hipStream_t st);
+                   const void* res, hipStream_t st);
 int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const float* mean,
                  const float* rstd, const float* gamma, const float* beta, int act,
                  const float* prelu_w, float* dprelu, float* dgamma, float* dbeta, float* ws, void* dx,
@@ -1086,8 +1087,15 @@ std::vector<Tensor> norm_fwd(const Tensor& x, double eps, const optional<Tensor>
                              int64_t act, const optional<Tensor>& run_mean,
                              const optional<Tensor>& run_var, double momentum, bool batch,
                              const optional<Tensor>& partials, const optional<Tensor>& qsite,
-                             const optional<Tensor>& q_out, int64_t qfmt) {
+                             const optional<Tensor>& q_out, int64_t qfmt, const optional<Tensor>& res) {
   check_act(x, "norm_fwd x");
+  // res: residual added before the activation (same shape / layout as x)
+  if (res) {
+    check_act(*res, "norm_fwd res");
+    TORCH_CHECK(res->sizes() == x.sizes(), "norm_fwd: residual shape");
+    TORCH_CHECK(!prelu_w, "norm_fwd: residual with the fused PReLU is unsupported");
+  }
+  const void* resp = res ? res->data_ptr() : nullptr;
   // optional fp8 shadow of y written by the apply pass (q_out: same shape, fp8, NHWC)
   void* qp = nullptr;
   int* qs = nullptr;
@@ -1119,7 +1127,7 @@ std::vector<Tensor> norm_fwd(const Tensor& x, double eps, const optional<Tensor>
                                    mean.data_ptr<float>(), rstd.data_ptr<float>(),
                                    run_mean ? run_mean->data_ptr<float>() : nullptr,
                                    run_var ? run_var->data_ptr<float>() : nullptr, (float)momentum,
-                                   y.data_ptr(), qp, qs, (int)qfmt, cur_stream(x)),
+                                   y.data_ptr(), qp, qs, (int)qfmt, resp, cur_stream(x)),
              "norm_fwd(partials)");
     return {y, mean, rstd};
   }
@@ -1132,15 +1140,19 @@ std::vector<Tensor> norm_fwd(const Tensor& x, double eps, const optional<Tensor>
                         mean.data_ptr<float>(), rstd.data_ptr<float>(),
                         run_mean ? run_mean->data_ptr<float>() : nullptr,
                         run_var ? run_var->data_ptr<float>() : nullptr, (float)momentum,
-                        ws.data_ptr<float>(), y.data_ptr(), qp, qs, (int)qfmt, cur_stream(x)),
+                        ws.data_ptr<float>(), y.data_ptr(), qp, qs, (int)qfmt, resp, cur_stream(x)),
            "norm_fwd");
   return {y, mean, rstd};
 }
 
 Tensor norm_apply(const Tensor& x, const Tensor& mean, const Tensor& rstd,
                   const optional<Tensor>& gamma, const optional<Tensor>& beta,
-                  const optional<Tensor>& prelu_w, int64_t act, bool batch) {
+                  const optional<Tensor>& prelu_w, int64_t act, bool batch, const optional<Tensor>& res) {
   check_act(x, "norm_apply x");
+  if (res) {
+    check_act(*res, "norm_apply res");
+    TORCH_CHECK(res->sizes() == x.sizes() && !prelu_w, "norm_apply: residual shape / PReLU");
+  }
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
   Tensor y = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   check_rc(p2p_norm_apply(x.data_ptr(), batch ? 1 : (int)N, batch ? (int)(N * HW) : (int)HW, (int)C,
@@ -1148,7 +1160,7 @@ Tensor norm_apply(const Tensor& x, const Tensor& mean, const Tensor& rstd,
                           gamma ? gamma->data_ptr<float>() : nullptr,
                           beta ? beta->data_ptr<float>() : nullptr,
                           prelu_w ? prelu_w->data_ptr<float>() : nullptr, (int)act, y.data_ptr(),
-                          cur_stream(x)),
+                          res ? res->data_ptr() : nullptr, cur_stream(x)),
            "norm_apply");
   return y;
 }
@@ -1826,9 +1838,9 @@ TORCH_LIBRARY(p2p, m) {
   m.def("weight_prep_multi(Tensor[] w, int[] swap, int[] xp, int[] yp) -> Tensor[]");
   m.def("norm_fwd(Tensor x, float eps, Tensor? gamma, Tensor? beta, Tensor? prelu_w, int act, "
         "Tensor(a!)? run_mean, Tensor(b!)? run_var, float momentum, bool batch, Tensor? partials=None, "
-        "Tensor(c!)? qsite=None, Tensor(d!)? q_out=None, int qfmt=0) -> Tensor[]");
+        "Tensor(c!)? qsite=None, Tensor(d!)? q_out=None, int qfmt=0, Tensor? res=None) -> Tensor[]");
   m.def("norm_apply(Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? prelu_w, "
-        "int act, bool batch) -> Tensor");
+        "int act, bool batch, Tensor? res=None) -> Tensor");
   m.def("norm_bwd(Tensor x, Tensor dy, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, int act, "
         "Tensor(a!)? dgamma, Tensor(b!)? dbeta, bool need_dx, bool batch, Tensor(c!)? dsum, "
         "Tensor(d!)? qsite=None, Tensor(e!)? q_out=None, int qfmt=0, Tensor? prelu_w=None, "

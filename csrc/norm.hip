@@ -248,9 +248,11 @@ static void with_act(int act, F&& f) {
   }
 }
 
-// y = act((x - mean) * rstd * gamma + beta); mean/rstd indexed [n][c] (BN: n == 0 always).
-// grid (chunks, N): each thread owns one 8-channel chunk (its 8 scale/shift pairs live in
-// registers) and strides over the block's pixels.
+// y = act((x - mean) * rstd * gamma + beta [+ res]); mean/rstd indexed [n][c] (BN: n == 0
+// always).  res (optional, x's shape): a residual added BEFORE the activation -- the family-R
+// residual block's relu(BN(conv(.)) + x) in this one pass instead of an apply pass plus an
+// add+act pass.  grid (chunks, N): each thread owns one 8-channel chunk (its 8 scale/shift
+// pairs live in registers) and strides over the block's pixels.
 template <int ACT>
 __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict__ x, NormGeom g,
                                                          const float* __restrict__ mean,
@@ -258,7 +260,8 @@ __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict_
                                                          const float* __restrict__ gamma,
                                                          const float* __restrict__ beta,
                                                          const float* __restrict__ prelu_w,
-                                                         bf16* __restrict__ y, Fp8Shadow sh) {
+                                                         bf16* __restrict__ y, Fp8Shadow sh,
+                                                         const bf16* __restrict__ res) {
   const int n = blockIdx.y, cb = blockIdx.x;
   const int CP = g.C >> 3;
   const int RP = 256 / CP;
@@ -281,12 +284,14 @@ __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict_
   // optional fp8 shadow of y (the next conv's operand) written in the same pass
   const float qsc = sh.q ? fp8_shadow_scale(sh) : 0.f;
   float qmax = 0.f;
-  auto one = [&](u32x4 v, long off) {
-    float f[8];
+  auto one = [&](u32x4 v, u32x4 rv, long off) {
+    float f[8], r8[8];
     unpack8(v, f);
+    if (res) unpack8(rv, r8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float t = f[j] * sc[j] + sf[j];
+      if (res) t += r8[j];
       if constexpr (ACT == ACT_PRELU_T) t = t > 0.f ? t : pw * t;
       else t = act_fwd(t, ACT);
       f[j] = t;
@@ -301,15 +306,21 @@ __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict_
       *reinterpret_cast<uint2*>(sh.q + off) = fp8_pack8(r, qsc, sh.fmt);
     }
   };
+  const u32x4 zero4 = {0u, 0u, 0u, 0u};   // +0.0 bf16 x 8
   int p = p0 + tr;
   for (; p + 3 * RP < p1; p += 4 * RP) {
-    u32x4 v[4];
+    u32x4 v[4], rv[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = ld_stream(x + base + (long)(p + u * RP) * g.C, g.nt);
+    for (int u = 0; u < 4; ++u) {
+      v[u] = ld_stream(x + base + (long)(p + u * RP) * g.C, g.nt);
+      rv[u] = res ? ld_stream(res + base + (long)(p + u * RP) * g.C, g.nt) : zero4;
+    }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) one(v[u], base + (long)(p + u * RP) * g.C);
+    for (int u = 0; u < 4; ++u) one(v[u], rv[u], base + (long)(p + u * RP) * g.C);
   }
-  for (; p < p1; p += RP) one(ld_stream(x + base + (long)p * g.C, g.nt), base + (long)p * g.C);
+  for (; p < p1; p += RP)
+    one(ld_stream(x + base + (long)p * g.C, g.nt), res ? ld_stream(res + base + (long)p * g.C, g.nt) : zero4,
+        base + (long)p * g.C);
   if (sh.q) fp8_amax_commit(qmax, sh.site);
 }
 
@@ -624,7 +635,7 @@ long p2p_norm_ws_floats(int N, int HW, int C) {
 int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* gamma,
                  const float* beta, const float* prelu_w, int act, float* mean, float* rstd,
                  float* run_mean, float* run_var, float momentum, float* ws, void* y,
-                 void* q, int* qsite, int qfmt, hipStream_t st) {
+                 void* q, int* qsite, int qfmt, const void* res, hipStream_t st) {
   using namespace p2p;
   NormGeom g = make_geom(N, HW, C);
   hipLaunchKernelGGL(norm_partial_kernel, dim3(g.nchunks, N), dim3(256), 0, st,
@@ -634,7 +645,7 @@ int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* ga
     with_act(prelu_w ? ACT_PRELU_T : act, [&](auto t) {
       hipLaunchKernelGGL((norm_apply_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st,
                          static_cast<const bf16*>(x), g, mean, rstd, gamma, beta, prelu_w, static_cast<bf16*>(y),
-                         Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
+                         Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt}, static_cast<const bf16*>(res));
     });
   return (int)hipGetLastError();
 }
@@ -645,7 +656,8 @@ int p2p_norm_fwd(const void* x, int N, int HW, int C, float eps, const float* ga
 int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, const float* partials,
                           float eps, const float* gamma, const float* beta, const float* prelu_w,
                           int act, float* mean, float* rstd, float* run_mean, float* run_var,
-                          float momentum, void* y, void* q, int* qsite, int qfmt, hipStream_t st) {
+                          float momentum, void* y, void* q, int* qsite, int qfmt, const void* res,
+                          hipStream_t st) {
   using namespace p2p;
   if (nchunks <= 0 || HW % nchunks) return -1;
   NormGeom pg;
@@ -660,7 +672,7 @@ int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, cons
   with_act(prelu_w ? ACT_PRELU_T : act, [&](auto t) {
     hipLaunchKernelGGL((norm_apply_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st,
                        static_cast<const bf16*>(x), g, mean, rstd, gamma, beta, prelu_w, static_cast<bf16*>(y),
-                       Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
+                       Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt}, static_cast<const bf16*>(res));
   });
   return (int)hipGetLastError();
 }
@@ -668,13 +680,13 @@ int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, cons
 // apply only (eval-mode BN with running stats: host passes mean/rstd computed from them)
 int p2p_norm_apply(const void* x, int N, int HW, int C, const float* mean, const float* rstd,
                    const float* gamma, const float* beta, const float* prelu_w, int act, void* y,
-                   hipStream_t st) {
+                   const void* res, hipStream_t st) {
   using namespace p2p;
   NormGeom g = make_geom(N, HW, C);
   with_act(prelu_w ? ACT_PRELU_T : act, [&](auto t) {
     hipLaunchKernelGGL((norm_apply_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st,
                        static_cast<const bf16*>(x), g, mean, rstd, gamma, beta, prelu_w, static_cast<bf16*>(y),
-                       Fp8Shadow{nullptr, nullptr, 0});
+                       Fp8Shadow{nullptr, nullptr, 0}, static_cast<const bf16*>(res));
   });
   return (int)hipGetLastError();
 }

@@ -243,6 +243,11 @@ class CompressGANStep:
                 self.reducer_c.finish()
             self._opt_step(self.opt_c, self.reducer_c, loss_c)
         elif self.c_phase_backward:
+            if self.reducer_g is None and os.environ.get("P2P_CPHASE_ASSIGN", "1") != "0":
+                # G's grads are dead from here (zeroed before the next G backward): let this
+                # backward assign them instead of adding onto the G-phase values (one aten
+                # add per G parameter saved; the backward's own work is unchanged)
+                self.opt_g.zero_grad(set_to_none=True)
             with paused_g:      # reference: grads land on G (zeroed next step) -- no effect
                 loss_c.backward()
             self._no_deferred(real_a)

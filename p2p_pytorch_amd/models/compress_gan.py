@@ -32,6 +32,8 @@ from .layers import BatchNorm2d, Conv2d, link_norm
 _FEAT_DEFER = os.environ.get("P2P_FEAT_DEFER", "1") != "0"
 # P2P_FAMR_STATS=0: the BNs compute their own statistics (A/B knob for the conv-epilogue stats)
 _FUSED_STATS = os.environ.get("P2P_FAMR_STATS", "1") != "0"
+# P2P_RES_FUSE=0: the residual join relu(BN(h) + x) as a separate add+act pass (A/B knob)
+_RES_FUSE = os.environ.get("P2P_RES_FUSE", "1") != "0"
 
 
 def ops_hip():
@@ -113,8 +115,11 @@ class ResidualBlock(nn.Module):
             link_norm(self.conv2.conv2d, self.in2)
 
     def forward(self, x):
-        out = self.in2(self.conv2(self.in1(self.conv1(x))))
-        return ops.add_act(out, x, "relu", defer_b=True)
+        h = self.conv2(self.in1(self.conv1(x)))
+        if _RES_FUSE:
+            # relu(BN(h) + x) in the BN apply pass; x's gradient goes to conv1's dgrad epilogue
+            return self.in2(h, residual=x, act="relu", defer_residual=True)
+        return ops.add_act(self.in2(h), x, "relu", defer_b=True)
 
 
 class ExpandNetwork(nn.Module):

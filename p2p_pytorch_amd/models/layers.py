@@ -126,8 +126,10 @@ class BatchNorm2d(nn.BatchNorm2d):
         super().__init__(num_features, eps=eps, momentum=momentum, affine=affine)
         self.act = act
 
-    def forward(self, x, prelu=None):
-        """``prelu``: slope Parameter of a following shared-slope PReLU, fused in."""
+    def forward(self, x, prelu=None, residual=None, act=None, defer_residual=False):
+        """``prelu``: slope Parameter of a following shared-slope PReLU, fused in.
+        ``residual`` / ``act``: y = act(BN(x) + residual) in the same apply pass (overrides the
+        module's own act); ``defer_residual``: see ``ops.batch_norm``."""
         training = self.training or not self.track_running_stats
         if self.training and self.track_running_stats:
             if self.num_batches_tracked.is_cuda and _native.use_native(x):
@@ -136,8 +138,10 @@ class BatchNorm2d(nn.BatchNorm2d):
                 self.num_batches_tracked.add_(1)
         return ops.batch_norm(x, self.running_mean if self.track_running_stats else None,
                               self.running_var if self.track_running_stats else None,
-                              self.weight, self.bias, training, self.momentum, self.eps, self.act,
-                              qkey=id(self), prelu_weight=prelu)
+                              self.weight, self.bias, training, self.momentum, self.eps,
+                              self.act if residual is None else act,
+                              qkey=id(self), prelu_weight=prelu, residual=residual,
+                              defer_residual=defer_residual)
 
 
 class Act(nn.Module):

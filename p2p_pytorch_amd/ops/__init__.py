@@ -54,12 +54,18 @@ def instance_norm(x, eps=1e-5, act=None, weight=None, bias=None, qkey=None):
 
 
 def batch_norm(x, running_mean, running_var, weight, bias, training, momentum=0.1, eps=1e-5,
-               act=None, qkey=None, prelu_weight=None):
+               act=None, qkey=None, prelu_weight=None, residual=None, defer_residual=False):
     """``prelu_weight``: a shared-slope PReLU applied to the output (fused into the apply pass
-    and, in the backward, into the norm's partial-sum pass -- slope gradient included)."""
+    and, in the backward, into the norm's partial-sum pass -- slope gradient included).
+    ``residual``: y = act(BN(x) + residual) in the apply pass (a residual block's join);
+    ``defer_residual`` (HIP path): residual's gradient goes to the conv that also reads it."""
     if _native.use_native(x):
         return _hip().batch_norm(x, running_mean, running_var, weight, bias, training, momentum,
-                                 eps, act, prelu_weight=prelu_weight, qkey=qkey)
+                                 eps, act, prelu_weight=prelu_weight, qkey=qkey,
+                                 residual=residual, defer_residual=defer_residual)
+    if residual is not None:
+        y = ref.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+        return ref.apply_act(y + residual, act)
     y = ref.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps, act)
     return y if prelu_weight is None else ref.prelu(y, prelu_weight)
 

@@ -1121,8 +1121,19 @@ def spectral_sigma(w2, u, v, iters=1):
 class NormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, prelu_w, run_mean, run_var, eps, momentum, act, batch,
-                training, qkey=None):
+                training, qkey=None, res=None, defer_res=False):
+        """``res``: residual added before ``act`` in the apply pass, y = act(norm(x) + res) (the
+        family-R residual join; ReLU / LeakyReLU only).  Its gradient is act'(y) * dy, parked
+        for the conv that also reads ``res`` when ``defer_res`` (``skip_grad="take"``)."""
         x = to_nhwc_bf16(x)
+        ctx.res_key = None
+        ctx.has_res = res is not None
+        if res is not None:
+            if prelu_w is not None or act not in ("relu", "lrelu"):
+                raise ValueError("norm with residual: ReLU / LeakyReLU only, no PReLU")
+            if defer_res and res.dtype == torch.bfloat16 and res.is_contiguous(memory_format=CL):
+                ctx.res_key = res.data_ptr()   # the storage the consuming conv reads
+            res = to_nhwc_bf16(res)
         g = gamma.detach().float().contiguous() if gamma is not None else None
         b = beta.detach().float().contiguous() if beta is not None else None
         pw = prelu_w.detach().float().contiguous() if prelu_w is not None else None
@@ -1140,7 +1151,7 @@ class NormFn(torch.autograd.Function):
                     qargs = (ysite, qy, _f8.E4M3)
             y, mean, rstd = P().norm_fwd(x, eps, g, b, pw, _act_code(act),
                                          run_mean if batch else None, run_var if batch else None,
-                                         momentum, batch, _take_stats(x), *qargs)
+                                         momentum, batch, _take_stats(x), *qargs, res=res)
             if qy is not None:
                 _f8.stash_shadow(y, qy, ysite)
             elif fresh:
@@ -1148,11 +1159,14 @@ class NormFn(torch.autograd.Function):
         else:
             mean = run_mean.float().view(1, -1)
             rstd = torch.rsqrt(run_var.float() + eps).view(1, -1)
-            y = P().norm_apply(x, mean, rstd, g, b, pw, _act_code(act), True)
+            y = P().norm_apply(x, mean, rstd, g, b, pw, _act_code(act), True, res=res)
         ctx.cfg = (eps, act, batch, training)
-        if training and pw is None and act in (None, "none", "relu", "lrelu") and _NB_FUSE:
+        if (training and pw is None and act in (None, "none", "relu", "lrelu") and _NB_FUSE
+                and res is None):
             _register_norm_out(y, (x, mean, rstd, g, b, _act_code(act), bool(batch)))
-        keep_y = act not in (None, "none") and (act not in ("relu", "lrelu") or not training)
+        # the gate of a post-residual activation needs y (not recomputable from x alone)
+        keep_y = act not in (None, "none") and (act not in ("relu", "lrelu") or not training
+                                                or res is not None)
         ctx.save_for_backward(x, mean, rstd, gamma, beta, prelu_w, y if keep_y else None)
         return y
 
@@ -1161,6 +1175,17 @@ class NormFn(torch.autograd.Function):
         x, mean, rstd, gamma, beta, prelu_w, y = ctx.saved_tensors
         eps, act, batch, training = ctx.cfg
         gy = to_nhwc_bf16(gy)
+        gres = None
+        if ctx.has_res:
+            # y = act(z + res): one gated gradient for both z (the norm) and res
+            gy = P().act(gy, y, _act_code(act), 2)
+            act = None
+            if ctx.res_key is not None and ctx.needs_input_grad[12]:
+                if ctx.res_key in _DEFERRED:
+                    raise RuntimeError("skip_grad: a deferred gradient of this tensor is pending")
+                _DEFERRED[ctx.res_key] = gy
+            elif ctx.needs_input_grad[12]:
+                gres = gy
         gpw = None
         fused_act = 0
         pw = None
@@ -1186,7 +1211,7 @@ class NormFn(torch.autograd.Function):
             # dx = rstd * gamma * dz (no mean terms) and the parameter / slope gradients
             dx = P().norm_bwd(x, gy, mean, rstd, g, b, fused_act, dg, db, need_x, True, None,
                               prelu_w=pw, dprelu=gpw, frozen=True)
-            return (dx if need_x else None), dg, db, gpw, None, None, None, None, None, None, None, None
+            return (dx if need_x else None), dg, db, gpw, None, None, None, None, None, None, None, None, gres, None
         dsum = torch.empty(x.shape[1], device=x.device, dtype=torch.float32) if need_x else None
         qargs, qd, dsite, fresh = (), None, None, False
         if ctx.qkey is not None and need_x:
@@ -1213,7 +1238,7 @@ class NormFn(torch.autograd.Function):
                 _f8.stash_shadow(dx, qd, dsite)
             elif fresh:
                 _f8.bootstrap_shadow(dx, (ctx.qkey, "dx"), _f8.E5M2)
-        return (dx if need_x else None), dg, db, gpw, None, None, None, None, None, None, None, None
+        return (dx if need_x else None), dg, db, gpw, None, None, None, None, None, None, None, None, gres, None
 
 
 class _PadCFn(torch.autograd.Function):
@@ -1277,9 +1302,14 @@ def instance_norm(x, eps=1e-5, act=None, weight=None, bias=None, qkey=None):
 
 
 def batch_norm(x, running_mean, running_var, weight, bias, training, momentum=0.1, eps=1e-5,
-               act=None, prelu_weight=None, qkey=None):
+               act=None, prelu_weight=None, qkey=None, residual=None, defer_residual=False):
     if not training and running_mean is None:
         training = True
+    if residual is not None:
+        if x.shape[1] % 8:
+            raise ValueError("batch_norm with residual: channels must be a multiple of 8")
+        return NormFn.apply(x, weight, bias, None, running_mean, running_var, eps, momentum, act,
+                            True, training, qkey, residual, defer_residual)
     return _norm_any_c(x, weight, bias, prelu_weight, running_mean, running_var, eps, momentum,
                        act, True, training, qkey)
 

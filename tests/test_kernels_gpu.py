@@ -408,6 +408,46 @@ def test_batch_norm_eval_backward(act):
         assert rel_err(hw.grad, rw.grad) < 1e-2
 
 
+@pytest.mark.parametrize("act,training", [("relu", True), ("lrelu", True), ("relu", False)])
+def test_batch_norm_residual_join(act, training):
+    """y = act(BN(x) + r) in the BN apply pass (family-R residual join): output, dx, dr,
+    d(gamma), d(beta) and the running statistics vs fp32 F.batch_norm + add + act; the
+    deferred form parks dr for the conv reading r (skip_grad="take"), which adds it."""
+    from p2p_pytorch_amd.ops import hip
+    N, C, H = 4, 128, 16
+    x = bf(torch.randn(N, C, H, H, device=DEV) * 2 + 0.3)
+    r = bf(torch.randn(N, C, H, H, device=DEV))
+    g = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV) * 0.3
+    rm, rv = torch.randn(C, device=DEV) * 0.2, torch.rand(C, device=DEV) + 0.5
+    gy = rand_img(N, C, H, H, seed=51)
+    hx, hr, hg, hb = _leaf(x), _leaf(r), _leaf(g), _leaf(b)
+    hrm, hrv = rm.clone(), rv.clone()
+    y = ops.batch_norm(hx, hrm, hrv, hg, hb, training, 0.1, 1e-5, act=act, residual=hr)
+    y.backward(gy)
+    rx, rr, rg, rb = _leaf(x.float()), _leaf(r.float()), _leaf(g), _leaf(b)
+    rrm, rrv = rm.clone(), rv.clone()
+    z = F.batch_norm(rx, rrm, rrv, rg, rb, training, 0.1, 1e-5) + rr
+    ry = F.relu(z) if act == "relu" else F.leaky_relu(z, 0.2)
+    ry.backward(gy.float())
+    assert rel_err(y, ry) < 2e-2
+    assert rel_err(hx.grad, rx.grad) < 3e-2
+    assert rel_err(hr.grad, rr.grad) < 1e-2
+    assert rel_err(hg.grad, rg.grad) < 2e-2 and rel_err(hb.grad, rb.grad) < 2e-2
+    if training:
+        assert rel_err(hrm, rrm) < 1e-3 and rel_err(hrv, rrv) < 1e-3
+    # deferred: the residual's gradient is parked under r's storage for its other consumer
+    hx2, hr2 = _leaf(x), _leaf(r)
+    y2 = ops.batch_norm(hx2, rm.clone(), rv.clone(), g, b, training, 0.1, 1e-5, act=act,
+                        residual=hr2, defer_residual=True)
+    y2.backward(gy)
+    assert hr2.grad is None
+    parked = hip._DEFERRED.pop(hr2.data_ptr())
+    hip.assert_no_deferred()
+    assert torch.equal(parked, hr.grad)
+    assert torch.equal(hx2.grad, hx.grad)
+
+
 @pytest.mark.parametrize("C", [32, 64, 3])
 def test_batch_norm_fused_prelu(C):
     """BN + shared-slope PReLU in one apply pass; backward gate and slope gradient reduced in
