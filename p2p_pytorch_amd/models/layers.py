@@ -11,6 +11,7 @@ import torch
 import torch.nn as nn
 
 from .. import _native, ops
+from ..ops.fp8 import obj_key as _f8_key
 
 
 class Conv2d(nn.Conv2d):
@@ -116,7 +117,7 @@ class InstanceNorm2d(nn.Module):
             self.register_parameter("bias", None)
 
     def forward(self, x):
-        return ops.instance_norm(x, self.eps, self.act, self.weight, self.bias, qkey=id(self))
+        return ops.instance_norm(x, self.eps, self.act, self.weight, self.bias, qkey=_f8_key(self))
 
 
 class BatchNorm2d(nn.BatchNorm2d):
@@ -140,7 +141,7 @@ class BatchNorm2d(nn.BatchNorm2d):
                               self.running_var if self.track_running_stats else None,
                               self.weight, self.bias, training, self.momentum, self.eps,
                               self.act if residual is None else act,
-                              qkey=id(self), prelu_weight=prelu, residual=residual,
+                              qkey=_f8_key(self), prelu_weight=prelu, residual=residual,
                               defer_residual=defer_residual)
 
 

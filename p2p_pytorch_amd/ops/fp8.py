@@ -24,11 +24,17 @@ two halves of a U-Net skip concat keep independent scales.  Scales live on the d
 * weights: *current* scaling -- exact amax of this step's weight image, then the cast.
 
 Sites are keyed by (consumer weight, operand role), so they are stable across steps and the
-whole step stays capturable in one hipGraph (no host sync anywhere).
+whole step stays capturable in one hipGraph (no host sync anywhere).  The object part of a key
+is ``obj_key(obj)``, never ``id(obj)``: ids are recycled once an object dies, and a new weight
+that inherited a dead one's amax window quantised its first steps with a foreign scale (the
+fp8 chain test saw 8-190x gradient errors after other tests' weights died).  A dead object's
+sites return to the pool (reset before reuse).
 """
 from __future__ import annotations
 
+import itertools
 import os
+import weakref
 
 import torch
 
@@ -63,16 +69,56 @@ class _Pool:
         self.sites = torch.zeros(_POOL_SITES, 4, dtype=torch.int32, device=device)
         self.index: dict = {}
         self.fresh: set = set()
+        self.free: list = []     # rows of released keys (reset when handed out again)
+        self.high = 0            # rows ever used: [0, high) is what the per-step roll covers
 
     def site(self, key):
         i = self.index.get(key)
         if i is None:
-            i = len(self.index)
-            if i >= _POOL_SITES:
-                raise RuntimeError("fp8: scale-site pool exhausted")
+            if self.free:
+                i = self.free.pop()
+                self.sites[i].zero_()    # no amax window inherited from the previous owner
+            else:
+                i = self.high
+                if i >= _POOL_SITES:
+                    raise RuntimeError("fp8: scale-site pool exhausted")
+                self.high += 1
             self.index[key] = i
             self.fresh.add(i)
         return i
+
+    def release(self, okey):
+        """Drop every site keyed by object key ``okey`` (alone or as a tuple's head)."""
+        dead = [k for k in self.index
+                if k == okey or (isinstance(k, tuple) and k and k[0] == okey)]
+        for k in dead:
+            i = self.index.pop(k)
+            self.fresh.discard(i)
+            self.free.append(i)
+
+
+# object -> key: id(obj) maps to (weakref, key); a recycled id with a dead weakref gets a new key
+_obj_keys: dict = {}
+_key_counter = itertools.count(1)
+
+
+def obj_key(obj):
+    """Process-unique scale-site key of a live object (weight tensor / norm module)."""
+    ent = _obj_keys.get(id(obj))
+    if ent is not None and ent[0]() is obj:
+        return ent[1]
+    k = ("obj", next(_key_counter))
+    oid = id(obj)
+
+    def _dead(_ref, oid=oid, k=k):
+        cur = _obj_keys.get(oid)
+        if cur is not None and cur[1] == k:
+            del _obj_keys[oid]
+        for pools in (_pools, _wpools):
+            for p in pools.values():
+                p.release(k)
+    _obj_keys[oid] = (weakref.ref(obj, _dead), k)
+    return k
 
 
 _pools: dict = {}
@@ -147,7 +193,7 @@ def begin_step() -> None:
     P = _native.ops()
     for p in _pools.values():
         if p.index:
-            P.fp8_roll(p.sites[: len(p.index)])
+            P.fp8_roll(p.sites[: p.high])
 
 
 def quant(x: torch.Tensor, key, fmt: int) -> tuple[torch.Tensor, torch.Tensor]:
@@ -194,8 +240,8 @@ def prepare_weight_pairs(ws, xa, xb):
         return []
     P = _native.ops()
     wp = wpool(ws[0].device)
-    idx = [wp.site(id(w)) for w in ws]
-    wp.sites[: len(wp.index), 0].zero_()
+    idx = [wp.site(obj_key(w)) for w in ws]
+    wp.sites[: wp.high, 0].zero_()
     P.fp8_amax_multi(list(ws), wp.sites, idx)
     imgs = P.weight_prep_pairs(list(ws), list(xa), list(xb), wp.sites, idx)
     return [(imgs[2 * j], imgs[2 * j + 1], wp.sites[i]) for j, i in enumerate(idx)]

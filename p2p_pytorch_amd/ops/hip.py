@@ -291,7 +291,7 @@ def _weight_image_fp8(w: torch.Tensor, swap: int, xp: int, yp: int):
     if ent is not None and ent[0] == ver and ent[1] == _gen[0]:
         return ent[2]
     img = _weight_image(w, swap, xp, yp)
-    out = _f8.quant_weight(img, (id(w), "w", swap))
+    out = _f8.quant_weight(img, (_f8.obj_key(w), "w", swap))
     w._p2p_cache[key] = (ver, _gen[0], out)
     return out
 
@@ -322,7 +322,7 @@ def _conv_call(x1, x2, wimg, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, 
         if y_qkey is not None:
             ysite, fresh = _f8.producer_site(x1.device, y_qkey)
             yq = (None, 0) if fresh else (ysite, _f8.E4M3)
-        k = id(weight)
+        k = _f8.obj_key(weight)
         a1, s1 = _f8.quant(x1, (k, role, 1), fmt)
         a2, s2 = _f8.quant(x2, (k, role, 2), fmt) if x2 is not None else (None, None)
         return P().conv_fwd(a1, a2, w8, bias, mode, KH, KW, s, p, reflect, up, act_in, OH, OW, Cout,
@@ -562,7 +562,7 @@ class ConvFn(torch.autograd.Function):
         y_qkey = None
         if (_f8.enabled() and not cfg.stats and Coutp == Cout and Cout % 32 == 0
                 and cfg.act_out in ("relu", "lrelu")):
-            y_qkey = (id(weight), "y")
+            y_qkey = (_f8.obj_key(weight), "y")
         outs = _conv_call(q1, q2, None, _bias_padded(bias, Coutp), mode, KH, KW, s, p,
                           int(cfg.reflect), cfg.up, _act_code(cfg.act_in), OH, OW, Coutp,
                           _act_code(cfg.act_out), Coutp, None, None, 0, Cout, want,
@@ -726,7 +726,7 @@ def _wgrad_fp8(cfg, weight, q1, q2, gyp, act_in):
     if not (_f8.conv_ok(C1, C2, Cout, act_in) and C1 % 16 == 0 and C2 % 16 == 0 and Cout % 64 == 0
             and (C1 + C2) % 64 == 0 and C1 + C2 >= 64):
         return None
-    k = id(weight)
+    k = _f8.obj_key(weight)
     x1q, sx = _f8.quant(q1, (k, "x", 1), _f8.E4M3)
     x2q = sx2 = None
     if q2 is not None:     # the concat halves keep their own scales (per-fragment exponents)
