@@ -138,7 +138,7 @@ def test_fp8_conv_fwd_dgrad_match_dequantised_oracle(case):
         assert any(want in k for k in names), (want, sorted(set(names)))
 
     # the fp8 operands exactly as the kernels saw them
-    kk = id(w)
+    kk = f8.obj_key(w)
     pool = f8._pool(torch.device(DEV, torch.cuda.current_device()))
     sx1 = pool.sites[pool.index[(kk, "x", 1)]]
     q1 = next(q for (x_, q) in f8._qcache.values() if x_.data_ptr() == xin1.data_ptr())
