@@ -25,6 +25,14 @@ static bool env_flag(const char* name, bool dflt) {
   return v ? v[0] != '0' : dflt;
 }
 
+// fp8 layers the stride-2 halo kernel takes (P2P_S2T_F8, read per call): bit 0 the e4m3
+// ConvT forward, bit 1 the e5m2 input gradient (extended epilogue)
+static int s2t_f8_mask() {
+  constexpr int kDefault = 3;
+  const char* v = std::getenv("P2P_S2T_F8");
+  return v ? std::atoi(v) & 3 : kDefault;
+}
+
 extern "C" {
 long p2p_sn_ws_floats(int h, int wd);
 int p2p_sn_power_iter(const float* W, int h, int wd, float* u, float* v, float* sigma, float* ws,
@@ -426,7 +434,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                       C1 + C2 >= s2t_chc && C1 + C2 <= 256 &&
                       (act_in == 0 || (act_in == 1 && act_bwd == 0 && !res)) && act_out <= 2 &&
                       (fp8 != 2 || act_in == 0) && (fp8 != 1 || (!act_bwd && !res)) &&
-                      std::getenv("P2P_NO_S2T") == nullptr;
+                      (!fp8 || (s2t_f8_mask() & (int)fp8)) && std::getenv("P2P_NO_S2T") == nullptr;
   if (s2t_ok) bm = 128;
   Tensor ws;
   if (splits > 1) {

@@ -41,20 +41,17 @@ __device__ __forceinline__ int unit_of(int hy, int hx) { return (hy * 2 + (hx & 
 
 }  // namespace
 
-// TN = 8 (128 channels) keeps 128 accumulators + 8 weight fragments live: one block per CU
-// (512-register budget; at two blocks per CU it spills); TN = 4 runs two blocks per CU.
+// TN = 8 (128 channels) keeps 128 accumulators + 8 B fragments live: one block per CU
+// (512-register budget, no spill); TN = 4 runs two blocks per CU
 // QS: also write the e4m3 / e5m2 shadow of the output (fp8 precision: the next conv's operand)
-//
-// Round 4: the MFMA operands are swapped (weight = src A, halo pixels = src B), so a lane's
-// accumulator holds 4 CONSECUTIVE output channels of one output pixel and the epilogue runs
-// from registers -- bf16 conversion, all of the tile's ReLU-gate loads in flight at once,
-// 8-byte stores -- instead of four 32-channel pieces staged through LDS behind barriers, each
-// one HBM round trip (the GATE variant, the generator head's input gradient, ran at 3 TB/s).
 template <int TN, int ACT, bool GATE, bool QS = false>
 __global__ void __launch_bounds__(256, TN >= 8 ? 1 : 2) halo_pk8_kernel(HaloPk8Args a) {
   float qsc = 0.f, qmax = 0.f;
   if constexpr (QS) qsc = fp8_shadow_scale(Fp8Shadow{a.q, a.q_site, a.q_fmt});
   constexpr int NC = TN * 16;              // output channels of the block (== Cout)
+  constexpr int PC = 32;                   // channels per epilogue piece
+  constexpr int LDC = PC + 8;              // staging row (80 B: 16-B aligned, spread banks)
+  static_assert(256 * LDC * 2 <= SUNITS * 16, "epilogue piece fits in one halo stage");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* As = reinterpret_cast<bf16*>(smem);                               // 2 x SUNITS units
   bf16* Bs = As + 2 * SUNITS * 8;                                         // NC x 16 units
@@ -92,18 +89,15 @@ __global__ void __launch_bounds__(256, TN >= 8 ? 1 : 2) halo_pk8_kernel(HaloPk8A
     int n, oy0, ox0;
     origin(k, n, oy0, ox0);
     bf16* dst = As + stage * SUNITS * 8;
-    // laundered: the per-lane unit geometry must not be hoisted into (spilled) registers
-    int w = wid;
-    asm volatile("" : "+v"(w));
 #pragma unroll
     for (int j = 0; j < NLD; ++j) {
       const int iy = 2 * oy0 - 1 + hy[j], ix = 2 * ox0 - 1 + hx[j];
       const bool inb = (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
-      glds16(inb ? a.x + ((long)(n * a.Hi + iy) * a.Wi + ix) * 8 : a.zero, dst + (j * 4 + w) * 64 * 8);
+      glds16(inb ? a.x + ((long)(n * a.Hi + iy) * a.Wi + ix) * 8 : a.zero, dst + (j * 4 + wid) * 64 * 8);
     }
   };
 
-  const int px = lane & 15, kq = lane >> 4, g = lane >> 4;
+  const int px = lane & 15, kq = lane >> 4;
   issue(0, 0);
   for (int k = 0; k < my_tiles; ++k) {
     const int stage = k & 1;
@@ -116,11 +110,6 @@ __global__ void __launch_bounds__(256, TN >= 8 ? 1 : 2) halo_pk8_kernel(HaloPk8A
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     bf16* A = As + stage * SUNITS * 8;
-    // the resident weight's fragments are the same for every tile: hoisted out of the tile
-    // loop they would pin 16 taps x TN fragments of registers (and spill at two blocks per
-    // CU) -- a per-tile laundered base keeps them per k-step LDS reads
-    const bf16* Bt = Bs;
-    asm volatile("" : "+v"(Bt));
     f32x4 acc[4][TN];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -133,105 +122,88 @@ __global__ void __launch_bounds__(256, TN >= 8 ? 1 : 2) halo_pk8_kernel(HaloPk8A
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = j * 16 + px;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bt + (n * 16 + (tap ^ (n & 15))) * 8);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (n * 16 + (tap ^ (n & 15))) * 8);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int py = wid * 4 + i;
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(A + unit_of(2 * py + ty, 2 * px + tx) * 8);
 #pragma unroll
-        for (int j = 0; j < TN; ++j)   // weights = src A (rows = channels), pixels = src B
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af, acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
       }
-      // one k-step's fragments live at a time (TN = 8: 128 accumulators + 48 fragment registers)
-      __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();     // every wave done with this stage: the next tile's lands here
-
-    // ---- register epilogue: acc[i][j][r] = channel 16 j + 4 g + r of output pixel
-    // (oy0 + 4 wid + i, ox0 + px)
+    __builtin_amdgcn_s_barrier();     // every wave done with this stage: it hosts the staging tile
+    // ---- epilogue, 32 channels at a time: bias + act staged as bf16 in this stage's LDS,
+    // then 16-B stores (the ReLU-gate inputs of a piece are loaded before any is used)
     int n, oy0, ox0;
     origin(k, n, oy0, ox0);
-    const int ox = ox0 + px;
-    uint2 v[4][TN];
+    bf16* Cs = A;
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      float bj[4];
+    for (int piece = 0; piece < NC / PC; ++piece) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bj[r] = a.bias ? a.bias[j * 16 + 4 * g + r] : 0.f;
+      for (int j = piece * 2; j < piece * 2 + 2; ++j) {
+        const int col = j * 16 + px;
+        const float bj = a.bias ? a.bias[col] : 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float f[4];
+        for (int i = 0; i < 4; ++i) {
+          const int rowb = wid * 64 + i * 16 + kq * 4;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) f[r] = act_fwd(acc[i][j][r] + bj[r], ACT);
-        const bf16 b0 = (bf16)f[0], b1 = (bf16)f[1], b2 = (bf16)f[2], b3 = (bf16)f[3];
-        v[i][j] = uint2{(uint32_t)__builtin_bit_cast(uint16_t, b0) | ((uint32_t)__builtin_bit_cast(uint16_t, b1) << 16),
-                        (uint32_t)__builtin_bit_cast(uint16_t, b2) | ((uint32_t)__builtin_bit_cast(uint16_t, b3) << 16)};
-      }
-    }
-    long pix[4];
-    bool ok[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int oy = oy0 + wid * 4 + i;
-      ok[i] = oy < a.Ho && ox < a.Wo;
-      pix[i] = ((long)n * a.Ho + (ok[i] ? oy : 0)) * a.Wo + (ok[i] ? ox : 0);
-    }
-    if constexpr (GATE) {
-      // ReLU' of the layer's input (dgrad of a ReLU-input conv): the gate loads of up to 4
-      // channel columns (16 loads of 8 B per lane) in flight at once
-      constexpr int JG = TN < 4 ? TN : 4;
-#pragma unroll
-      for (int j0 = 0; j0 < TN; j0 += JG) {
-        uint2 xv[4][JG];
-#pragma unroll
-        for (int jj = 0; jj < JG; ++jj) {
-          const int co = (j0 + jj) * 16 + 4 * g;
-          const bool first = co < a.Csplit;        // a 16-channel column never straddles the split
-          const int ld = first ? a.Csplit : NC - a.Csplit;
-          const bf16* xb = first ? a.xb1 : a.xb2;
-          const int cof = first ? co : co - a.Csplit;
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            xv[i][jj] = (xb && ok[i]) ? *reinterpret_cast<const uint2*>(xb + pix[i] * ld + cof)
-                                      : uint2{0x3f803f80u, 0x3f803f80u};
+          for (int r = 0; r < 4; ++r)
+            Cs[(rowb + r) * LDC + (col - piece * PC)] = (bf16)act_fwd(acc[i][j][r] + bj, ACT);
         }
-#pragma unroll
-        for (int jj = 0; jj < JG; ++jj)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t x0 = xv[i][jj].x, x1 = xv[i][jj].y;
-            uint2& w = v[i][j0 + jj];
-            w.x &= (((int16_t)(x0 & 0xffffu) > 0) ? 0xffffu : 0u) | (((int16_t)(x0 >> 16) > 0) ? 0xffff0000u : 0u);
-            w.y &= (((int16_t)(x1 & 0xffffu) > 0) ? 0xffffu : 0u) | (((int16_t)(x1 >> 16) > 0) ? 0xffff0000u : 0u);
-          }
       }
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int co = j * 16 + 4 * g;
-      const bool first = co < a.Csplit;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      const int co0 = piece * PC;
+      const bool first = co0 < a.Csplit;          // a piece never straddles the split (host)
       const int ld = first ? a.Csplit : NC - a.Csplit;
-      const int cof = first ? co : co - a.Csplit;
+      const int cof0 = first ? co0 : co0 - a.Csplit;
       bf16* yb = first ? a.y1 : a.y2;
+      const bf16* xb = first ? a.xb1 : a.xb2;
+      long pix[4];
+      bool ok[4];
+      u32x4 xv[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (!ok[i]) continue;
-        *reinterpret_cast<uint2*>(yb + pix[i] * ld + cof) = v[i][j];
-        if constexpr (QS) {   // host: unsplit output (ld == Cout)
-          const float fm = fp8_max(a.q_fmt);
-          float f[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const uint32_t w = r < 2 ? v[i][j].x : v[i][j].y;
-            f[r] = __uint_as_float((r & 1) ? (w & 0xffff0000u) : (w << 16));
-            qmax = fmaxf(qmax, fabsf(f[r]));
-            f[r] = fminf(fmaxf(f[r] * qsc, -fm), fm);
-          }
-          *reinterpret_cast<uint32_t*>(a.q + pix[i] * ld + cof) = cvt4(f[0], f[1], f[2], f[3], a.q_fmt);
+      for (int q = 0; q < 4; ++q) {               // 256 pixels x 4 chunks of 8 channels
+        const int it = tid + q * 256, row = it >> 2;
+        const int oy = oy0 + (row >> 4), ox = ox0 + (row & 15);
+        ok[q] = oy < a.Ho && ox < a.Wo;
+        pix[q] = ((long)n * a.Ho + (ok[q] ? oy : 0)) * a.Wo + (ok[q] ? ox : 0);
+        if constexpr (GATE) {
+          xv[q] = xb ? *reinterpret_cast<const u32x4*>(xb + pix[q] * ld + cof0 + (it & 3) * 8)
+                     : u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};
         }
       }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int it = tid + q * 256, row = it >> 2, cc = it & 3;
+        if (!ok[q]) continue;
+        u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * LDC + cc * 8);
+        if constexpr (GATE) {   // ReLU' of the layer's input (dgrad of a ReLU-input conv)
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const uint32_t xw = xv[q][w];
+            uint32_t keep = 0;
+            if ((int16_t)(xw & 0xffffu) > 0) keep |= 0xffffu;
+            if ((int16_t)(xw >> 16) > 0) keep |= 0xffff0000u;
+            v[w] &= keep;
+          }
+        }
+        *reinterpret_cast<u32x4*>(yb + pix[q] * ld + cof0 + cc * 8) = v;
+        if constexpr (QS) {   // host: unsplit output (ld == Cout)
+          const bf16x8 vb = __builtin_bit_cast(bf16x8, v);
+          float r[8];
+#pragma unroll
+          for (int w = 0; w < 8; ++w) {
+            r[w] = (float)vb[w];
+            qmax = fmaxf(qmax, fabsf(r[w]));
+          }
+          *reinterpret_cast<uint2*>(a.q + pix[q] * ld + cof0 + cc * 8) = fp8_pack8(r, qsc, a.q_fmt);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     }
   }
   if constexpr (QS) fp8_amax_commit(qmax, a.q_site);

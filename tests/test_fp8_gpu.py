@@ -22,6 +22,13 @@ DEV = "cuda"
 
 
 @pytest.fixture(autouse=True)
+def _s2t_f8_all(monkeypatch):
+    """Both fp8 halo-kernel variants routed (P2P_S2T_F8 bits, csrc/bindings.cpp): the tests
+    that assert the kernel ran keep covering it whatever the step's default routing is."""
+    monkeypatch.setenv("P2P_S2T_F8", "3")
+
+
+@pytest.fixture(autouse=True)
 def _fp8_mode():
     _native.set_backend("native")
     assert _native.load(), _native.load_error()
