@@ -28,7 +28,7 @@ static bool env_flag(const char* name, bool dflt) {
 // fp8 layers the stride-2 halo kernel takes (P2P_S2T_F8, read per call): bit 0 the e4m3
 // ConvT forward, bit 1 the e5m2 input gradient (extended epilogue)
 static int s2t_f8_mask() {
-  constexpr int kDefault = 3;
+  constexpr int kDefault = 1;   // input gradient off: B=256 fp8 8955 (both) vs 9087 (forward only), profiles/bench_fp8_r4fb.jsonl
   const char* v = std::getenv("P2P_S2T_F8");
   return v ? std::atoi(v) & 3 : kDefault;
 }
