@@ -14,6 +14,7 @@
 #include <torch/library.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -436,6 +437,11 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                       (fp8 != 2 || act_in == 0) && (fp8 != 1 || (!act_bwd && !res)) &&
                       (!fp8 || (s2t_f8_mask() & (int)fp8)) && std::getenv("P2P_NO_S2T") == nullptr;
   if (s2t_ok) bm = 128;
+  if (env_flag("P2P_ROUTE_LOG", false))   // routing trace (tools): one line per conv call
+    fprintf(stderr, "[route] mode %d N %ld C %ld+%ld %ldx%ld -> %ld %ldx%ld k%d s%d p%d act_in %d act_bwd %d res %d "
+            "fp8 %d splits %d s2t %d bm %d bn %d tiles %ld\n", (int)mode, (long)N, (long)C1, (long)C2, (long)H,
+            (long)W, (long)Cout, (long)OH, (long)OW, (int)KH, (int)stride, (int)pad, (int)act_in, (int)act_bwd,
+            res ? 1 : 0, (int)fp8, splits, (int)s2t_ok, (int)bm, (int)bn, (long)tiles);
   Tensor ws;
   if (splits > 1) {
     // per-split fp32 slabs (plain stores, no zero fill) summed in split order by

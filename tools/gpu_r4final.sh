@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-4 final: the full GPU suite, the benches (family R, headline B = 1024 / 256, fp8) and a
+# conv routing census of one eager B = 256 step.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/r4final
+mkdir -p $O
+fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1: stopping"; exit $1;; esac; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1; rc=$?
+echo "tests rc=$rc"; grep -E "passed|failed|FAILED|Error" $O/tests.log | tail -8; fatal $rc; [ $rc -eq 0 ] || exit $rc
+j() { python - "$1" <<'PY'
+import json, sys
+d = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")][-1]
+print(d["value"], d["ms_per_step"], d.get("max_mem_gib"))
+PY
+}
+run() { local tag=$1; shift; timeout -k 10 300 python bench.py "$@" > $O/$tag.json 2>> $O/err.log; local rc=$?; fatal $rc; [ $rc -eq 0 ] || { echo "$tag FAILED rc=$rc"; return 1; }; echo "$tag $(j $O/$tag.json)"; grep "^{" $O/$tag.json >> $O/all.jsonl; }
+run famR --family ref --batch 64 || exit 1
+run headline
+run headline_b256 --batch 256
+run fp8 --precision fp8
+P2P_ROUTE_LOG=1 timeout -k 10 300 python bench.py --batch 256 --steps 1 --warmup 1 --no_graph > $O/route.json 2> $O/route.err; rc=$?; fatal $rc
+grep "^\[route\] mode 1" $O/route.err | sort | uniq -c | sort -rn | head -40
+exit 0
