@@ -39,10 +39,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=1024,
-                   help="images per GPU, sized for the 288 GB HBM at the throughput knee: 256 / 512 / "
-                        "1024 measured 6841 / 7059 / 7116 img/s at 12.6 / 23.7 / 45.9 GiB "
-                        "(profiles/batch_sweep_r3.jsonl); the eager baseline's best batch was 128")
+    p.add_argument("--batch", type=int, default=None,
+                   help="images per GPU (default: 2048 for the pix2pix headline; 64 for --family ref, 256 "
+                        "for --mode infer, 128 for --impl torch), sized for the 288 GB HBM: pix2pix 1024 / 1536 / 2048 measured "
+                        "7387 / 7400 / 7444 img/s at 50.8 / 75.3 / 99.8 GiB (profiles/batch_sweep_r4.jsonl; "
+                        "fp8 9951 / 10139 at 1024 / 2048); the eager baseline's best batch was 128")
     p.add_argument("--size", type=int, default=256)
     p.add_argument("--family", default="pix2pix", choices=["pix2pix", "ref"],
                    help="pix2pix: the headline U-Net + PatchGAN step (BASELINE.json); ref: the reference "
@@ -140,6 +141,9 @@ def main():
                               lambda_L1=args.lamb, reducer_g=reducer_g, reducer_d=reducer_d,
                               autocast_dtype=autocast)
 
+    if args.batch is None:
+        args.batch = (64 if args.family == "ref" else 128 if args.impl == "torch"
+                      else 256 if args.mode == "infer" else 2048)
     B, S = args.batch, args.size
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     real_A = (torch.rand(B, 3, S, S, device=dev, generator=gen) * 2 - 1).to(act_dtype)
