@@ -139,12 +139,13 @@ def test_family_r_step_gpu_matches_cpu_oracle():
                 # -- and the native value moves with any rounding change upstream (0.025 ->
                 # 0.060 when the residual joins fused their add into the BN apply, every
                 # other tensor unchanged).  Bound from its conditioning, measured on the
-                # oracle: S = sum |dy * x| over the summed terms; a 2 % relative error of the
-                # bf16 dy / x (the size of this step's conv-gradient errors) moves the sum by
-                # up to 0.02 * S.  Recorded with kappa = S / |g|.
+                # oracle: S = sum |dy * x| over the summed terms (S = 36.5 for |g| = 0.084:
+                # kappa = S / |g| = 432, so one bf16 rounding of each term alone can move the
+                # sum by ~0.4 % of S = 1.7x the value); the native error must stay within one
+                # bf16 step of S (2^-8 S; measured 0.17 % of S).  Recorded with kappa.
                 S = _COND.get("slope_abs_sum", 0.0)
                 rows.append(("relu.weight:abs_sum_S,kappa", S, S / max(scale, 1e-12), scale))
-                if err > max(0.35 * scale, 0.02 * S):
+                if err > max(0.35 * scale, S * 2.0 ** -8):
                     bad.append((n, err, erre, scale, S))
                 continue
             if err > 2 * erre + floor and err > 1e-3 * gscale:
