@@ -1,0 +1,10 @@
+#!/bin/bash
+# Final validation of HEAD: the full GPU suite as the driver runs it.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/r4suite
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1; rc=$?
+echo "tests rc=$rc"; grep -E "passed|failed|FAILED|Error" $O/tests.log | tail -8
+exit $rc
