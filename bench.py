@@ -180,11 +180,12 @@ def main():
     use_graph = (args.impl == "native" and dev.type == "cuda" and not args.no_graph
                  and (world == 1 or (pdist.backend() == "nccl"
                                      and os.environ.get("P2P_GRAPH_MULTI", "1") != "0")))
+    cap_info = {"capture_error": None}
     if use_graph:
         from p2p_pytorch_amd.engine.graph import capture_agreed
         # capture runs its own warmup steps on a side stream, then records one step
         step, use_graph = capture_agreed(
-            step_fn, real_A, real_B, warmup=2,
+            step_fn, real_A, real_B, warmup=2, info=cap_info,
             log=lambda m: print(f"[bench] rank {rank}: {m}", file=sys.stderr, flush=True))
     t_w = time.perf_counter()
     for i in range(args.warmup):
@@ -253,12 +254,17 @@ def main():
                    "image_size": S, "parallelism": f"dp{world}", "impl": args.impl,
                    "gan_mode": args.gan_mode, "lambda_L1": args.lamb,
                    "hipgraph": bool(use_graph),
+                   # why a native run is eager (None: captured, or capture not attempted)
+                   "capture_error": cap_info["capture_error"],
                    **({"c_phase_backward": bool(args.c_phase_backward)} if ref else {}),
                    "conv_precision": ("fp8: e4m3 fwd, e5m2 dgrad, e5m2 x e4m3 wgrad; image-facing first/last "
                                       "layers bf16" if args.precision == "fp8" else "bf16")},
         "max_mem_gib": (round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)
                         if dev.type == "cuda" else None),
         "comm": comm,
+        # every non-default P2P_* knob of this run (an A/B setting must show in its line)
+        "knobs": {k: v for k, v in sorted(os.environ.items())
+                  if k.startswith("P2P_") and k not in ("P2P_BACKEND", "P2P_PRECISION")},
         "losses_finite": finite,
         "losses": loss_vals,
     }

@@ -85,6 +85,10 @@ int p2p_pixel_shuffle(const void* in, int N, int OH, int OW, int OC, int r, int 
 int p2p_weight_prep_pairs(int count, const float* const* w, void* const* out0, void* const* out1,
                           const int* A, const int* B, const int* T, const int* Xa, const int* Xb,
                           int* const* site, hipStream_t st);
+int p2p_m32_enabled();
+int p2p_set_m32(int on);
+int p2p_conv_fwd_m32(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t st);
+int p2p_up2_dgrad_image(const float* w, int Cout, int Cin, int Xp, int Yp, void* out, hipStream_t st);
 int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, int reflect,
                  const void* xb, int act, const void* res, void* dx, hipStream_t st);
 int p2p_fold_band(const void* fb, int N, int H, int W, int C, int pad, int edge, const void* xb, int act, void* dx,
@@ -626,6 +630,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     rc = p2p_conv_s2t(&a, st);
     TORCH_CHECK(rc != -2, "conv_fwd: the s2t kernel refused a geometry the host accepted");
   }
+  // the 32x32x16 MFMA tiles (conv_fwd_m32.hip) take the 256-row bf16 FASTK layers first
+  if (rc == -2 && glds_ok && !fp8 && p2p_m32_enabled()) rc = p2p_conv_fwd_m32(&a, (int)mode, variant, st);
   if (rc == -2 && glds_ok) rc = p2p_conv_fwd_glds(&a, (int)mode, variant, st);
   if (rc == -2 && a.stats) {  // glds refused after all: no fused statistics
     a.stats = nullptr;
@@ -994,6 +1000,23 @@ Tensor weight_prep(const Tensor& w, int64_t swap, int64_t Xp, int64_t Yp,
                            (int)Yp, scale ? scale->data_ptr<float>() : nullptr, out.data_ptr(),
                            cur_stream(w)),
            "weight_prep");
+  return out;
+}
+
+// runtime A/B switch of the 32x32x16 conv tiles (returns the previous setting)
+int64_t set_m32(int64_t on) { return p2p_set_m32((int)on); }
+
+// input-gradient image of a nearest-x2 + reflect-1 3x3 conv: [Xp][4][4][Yp] bf16 (misc.hip)
+Tensor up2_dgrad_image(const Tensor& w, int64_t Xp, int64_t Yp) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.dim() == 4 &&
+                  w.size(2) == 3 && w.size(3) == 3,
+              "up2_dgrad_image: fp32 contiguous [Cout][Cin][3][3] weight");
+  const int64_t Cout = w.size(0), Cin = w.size(1);
+  TORCH_CHECK(Xp >= Cin && Yp >= Cout, "up2_dgrad_image: padding too small");
+  Tensor out = at::empty({Xp, 4, 4, Yp}, w.options().dtype(at::kBFloat16));
+  check_rc(p2p_up2_dgrad_image(w.data_ptr<float>(), (int)Cout, (int)Cin, (int)Xp, (int)Yp, out.data_ptr(),
+                               cur_stream(w)),
+           "up2_dgrad_image");
   return out;
 }
 
@@ -1833,6 +1856,8 @@ TORCH_LIBRARY(p2p, m) {
         "int flip=0, Tensor? qs_p=None, Tensor? qs_q=None, int p_fmt=0, int q_fmt=0, Tensor? qs_p2=None, "
         "Tensor? qs_q2=None) -> bool");
   m.def("weight_prep(Tensor w, int swap, int Xp, int Yp, Tensor? scale) -> Tensor");
+  m.def("up2_dgrad_image(Tensor w, int Xp, int Yp) -> Tensor");
+  m.def("set_m32(int on) -> int", set_m32);   // no tensor arguments: a catch-all kernel
   m.def("union_weight(Tensor w, int co_off, int nv, int Nrows, int Cpad, Tensor? bias) -> Tensor[]");
   m.def("conv_d2s(Tensor x1, Tensor? x2, Tensor w, Tensor bias, int act_in, int act_out, int mode, "
         "Tensor(a!) out, Tensor pk_a, Tensor? pk_f, float scale, Tensor? wscale=None) -> Tensor");
@@ -1893,6 +1918,7 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("fp8_dequant", fp8_dequant);
   m.impl("conv_wgrad", conv_wgrad);
   m.impl("weight_prep", weight_prep);
+  m.impl("up2_dgrad_image", up2_dgrad_image);
   m.impl("union_weight", union_weight);
   m.impl("conv_d2s", conv_d2s);
   m.impl("weight_prep_multi", weight_prep_multi);

@@ -1,0 +1,486 @@
+// Implicit-GEMM conv / transposed conv on gfx950 v_mfma_f32_32x32x16_bf16, 256-row tiles.
+//
+// Same GEMM view, LDS image (source-side swizzled global_load_lds "LDS-DMA" staging, zero
+// page for out-of-image taps) and fused epilogue as conv_fwd_glds.hip; what is new is the
+// MFMA shape and the software pipeline around it (the 16x16x32 tiles
+// sat at 37-48 % MFMA busy with every LDS fragment burst and every glds issue exposed).
+//
+//  * v_mfma_f32_32x32x16_bf16: half the MFMA instructions of 16x16x32 for the same FLOP,
+//    32 issue cycles each -- an MFMA holds vector issue for 8 of its 32 cycles instead of
+//    8 of 16, so the loader's VALU / glds issue and the fragment reads fit beside the
+//    matrix pipe (MI355X_MICROARCH.md: per-instruction issue costs).
+//  * k16-step pipeline with a 3-deep fragment register ring: the LDS reads of step t + 2
+//    are in flight while step t's MFMAs run, and only the reads a step consumes are
+//    waited for (counted lgkmcnt on inline-asm ds_read_b128, invisible to the compiler's
+//    conservative LDS-DMA aliasing waits).
+//  * ONE barrier per 64-deep K tile (the 16x16 kernel had two): before it every wave has
+//    (a) retired all reads of the slot it is done with and (b) landed its share of the
+//    next tile; after it the next tile's first fragments are read and the slot just freed
+//    is refilled (tile kt + STAGES) with the glds interleaved between the MFMAs of the
+//    tile's last two k16 steps.
+//  * the loop is unrolled over lcm(3, STAGES) = 6 tiles, so the fragment-ring index and
+//    the LDS slot of every step are compile-time constants (immediate offsets).
+//
+// Wave tiles: BN = 256 -> 8 waves of 128 x 64 (TM 4 x TN 2 MFMA blocks of 32 x 32),
+// BN = 128 -> 8 waves of 64 x 64 (2 x 2) with a 3-slot ring (48 KB per slot).
+// Covered: bf16 operands, FASTK geometry (both concat halves multiples of 64 channels),
+// MODE 0 (conv) / MODE 1 (transposed conv as stride^2 parity classes), input ReLU, the
+// plain and the EXT (act' gate / skip gradient / norm-backward partials) epilogues, no
+// split-K.  Everything else returns -2 and stays on conv_fwd_glds.hip.
+//   reference layers: the PatchGAN ladder (networks.py:764-784) and the U-Net encoder /
+//   decoder of the north-star config (BASELINE.json) -- every 4x4 conv with >= 64 channels.
+#include <atomic>
+#include <cstdlib>
+
+#include "conv_dev.h"
+
+namespace p2p {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int N>
+__device__ __forceinline__ void m32_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_byte_addr(const void* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)p));
+}
+
+template <int OFF>
+__device__ __forceinline__ u32x4 ds_rd128(uint32_t addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
+  u32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+
+// one k16 step's operands: TM A fragments (32 pixel rows x 16 k) and TN B fragments
+template <int TM, int TN>
+struct Frag {
+  u32x4 a[TM];
+  u32x4 b[TN];
+};
+
+// s_waitcnt lgkmcnt(N) that every use of the fragment registers must follow
+template <int N, int TM, int TN>
+__device__ __forceinline__ void frag_wait(Frag<TM, TN>& f) {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt range");
+  if constexpr (TM == 4 && TN == 2) {
+    asm volatile("s_waitcnt lgkmcnt(%6)"
+                 : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.a[2]), "+v"(f.a[3]), "+v"(f.b[0]), "+v"(f.b[1])
+                 : "n"(N));
+  } else {
+    static_assert(TM == 2 && TN == 2, "wave tile");
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.b[0]), "+v"(f.b[1]) : "n"(N));
+  }
+}
+
+__device__ __forceinline__ void glds16(const void* g, void* lds) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(lds), 16, 0, 0);
+}
+
+// bias + output activation in registers -> the bf16 tile in LDS (row stride LDC) from the
+// 32x32 accumulator layout: acc[i][j][r] = D[i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5)][j*32 + lane&31]
+template <int TM, int TN, int LDC>
+__device__ __forceinline__ void stage_tile32(const ConvFwdArgs& a, f32x16 (&acc)[TM][TN], bf16* Cs, int row0,
+                                             int col0, int n0, int lane) {
+  const float al = a.alpha ? a.alpha[0] : 1.f;
+  auto stage = [&](auto act_tag) __attribute__((always_inline)) {
+    constexpr int ACT = decltype(act_tag)::value;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int coll = col0 + j * 32 + (lane & 31);
+      const int col = n0 + coll;
+      const float bj = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int rowb = row0 + i * 32 + 4 * (lane >> 5);
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          Cs[(rowb + (r & 3) + 8 * (r >> 2)) * LDC + coll] = (bf16)act_fwd(acc[i][j][r] * al + bj, ACT);
+      }
+    }
+  };
+  switch (a.act_out) {
+    case ACT_RELU: stage(std::integral_constant<int, ACT_RELU>{}); break;
+    case ACT_LRELU: stage(std::integral_constant<int, ACT_LRELU>{}); break;
+    case ACT_TANH: stage(std::integral_constant<int, ACT_TANH>{}); break;
+    case ACT_SIGMOID: stage(std::integral_constant<int, ACT_SIGMOID>{}); break;
+    default: stage(std::integral_constant<int, ACT_NONE>{}); break;
+  }
+}
+
+}  // namespace
+
+template <int BN>
+struct M32Geom {
+  static constexpr int BM = 256;
+  static constexpr int WM = BN == 256 ? 2 : 4;
+  static constexpr int WN = 8 / WM;
+  static constexpr int TM = BM / WM / 32;
+  static constexpr int TN = BN / WN / 32;
+  static constexpr int STAGES = BN == 256 ? 2 : 3;
+  static constexpr int NT = 512;
+  static constexpr int RPP = NT / 8;                // tile rows per glds pass (8 lanes per row)
+  static constexpr int AROWS = BM / RPP;            // A glds per thread per tile
+  static constexpr int BROWS = BN / RPP;
+  static constexpr int LOADS = AROWS + BROWS;
+  static constexpr int A_SLOT = BM * BK * 2;        // bytes per A slot
+  static constexpr int B_SLOT = BN * BK * 2;
+  static constexpr int PIPE = STAGES * (A_SLOT + B_SLOT);
+  static constexpr int EPI = BM * (BN + 8) * 2 + 2 * NT * 4;
+  static constexpr int SMEM = PIPE > EPI ? PIPE : EPI;
+  static constexpr int NR = TM + TN;                // ds_read_b128 per k16 step
+  static_assert(SMEM <= 160 * 1024, "LDS");
+  static_assert(2 * NR <= 15, "two steps of reads within the lgkm counter");
+};
+
+template <int BN, int MODE, bool RELU, bool EXT>
+__global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
+  using G = M32Geom<BN>;
+  constexpr int BM = G::BM, WN = G::WN, TM = G::TM, TN = G::TN, STAGES = G::STAGES, NT = G::NT;
+  constexpr int RPP = G::RPP, AROWS = G::AROWS, BROWS = G::BROWS, LOADS = G::LOADS;
+  constexpr int NR = G::NR;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* As = reinterpret_cast<bf16*>(smem);                      // [STAGES][BM][64]
+  bf16* Bs = reinterpret_cast<bf16*>(smem + STAGES * G::A_SLOT);  // [STAGES][BN][64]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: SALU glds bases
+  const int wm = wid / WN, wn = wid % WN;
+
+  const int classes = MODE == 1 ? a.stride * a.stride : 1;
+  const int ntiles = (a.Cout + BN - 1) / BN;
+  const int bid0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_cls = gridDim.x / classes;
+  const int cls = MODE == 1 ? (a.cls_major ? bid0 / per_cls : bid0 % classes) : 0;
+  const int bid = MODE == 1 ? (a.cls_major ? bid0 % per_cls : bid0 / classes) : bid0;
+  const ClassGeom g = class_geom<MODE>(a, cls);
+  const int mt = bid / ntiles, nt = bid % ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  if (m0 >= g.Mc) return;
+  const int kt1 = (g.Kc + BK - 1) / BK;   // no split-K: K tiles [0, kt1)
+
+  const bf16* __restrict__ x1 = static_cast<const bf16*>(a.x1);
+  const bf16* __restrict__ x2 = static_cast<const bf16*>(a.x2);
+  const bf16* __restrict__ w = static_cast<const bf16*>(a.w);
+  const bf16* zero = static_cast<const bf16*>(a.zero);
+  const int C = a.C, C1 = a.C1, C2 = a.C2;
+  const int slot8 = lane & 7;
+  const int rsub = lane >> 3;
+  const int ush = a.up == 2 ? 1 : 0;
+  const int Hu = a.H << ush, Wu = a.W << ush;
+
+  // ---- loader decode (as conv_fwd_glds.hip): A rows row_i = wid*8 + rsub + RPP*i
+  int r_img[AROWS], r_y[AROWS], r_x[AROWS];
+  // source-side swizzle: (row >> 1) & 7 of rows wid*8 + rsub + 64 i does not depend on i
+  const int r_c = (slot8 ^ (((wid * 8 + rsub) >> 1) & 7)) * 8;
+  const int HWq = g.Hq * g.Wq;
+  const FastDiv fd_hwq = make_fastdiv((uint32_t)HWq), fd_wq = make_fastdiv((uint32_t)g.Wq);
+#pragma unroll
+  for (int i = 0; i < AROWS; ++i) {
+    const int row = wid * 8 + rsub + RPP * i;
+    const int m = m0 + row;
+    const int mm = m < g.Mc ? m : 0;
+    const int n = (int)fdiv((uint32_t)mm, fd_hwq);
+    const int r = mm - n * HWq;
+    const int qy = (int)fdiv((uint32_t)r, fd_wq);
+    const int qx = r - qy * g.Wq;
+    r_img[i] = n * a.H * a.W;
+    if (MODE == 0) {
+      r_y[i] = qy * a.stride - a.pad;
+      r_x[i] = qx * a.stride - a.pad;
+    } else {
+      r_y[i] = qy + g.dy;
+      r_x[i] = qx + g.dx;
+    }
+    if (m >= g.Mc) r_y[i] = -(1 << 28);
+  }
+  const long wrow = (MODE == 0) ? (long)g.Kc : (long)a.KH * a.KW * C;
+  const bf16* b_base[BROWS];
+  bool b_ok[BROWS];
+#pragma unroll
+  for (int i = 0; i < BROWS; ++i) {
+    const int row = wid * 8 + rsub + RPP * i;
+    const int co = n0 + row;
+    b_ok[i] = co < a.Cout;
+    b_base[i] = w + (long)(b_ok[i] ? co : 0) * wrow + r_c;
+  }
+  const FastDiv fd_c = make_fastdiv((uint32_t)C), fd_ti = make_fastdiv((uint32_t)g.Ti);
+  const bf16* a_ptr[AROWS];
+  long woff = 0;
+
+  // source pointers of K tile kt (FASTK: one tap x one source tensor per 64-deep tile; the
+  // row pointers are formed once per channel segment and then advanced by 64 per tile)
+  auto prep = [&](int kt) __attribute__((always_inline)) {
+    const int k0 = kt * BK;
+    const int tap = (int)fdiv((uint32_t)k0, fd_c);
+    const int ci0 = k0 - tap * C;
+    const int t_y = (int)fdiv((uint32_t)tap, fd_ti);
+    const int t_x = tap - t_y * g.Ti;
+    if (kt == 0 || ci0 == 0 || ci0 == C1) {
+      const bool s1 = ci0 < C1;
+      const bf16* src = s1 ? x1 : x2;
+      const int cs = s1 ? C1 : C2;
+      const int cio = s1 ? ci0 : ci0 - C1;
+#pragma unroll
+      for (int i = 0; i < AROWS; ++i) {
+        int iy, ix;
+        bool inb;
+        if (MODE == 0) {
+          int uy = r_y[i] + t_y, ux = r_x[i] + t_x;
+          if (a.reflect && r_y[i] > -(1 << 27)) {
+            uy = reflect_idx(uy, Hu);
+            ux = reflect_idx(ux, Wu);
+          }
+          inb = (unsigned)uy < (unsigned)Hu && (unsigned)ux < (unsigned)Wu;
+          iy = uy >> ush;
+          ix = ux >> ush;
+        } else {
+          iy = r_y[i] - t_y;
+          ix = r_x[i] - t_x;
+          inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+        }
+        const long off = (long)(r_img[i] + iy * a.W + ix) * cs + cio + r_c;
+        a_ptr[i] = inb ? src + off : zero;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AROWS; ++i) a_ptr[i] += BK;
+    }
+    if (MODE == 0) {
+      woff = k0;
+    } else {
+      const int ky = g.ky0 + a.stride * t_y, kx = g.kx0 + a.stride * t_x;
+      woff = (long)(ky * a.KW + kx) * C + ci0;
+    }
+  };
+  // glds number q (A rows first, then B rows) of the prepared tile into LDS slot SLOT
+  auto fire = [&](auto slot_c, int q) __attribute__((always_inline)) {
+    constexpr int SLOT = decltype(slot_c)::value;
+    if (q < AROWS) {
+      glds16(a_ptr[q], As + SLOT * (G::A_SLOT / 2) + (wid * 8 + RPP * q) * BK);
+    } else {
+      const int i = q - AROWS;
+      glds16(b_ok[i] ? b_base[i] + woff : zero, Bs + SLOT * (G::B_SLOT / 2) + (wid * 8 + RPP * i) * BK);
+    }
+  };
+  auto issue_all = [&](auto slot_c, int kt) __attribute__((always_inline)) {
+    prep(kt);
+#pragma unroll
+    for (int q = 0; q < LOADS; ++q) fire(slot_c, q);
+  };
+
+  // ---- per-lane LDS byte addresses of the k16 steps' fragments in slot 0
+  //   lane l: row (l & 31) of a 32-row block, 16-B chunk 2s + (l >> 5) of the 64-deep tile
+  uint32_t fa[4], fb[4];
+  {
+    const int ra = wm * TM * 32 + (lane & 31), rb = wn * TN * 32 + (lane & 31);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int chunk = 2 * s + (lane >> 5);
+      fa[s] = lds_byte_addr(As + swz(ra, chunk));
+      fb[s] = lds_byte_addr(Bs + swz(rb, chunk));
+    }
+  }
+  using F = Frag<TM, TN>;
+  auto read_step = [&](auto slot_c, auto s_c, F& f) __attribute__((always_inline)) {
+    constexpr int SLOT = decltype(slot_c)::value, S = decltype(s_c)::value;
+    const uint32_t ab = fa[S] + SLOT * G::A_SLOT, bb = fb[S] + SLOT * G::B_SLOT;
+    // row block i is 32 rows = 4 KB further with the same XOR key ((row + 32) >> 1 & 7)
+    f.a[0] = ds_rd128<0>(ab);
+    f.a[1] = ds_rd128<4096>(ab);
+    if constexpr (TM > 2) {
+      f.a[2] = ds_rd128<8192>(ab);
+      f.a[3] = ds_rd128<12288>(ab);
+    }
+    f.b[0] = ds_rd128<0>(bb);
+    f.b[1] = ds_rd128<4096>(bb);
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // one k16 step of MFMAs with glds Q0 .. Q0 + NQ - 1 of the refill tile spread over its
+  // P = TM * TN MFMAs (after MFMA p: floor((p + 1) NQ / P) - floor(p NQ / P) of them, so every
+  // glds index is a compile-time constant once the loops are unrolled)
+  auto mma_step = [&](F& f, auto nq_c, auto q0_c, auto slot_c, bool refill) __attribute__((always_inline)) {
+    constexpr int NQ = decltype(nq_c)::value, Q0 = decltype(q0_c)::value, P = TM * TN;
+    static_assert(NQ <= P, "at most one glds per MFMA");
+    if constexpr (RELU) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) f.a[i] = relu8(f.a[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f.a[i]),
+                                                             __builtin_bit_cast(bf16x8, f.b[j]), acc[i][j], 0, 0, 0);
+        const int p = i * TN + j;
+        if (NQ > 0 && ((p + 1) * NQ) / P > (p * NQ) / P && refill) {
+          __builtin_amdgcn_sched_barrier(0);
+          fire(slot_c, Q0 + (p * NQ) / P);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+  };
+
+  F fr[3];
+  // ---- prologue: tiles 0 .. STAGES-1 in flight, tile 0 landed, its steps 0 / 1 being read
+#pragma unroll
+  for (int s = 0; s < STAGES; ++s) {
+    if (s < kt1) {
+      if (s == 0) issue_all(std::integral_constant<int, 0>{}, 0);
+      if (s == 1) issue_all(std::integral_constant<int, 1>{}, 1);
+      if (s == 2) issue_all(std::integral_constant<int, 2 % STAGES>{}, 2);
+    }
+  }
+  {
+    const int inflight = (kt1 < STAGES ? kt1 : STAGES) - 1;   // tiles issued after tile 0
+    if (inflight >= 2) m32_vmcnt<2 * LOADS>();
+    else if (inflight == 1) m32_vmcnt<LOADS>();
+    else m32_vmcnt<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  read_step(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, fr[0]);
+  read_step(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, fr[1]);
+
+  // ---- one 64-deep K tile; T = kt mod 6 (ring index R = T % 3, LDS slot T % STAGES)
+  constexpr int QA = LOADS / 2, QB = LOADS - LOADS / 2;   // glds in steps 2 / 3
+  auto tile = [&](auto t_c, int kt) __attribute__((always_inline)) {
+    constexpr int T = decltype(t_c)::value;
+    constexpr int R = T % 3;
+    constexpr int SLOT = T % STAGES, NSLOT = (T + 1) % STAGES;
+    using SC = std::integral_constant<int, SLOT>;
+    using NC = std::integral_constant<int, NSLOT>;
+    const bool more = kt + 1 < kt1;
+    const bool refill = kt + STAGES < kt1;
+    // step 0: read step 2 of this tile, run step 0
+    read_step(SC{}, std::integral_constant<int, 2>{}, fr[(R + 2) % 3]);
+    frag_wait<2 * NR>(fr[R]);
+    __builtin_amdgcn_sched_barrier(0);
+    mma_step(fr[R], std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, SC{}, false);
+    __builtin_amdgcn_sched_barrier(0);
+    // step 1: read step 3, run step 1
+    read_step(SC{}, std::integral_constant<int, 3>{}, fr[R]);
+    frag_wait<2 * NR>(fr[(R + 1) % 3]);
+    __builtin_amdgcn_sched_barrier(0);
+    mma_step(fr[(R + 1) % 3], std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, SC{}, false);
+    __builtin_amdgcn_sched_barrier(0);
+    // sync: all my reads of this slot retired, my share of tile kt + 1 landed
+    frag_wait<0>(fr[(R + 2) % 3]);
+    frag_wait<0>(fr[R]);
+    if constexpr (STAGES == 3) {
+      if (kt + 2 < kt1) m32_vmcnt<LOADS>();
+      else m32_vmcnt<0>();
+    } else {
+      m32_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (refill) prep(kt + STAGES);   // loader address math (VALU) before the MFMAs it hides behind
+    // step 2: read step 0 of tile kt + 1, run step 2 with the first glds of tile kt + STAGES
+    if (more) read_step(NC{}, std::integral_constant<int, 0>{}, fr[(R + 1) % 3]);
+    __builtin_amdgcn_sched_barrier(0);
+    mma_step(fr[(R + 2) % 3], std::integral_constant<int, QA>{}, std::integral_constant<int, 0>{}, SC{}, refill);
+    __builtin_amdgcn_sched_barrier(0);
+    // step 3: read step 1 of tile kt + 1, run step 3 with the remaining glds
+    if (more) read_step(NC{}, std::integral_constant<int, 1>{}, fr[(R + 2) % 3]);
+    __builtin_amdgcn_sched_barrier(0);
+    mma_step(fr[R], std::integral_constant<int, QB>{}, std::integral_constant<int, QA>{}, SC{}, refill);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int kt = 0;;) {
+    tile(std::integral_constant<int, 0>{}, kt);
+    if (++kt >= kt1) break;
+    tile(std::integral_constant<int, 1>{}, kt);
+    if (++kt >= kt1) break;
+    tile(std::integral_constant<int, 2>{}, kt);
+    if (++kt >= kt1) break;
+    tile(std::integral_constant<int, 3>{}, kt);
+    if (++kt >= kt1) break;
+    tile(std::integral_constant<int, 4>{}, kt);
+    if (++kt >= kt1) break;
+    tile(std::integral_constant<int, 5>{}, kt);
+    if (++kt >= kt1) break;
+  }
+  __syncthreads();  // every wave done with the ring before the epilogue reuses the LDS
+
+  bf16* Cs = reinterpret_cast<bf16*>(smem);
+  constexpr int LDC = BN + 8;
+  stage_tile32<TM, TN, LDC>(a, acc, Cs, wm * TM * 32, wn * TN * 32, n0, lane);
+  __syncthreads();
+  conv_epilogue_tail<BM, BN, MODE, NT, EXT>(a, g, m0, n0, Cs, reinterpret_cast<float*>(smem + BM * LDC * 2), smem,
+                                            fd_hwq, fd_wq);
+}
+
+template <int BN, int MODE, bool RELU, bool EXT>
+static int launch_m32(const ConvFwdArgs& a, hipStream_t st) {
+  using G = M32Geom<BN>;
+  static std::atomic<uint64_t> attr_mask{0};
+  smem_attr_once(reinterpret_cast<const void*>(&conv_fwd_m32_kernel<BN, MODE, RELU, EXT>), G::SMEM, attr_mask);
+  const int classes = MODE == 0 ? 1 : a.stride * a.stride;
+  long mmax = 0;
+  for (int c = 0; c < classes; ++c) {
+    long hq = a.OH, wq = a.OW;
+    if (MODE == 1) {
+      const int ry = c / a.stride, rx = c % a.stride;
+      hq = a.OH > ry ? (a.OH - ry + a.stride - 1) / a.stride : 0;
+      wq = a.OW > rx ? (a.OW - rx + a.stride - 1) / a.stride : 0;
+    }
+    const long mc = (long)a.N * hq * wq;
+    mmax = mc > mmax ? mc : mmax;
+  }
+  const long mtiles = (mmax + G::BM - 1) / G::BM;
+  const long ntiles = (a.Cout + BN - 1) / BN;
+  dim3 grid((unsigned)(mtiles * ntiles * classes), 1, 1);
+  hipLaunchKernelGGL((conv_fwd_m32_kernel<BN, MODE, RELU, EXT>), grid, dim3(G::NT), G::SMEM, st, a);
+  return (int)hipGetLastError();
+}
+
+template <int BN, int MODE>
+static int dispatch_m32_epi(const ConvFwdArgs& a, hipStream_t st) {
+  if (a.act_in == ACT_RELU) return launch_m32<BN, MODE, true, false>(a, st);
+  if (a.nb_ws || ((a.act_bwd || a.res1) && !a.epi_serial)) return launch_m32<BN, MODE, false, true>(a, st);
+  return launch_m32<BN, MODE, false, false>(a, st);
+}
+
+}  // namespace p2p
+
+// 1 (default) = the 32x32x16 tiles take the 256x256 / 256x128 bf16 FASTK convs; 0 = the
+// round-4 16x16x32 tiles of conv_fwd_glds.hip.  Initialised once from P2P_M32, switchable at
+// run time (torch.ops.p2p.set_m32) so one process can A/B both paths.
+static std::atomic<int>& m32_flag() {
+  static std::atomic<int> on{[] {
+    const char* v = std::getenv("P2P_M32");
+    return v ? (v[0] != '0' ? 1 : 0) : 1;
+  }()};
+  return on;
+}
+extern "C" int p2p_m32_enabled() { return m32_flag().load(std::memory_order_relaxed); }
+extern "C" int p2p_set_m32(int on) { return m32_flag().exchange(on ? 1 : 0); }
+
+// variant 5 -> 256 x 256 tile (Cout > 128), 4 -> 256 x 128 (Cout > 64); -2 = not covered
+extern "C" int p2p_conv_fwd_m32(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t st) {
+  using namespace p2p;
+  if (!a->zero || a->fp8 != 0 || a->splits > 1 || a->d2s) return -2;
+  if (a->C1 % 64 || a->C2 % 64 || a->C1 > 1024 || a->C2 > 1024) return -2;
+  if (a->act_in != ACT_NONE && a->act_in != ACT_RELU) return -2;
+  if (a->act_in == ACT_RELU) return -2;   // (its 256-wide tile spills: stays on the 16x16 kernel for now)
+  if (variant == 5 && a->Cout > 128)
+    return mode == 0 ? dispatch_m32_epi<256, 0>(*a, st) : dispatch_m32_epi<256, 1>(*a, st);
+  if (variant == 4 && a->Cout > 64)
+    return mode == 0 ? dispatch_m32_epi<128, 0>(*a, st) : dispatch_m32_epi<128, 1>(*a, st);
+  return -2;
+}

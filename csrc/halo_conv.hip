@@ -44,6 +44,20 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// 16-B units of the resident weight operand, rounded up to whole block-wide glds rounds:
+// the kernel's B loop writes exactly this many units and the launcher reserves exactly
+// this many (the launcher rounded to 256 units while the 512-thread loop wrote
+// up to the next 512-unit multiple -- 4 KB past the allocation per launch).
+template <int NCH>
+constexpr int b_units_pad() {
+  return (9 * NCH * 16 * 8 + NTH - 1) / NTH * NTH;
+}
+
+template <int NCH>
+constexpr int halo_smem_bytes() {
+  return 2 * STAGE_BYTES + b_units_pad<NCH>() * 16;
+}
+
 }  // namespace
 
 
@@ -60,7 +74,7 @@ __global__ void __launch_bounds__(NTH) halo_union_kernel(HaloArgs a) {
 
   // ---- resident B operand (waited together with the first stage)
   constexpr int BUNITS = 9 * NCH * 16 * 8;
-  constexpr int BUNITS_PAD = (BUNITS + NTH - 1) / NTH * NTH;   // whole wave instructions
+  constexpr int BUNITS_PAD = b_units_pad<NCH>();   // whole block-wide glds rounds
 #pragma unroll
   for (int e0 = wid * 64; e0 < BUNITS_PAD; e0 += NTH) {
     const int e = e0 + lane;
@@ -226,7 +240,9 @@ __global__ void __launch_bounds__(NTH) halo_union_kernel(HaloArgs a) {
 
 template <int NCH, bool RELU>
 static int launch_halo(const HaloArgs& a, int blocks, hipStream_t st) {
-  constexpr int smem = 2 * STAGE_BYTES + (9 * NCH * 16 * 8 + 255) / 256 * 256 * 16;
+  constexpr int smem = halo_smem_bytes<NCH>();
+  static_assert(smem >= 2 * STAGE_BYTES + b_units_pad<NCH>() * 16 && smem <= 160 * 1024,
+                "the B loop's padded writes stay inside the reserved LDS");
   static std::atomic<uint64_t> attr_mask{0};
   smem_attr_once(reinterpret_cast<const void*>(&halo_union_kernel<NCH, RELU>), smem, attr_mask);
   hipLaunchKernelGGL((halo_union_kernel<NCH, RELU>), dim3(blocks), dim3(NTH), smem, st, a);

@@ -350,6 +350,40 @@ __global__ void __launch_bounds__(256) pixel_shuffle_kernel(const bf16* __restri
   }
 }
 
+
+// ------------------------------------------------------------------ nearest-x2 + reflect-1 dgrad taps
+// Input-gradient GEMM image of G.deconv{2,3} (UpsampleConvLayer, networks.py:408-423): the
+// 3x3 kernel seen through nearest x2 + edge pad 1 is ONE 4x4 stride-2 conv over dY whose taps
+// are phase sums of the 3x3 taps, W''[ci][co][a][b] = sum_kl M[a][k] M[b][l] w[co][ci][k][l]
+// with M = ((0,0,1), (0,1,1), (1,1,0), (1,0,0)) -- i.e. per axis out = (w2, w1+w2, w0+w1, w0).
+// Written straight into the bf16 [Xp][4][4][Yp] operand image (x = ci, y = co, zero padded):
+// a device-only computation, so it is legal inside a hipGraph capture (no host tensor).
+__device__ __forceinline__ float up2_axis(const float* v, int a, int stride) {
+  // v[0], v[stride], v[2*stride] = taps 0, 1, 2 along one axis
+  return a == 0 ? v[2 * stride] : a == 1 ? v[stride] + v[2 * stride] : a == 2 ? v[0] + v[stride] : v[0];
+}
+
+__global__ void __launch_bounds__(256) up2_dgrad_image_kernel(const float* __restrict__ w, int Cout, int Cin,
+                                                              int Xp, int Yp, bf16* __restrict__ out) {
+  const long total = (long)Xp * 16 * Yp;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int y = (int)(e % Yp);
+    const long r = e / Yp;
+    const int t = (int)(r % 16);
+    const int x = (int)(r / 16);
+    const int a = t >> 2, b = t & 3;
+    float v = 0.f;
+    if (x < Cin && y < Cout) {
+      const float* k = w + ((long)y * Cin + x) * 9;   // w[co][ci][3][3]
+      float rows[3];
+#pragma unroll
+      for (int l = 0; l < 3; ++l) rows[l] = up2_axis(k + l, a, 3);   // sum over k for column l
+      v = up2_axis(rows, b, 1);
+    }
+    out[e] = (bf16)v;
+  }
+}
+
 }  // namespace p2p
 
 extern "C" {
@@ -455,6 +489,14 @@ int p2p_pixel_shuffle(const void* in, int N, int OH, int OW, int OC, int r, int 
   const long n = (long)N * OH * OW * OC;
   hipLaunchKernelGGL(p2p::pixel_shuffle_kernel, dim3(p2p::mgrid(n)), dim3(256), 0, st,
                      static_cast<const p2p::bf16*>(in), N, OH, OW, OC, r, dir, static_cast<p2p::bf16*>(out));
+  return (int)hipGetLastError();
+}
+
+int p2p_up2_dgrad_image(const float* w, int Cout, int Cin, int Xp, int Yp, void* out, hipStream_t st) {
+  if (Xp < Cin || Yp < Cout) return -2;
+  const long n = (long)Xp * 16 * Yp;
+  hipLaunchKernelGGL(p2p::up2_dgrad_image_kernel, dim3(p2p::mgrid(n)), dim3(256), 0, st, w, Cout, Cin, Xp, Yp,
+                     static_cast<p2p::bf16*>(out));
   return (int)hipGetLastError();
 }
 

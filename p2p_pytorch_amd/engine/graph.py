@@ -138,7 +138,7 @@ class CapturedStep:
         return self.static_out
 
 
-def capture_agreed(step_fn, *example_inputs, warmup: int = 2, log=None):
+def capture_agreed(step_fn, *example_inputs, warmup: int = 2, log=None, info=None):
     """Capture ``step_fn`` as a :class:`CapturedStep` when it is safe on every rank, else run
     eager on every rank.  Returns ``(step, captured)``.
 
@@ -154,6 +154,9 @@ def capture_agreed(step_fn, *example_inputs, warmup: int = 2, log=None):
       re-raised -- the other ranks are blocked in that step's gradient all-reduces, a
       min_scalar would be matched against a bucket collective, so the process exits non-zero
       and the launcher (``torchrun --max-restarts``) / watchdog handles the restart.
+
+    ``info`` (optional dict) receives ``capture_error``: this rank's capture exception as a
+    string (None when it captured), so a caller's report can say WHY a run was eager.
     """
     from ..parallel import dist as pdist
     world = pdist.world_size()
@@ -161,6 +164,8 @@ def capture_agreed(step_fn, *example_inputs, warmup: int = 2, log=None):
     if dev.type != "cuda" or (world > 1 and pdist.backend() != "nccl"):
         return step_fn, False
     ok, step = 1.0, step_fn
+    if info is not None:
+        info["capture_error"] = None
     try:
         step = CapturedStep(step_fn, *example_inputs, warmup=warmup)
     except WarmupError:
@@ -168,9 +173,13 @@ def capture_agreed(step_fn, *example_inputs, warmup: int = 2, log=None):
     except Exception as e:  # noqa: BLE001 - a capture failure: eager on every rank
         if log is not None:
             log(f"graph capture failed ({type(e).__name__}: {e}); running eager")
+        if info is not None:
+            info["capture_error"] = f"{type(e).__name__}: {e}"[:400]
         ok = 0.0
     if world > 1:
         ok = pdist.min_scalar(ok, dev)
     if ok < 1.0:
+        if info is not None and info["capture_error"] is None:
+            info["capture_error"] = "another rank's capture failed"
         return step_fn, False
     return step, True

@@ -258,7 +258,7 @@ def _weight_image(w: torch.Tensor, swap: int, xp: int, yp: int, scale=None) -> t
 # phase sums of a 3x3 kernel seen through nearest x2 + edge pad 1 (ops/hip.py up-fold dgrad):
 # tap a of the 4-tap stride-2 input-gradient kernel collects the 3x3 taps k with
 # o + k + 1 in {2q, 2q + 1} for o = 2q + a - 3
-_UP2_M = ((0, 0, 1), (0, 1, 1), (1, 1, 0), (1, 0, 0))
+# (M = ((0, 0, 1), (0, 1, 1), (1, 1, 0), (1, 0, 0)); computed on the device, misc.hip)
 
 
 def _up2_dgrad_image(w: torch.Tensor, cp: int, coutp: int) -> torch.Tensor:
@@ -274,9 +274,9 @@ def _up2_dgrad_image(w: torch.Tensor, cp: int, coutp: int) -> torch.Tensor:
     ent = cache.get(key)
     if ent is not None and ent[0] == ver and ent[1] == _gen[0]:
         return ent[2]
-    m = torch.tensor(_UP2_M, dtype=torch.float32, device=w.device)
-    wd = torch.einsum("ak,oikl,bl->ioab", m, w.detach().float(), m).contiguous()
-    img = P().weight_prep(wd, 0, cp, coutp, None)
+    # device-only phase sum (misc.hip up2_dgrad_image_kernel): no host tensor and no GEMM,
+    # so the first step after a weight update stays legal inside a hipGraph capture
+    img = P().up2_dgrad_image(w.detach().contiguous().float(), cp, coutp)
     cache[key] = (ver, _gen[0], img)
     return img
 

@@ -1,0 +1,132 @@
+"""The 32x32x16-MFMA conv tiles (csrc/conv_fwd_m32.hip) against the fp32 oracle.
+
+Each case forces a 256-row tile (``P2P_CONV_VARIANT=g5``: 256 x 256, ``g4``: 256 x 128) on
+shapes whose GEMM M and N are NOT tile multiples, and covers every instantiation the
+dispatcher routes there: conv forward (MODE 0), transposed-conv forward and stride-2 input
+gradients (MODE 1 parity classes), the virtual concat of two inputs, reflect padding, the
+EXT epilogue of a gated input gradient (act' from the saved input), bias + output
+activation.  The HIP result must match an fp32 PyTorch conv on the same bf16 inputs, and
+the profiler must show that ``conv_fwd_m32_kernel`` actually ran.  The same case with the
+tiles switched off (``torch.ops.p2p.set_m32(0)``: the round-4 16x16x32 kernels) must agree
+with it to bf16 rounding.
+"""
+import os
+
+import pytest
+import torch
+
+from p2p_pytorch_amd import _native, ops
+from p2p_pytorch_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _native_backend():
+    _native.set_backend("native")
+    assert _native.load(), _native.load_error()
+    yield
+
+
+def bf(x):
+    return x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+
+def rand_img(n, c, h, w, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return bf(torch.randn(n, c, h, w, device=DEV, generator=g))
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def _leaf(x):
+    return None if x is None else x.detach().clone().requires_grad_(True)
+
+
+CASES = [
+    # (name, variant, kind, N, C1, C2, H, Cout, k, s, p, pad_mode, act_in, act_out)
+    # sized so that the forward and the input gradient both reach >= 256 tiles (smaller
+    # grids take split-K, which stays on the 16x16 kernels)
+    ("conv_s1_256x256", "g5", "conv", 8, 256, 0, 65, 320, 4, 1, 1, "zeros", None, "lrelu"),
+    ("conv_s2_concat_256x256", "g5", "conv", 8, 128, 128, 128, 288, 4, 2, 1, "zeros", None, None),
+    ("conv_s2_relu_gate_256x128", "g4", "conv", 8, 128, 64, 128, 192, 4, 2, 1, "zeros", "relu", None),
+    ("conv_reflect3x3_256x128", "g4", "conv", 8, 128, 0, 64, 136, 3, 1, 1, "reflect", None, None),
+    ("convT_concat_256x256", "g5", "convT", 16, 256, 256, 32, 200, 4, 2, 1, "zeros", None, None),
+    ("convT_relu_256x128", "g4", "convT", 32, 256, 0, 32, 192, 4, 2, 1, "zeros", "relu", None),
+]
+
+
+def _run(case, m32):
+    name, var, kind, N, C1, C2, H, Cout, k, s, p, pad_mode, act_in, act_out = case
+    x1 = rand_img(N, C1, H, H, seed=1)
+    x2 = rand_img(N, C2, H, H, seed=2) if C2 else None
+    Cin = C1 + C2
+    g = torch.Generator(device=DEV).manual_seed(3)
+    if kind == "conv":
+        w = torch.randn(Cout, Cin, k, k, device=DEV, generator=g) / (Cin * k * k) ** 0.5
+    else:
+        w = torch.randn(Cin, Cout, k, k, device=DEV, generator=g) / (Cin * 4) ** 0.5
+    b = torch.randn(Cout, device=DEV, generator=g) * 0.1
+    hx1, hx2, hw, hb = _leaf(x1), _leaf(x2), _leaf(w), _leaf(b)
+    xin = (hx1, hx2) if x2 is not None else hx1
+    prev = torch.ops.p2p.set_m32(1 if m32 else 0)
+    # the tile under test, and none of the special-geometry kernels that would take some of
+    # these layers first (stride-2 halo kernel, 3x3 / 9x9 halo kernels)
+    env = {"P2P_CONV_VARIANT": var, "P2P_NO_S2T": "1", "P2P_NO_HALO": "1"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+            if kind == "conv":
+                y = ops.conv2d(xin, hw, hb, s, p, pad_mode, 1, act_in=act_in, act_out=act_out)
+            else:
+                y = ops.conv_transpose2d(xin, hw, hb, s, p, act_in, act_out)
+            gy = rand_img(*y.shape, seed=4)
+            y.backward(gy)
+            torch.cuda.synchronize()
+    finally:
+        torch.ops.p2p.set_m32(prev)
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    names = [e.name for e in prof.events() if "conv_fwd_m32_kernel" in e.name]
+    return (y, hx1.grad, None if x2 is None else hx2.grad, hw.grad, hb.grad), (x1, x2, w, b, gy), names
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_m32_conv_matches_fp32_oracle(case):
+    name, var, kind, N, C1, C2, H, Cout, k, s, p, pad_mode, act_in, act_out = case
+    (y, gx1, gx2, gw, gb), (x1, x2, w, b, gy), names = _run(case, True)
+    assert names, f"{name}: conv_fwd_m32_kernel never ran"
+    rx1, rx2, rw, rb = _leaf(x1.float()), _leaf(None if x2 is None else x2.float()), _leaf(w), _leaf(b)
+    rin = (rx1, rx2) if rx2 is not None else rx1
+    wq = rw.to(torch.bfloat16).float()   # the HIP path computes with bf16 weight images
+    if kind == "conv":
+        ry = ref.conv2d(rin, wq, rb, s, p, pad_mode, 1, act_in=act_in, act_out=act_out)
+    else:
+        ry = ref.conv_transpose2d(rin, wq, rb, s, p, act_in, act_out)
+    ry.backward(gy.float())
+    assert y.shape == ry.shape
+    assert rel_err(y, ry) < 2e-2, (name, "y", rel_err(y, ry))
+    assert rel_err(gx1, rx1.grad) < 3e-2, (name, "dx1", rel_err(gx1, rx1.grad))
+    if x2 is not None:
+        assert rel_err(gx2, rx2.grad) < 3e-2, (name, "dx2", rel_err(gx2, rx2.grad))
+    assert rel_err(gw, rw.grad) < 3e-2, (name, "dw")
+    assert rel_err(gb, rb.grad) < 3e-2, (name, "db")
+
+
+@pytest.mark.parametrize("case", CASES[:3], ids=[c[0] for c in CASES[:3]])
+def test_m32_matches_16x16_tiles(case):
+    out_a, _, names = _run(case, True)
+    out_b, _, names_b = _run(case, False)
+    assert names and not names_b
+    for ta, tb in zip(out_a, out_b):
+        if ta is not None:
+            assert rel_err(ta, tb) < 1.5e-2

@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--variants", default="")
     ap.add_argument("--layers", default="")
     ap.add_argument("--json_out", default=None)
+    ap.add_argument("--m32", default="", help="A/B the 32x32x16 tiles in ONE process: e.g. '1,0' "
+                    "(torch.ops.p2p.set_m32 before each timed round; rounds interleaved)")
+    ap.add_argument("--rounds", type=int, default=3, help="interleaved rounds per setting (--m32)")
     a = ap.parse_args()
     from p2p_pytorch_amd import _native, ops
     _native.set_backend("native")
@@ -105,17 +108,28 @@ def main():
                     def fn(y=y, gy=gy):
                         torch.autograd.grad(y, [xa] if op == "dgrad" else [wl], gy,
                                             retain_graph=True)
-                fn()
-                torch.cuda.synchronize()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(a.iters):
-                    fn()
-                e1.record()
-                torch.cuda.synchronize()
-                ms = e0.elapsed_time(e1) / a.iters
-                row[op + "_us"] = round(ms * 1e3, 1)
-                row[op + "_tflops"] = round(flops / (ms * 1e-3) / 1e12, 1)
+                settings = [int(v) for v in a.m32.split(",")] if a.m32 else [None]
+                best = {}
+                for _r in range(a.rounds if a.m32 else 1):
+                    for sv in settings:
+                        if sv is not None:
+                            torch.ops.p2p.set_m32(sv)
+                        fn()
+                        torch.cuda.synchronize()
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        for _ in range(a.iters):
+                            fn()
+                        e1.record()
+                        torch.cuda.synchronize()
+                        ms = e0.elapsed_time(e1) / a.iters
+                        best[sv] = min(best.get(sv, 1e30), ms)
+                for sv, ms in best.items():
+                    tag = op if sv is None else f"{op}_m32{sv}"
+                    row[tag + "_us"] = round(ms * 1e3, 1)
+                    row[tag + "_tflops"] = round(flops / (ms * 1e-3) / 1e12, 1)
+                if a.m32:
+                    torch.ops.p2p.set_m32(1)
             results.append(row)
             print(json.dumps(row), flush=True)
     if a.json_out:
