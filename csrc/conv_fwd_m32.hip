@@ -78,8 +78,16 @@ __device__ __forceinline__ void frag_wait(Frag<TM, TN>& f) {
   }
 }
 
-__device__ __forceinline__ void glds16(const void* g, void* lds) {
-  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(lds), 16, 0, 0);
+// 16-B buffer_load ... lds (M0 = the wave's LDS destination).  Kept in a __device__ helper:
+// called straight from the kernel's (host + device) lambdas, hipcc's host pass silently
+// dropped the kernels' launch stubs (undefined symbols at dlopen).
+__device__ __forceinline__ void bld16(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(lds), 16, voff, soff, 0, 0);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL), 0x00020000);
 }
 
 // bias + output activation in registers -> the bf16 tile in LDS (row stride LDC) from the
@@ -114,6 +122,22 @@ __device__ __forceinline__ void stage_tile32(const ConvFwdArgs& a, f32x16 (&acc)
 }
 
 }  // namespace
+
+#ifdef P2P_M32_STAMPS
+// diagnostic build only (tools/build_ext.py --define P2P_M32_STAMPS --out ...): per block,
+// s_memtime at kernel start / after the prologue / after the K loop / at the end, and
+// s_memrealtime at start and end -- written by lane 0 of wave 0 with vector stores into a
+// buffer no output is computed from (tools/m32_stamps.py reads it back)
+__device__ unsigned long long m32_stamps[65536 * 6];
+#define M32_STAMP(i, v)                                                        \
+  do {                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) m32_stamps[blockIdx.x * 6 + (i)] = (v); \
+  } while (0)
+#else
+#define M32_STAMP(i, v) \
+  do {                  \
+  } while (0)
+#endif
 
 template <int BN>
 struct M32Geom {
@@ -163,23 +187,38 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
   const int m0 = mt * BM, n0 = nt * BN;
   if (m0 >= g.Mc) return;
   const int kt1 = (g.Kc + BK - 1) / BK;   // no split-K: K tiles [0, kt1)
+  M32_STAMP(0, __builtin_amdgcn_s_memtime());
+  M32_STAMP(4, __builtin_amdgcn_s_memrealtime());
 
-  const bf16* __restrict__ x1 = static_cast<const bf16*>(a.x1);
-  const bf16* __restrict__ x2 = static_cast<const bf16*>(a.x2);
-  const bf16* __restrict__ w = static_cast<const bf16*>(a.w);
-  const bf16* zero = static_cast<const bf16*>(a.zero);
   const int C = a.C, C1 = a.C1, C2 = a.C2;
   const int slot8 = lane & 7;
   const int rsub = lane >> 3;
   const int ush = a.up == 2 ? 1 : 0;
   const int Hu = a.H << ush, Wu = a.W << ush;
-
-  // ---- loader decode (as conv_fwd_glds.hip): A rows row_i = wid*8 + rsub + RPP*i
-  int r_img[AROWS], r_y[AROWS], r_x[AROWS];
-  // source-side swizzle: (row >> 1) & 7 of rows wid*8 + rsub + 64 i does not depend on i
-  const int r_c = (slot8 ^ (((wid * 8 + rsub) >> 1) & 7)) * 8;
   const int HWq = g.Hq * g.Wq;
   const FastDiv fd_hwq = make_fastdiv((uint32_t)HWq), fd_wq = make_fastdiv((uint32_t)g.Wq);
+
+  // ---- buffer-resource LDS-DMA (buffer_load_dwordx4 ... lds): 32-bit per-lane byte offsets
+  // from a block-uniform base, and out-of-range offsets read ZERO -- the out-of-image taps,
+  // padded GEMM rows and output channels beyond Cout need no zero page and no 64-bit
+  // pointer per row.  The A base is the block's first image (a 256-row tile spans a few
+  // images, so offsets stay far below 2^31 whatever the batch).
+  constexpr uint32_t OOB = 0x80000000u;
+  const int img0 = (int)fdiv((uint32_t)m0, fd_hwq);
+  const long img_elems = (long)a.H * a.W;
+  auto img_rsrc = [&](const void* base, int cs) __attribute__((always_inline)) {
+    const long first = (long)img0 * img_elems * cs;
+    return make_rsrc(static_cast<const bf16*>(base) + first, ((long)a.N * img_elems * cs - first) * 2);
+  };
+  const auto rx1 = img_rsrc(a.x1, C1);
+  const auto rx2 = img_rsrc(C2 > 0 ? a.x2 : a.x1, C2 > 0 ? C2 : C1);
+  const long wrow = (MODE == 0) ? (long)g.Kc : (long)a.KH * a.KW * C;
+  const auto rw = make_rsrc(a.w, a.Cout * wrow * 2);
+
+  // ---- loader decode: A rows row_i = wid*8 + rsub + RPP*i (pixel of the block's first image
+  // + y / x origin of its taps); the source-side swizzle (row >> 1) & 7 does not depend on i
+  int r_img[AROWS], r_y[AROWS], r_x[AROWS];
+  const int r_c = (slot8 ^ (((wid * 8 + rsub) >> 1) & 7)) * 8;
 #pragma unroll
   for (int i = 0; i < AROWS; ++i) {
     const int row = wid * 8 + rsub + RPP * i;
@@ -189,7 +228,7 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
     const int r = mm - n * HWq;
     const int qy = (int)fdiv((uint32_t)r, fd_wq);
     const int qx = r - qy * g.Wq;
-    r_img[i] = n * a.H * a.W;
+    r_img[i] = (n - img0) * a.H * a.W;
     if (MODE == 0) {
       r_y[i] = qy * a.stride - a.pad;
       r_x[i] = qx * a.stride - a.pad;
@@ -199,22 +238,20 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
     }
     if (m >= g.Mc) r_y[i] = -(1 << 28);
   }
-  const long wrow = (MODE == 0) ? (long)g.Kc : (long)a.KH * a.KW * C;
-  const bf16* b_base[BROWS];
-  bool b_ok[BROWS];
+  uint32_t b_vo[BROWS];
 #pragma unroll
   for (int i = 0; i < BROWS; ++i) {
-    const int row = wid * 8 + rsub + RPP * i;
-    const int co = n0 + row;
-    b_ok[i] = co < a.Cout;
-    b_base[i] = w + (long)(b_ok[i] ? co : 0) * wrow + r_c;
+    const int co = n0 + wid * 8 + rsub + RPP * i;
+    b_vo[i] = co < a.Cout ? (uint32_t)((co * wrow + r_c) * 2) : OOB;
   }
   const FastDiv fd_c = make_fastdiv((uint32_t)C), fd_ti = make_fastdiv((uint32_t)g.Ti);
-  const bf16* a_ptr[AROWS];
-  long woff = 0;
+  uint32_t a_vo[AROWS];
+  int a_soff = 0, w_soff = 0;
+  bool a_first = true;
 
-  // source pointers of K tile kt (FASTK: one tap x one source tensor per 64-deep tile; the
-  // row pointers are formed once per channel segment and then advanced by 64 per tile)
+  // offsets of K tile kt (FASTK: one tap x one source tensor per 64-deep tile; the row
+  // offsets are formed once per channel segment, later tiles of the segment only move the
+  // uniform soffset by 128 B)
   auto prep = [&](int kt) __attribute__((always_inline)) {
     const int k0 = kt * BK;
     const int tap = (int)fdiv((uint32_t)k0, fd_c);
@@ -223,7 +260,7 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
     const int t_x = tap - t_y * g.Ti;
     if (kt == 0 || ci0 == 0 || ci0 == C1) {
       const bool s1 = ci0 < C1;
-      const bf16* src = s1 ? x1 : x2;
+      a_first = s1;
       const int cs = s1 ? C1 : C2;
       const int cio = s1 ? ci0 : ci0 - C1;
 #pragma unroll
@@ -244,28 +281,27 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
           ix = r_x[i] - t_x;
           inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
         }
-        const long off = (long)(r_img[i] + iy * a.W + ix) * cs + cio + r_c;
-        a_ptr[i] = inb ? src + off : zero;
+        a_vo[i] = inb ? (uint32_t)(((r_img[i] + iy * a.W + ix) * cs + cio + r_c) * 2) : OOB;
       }
+      a_soff = 0;
     } else {
-#pragma unroll
-      for (int i = 0; i < AROWS; ++i) a_ptr[i] += BK;
+      a_soff += BK * 2;
     }
     if (MODE == 0) {
-      woff = k0;
+      w_soff = k0 * 2;
     } else {
       const int ky = g.ky0 + a.stride * t_y, kx = g.kx0 + a.stride * t_x;
-      woff = (long)(ky * a.KW + kx) * C + ci0;
+      w_soff = ((ky * a.KW + kx) * C + ci0) * 2;
     }
   };
-  // glds number q (A rows first, then B rows) of the prepared tile into LDS slot SLOT
+  // load number q (A rows first, then B rows) of the prepared tile into LDS slot SLOT
   auto fire = [&](auto slot_c, int q) __attribute__((always_inline)) {
     constexpr int SLOT = decltype(slot_c)::value;
     if (q < AROWS) {
-      glds16(a_ptr[q], As + SLOT * (G::A_SLOT / 2) + (wid * 8 + RPP * q) * BK);
+      bld16(a_first ? rx1 : rx2, As + SLOT * (G::A_SLOT / 2) + (wid * 8 + RPP * q) * BK, a_vo[q], a_soff);
     } else {
       const int i = q - AROWS;
-      glds16(b_ok[i] ? b_base[i] + woff : zero, Bs + SLOT * (G::B_SLOT / 2) + (wid * 8 + RPP * i) * BK);
+      bld16(rw, Bs + SLOT * (G::B_SLOT / 2) + (wid * 8 + RPP * i) * BK, b_vo[i], w_soff);
     }
   };
   auto issue_all = [&](auto slot_c, int kt) __attribute__((always_inline)) {
@@ -355,6 +391,7 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
   __builtin_amdgcn_sched_barrier(0);
   read_step(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, fr[0]);
   read_step(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, fr[1]);
+  M32_STAMP(1, __builtin_amdgcn_s_memtime());
 
   // ---- one 64-deep K tile; T = kt mod 6 (ring index R = T % 3, LDS slot T % STAGES)
   constexpr int QA = LOADS / 2, QB = LOADS - LOADS / 2;   // glds in steps 2 / 3
@@ -416,6 +453,7 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
     if (++kt >= kt1) break;
   }
   __syncthreads();  // every wave done with the ring before the epilogue reuses the LDS
+  M32_STAMP(2, __builtin_amdgcn_s_memtime());
 
   bf16* Cs = reinterpret_cast<bf16*>(smem);
   constexpr int LDC = BN + 8;
@@ -423,6 +461,11 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
   __syncthreads();
   conv_epilogue_tail<BM, BN, MODE, NT, EXT>(a, g, m0, n0, Cs, reinterpret_cast<float*>(smem + BM * LDC * 2), smem,
                                             fd_hwq, fd_wq);
+#ifdef P2P_M32_STAMPS
+  __syncthreads();
+  M32_STAMP(3, __builtin_amdgcn_s_memtime());
+  M32_STAMP(5, __builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 template <int BN, int MODE, bool RELU, bool EXT>
@@ -471,13 +514,21 @@ static std::atomic<int>& m32_flag() {
 extern "C" int p2p_m32_enabled() { return m32_flag().load(std::memory_order_relaxed); }
 extern "C" int p2p_set_m32(int on) { return m32_flag().exchange(on ? 1 : 0); }
 
+#ifdef P2P_M32_STAMPS
+extern "C" int p2p_m32_stamps(void* host_out, int nblocks) {
+  if (nblocks > 65536) nblocks = 65536;
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(p2p::m32_stamps), (size_t)nblocks * 6 * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
+
 // variant 5 -> 256 x 256 tile (Cout > 128), 4 -> 256 x 128 (Cout > 64); -2 = not covered
 extern "C" int p2p_conv_fwd_m32(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t st) {
   using namespace p2p;
-  if (!a->zero || a->fp8 != 0 || a->splits > 1 || a->d2s) return -2;
+  if (a->fp8 != 0 || a->splits > 1 || a->d2s) return -2;
   if (a->C1 % 64 || a->C2 % 64 || a->C1 > 1024 || a->C2 > 1024) return -2;
   if (a->act_in != ACT_NONE && a->act_in != ACT_RELU) return -2;
-  if (a->act_in == ACT_RELU) return -2;   // (its 256-wide tile spills: stays on the 16x16 kernel for now)
+  // (the ReLU 256-wide variants spill a few loop-invariant epilogue values before the K loop; the loop itself is spill-free)
   if (variant == 5 && a->Cout > 128)
     return mode == 0 ? dispatch_m32_epi<256, 0>(*a, st) : dispatch_m32_epi<256, 1>(*a, st);
   if (variant == 4 && a->Cout > 64)

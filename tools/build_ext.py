@@ -109,6 +109,12 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False, defines=(),
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
+        # a kernel whose host launch stub hipcc silently dropped links fine and only fails at
+        # dlopen (undefined __device_stub__ symbol): refuse such a library here
+        nm = subprocess.run(["nm", "-u", "-C", OUT + ".tmp"], capture_output=True, text=True)
+        bad = [ln.strip() for ln in nm.stdout.splitlines() if "__device_stub__" in ln or "p2p::" in ln]
+        if bad:
+            raise RuntimeError("undefined kernel symbols in the linked library:\n" + "\n".join(bad[:20]))
         os.replace(OUT + ".tmp", OUT)
     return OUT
 
