@@ -90,25 +90,35 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
                                            (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL), 0x00020000);
 }
 
-// bias + output activation in registers -> the bf16 tile in LDS (row stride LDC) from the
-// 32x32 accumulator layout: acc[i][j][r] = D[i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5)][j*32 + lane&31]
+// bias + output activation in registers -> the bf16 tile in LDS (row stride LDC).  The MFMAs
+// run with the operands swapped (weights = src A, pixels = src B), so the 32x32 accumulator
+// holds D[pixel][channel] transposed: acc[i][j][4 g + e] = D[i*32 + (lane & 31)]
+// [j*32 + 8 g + 4 (lane >> 5) + e] -- a lane owns 4 consecutive channels of one pixel per
+// register quad and stages them with ONE ds_write_b64 (a quarter of the 2-B stores).
 template <int TM, int TN, int LDC>
 __device__ __forceinline__ void stage_tile32(const ConvFwdArgs& a, f32x16 (&acc)[TM][TN], bf16* Cs, int row0,
                                              int col0, int n0, int lane) {
+  static_assert(LDC % 4 == 0, "8-B aligned staging rows");
   const float al = a.alpha ? a.alpha[0] : 1.f;
+  const int h = lane >> 5, pr = lane & 31;
   auto stage = [&](auto act_tag) __attribute__((always_inline)) {
     constexpr int ACT = decltype(act_tag)::value;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int coll = col0 + j * 32 + (lane & 31);
-      const int col = n0 + coll;
-      const float bj = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int rowb = row0 + i * 32 + 4 * (lane >> 5);
+      for (int q = 0; q < 4; ++q) {
+        const int coll = col0 + j * 32 + 8 * q + 4 * h;
+        const int col = n0 + coll;
+        float bj[4];
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          Cs[(rowb + (r & 3) + 8 * (r >> 2)) * LDC + coll] = (bf16)act_fwd(acc[i][j][r] * al + bj, ACT);
+        for (int e = 0; e < 4; ++e) bj[e] = (a.bias && col + e < a.Cout) ? a.bias[col + e] : 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          bf16x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (bf16)act_fwd(acc[i][j][4 * q + e] * al + bj[e], ACT);
+          *reinterpret_cast<bf16x4*>(Cs + (row0 + i * 32 + pr) * LDC + coll) = v;
+        }
       }
     }
   };
@@ -359,8 +369,9 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f.a[i]),
-                                                             __builtin_bit_cast(bf16x8, f.b[j]), acc[i][j], 0, 0, 0);
+        // weights as src A, pixels as src B: the accumulator comes out pixel-major (stage_tile32)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f.b[j]),
+                                                             __builtin_bit_cast(bf16x8, f.a[i]), acc[i][j], 0, 0, 0);
         const int p = i * TN + j;
         if (NQ > 0 && ((p + 1) * NQ) / P > (p * NQ) / P && refill) {
           __builtin_amdgcn_sched_barrier(0);
