@@ -19,16 +19,11 @@
 #include <vector>
 
 #include "conv.h"
-
-// boolean environment knob (A/B experiments): unset -> dflt, "0" -> false, else true
-static bool env_flag(const char* name, bool dflt) {
-  const char* v = std::getenv(name);
-  return v ? v[0] != '0' : dflt;
-}
+#include "knobs.h"
 
 // fp8 layers the stride-2 halo kernel takes (P2P_S2T_F8, read per call): bit 0 the e4m3
 // ConvT forward, bit 1 the e5m2 input gradient (extended epilogue)
-static int s2t_f8_mask() {
+static int s2t_f8_mask() {   // (read per call: tests/test_fp8_gpu.py pins both variants on)
   constexpr int kDefault = 1;   // input gradient off: B=256 fp8 8955 (both) vs 9087 (forward only), profiles/bench_fp8_r4fb.jsonl
   const char* v = std::getenv("P2P_S2T_F8");
   return v ? std::atoi(v) & 3 : kDefault;
@@ -168,7 +163,7 @@ const void* zero_page(const Tensor& like) {
 // Auto: 5 when it still yields >= 256 tiles (one per CU; measured: it wins on every such
 // U-Net / PatchGAN layer and loses below, profiles/conv_layers_r1d.jsonl), else 4 / 2.
 int conv_variant(int64_t Cout, int64_t kmax, int64_t tiles256 = 0) {
-  const char* v = std::getenv("P2P_CONV_VARIANT");
+  const char* v = std::getenv("P2P_CONV_VARIANT");   // per call: tests force tiles per case
   if (v && v[0] == 'v') return 1;
   const int v4 = (Cout > 64 && kmax > 256) ? 4 : 2;
   const bool big = Cout > 128 && kmax > 256;
@@ -306,9 +301,9 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   a.splits = 1;
   a.zero = zero_page(x1);
   {
-    const char* cm = std::getenv("P2P_CLASS_MAJOR");
+    const char* cm = P2P_KNOB_ONCE("P2P_CLASS_MAJOR");
     a.cls_major = (cm && cm[0] == '1') ? 1 : 0;
-    const char* es = std::getenv("P2P_EPI_SERIAL");
+    const char* es = P2P_KNOB_ONCE("P2P_EPI_SERIAL");
     a.epi_serial = (es && es[0] == '1') ? 1 : 0;
   }
   a.stats = nullptr;
@@ -434,14 +429,14 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   const int64_t s2t_chc = fp8 ? 128 : 64;
   const bool s2t_ok = mode == 1 && splits == 1 && KH == 4 && KW == 4 && stride == 2 && pad == 1 &&
                       !reflect && up == 1 && OH == 2 * H && OW == 2 * W &&
-                      (W == 64 || (W == 32 && !fp8 && env_flag("P2P_S2T_W32", false))) &&
+                      W == 64 &&
                       (H * W) % 128 == 0 && Cout % 64 == 0 && C1 % s2t_chc == 0 && C2 % s2t_chc == 0 &&
                       C1 + C2 >= s2t_chc && C1 + C2 <= 256 &&
                       (act_in == 0 || (act_in == 1 && act_bwd == 0 && !res)) && act_out <= 2 &&
                       (fp8 != 2 || act_in == 0) && (fp8 != 1 || (!act_bwd && !res)) &&
                       (!fp8 || (s2t_f8_mask() & (int)fp8)) && std::getenv("P2P_NO_S2T") == nullptr;
   if (s2t_ok) bm = 128;
-  if (env_flag("P2P_ROUTE_LOG", false))   // routing trace (tools): one line per conv call
+  if (P2P_KNOB_ONCE("P2P_ROUTE_LOG"))   // routing trace (tools): one line per conv call
     fprintf(stderr, "[route] mode %d N %ld C %ld+%ld %ldx%ld -> %ld %ldx%ld k%d s%d p%d act_in %d act_bwd %d res %d "
             "fp8 %d splits %d s2t %d bm %d bn %d tiles %ld\n", (int)mode, (long)N, (long)C1, (long)C2, (long)H,
             (long)W, (long)Cout, (long)OH, (long)OW, (int)KH, (int)stride, (int)pad, (int)act_in, (int)act_bwd,
@@ -451,7 +446,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     // per-split fp32 slabs (plain stores, no zero fill) summed in split order by
     // conv_finalize: deterministic, and no atomics; P2P_SPLITK_ATOMIC=1 restores the
     // fp32-atomic accumulation into one zero-filled buffer (A/B only)
-    const char* av = std::getenv("P2P_SPLITK_ATOMIC");
+    const char* av = P2P_KNOB_ONCE("P2P_SPLITK_ATOMIC");
     a.det = (av && av[0] == '1') ? 0 : 1;
     ws = a.det ? at::empty({splits, N * OH * OW, Cout}, obf.options().dtype(at::kFloat))
                : at::zeros({1, N * OH * OW, Cout}, obf.options().dtype(at::kFloat));
@@ -513,7 +508,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       a.nb_gamma = nb_gamma ? nb_gamma->data_ptr<float>() : nullptr;
       a.nb_beta = nb_gamma ? nb_beta->data_ptr<float>() : nullptr;
       a.nb_act = (int)nb_act;
-      a.nb_gate = (nb_gate && !nb_colsum && nb_act == 0 && std::getenv("P2P_NB_GATE_LOAD") == nullptr) ? 1 : 0;
+      a.nb_gate = (nb_gate && !nb_colsum && nb_act == 0 && P2P_KNOB_ONCE("P2P_NB_GATE_LOAD") == nullptr) ? 1 : 0;
       a.nb_batch = nb_batch ? 1 : 0;
       a.nb_c0 = (int)c0;
       a.nb_C = (int)nC;
@@ -545,8 +540,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   bool fold_late = false;
   if (fold) {
     const int64_t bw = fold_edge ? 1 : fold_p;   // band rows / columns per side (elementwise.hip fold_band)
-    fold_late = splits > 1 || halo_cond || fold_H < 2 * bw + 2 || fold_W < 2 * bw + 2 ||
-                std::getenv("P2P_FOLD_LATE") != nullptr;
+    fold_late = splits > 1 || halo_cond || fold_H < 2 * bw + 2 || fold_W < 2 * bw + 2;
     if (fold_late) {
       a.y1 = fbuf.data_ptr();
       a.xb1 = nullptr;

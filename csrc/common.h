@@ -1,5 +1,6 @@
 // Shared device helpers for the p2p_pytorch_amd HIP/CDNA4 (gfx950) kernels.
 #pragma once
+#include "knobs.h"
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -130,6 +131,7 @@ __device__ __forceinline__ float warp_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+
 
 // Raise a kernel's dynamic-LDS limit once per DEVICE (the attribute is per device: a second
 // GPU driven by the same process needs its own call).  ``mask``: one static per kernel

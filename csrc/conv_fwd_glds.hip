@@ -36,20 +36,6 @@ __device__ __forceinline__ i32x8 cat8(u32x4 lo, u32x4 hi) {
                                  6, 7);
 }
 
-#ifdef P2P_EXP_NORMFRAG
-// Experiment (profiles/kernel_experiments_r3.md): the consumer-side instance
-// norm apply, y = lrelu(x * s + t), on every A fragment after its ds_read -- the VALU cost a
-// fused "normalise in the consumer's operand path" adds to each conv.  s, t are per-lane
-// registers set once (a LOWER bound: the real fusion also reloads them per channel block).
-__device__ __forceinline__ bf16x8 normfrag8(bf16x8 v, const float (&s)[8], const float (&t)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float f = fmaf((float)v[j], s[j], t[j]);
-    v[j] = (bf16)fmaxf(f, 0.2f * f);
-  }
-  return v;
-}
-#endif
 
 // ReLU on 16 packed fp8 (e4m3 / e5m2: sign = bit 7 of each byte): zero the negative bytes
 __device__ __forceinline__ uint32_t relu_fp8x4(uint32_t w) {
@@ -323,20 +309,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#ifdef P2P_EXP_NORMFRAG
-  float nf_s[8], nf_t[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    nf_s[j] = 1.f + 1e-3f * (float)((lane + j) & 7);
-    nf_t[j] = 1e-3f * (float)((lane >> 3) & 7);
-  }
-#endif
 
-#ifdef P2P_NO_LATE
-  constexpr bool LATE = false;
-#else
   constexpr bool LATE = STAGES == 2 && F8 == 0;
-#endif
   if constexpr (LATE) {
     // 2-slot ring with prefetch distance 2: each K tile's fragments are read into registers
     // up front (they already were), a second barrier then frees its slot, and tile kt + 2 is
@@ -380,10 +354,6 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
           for (int i = 0; i < TM; ++i)
             af[i] = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, af[i])));
         }
-#ifdef P2P_EXP_NORMFRAG
-#pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = normfrag8(af[i], nf_s, nf_t);
-#endif
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -477,10 +447,6 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
           for (int i = 0; i < TM; ++i)
             af[kk][i] = __builtin_bit_cast(bf16x8, relu8(__builtin_bit_cast(u32x4, af[kk][i])));
         }
-#ifdef P2P_EXP_NORMFRAG
-  #pragma unroll
-        for (int i = 0; i < TM; ++i) af[kk][i] = normfrag8(af[kk][i], nf_s, nf_t);
-#endif
   #pragma unroll
         for (int i = 0; i < TM; ++i)
   #pragma unroll

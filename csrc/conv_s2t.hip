@@ -485,9 +485,6 @@ __device__ __forceinline__ void s2t_epilogue(const ConvFwdArgs& a, f32x4 (&acc)[
 
 }  // namespace
 
-// arrival counters of the persistent blocks per CU (key: XCC, SE, SH, CU of the hardware id)
-__device__ unsigned s2t_cu_arrivals[8 * 512];
-
 // timeline probe (P2P_S2T_DEBUG=1, tools/s2t_timeline.py): per block and tile, wave 0's
 // s_memrealtime (100 MHz) at the tile's loop start, epilogue start, epilogue end, and the
 // block's hardware id (XCC << 16 | HW_ID >> 8) -- diagnostics only, never in a timed run
@@ -499,7 +496,7 @@ __device__ __forceinline__ void s2t_stamp(int dbg, int k, int field) {
 }
 
 template <int W, bool RELU, bool EXT, int F8 = 0>
-__global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a, int ntiles, int stagger_ns, int stagger_mode, int dbg) {
+__global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a, int ntiles, int dbg) {
   using G = S2TGeom<W>;
   constexpr int ES = F8 ? 1 : 2;      // bytes per operand element
   constexpr int CHC = 128 / ES;       // channels per 128-B halo chunk
@@ -521,37 +518,11 @@ __global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a, int nti
   const int grid = gridDim.x;
   int L = xcd_remap(blockIdx.x, grid);
   if (L >= ntiles) return;
-  // two persistent blocks share a CU and run identical tiles: started together they stay in
-  // lockstep, both in their MFMA loops, then both in their memory-bound epilogues.  The
-  // second block to arrive on a CU starts stagger_ns later, so one block's epilogue runs
-  // beside the other's MFMAs (a speed heuristic only: any placement computes the same tiles)
   if (dbg && tid == 0 && blockIdx.x < S2T_DBG_BLOCKS) {
     unsigned hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     s2t_dbg[(size_t)blockIdx.x * S2T_DBG_TILES * 4 + 3] = ((unsigned long long)xcc << 16) | (hw >> 8);
-  }
-  if (stagger_ns > 0 && stagger_mode == 1) {
-    // blocks 0 .. grid/2 - 1 fill one slot per CU first, the second half pairs with them
-    if (blockIdx.x >= grid / 2) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) * 10 < stagger_ns) __builtin_amdgcn_s_sleep(32);
-    }
-  } else if (stagger_ns > 0) {
-    if (tid == 0) {
-      unsigned hw, xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      const unsigned key = ((xcc & 7u) << 9) | ((hw >> 8) & 511u);
-      *reinterpret_cast<volatile int*>(ring) = (int)(atomicAdd(&s2t_cu_arrivals[key], 1u) & 1u);
-    }
-    __syncthreads();
-    const int late = *reinterpret_cast<volatile int*>(ring);
-    __syncthreads();
-    if (late) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) * 10 < stagger_ns) __builtin_amdgcn_s_sleep(32);
-    }
   }
   auto tile_geo = [&](int Lt, int& m0, int& n0, int& img, int& qy0) __attribute__((always_inline)) {
     const int mt = Lt / ntiles_n;
@@ -814,14 +785,10 @@ static int launch_s2t(const ConvFwdArgs& a, hipStream_t st) {
   static std::atomic<uint64_t> attr_mask{0};
   smem_attr_once(reinterpret_cast<const void*>(&conv_s2t_kernel<W, RELU, EXT, F8>), smem, attr_mask);
   const long tiles = (long)a.N * a.H * a.W / BM * (a.Cout / BN);
-  const char* e = std::getenv("P2P_S2T_STAGGER");   // ns (A/B knob)
-  const int stagger = e ? std::atoi(e) : 0;
-  const char* em = std::getenv("P2P_S2T_STAGGER_MODE");   // 0: per-CU arrival order, 1: grid halves
-  const int smode = em ? std::atoi(em) : 0;
-  const char* ed = std::getenv("P2P_S2T_DEBUG");
+  const char* ed = P2P_KNOB_ONCE("P2P_S2T_DEBUG");   // timeline stamps (tools/s2t_timeline.py)
   const int dbg = (ed && ed[0] == '1') ? 1 : 0;
   hipLaunchKernelGGL((conv_s2t_kernel<W, RELU, EXT, F8>), dim3((unsigned)s2t_grid(tiles)), dim3(NT), smem, st, a,
-                     (int)tiles, stagger, smode, dbg);
+                     (int)tiles, dbg);
   return (int)hipGetLastError();
 }
 
@@ -861,11 +828,10 @@ extern "C" int p2p_conv_s2t(const p2p::ConvFwdArgs* a, hipStream_t st) {
     if (a->W != 64) return -2;
     return a->fp8 == 1 ? dispatch_s2t_w<64, 1>(*a, ext, st) : dispatch_s2t_w<64, 2>(*a, ext, st);
   }
-  switch (a->W) {
-    case 32: return dispatch_s2t_w<32, 0>(*a, ext, st);
-    case 64: return dispatch_s2t_w<64, 0>(*a, ext, st);
-    default: return -2;
-  }
+  // 64-wide grids only: the 32-wide variant measured slower at the step level
+  // (profiles/kernel_experiments_r4.md section 1; its P2P_S2T_W32 opt-in was removed in round 5)
+  if (a->W != 64) return -2;
+  return dispatch_s2t_w<64, 0>(*a, ext, st);
 }
 
 // timeline probe read-out (tools/s2t_timeline.py through torch.ops.p2p.s2t_debug)

@@ -950,7 +950,7 @@ static int wgrad_glds_shape(const p2p::ConvWgradArgs* a) {
     if ((a->p_act != p2p::ACT_NONE && a->p_act != p2p::ACT_RELU) ||
         (a->q_act != p2p::ACT_NONE && a->q_act != p2p::ACT_RELU))
       return 0;
-    const char* v0 = std::getenv("P2P_CONV_VARIANT");
+    const char* v0 = std::getenv("P2P_CONV_VARIANT");   // per call: tests force tiles per case
     return (v0 && v0[0] == 'v') ? 0 : 3;
   }
   if (a->R % 128) return 0;
@@ -962,7 +962,7 @@ static int wgrad_glds_shape(const p2p::ConvWgradArgs* a) {
   if (v && v[0] == 'v') return 0;
   // 4 = 256x256 (half the VALU + LDS fragment traffic per MFMA of 1 / 2); P2P_WGRAD_TILE=256
   // selects it for the weight gradients alone (census A/B)
-  const char* wt = std::getenv("P2P_WGRAD_TILE");
+  const char* wt = P2P_KNOB_ONCE("P2P_WGRAD_TILE");
   const bool w256 = (v && v[0] == 'g' && v[1] == '5') || (wt && wt[0] == '2' && wt[1] == '5');
   if (w256 && a->R % 256 == 0 && a->Kq % 256 == 0) return 4;
   if (a->R >= 256) return 1;
@@ -972,7 +972,16 @@ static int wgrad_glds_shape(const p2p::ConvWgradArgs* a) {
   return a->Kq >= 256 ? 2 : 0;
 }
 
+extern "C" int p2p_m32_enabled();
+extern "C" int p2p_conv_wgrad_m32_ok(const p2p::ConvWgradArgs* a);
+extern "C" int p2p_conv_wgrad_m32(const p2p::ConvWgradArgs* a, hipStream_t st);
+
 extern "C" int p2p_conv_wgrad_tile(const p2p::ConvWgradArgs* a, int* tr, int* tq) {
+  if (p2p_m32_enabled() && p2p_conv_wgrad_m32_ok(a)) {   // conv_wgrad_m32.hip: 256 x 256
+    *tr = 256;
+    *tq = 256;
+    return 6;
+  }
   const int shape = wgrad_glds_shape(a);
   if (shape == 1) { *tr = 256; *tq = 128; return shape; }
   if (shape == 2) { *tr = 128; *tq = 256; return shape; }
@@ -1054,6 +1063,10 @@ extern "C" int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t st) {
     if (shape8 == 1) return wg8_launch_rm<256, 128, 4, 2, 3>(rm, *a, st);
     return wg8_launch_rm<128, 256, 2, 4, 3>(rm, *a, st);
   }
+  if (p2p_m32_enabled()) {
+    const int rc = p2p_conv_wgrad_m32(a, st);
+    if (rc != -2) return rc;
+  }
   const int shape = wgrad_glds_shape(a);
   if (shape) {
     constexpr int STG = 3;
@@ -1096,8 +1109,7 @@ extern "C" int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int 
   const long total = (long)R * KH * KW * C;
   int G = 1;
   while (G < 32 && splits > 8 * G) G *= 2;   // <= ~8 slab reads per thread
-  const bool old_red = std::getenv("P2P_WRED_OLD") != nullptr;   // A/B: 4-B scattered stores (per call)
-  if (!old_red && KH * KW <= 81) {
+  if (KH * KW <= 81) {
     const dim3 grid((unsigned)((C + 31) / 32), (unsigned)R);
 #define P2P_REDT(g)                                                                                       \
   case g:                                                                                                  \

@@ -1,0 +1,436 @@
+// Weight gradient of conv / transposed conv on gfx950 v_mfma_f32_32x32x16_bf16, 256 x 256 tiles.
+//
+//   dW[R][Kq] = sum_m P[m][R] * im2col(Q)[m][Kq]      (conv_wgrad.hip has the GEMM view)
+//
+// the 16x16x32 256x128 tile ran at 31-34 % MFMA busy with 4.5-5.5 VALU
+// per MFMA.  This kernel is the conv_fwd_m32.hip recipe applied to the weight gradient:
+//  * 256 (R) x 256 (Kq) output tile, 8 waves of 128 x 64 -- 128 FLOP per staged byte
+//    instead of the 256x128 tile's 85 -- on v_mfma_f32_32x32x16_bf16 (half the MFMA
+//    instructions; each leaves 24 of its 32 issue cycles to the loader / fragment reads);
+//  * both operands are read k-transposed (the reduction index m is the OUTER dimension of
+//    the NHWC tensors) with ds_read_b64_tr_b16: a 32x32x16 fragment is two of them (k rows
+//    8h..8h+3 and 8h+4..8h+7 of 32 columns).  LDS sub-tiles are [64 m][128 cols] with the
+//    16-B chunk XOR-swizzled by 4 * (row & 3): the 4 rows x 4 chunks a half-wave reads per
+//    transposed load land on 16 distinct chunks -- every bank once;
+//  * a 2-deep fragment ring (12 transposed reads per k16 step: two steps in flight would
+//    overflow the 4-bit lgkm counter), counted waits, ONE barrier per 64-pixel stage, the
+//    refill loads interleaved one per MFMA in the stage's last k16 step;
+//  * the Q (im2col) rows walk the pixels incrementally: (n, oh, ow) advance by the constant
+//    decomposition of 64 pixels per stage with two carries (no divisions in the loop).
+// Split-K over m is kept (fp32 slabs, ordered reduce in conv_wgrad.hip), so results stay
+// bitwise deterministic for a given split count.
+#include <atomic>
+#include <cstdlib>
+
+#include "common.h"
+#include "conv.h"
+
+namespace p2p {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int WM32_SROWS = 64;     // pixels per stage (4 k16 steps)
+constexpr int WM32_TB = 256;       // tile edge (R and Kq)
+constexpr int WM32_NT = 512;
+constexpr int WM32_SUB = 64 * 128 * 2;              // bytes of a [64][128] bf16 sub-tile
+constexpr int WM32_STAGE = 4 * WM32_SUB;            // P: 2 sub-tiles, Q: 2 sub-tiles
+constexpr int WM32_SMEM = 2 * WM32_STAGE;           // 2-slot ring, 128 KB
+
+template <int N>
+__device__ __forceinline__ void wm32_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ uint32_t wm32_lds(const void* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)p));
+}
+
+// (device-only helpers: the builtins called from the kernel's lambdas made hipcc's host pass
+// drop the kernel launch stubs -- see conv_fwd_m32.hip bld16)
+__device__ __forceinline__ void wm32_bld(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(lds), 16, voff, soff, 0, 0);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wm32_rsrc(const void* base, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL), 0x00020000);
+}
+
+// one 32x32x16 operand fragment from a per-lane address: k rows 8h..8h+3 / 8h+4..8h+7 are
+// immediate offsets (row & 3 -- the swizzle key -- is the same for both)
+template <int OFF>
+__device__ __forceinline__ u32x4 tr_frag32(uint32_t addr) {
+  static_assert(OFF >= 0 && OFF + 4 * 256 < 65536, "ds offset field");
+  uint64_t lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(addr), "i"(OFF));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(addr), "i"(OFF + 4 * 256));
+  return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+}
+
+struct WFrag {
+  u32x4 a[4];   // P^T fragments (R rows)
+  u32x4 b[2];   // Q fragments (Kq columns)
+};
+
+template <int N>
+__device__ __forceinline__ void wfrag_wait(WFrag& f) {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt range");
+  asm volatile("s_waitcnt lgkmcnt(%6)"
+               : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.a[2]), "+v"(f.a[3]), "+v"(f.b[0]), "+v"(f.b[1])
+               : "n"(N));
+}
+
+// physical 16-B chunk of logical chunk c in row r of a [64][128] sub-tile
+__device__ __forceinline__ int wm32_chunk(int r, int c) { return c ^ (4 * (r & 3)); }
+
+}  // namespace
+
+// RM: bit 0 = ReLU on the P fragments, bit 1 = ReLU on the Q fragments
+template <int RM>
+__global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
+  constexpr int TM = 4, TN = 2, WN = 4;
+  constexpr int NR = 2 * (TM + TN);    // transposed reads per k16 step
+  constexpr int PL = 4, QL = 4, LOADS = PL + QL;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int qtiles = (a.Kq + WM32_TB - 1) / WM32_TB;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int rt = bid / qtiles, qt = bid % qtiles;
+  const int r0 = rt * WM32_TB, q0 = qt * WM32_TB;
+
+  const int stages = (a.M + WM32_SROWS - 1) / WM32_SROWS;
+  const int sps = (stages + a.splits - 1) / a.splits;
+  const int s0 = blockIdx.y * sps;
+  const int s1 = min(stages, s0 + sps);
+
+  // ---- loader: buffer_load ... lds (32-bit offsets from a per-split base, out-of-range
+  // offsets read zero).  A wave instruction fills 4 rows x 16 chunks (1 KB) of one sub-tile;
+  // load i of wave w: sub-tile i & 1, rows 4 (w + 8 (i >> 1)) + (lane >> 4) -> every lane has
+  // TWO pixel rows (rr = i >> 1) and TWO column chunks (s = i & 1) per operand.  The host
+  // guarantees each 128-column sub-tile lies inside one concat half (R1 / C1 % 128 == 0) and
+  // a split's byte span fits in 31 bits (p2p_conv_wgrad_m32_ok).
+  constexpr uint32_t OOB = 0x80000000u;
+  const int lrow = lane >> 4, pch = lane & 15;
+  const int rowi0 = 4 * wid + lrow;               // rows rowi0 and rowi0 + 32 (same row & 3)
+  const int lch = wm32_chunk(rowi0, pch);        // logical chunk this lane fetches
+  const long pm0 = (long)s0 * WM32_SROWS;         // first pixel of this split
+  // P: [M][ld] per concat half; sub s covers columns r0 + 128 s + [0, 128)
+  __amdgpu_buffer_rsrc_t rp[2];
+  uint32_t p_vo[2];
+  int p_ld2[2];   // row stride in bytes
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int cb = r0 + 128 * s;                  // sub-tile's first column (uniform)
+    const bool first = cb < a.R1;
+    const int ld = first ? a.R1 : a.R2;
+    const bf16* src = first ? static_cast<const bf16*>(a.p1) : static_cast<const bf16*>(a.p2);
+    rp[s] = wm32_rsrc(src + pm0 * ld, ((long)a.M - pm0) * ld * 2);
+    const int col = cb + 8 * lch - (first ? 0 : a.R1);
+    p_vo[s] = (cb + 8 * lch < a.R) ? (uint32_t)((rowi0 * ld + col) * 2) : OOB;
+    p_ld2[s] = ld * 2;
+  }
+  // Q (im2col of an NHWC image tensor): kq = q0 + 128 s + 8 * lch -> (tap, ci); the resource
+  // base is this split's first image
+  const int OHW = a.OH * a.OW;
+  const FastDiv fd_ohw = make_fastdiv((uint32_t)OHW), fd_ow = make_fastdiv((uint32_t)a.OW);
+  const int n_base = (int)fdiv((uint32_t)pm0, fd_ohw);
+  const long img = (long)a.H * a.W;
+  __amdgpu_buffer_rsrc_t rq[2];
+  int q_kh[2], q_kw[2];
+  uint32_t q_cofs[2];        // channel byte offset within a pixel, OOB for kq >= Kq
+  int q_ld2[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int kqb = q0 + 128 * s;                 // sub-tile's first kq (uniform)
+    const int kq = kqb + 8 * lch;
+    const int tapb = kqb / a.C, cib = kqb - tapb * a.C;
+    const bool first = cib < a.C1;                // whole sub in one half (host)
+    const int ld = first ? a.C1 : a.C2;
+    const bf16* src = first ? static_cast<const bf16*>(a.q1) : static_cast<const bf16*>(a.q2);
+    rq[s] = wm32_rsrc(src + n_base * img * ld, ((long)a.N - n_base) * img * ld * 2);
+    const int tap = kq / a.C, ci = kq - tap * a.C;
+    q_kh[s] = tap / a.KW;
+    q_kw[s] = tap - q_kh[s] * a.KW;
+    q_cofs[s] = kq < a.Kq ? (uint32_t)((ci - (first ? 0 : a.C1)) * 2) : OOB;
+    q_ld2[s] = ld * 2;
+  }
+  const int ush = a.up == 2 ? 1 : 0;
+  const int Hu = a.H << ush, Wu = a.W << ush;
+  int q_n[2], q_oh[2], q_ow[2];
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr) {
+    const int m = (int)pm0 + rowi0 + 32 * rr;
+    const int mm = m < a.M ? m : 0;
+    q_n[rr] = (int)fdiv((uint32_t)mm, fd_ohw);
+    const int rem = mm - q_n[rr] * OHW;
+    q_oh[rr] = (int)fdiv((uint32_t)rem, fd_ow);
+    q_ow[rr] = rem - q_oh[rr] * a.OW;
+    q_n[rr] -= n_base;
+  }
+  const int d_n = WM32_SROWS / OHW, d_rem = WM32_SROWS % OHW;
+  const int d_h = d_rem / a.OW, d_w = d_rem % a.OW;
+  uint32_t q_vo[2][2];       // [rr][s]: this stage's gather offsets
+  int p_soff[2] = {0, 0};    // stage displacement of the P rows (uniform)
+
+  // advance the pixel rows to stage st (called for consecutive stages from s0) and form the
+  // gather offsets of its Q loads; the P rows only move their uniform soffset
+  auto prep = [&](int st) __attribute__((always_inline)) {
+    const int ds = st - s0;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) p_soff[s] = ds * WM32_SROWS * p_ld2[s];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      if (ds != 0) {
+        int ow = q_ow[rr] + d_w, oh = q_oh[rr] + d_h, n = q_n[rr] + d_n;
+        if (ow >= a.OW) {
+          ow -= a.OW;
+          ++oh;
+        }
+        if (oh >= a.OH) {
+          oh -= a.OH;
+          ++n;
+        }
+        q_ow[rr] = ow;
+        q_oh[rr] = oh;
+        q_n[rr] = n;
+      }
+      const bool mok = (int)pm0 + ds * WM32_SROWS + rowi0 + 32 * rr < a.M;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        int uy = q_oh[rr] * a.stride - a.pad + q_kh[s];
+        int ux = q_ow[rr] * a.stride - a.pad + q_kw[s];
+        if (a.reflect) {
+          uy = reflect_idx(uy, Hu);
+          ux = reflect_idx(ux, Wu);
+        }
+        const bool ok = mok && (unsigned)uy < (unsigned)Hu && (unsigned)ux < (unsigned)Wu;
+        const uint32_t pix = (uint32_t)((q_n[rr] * a.H + (uy >> ush)) * a.W + (ux >> ush));
+        q_vo[rr][s] = ok ? pix * (uint32_t)q_ld2[s] + q_cofs[s] : OOB;
+      }
+    }
+  };
+  // load q of the prepared stage into slot SLOT: q 0..3 = P (row sel q >> 1, sub q & 1),
+  // q 4..7 = Q; the wave's 1 KB lands at rows 4 (wid + 8 rr) of the sub-tile
+  auto fire = [&](int slot, auto q_c) __attribute__((always_inline)) {
+    constexpr int Q = decltype(q_c)::value;
+    constexpr int RR = (Q & 3) >> 1, S = Q & 1;
+    char* dst = smem + slot * WM32_STAGE + (Q < 4 ? 0 : 2 * WM32_SUB) + S * WM32_SUB + (4 * (wid + 8 * RR)) * 256;
+    if constexpr (Q < 4) {
+      wm32_bld(rp[S], dst, p_vo[S] + RR * 32 * p_ld2[S], __builtin_amdgcn_readfirstlane(p_soff[S]));
+    } else {
+      wm32_bld(rq[S], dst, q_vo[RR][S], 0);
+    }
+  };
+
+  // ---- fragment addresses (slot 0, k16 step 0): 32x32x16 lane map -- group G = lane >> 4
+  // covers columns 16 (G & 1) + 4 p .. +3 of k rows 8 (G >> 1) + q (+4 for the high half);
+  // after the transpose lane l holds column l & 31, k = 8 (l >> 5) + j
+  uint32_t fa[TM], fb[TN];
+  {
+    const int G = lane >> 4, qq = (lane & 15) >> 2, p = lane & 3;
+    const int krow = 8 * (G >> 1) + qq;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int col = i * 32 + 16 * (G & 1) + 4 * p;   // within P sub-tile wm
+      const int ch = wm32_chunk(krow, col >> 3);
+      fa[i] = wm32_lds(smem + wm * WM32_SUB + krow * 256 + ch * 16 + (col & 7) * 2);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int colq = wn * 64 + j * 32 + 16 * (G & 1) + 4 * p;   // 0..255 over the two Q subs
+      const int sub = colq >> 7, col = colq & 127;
+      const int ch = wm32_chunk(krow, col >> 3);
+      fb[j] = wm32_lds(smem + 2 * WM32_SUB + sub * WM32_SUB + krow * 256 + ch * 16 + (col & 7) * 2);
+    }
+  }
+  // the P fragment address above is relative to sub-tile wm: wave row wm reads P columns
+  // r0 + 128 wm + [0, 128), i.e. exactly sub-tile wm (its 4 fragments are 32 columns apart)
+  // fa / fb address the CURRENT slot: toggled (bit 16 = the 64 KB slot offset) per stage
+  auto read_step = [&](auto s_c, WFrag& f) __attribute__((always_inline)) {
+    constexpr int S = decltype(s_c)::value;
+    constexpr int OFF = S * 16 * 256;   // k16 step: 16 rows further
+#pragma unroll
+    for (int i = 0; i < TM; ++i) f.a[i] = tr_frag32<OFF>(fa[i]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) f.b[j] = tr_frag32<OFF>(fb[j]);
+  };
+  auto toggle_slot = [&]() __attribute__((always_inline)) {
+    static_assert(WM32_STAGE == 1 << 16, "slot toggle = bit 16");
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa[i] ^= (uint32_t)WM32_STAGE;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[j] ^= (uint32_t)WM32_STAGE;
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // one k16 step; with `refill` one load of the next-next stage after each of the first
+  // LOADS MFMAs (TM * TN = 8 = LOADS)
+  // fire with a loop-index q (0..7): dispatched to the compile-time loads
+  auto fire_at = [&](int slot, int q) __attribute__((always_inline)) {
+    switch (q) {
+      case 0: fire(slot, std::integral_constant<int, 0>{}); break;
+      case 1: fire(slot, std::integral_constant<int, 1>{}); break;
+      case 2: fire(slot, std::integral_constant<int, 2>{}); break;
+      case 3: fire(slot, std::integral_constant<int, 3>{}); break;
+      case 4: fire(slot, std::integral_constant<int, 4>{}); break;
+      case 5: fire(slot, std::integral_constant<int, 5>{}); break;
+      case 6: fire(slot, std::integral_constant<int, 6>{}); break;
+      default: fire(slot, std::integral_constant<int, 7>{}); break;
+    }
+  };
+  auto mma_step = [&](WFrag& f, int slot, bool refill) __attribute__((always_inline)) {
+    if constexpr (RM & 1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) f.a[i] = relu8(f.a[i]);
+    }
+    if constexpr (RM & 2) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) f.b[j] = relu8(f.b[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f.a[i]),
+                                                             __builtin_bit_cast(bf16x8, f.b[j]), acc[i][j], 0, 0, 0);
+        if (refill) {
+          __builtin_amdgcn_sched_barrier(0);
+          fire_at(slot, i * TN + j);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+  };
+
+  WFrag fr[2];
+  if (s0 < s1) {
+    // ---- prologue: stages s0, s0 + 1 in flight, s0 landed, its first step being read
+    prep(s0);
+#pragma unroll
+    for (int q = 0; q < LOADS; ++q) fire_at(0, q);
+    if (s0 + 1 < s1) {
+      prep(s0 + 1);
+#pragma unroll
+      for (int q = 0; q < LOADS; ++q) fire_at(1, q);
+      wm32_vmcnt<LOADS>();
+    } else {
+      wm32_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    read_step(std::integral_constant<int, 0>{}, fr[0]);
+
+    // ---- one 64-pixel stage per iteration (2-slot ring; the loop is NOT unrolled over the
+    // slot parity: two copies of the body made the register allocator rotate the 128
+    // accumulator registers between them -- copies and spills -- so the slot is a toggled
+    // address bit and a uniform M0 offset instead)
+    int cur = 0;
+    for (int st = s0; st < s1; ++st) {
+      const bool more = st + 1 < s1;
+      const bool refill = st + 2 < s1;
+      read_step(std::integral_constant<int, 1>{}, fr[1]);
+      wfrag_wait<NR>(fr[0]);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_step(fr[0], cur, false);
+      __builtin_amdgcn_sched_barrier(0);
+      // loader address math of stage st + 2 here, beside the partner wave's MFMAs (its loads
+      // of stage st + 1 were issued one stage ago, so their addresses are no longer needed)
+      if (refill) prep(st + 2);
+      read_step(std::integral_constant<int, 2>{}, fr[0]);
+      wfrag_wait<NR>(fr[1]);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_step(fr[1], cur, false);
+      __builtin_amdgcn_sched_barrier(0);
+      read_step(std::integral_constant<int, 3>{}, fr[1]);
+      wfrag_wait<NR>(fr[0]);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_step(fr[0], cur, false);
+      __builtin_amdgcn_sched_barrier(0);
+      // sync: every read of this slot retired (step 3 landed), my share of stage st + 1 landed
+      wfrag_wait<0>(fr[1]);
+      wm32_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      toggle_slot();
+      if (more) read_step(std::integral_constant<int, 0>{}, fr[0]);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_step(fr[1], cur, refill);   // refill: stage st + 2 -> the slot just freed
+      __builtin_amdgcn_sched_barrier(0);
+      cur ^= 1;
+    }
+  }
+
+  // ---- fp32 partial slab ws[split][R][Kq]: acc[i][j][reg] = D[row (reg&3) + 8 (reg>>2) + 4 h][col l&31]
+  float* slab = a.ws + (long)blockIdx.y * a.R * a.Kq;
+  const int h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = q0 + wn * 64 + j * 32 + (lane & 31);
+      const int rowb = r0 + wm * 128 + i * 32 + 4 * h;
+      if (col < a.Kq) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = rowb + (r & 3) + 8 * (r >> 2);
+          if (row < a.R) slab[(long)row * a.Kq + col] = acc[i][j][r];
+        }
+      }
+    }
+}
+
+template <int RM>
+static int launch_wm32(const ConvWgradArgs& a, hipStream_t st) {
+  static std::atomic<uint64_t> attr_mask{0};
+  smem_attr_once(reinterpret_cast<const void*>(&conv_wgrad_m32_kernel<RM>), WM32_SMEM, attr_mask);
+  dim3 grid(((a.R + WM32_TB - 1) / WM32_TB) * ((a.Kq + WM32_TB - 1) / WM32_TB), a.splits, 1);
+  hipLaunchKernelGGL((conv_wgrad_m32_kernel<RM>), grid, dim3(WM32_NT), WM32_SMEM, st, a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace p2p
+
+// the 256x256 32x32x16 weight-gradient tile (Kq % 128 == 0, R % 128 == 0 with R >= 256 or
+// Kq >= 256; ReLU-only operand activations); -2 = not covered
+extern "C" int p2p_conv_wgrad_m32_ok(const p2p::ConvWgradArgs* a) {
+  using namespace p2p;
+  if (a->f8 || a->Kq % 128 || a->R % 128 || a->R < 256 || a->Kq < 256) return 0;
+  if ((a->p_act != ACT_NONE && a->p_act != ACT_RELU) || (a->q_act != ACT_NONE && a->q_act != ACT_RELU)) return 0;
+  // buffer resources are per 128-column sub-tile: each must lie inside one concat half
+  if ((a->R2 > 0 && a->R1 % 128) || (a->C2 > 0 && (a->C1 % 128 || a->C % 128))) return 0;
+  // 31-bit byte offsets from a split's first pixel / first image
+  // (p2p_conv_wgrad_tile asks before the host has chosen the split count: assume 1 then --
+  // the strictest span; the launch re-checks with the real count)
+  const long splits = a->splits > 0 ? a->splits : 1;
+  const long stages = (a->M + 63) / 64, sps = (stages + splits - 1) / splits;
+  const long rows = sps * 64;
+  const long ldp = a->R1 > a->R2 ? a->R1 : a->R2, ldq = a->C1 > a->C2 ? a->C1 : a->C2;
+  const long ohw = (long)a->OH * a->OW;
+  const long imgs = rows / (ohw > 0 ? ohw : 1) + 2;
+  if (rows * ldp * 2 >= (1L << 31) || imgs * a->H * a->W * ldq * 2 >= (1L << 31)) return 0;
+  return 1;
+}
+
+extern "C" int p2p_conv_wgrad_m32(const p2p::ConvWgradArgs* a, hipStream_t st) {
+  using namespace p2p;
+  if (!p2p_conv_wgrad_m32_ok(a)) return -2;
+  const int rm = (a->p_act == ACT_RELU ? 1 : 0) | (a->q_act == ACT_RELU ? 2 : 0);
+  switch (rm) {
+    case 1: return launch_wm32<1>(*a, st);
+    case 2: return launch_wm32<2>(*a, st);
+    case 3: return launch_wm32<3>(*a, st);
+    default: return launch_wm32<0>(*a, st);
+  }
+}

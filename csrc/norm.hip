@@ -27,19 +27,11 @@ struct NormGeom {
   int N, HW, C;   // groups: N x C; pixels per group: HW
   int chunk;      // pixels per block
   int nchunks;    // blocks per sample
-  int nt;         // apply passes: bit 0 nontemporal stores, bit 1 nontemporal loads (P2P_NORM_NT)
 };
 
 // streaming 16-B accesses of the apply passes (every byte touched once per pass)
-__device__ __forceinline__ u32x4 ld_stream(const bf16* p, int nt) {
-  const u32x4* q = reinterpret_cast<const u32x4*>(p);
-  return (nt & 2) ? __builtin_nontemporal_load(q) : *q;
-}
-__device__ __forceinline__ void st_stream(bf16* p, u32x4 v, int nt) {
-  u32x4* q = reinterpret_cast<u32x4*>(p);
-  if (nt & 1) __builtin_nontemporal_store(v, q);
-  else *q = v;
-}
+__device__ __forceinline__ u32x4 ld_stream(const bf16* p) { return *reinterpret_cast<const u32x4*>(p); }
+__device__ __forceinline__ void st_stream(bf16* p, u32x4 v) { *reinterpret_cast<u32x4*>(p) = v; }
 
 __device__ __forceinline__ void unpack8(u32x4 v, float* f) {
   bf16x8 b = __builtin_bit_cast(bf16x8, v);
@@ -297,7 +289,7 @@ __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict_
       f[j] = t;
     }
     const u32x4 o = pack8(f);
-    st_stream(y + off, o, g.nt);
+    st_stream(y + off, o);
     if (sh.q) {
       float r[8];
       unpack8(o, r);   // quantise the stored bf16 value: shadow == fp8(y) exactly
@@ -312,14 +304,14 @@ __global__ void __launch_bounds__(256) norm_apply_kernel(const bf16* __restrict_
     u32x4 v[4], rv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      v[u] = ld_stream(x + base + (long)(p + u * RP) * g.C, g.nt);
-      rv[u] = res ? ld_stream(res + base + (long)(p + u * RP) * g.C, g.nt) : zero4;
+      v[u] = ld_stream(x + base + (long)(p + u * RP) * g.C);
+      rv[u] = res ? ld_stream(res + base + (long)(p + u * RP) * g.C) : zero4;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) one(v[u], rv[u], base + (long)(p + u * RP) * g.C);
   }
   for (; p < p1; p += RP)
-    one(ld_stream(x + base + (long)p * g.C, g.nt), res ? ld_stream(res + base + (long)p * g.C, g.nt) : zero4,
+    one(ld_stream(x + base + (long)p * g.C), res ? ld_stream(res + base + (long)p * g.C) : zero4,
         base + (long)p * g.C);
   if (sh.q) fp8_amax_commit(qmax, sh.site);
 }
@@ -550,7 +542,7 @@ __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
       fd[j] = fmaf(ca[j], d, fmaf(k1[j], fx[j], k0[j]));
     }
     const u32x4 o = pack8(fd);
-    st_stream(dx + off, o, g.nt);
+    st_stream(dx + off, o);
     if (sh.q) {
       float r[8];
       unpack8(o, r);
@@ -564,14 +556,14 @@ __global__ void __launch_bounds__(256) norm_bwd_apply_kernel(
     u32x4 vx[4], vd[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      vx[u] = ld_stream(x + base + (long)(p + u * RP) * g.C, g.nt);
-      vd[u] = ld_stream(dy + base + (long)(p + u * RP) * g.C, g.nt);
+      vx[u] = ld_stream(x + base + (long)(p + u * RP) * g.C);
+      vd[u] = ld_stream(dy + base + (long)(p + u * RP) * g.C);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) one(vx[u], vd[u], base + (long)(p + u * RP) * g.C);
   }
   for (; p < p1; p += RP)
-    one(ld_stream(x + base + (long)p * g.C, g.nt), ld_stream(dy + base + (long)p * g.C, g.nt),
+    one(ld_stream(x + base + (long)p * g.C), ld_stream(dy + base + (long)p * g.C),
         base + (long)p * g.C);
   if (sh.q) fp8_amax_commit(qmax, sh.site);
 }
@@ -593,17 +585,8 @@ static inline bool fin_huge(const NormGeom& g) { return g.nchunks >= 512; }
       hipLaunchKernelGGL((KERNEL<32, 8>), dim3(((g).C + 31) / 32, ny), dim3(256), 0, st, __VA_ARGS__);   \
   } while (0)
 
-static int norm_nt() {
-  static const int v = [] {
-    const char* e = std::getenv("P2P_NORM_NT");
-    return e ? std::atoi(e) & 3 : 0;
-  }();
-  return v;
-}
-
 static inline NormGeom make_geom(int N, int HW, int C) {
   NormGeom g;
-  g.nt = norm_nt();
   g.N = N;
   g.HW = HW;
   g.C = C;
@@ -661,7 +644,6 @@ int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, cons
   using namespace p2p;
   if (nchunks <= 0 || HW % nchunks) return -1;
   NormGeom pg;
-  pg.nt = 0;
   pg.N = N;
   pg.HW = HW;
   pg.C = C;
@@ -754,7 +736,6 @@ int p2p_norm_bwd_partials(const void* x, const void* dy, int N, int HW, int C, i
   using namespace p2p;
   if (nchunks <= 0 || HW % nchunks) return -1;
   NormGeom pg;
-  pg.nt = 0;
   pg.N = N;
   pg.HW = HW;
   pg.C = C;

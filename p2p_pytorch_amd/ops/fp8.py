@@ -75,6 +75,12 @@ class _Pool:
     def site(self, key):
         i = self.index.get(key)
         if i is None:
+            if self.sites.is_cuda and torch.cuda.is_current_stream_capturing():
+                # a new site inside a hipGraph capture would bake its (re)initialisation into
+                # every replay and its row pointer into the graph: only sites
+                # registered by the eager warmup steps may be used under capture
+                raise RuntimeError(f"fp8: new scale site {key!r} requested during graph capture; "
+                                   "run an eager warmup step first")
             if self.free:
                 i = self.free.pop()
                 self.sites[i].zero_()    # no amax window inherited from the previous owner

@@ -857,6 +857,13 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
         if direct:
             gw, wscale, wacc = weight.grad, red.scale, 1
         else:
+            red_any = getattr(weight, "_p2p_direct", None)
+            if (red_any is not None and id(weight) in red_any._direct_seen and _WgradSide.on is not None
+                    and weight.is_cuda):
+                # this weight was already written directly (side stream) in this backward and
+                # now gets an autograd contribution: AccumulateGrad adds it on the compute
+                # stream, which must not race the side-stream write
+                torch.cuda.current_stream(weight.device).wait_stream(_WgradSide.on)
             gw = torch.empty_like(weight, dtype=torch.float32, memory_format=torch.contiguous_format)
             wscale, wacc = 1.0, 0
         act_in = _act_code(cfg.act_in)

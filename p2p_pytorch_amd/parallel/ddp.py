@@ -25,12 +25,16 @@ Mechanism
     silently half-reduced.
   * ``paused()``: a backward whose gradients will be discarded (the reference's D grads
     from the G loss, the C-phase backward) launches no collective.
-  * ``comm_dtype=torch.bfloat16``: the bucket is pre-scaled by 1/world into a bf16 comm
-    buffer (exact for power-of-two worlds), all-reduced in bf16 (half the xGMI bytes) and
-    widened back into the fp32 grads by ``finish``.
+  * Averaging (round 5): on RCCL the bucket all-reduce is
+    ``ReduceOp.AVG`` (ncclAvg: the division happens inside the collective), so no gradient
+    is ever rescaled on the compute stream -- the round-4 reducer issued one ``mul_(1/world)``
+    per parameter in its hook (~130 extra launches per step at world 8).  Process groups
+    without AVG (gloo: the CPU / one-GPU rehearsal backend) sum and scale each BUCKET once in
+    ``finish``.
+  * ``comm_dtype=torch.bfloat16``: the bucket is copied into a bf16 comm buffer, averaged in
+    bf16 (half the xGMI bytes) and widened back into the fp32 grads by ``finish``.
   * ``finish()`` enqueues any incomplete bucket (params that got no grad contribute
-    zeros), makes the compute stream wait on every collective (no host sync) and scales
-    by 1/world.  Nothing in ``_on_grad`` / ``finish`` synchronises the host, so a step with
+    zeros) and makes the compute stream wait on every collective (no host sync).  Nothing in ``_on_grad`` / ``finish`` synchronises the host, so a step with
     reducers can be captured into one hipGraph (RCCL collectives are graph-capturable).
   * ``force_comm=True`` issues the collectives even at world size 1 (exercises the RCCL
     and capture path on a single GPU).
@@ -47,9 +51,9 @@ Mechanism
     of its producers ran, also when they all returned None because they wrote the bucket
     themselves; ``direct_done`` only records the side-stream event the bucket's all-reduce
     must wait on (it is issued from a comm stream that waits on both streams) and marks the
-    param as already scaled.  Gradients that arrive through autograd are scaled by 1/world in
-    their hook, so ``finish`` never rescales.  Opt-in (``P2P_DIRECT_GRAD=1``) until the
-    hardware A/B is in.
+    param as written.  Nothing is pre-scaled (the collective averages), so a direct write and
+    an autograd contribution to the same bucket mix freely.  Opt-in (``P2P_DIRECT_GRAD=1``)
+    until the hardware A/B is in.
   * Bucket size: xGMI is point-to-point (7 links x ~153 GB/s per GPU); RCCL's ring /
     direct algorithms are per-link bound, so few large buckets (tens of MB) amortise the
     per-collective latency while still leaving >= 2-4 buckets per network to overlap.
@@ -147,8 +151,11 @@ class GradReducer:
         # collectives are ordered and capture-checked against this one, not the hook's
         self._compute_stream = None
         self._last = None        # (bucket events, end-of-backward event) of the last finish()
-        # every gradient lands pre-scaled by 1/world (direct writes and autograd hooks alike)
-        self.scale = 1.0 / self.world if (self.comm and self.world > 1) else 1.0
+        # gradients land unscaled (direct writes and autograd alike): RCCL averages inside the
+        # collective (ReduceOp.AVG); other backends sum and scale each bucket once in finish()
+        self.scale = 1.0
+        self._avg = self.comm and self.world > 1 and self.backend == "nccl"
+        self._post_scale = (1.0 / self.world) if (self.comm and self.world > 1 and not self._avg) else None
         if direct is None:   # opt-in until the native path's use counting is hardware-verified
             direct = os.environ.get("P2P_DIRECT_GRAD", "0") == "1"
         self.direct = bool(direct)
@@ -232,8 +239,6 @@ class GradReducer:
         if not (lo <= p.grad.data_ptr() < lo + b.flat.numel() * b.flat.element_size()):
             self._rebind(p, b, copy=True)
         if id(p) not in self._direct_seen:
-            if self.scale != 1.0:
-                p.grad.mul_(self.scale)      # this backward's gradient alone (bucket zeroed)
             if p.grad.is_cuda:
                 hs = torch.cuda.current_stream(p.grad.device)
                 if hs != self._stream(p.grad.device):
@@ -281,6 +286,9 @@ class GradReducer:
             dst.copy_(p.grad)
         p.grad = dst
 
+    def _op(self):
+        return dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
+
     def _launch(self, b: _Bucket):
         if b.work is not None:
             return
@@ -295,7 +303,7 @@ class GradReducer:
                 b.cbuf.copy_(b.flat)
                 buf = b.cbuf
             e0, e1 = _HostEvent().record(), _HostEvent()
-            b.work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            b.work = dist.all_reduce(buf, op=self._op(), group=self.pg, async_op=True)
             b.work.get_future().then(lambda _f, e=e1: e.record())
             b.events = (e0, e1)
             return
@@ -333,14 +341,12 @@ class GradReducer:
         with ctx:
             buf = b.flat
             if b.cbuf is not None:
-                # the narrow comm buffer (gradients arrive pre-scaled by 1/world: the bf16 sum
-                # of world terms x/world is exact in scale for power-of-two worlds)
-                b.cbuf.copy_(b.flat)
+                b.cbuf.copy_(b.flat)            # the narrow comm buffer
                 buf = b.cbuf
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(cs)
-                work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                work = dist.all_reduce(buf, op=self._op(), group=self.pg, async_op=True)
                 work.wait()                     # cs waits for RCCL's stream (no host sync)
                 e1.record(cs)
                 b.flat.record_stream(cs)
@@ -349,11 +355,11 @@ class GradReducer:
                 b.events = (e0, e1)
                 b.work = _StreamJoin(cs)
             elif side:
-                work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                work = dist.all_reduce(buf, op=self._op(), group=self.pg, async_op=True)
                 work.wait()                     # cs waits for RCCL's stream (no host sync)
                 b.work = _StreamJoin(cs)
             else:
-                b.work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                b.work = dist.all_reduce(buf, op=self._op(), group=self.pg, async_op=True)
 
     def _reset(self):
         for b in self.buckets:
@@ -404,7 +410,9 @@ class GradReducer:
                 for ev in b.side:
                     self._stream(b.flat.device).wait_event(ev)
             if b.cbuf is not None:
-                b.flat.copy_(b.cbuf)            # already averaged (pre-scaled)
+                b.flat.copy_(b.cbuf)            # averaged by the collective
+            if self._post_scale is not None and b.work is not None and b.work is not True:
+                b.flat.mul_(self._post_scale)   # SUM backends: one scale per bucket
         self._reset()
 
     def enable_timing(self, on: bool = True):

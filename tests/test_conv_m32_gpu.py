@@ -58,7 +58,15 @@ CASES = [
     ("conv_reflect3x3_256x128", "g4", "conv", 8, 128, 0, 64, 136, 3, 1, 1, "reflect", None, None),
     ("convT_concat_256x256", "g5", "convT", 16, 256, 256, 32, 200, 4, 2, 1, "zeros", None, None),
     ("convT_relu_256x128", "g4", "convT", 32, 256, 0, 32, 192, 4, 2, 1, "zeros", "relu", None),
+    # weight gradients on the 256 x 256 32x32x16 tile (R, Kq multiples of 128, >= 256):
+    # conv (R = Cout), transposed conv on a virtual concat (R = Cin halves of 256), reflect
+    # 3x3 (Kq = 9 x 256), and a ReLU'd operand
+    ("wgrad_conv_s2_r512", "g5", "conv", 32, 256, 0, 64, 512, 4, 2, 1, "zeros", None, None),
+    ("wgrad_convT_concat", "g5", "convT", 16, 256, 256, 32, 256, 4, 2, 1, "zeros", None, None),
+    ("wgrad_reflect3x3_r256", "g5", "conv", 32, 256, 0, 48, 256, 3, 1, 1, "reflect", None, None),
+    ("wgrad_conv_relu_r256", "g5", "conv", 64, 256, 0, 64, 256, 4, 2, 1, "zeros", "relu", None),
 ]
+WGRAD_M32 = {c[0] for c in CASES if c[0].startswith("wgrad_")}
 
 
 def _run(case, m32):
@@ -97,6 +105,8 @@ def _run(case, m32):
             else:
                 os.environ[k] = v
     names = [e.name for e in prof.events() if "conv_fwd_m32_kernel" in e.name]
+    if name in WGRAD_M32 and m32:
+        assert any("conv_wgrad_m32_kernel" in e.name for e in prof.events()), f"{name}: wgrad m32 never ran"
     return (y, hx1.grad, None if x2 is None else hx2.grad, hw.grad, hb.grad), (x1, x2, w, b, gy), names
 
 
@@ -122,7 +132,10 @@ def test_m32_conv_matches_fp32_oracle(case):
     assert rel_err(gb, rb.grad) < 3e-2, (name, "db")
 
 
-@pytest.mark.parametrize("case", CASES[:3], ids=[c[0] for c in CASES[:3]])
+AB_CASES = CASES[:3] + [c for c in CASES if c[0] in WGRAD_M32][:2]
+
+
+@pytest.mark.parametrize("case", AB_CASES, ids=[c[0] for c in AB_CASES])
 def test_m32_matches_16x16_tiles(case):
     out_a, _, names = _run(case, True)
     out_b, _, names_b = _run(case, False)

@@ -18,13 +18,6 @@ from p2p_pytorch_amd.ops import reference as ref
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True)
-def _w32_on(monkeypatch):
-    """The 32-wide grids are off by default since round 4 (no step-level gain, see
-    profiles/kernel_experiments_r4.md); these tests keep them covered."""
-    monkeypatch.setenv("P2P_S2T_W32", "1")
-
-
 DEV = "cuda"
 
 

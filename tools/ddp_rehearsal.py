@@ -99,10 +99,9 @@ def family_r_phase(world, rank, dev, steps=3):
         for bk in red_d.buckets:
             gl = [torch.zeros_like(local[bk.index]) for _ in range(world)]
             dist.all_gather(gl, local[bk.index])
-            # the buckets hold gradients pre-scaled by red_d.scale (1/world): the reduced bucket
-            # is the SUM of the ranks' local buckets (= the mean of their raw gradients)
+            # the buckets hold the raw local gradients; the reduced bucket is their mean
             stk = torch.stack(gl).float()
-            mean = stk.sum(0) if red_d.scale != 1.0 else stk.mean(0)
+            mean = stk.mean(0)
             worst = max(worst, float((bk.flat.float() - mean).abs().max() / mean.abs().max().clamp_min(1e-12)))
         for m in (G, D, C):
             f = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
@@ -111,6 +110,47 @@ def family_r_phase(world, rank, dev, steps=3):
             same = same and all(torch.equal(gg[0], t) for t in gg)
     return {"d_buckets_once_per_step": once, "d_grad_rel_err_vs_rank_mean": worst,
             "params_identical": same, "ok": bool(once and same and worst < 1e-5)}
+
+
+def direct_phase(world, rank, dev, a, b):
+    """Direct bucket gradients: the conv weight gradients written into the
+    buckets by the wgrad kernels (accumulate mode, weight-gradient side stream) must give
+    bitwise the parameters of the autograd path after two Pix2Pix steps, on every rank, and
+    the direct path must actually have been taken."""
+    from p2p_pytorch_amd.engine.pix2pix import Pix2PixStep
+    from p2p_pytorch_amd.parallel import GradReducer
+    from p2p_pytorch_amd.parallel import dist as pdist
+    n_direct = [0]
+    orig = GradReducer.direct_done
+
+    def counted(self, p, stream=None):
+        n_direct[0] += 1
+        return orig(self, p, stream)
+
+    out = {}
+    GradReducer.direct_done = counted
+    try:
+        for direct in (False, True):
+            G, D = build(400 + rank, dev)
+            pdist.broadcast_module(G)
+            pdist.broadcast_module(D)
+            rg, rd = GradReducer(G, bucket_mb=0.5, direct=direct), GradReducer(D, bucket_mb=0.5, direct=direct)
+            step = Pix2PixStep(G, D, reducer_g=rg, reducer_d=rd)
+            for _ in range(2):
+                step.step(a, b)
+            torch.cuda.synchronize()
+            out[direct] = torch.cat([p.detach().reshape(-1) for p in list(G.parameters()) + list(D.parameters())])
+            rg.remove()
+            rd.remove()
+    finally:
+        GradReducer.direct_done = orig
+    gathered = [torch.zeros_like(out[True]) for _ in range(world)]
+    dist.all_gather(gathered, out[True])
+    same_ranks = all(torch.equal(gathered[0], t) for t in gathered)
+    equal = torch.equal(out[False], out[True])
+    diff = float((out[False] - out[True]).abs().max())
+    return {"direct_writes": n_direct[0], "direct_equals_autograd": equal, "max_abs_diff": diff,
+            "ranks_identical": same_ranks, "ok": bool(n_direct[0] > 0 and equal and same_ranks)}
 
 
 def main():
@@ -185,12 +225,13 @@ def main():
     same = all(torch.equal(gathered[0], t) for t in gathered)
     finite = all(torch.isfinite(v).all().item() for v in losses.values())
     fam_r = family_r_phase(world, rank, dev)
-    ok = same and finite and worst < 1e-4 and timed and fam_r["ok"]
+    direct = direct_phase(world, rank, dev, a, b)
+    ok = same and finite and worst < 1e-4 and timed and fam_r["ok"] and direct["ok"]
     if rank == 0:
         print(json.dumps({"world": world, "backend": dist.get_backend(), "grad_rel_err_vs_shard_mean": worst,
                           "worst_params": errs[:4],
                           "params_identical": same, "losses_finite": finite, "comm": comm,
-                          "phase_ms": phases, "family_r": fam_r, "ok": ok}), flush=True)
+                          "phase_ms": phases, "family_r": fam_r, "direct": direct, "ok": ok}), flush=True)
     pdist.destroy()
     sys.exit(0 if ok else 1)
 
