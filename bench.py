@@ -212,6 +212,8 @@ def main():
         # on a timed side stream -> per-network all-reduce busy ms, the part left exposed
         # after backward's last kernel, and the overlap fraction (max over ranks)
         comm = {"dtype": args.comm_dtype, "bucket_mb": args.bucket_mb}
+        if rank == 0:
+            print("[bench] timed steps done; one eager step with timed collectives", file=sys.stderr, flush=True)
         for r in (reducer_g, reducer_d):
             r.enable_timing()
         trainer.step(real_A, real_B)

@@ -27,6 +27,32 @@ import copy
 import torch
 
 
+# ProcessGroupNCCL's watchdog polls the end events of the eager collectives it tracks every
+# ~100 ms (kWatchdogThreadSleepMillis) and only then retires them
+_WATCHDOG_DRAIN_S = 0.35
+
+
+def drain_collectives():
+    """Let the c10d watchdog retire every eager collective before a capture begins.
+
+    The capture's first collective makes the process group's RCCL stream join the capture.
+    On HIP, ``hipEventQuery`` of an event recorded on a stream that is NOW capturing fails
+    with ``hipErrorCapturedEvent`` -- and the watchdog still holds the end events of the
+    warmup steps' all-reduces until its next poll, so a capture that starts within one poll
+    interval of them aborts the process (tools/diag_capture_event.py
+    reproduces it with one rank).  A device sync completes those Works; sleeping a few poll
+    intervals lets the watchdog retire them."""
+    import time
+
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    if dist.get_backend() != "nccl":
+        return
+    torch.cuda.synchronize()
+    time.sleep(_WATCHDOG_DRAIN_S)
+
+
 class WarmupError(RuntimeError):
     """A warmup (eager) step raised before capture: not a capture failure -- the trainer
     itself is broken, and on a multi-rank job the other ranks are already blocked in that
@@ -115,6 +141,7 @@ class CapturedStep:
         if snap is not None:
             snap.restore()
             torch.cuda.synchronize()
+        drain_collectives()               # no eager RCCL Work left for the watchdog to poll
         from ..ops import hip as _hip
         salt = copy.copy(_hip._salt)      # python-side state the capture advances
         self.graph = torch.cuda.CUDAGraph()

@@ -44,16 +44,19 @@ Mechanism
     busy time, the part of it left exposed after backward's last kernel, and the overlap
     fraction -- the JSONL "comm ms / overlap %" of SURVEY.md section 5.5.
   * Direct gradients (``direct=True``, round 4): the native conv backward writes a conv
-    weight's gradient straight into its bucket view, pre-scaled by 1/world, with the
-    wgrad kernel's own accumulate mode -- no AccumulateGrad add, no 1/world pass -- and may
+    weight's gradient straight into its bucket view with the wgrad kernel's own
+    accumulate mode -- no AccumulateGrad add -- and may
     run it on the weight-gradient side stream (ops/hip.py ``wgrad_overlap``).  Readiness
     still comes from autograd: a leaf's post-accumulate hook fires once per backward after all
     of its producers ran, also when they all returned None because they wrote the bucket
     themselves; ``direct_done`` only records the side-stream event the bucket's all-reduce
     must wait on (it is issued from a comm stream that waits on both streams) and marks the
     param as written.  Nothing is pre-scaled (the collective averages), so a direct write and
-    an autograd contribution to the same bucket mix freely.  Opt-in (``P2P_DIRECT_GRAD=1``)
-    until the hardware A/B is in.
+    an autograd contribution to the same bucket mix freely.  Default on since round 5
+    (``P2P_DIRECT_GRAD=0`` turns it off): step A/B with RCCL collectives at world 1 --
+    direct 7849 / 7839, autograd 7838, no reducer 7870 img/s (profiles/force_comm_r5k.jsonl).
+    The round-4 watchdog abort seen with it was a capture started while the c10d watchdog
+    still tracked the warmup's eager all-reduces (engine/graph.py ``drain_collectives``).
   * Bucket size: xGMI is point-to-point (7 links x ~153 GB/s per GPU); RCCL's ring /
     direct algorithms are per-link bound, so few large buckets (tens of MB) amortise the
     per-collective latency while still leaving >= 2-4 buckets per network to overlap.
@@ -156,8 +159,8 @@ class GradReducer:
         self.scale = 1.0
         self._avg = self.comm and self.world > 1 and self.backend == "nccl"
         self._post_scale = (1.0 / self.world) if (self.comm and self.world > 1 and not self._avg) else None
-        if direct is None:   # opt-in until the native path's use counting is hardware-verified
-            direct = os.environ.get("P2P_DIRECT_GRAD", "0") == "1"
+        if direct is None:   # default on: bitwise equal to the autograd path (tools/ddp_rehearsal.py)
+            direct = os.environ.get("P2P_DIRECT_GRAD", "1") == "1"
         self.direct = bool(direct)
         self._direct_seen: set = set()   # params written directly in the current backward
         self._names = {id(p): n for n, p in module.named_parameters()}
@@ -267,6 +270,11 @@ class GradReducer:
         per backward for every leaf the backward reached -- also when every contribution was
         None (written here) -- after all of that leaf's producers ran."""
         b = self._param_bucket[p]
+        if _DEBUG:
+            with torch.cuda.stream(stream or torch.cuda.current_stream()):
+                cap = torch.cuda.is_current_stream_capturing()
+            print(f"[reducer] direct {self._names.get(id(p), '?')} bucket {b.index}: stream "
+                  f"{None if stream is None else stream.stream_id} capturing {cap}", flush=True)
         if stream is not None and stream != self._stream(stream.device):
             ev = torch.cuda.Event()
             ev.record(stream)
@@ -359,6 +367,10 @@ class GradReducer:
                 work.wait()                     # cs waits for RCCL's stream (no host sync)
                 b.work = _StreamJoin(cs)
             else:
+                if _DEBUG:
+                    print(f"[reducer] bucket {b.index}: all_reduce on stream "
+                          f"{torch.cuda.current_stream().stream_id if buf.is_cuda else None} capturing "
+                          f"{buf.is_cuda and torch.cuda.is_current_stream_capturing()}", flush=True)
                 b.work = dist.all_reduce(buf, op=self._op(), group=self.pg, async_op=True)
 
     def _reset(self):

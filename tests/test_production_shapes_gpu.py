@@ -96,11 +96,18 @@ ZERO_REL = 1e-5
 # bf16-unresolvable gradients: where the eager bf16 autocast step itself is off by more than
 # ILL_REL of the tensor's own magnitude, the tensor carries no bf16-resolvable signal -- the
 # innermost normalised U-Net levels (instance norm over 4x4 / 2x2 planes): against an fp64
-# oracle fp32 is within 1.2 %, eager bf16 34-74 % and native 36-190 % off there
-# (profiles/diag_inner_grad_r4.txt, tools/diag_inner_grad.py).  These are bounded in relative
-# L2 instead of max-abs: ||native - fp32|| <= ILL_K ||eager - fp32|| + 1 % ||fp32||.
+# oracle fp32 is within 1.2 %, eager bf16 34-89 % and native 36-190 % off there in MAX-ABS
+# terms.  That max-abs error is decided by the few (n, c) planes whose 4 values happen to
+# nearly coincide, so it is a lottery: over 5 seeds the native / eager max-abs ratio on
+# downs.6.weight is 3.42 / 1.65 / 0.75 / 1.12 / 1.11 (median 1.12), and an eager variant that
+# keeps those planes' pre-norm values in fp32 (VERDICT r4 W7's proposal, emulated) scatters
+# the same way, 0.61-1.64 (median 1.03) -- fp32 storage buys nothing: the noise comes from
+# the bf16 operands upstream (profiles/diag_inner_grad_r5.txt, tools/diag_inner_grad.py).
+# These tensors are bounded in relative L2 instead, where two equally precise bf16 steps
+# agree: ||native - fp32|| <= ILL_K ||eager - fp32|| + 1 % ||fp32|| (measured ratios
+# 0.91-1.09 at this seed, profiles/bounds_production_r4.jsonl).
 ILL_REL = 0.25
-ILL_K = 3.0
+ILL_K = 1.5
 
 
 def _log(test, rows, extra):
@@ -118,17 +125,20 @@ def test_headline_step_at_production_shape_matches_fp32(refs):
     with profile(activities=[ProfilerActivity.CUDA]) as prof:
         ln, gn = _run("native", G0, D0, a, b)
     names = {e.name for e in prof.events()}
-    want = {"256x256 LATE fwd": "conv_fwd_glds_kernel<256, 256, 2, 4, 0, 2",
-            "256x256 MODE-1": "conv_fwd_glds_kernel<256, 256, 2, 4, 1, 2",
-            "256x128 3-stage": "conv_fwd_glds_kernel<256, 128, 4, 2,",
-            "EXT epilogue": "true>(p2p::ConvFwdArgs)",
-            "wgrad 256x128": "conv_wgrad_glds_kernel<256, 128",
-            "image head": "halo_union_kernel",
+    # (any pattern of a class counts: the 32x32x16 tiles of round 5 took over the round-4
+    # 16x16x32 tiles on most layers, the latter still serve shapes the former reject)
+    want = {"256x256 fwd tile": ("conv_fwd_m32_kernel<256, 0", "conv_fwd_glds_kernel<256, 256, 2, 4, 0, 2"),
+            "256-row MODE-1 tile": ("conv_fwd_m32_kernel<256, 1", "conv_fwd_m32_kernel<128, 1",
+                                    "conv_fwd_glds_kernel<256, 256, 2, 4, 1, 2"),
+            "256x128 tile": ("conv_fwd_m32_kernel<128, ", "conv_fwd_glds_kernel<256, 128, 4, 2,"),
+            "EXT epilogue": ("true>(p2p::ConvFwdArgs)",),
+            "256-row wgrad tile": ("conv_wgrad_m32_kernel", "conv_wgrad_glds_kernel<256, 128"),
+            "image head": ("halo_union_kernel",),
             # the class-shared halo kernel of the stride-2 transposed convs / dgrads onto
             # 64x64 grids (d2 forward with input ReLU, the EXT dgrads)
-            "s2t halo ConvT": "conv_s2t_kernel<64, true, false, 0>",
-            "s2t halo EXT dgrad": "conv_s2t_kernel<64, false, true, 0>"}
-    missing = [k for k, pat in want.items() if not any(pat in n for n in names)]
+            "s2t halo ConvT": ("conv_s2t_kernel<64, true, false, 0>",),
+            "s2t halo EXT dgrad": ("conv_s2t_kernel<64, false, true, 0>",)}
+    missing = [k for k, pats in want.items() if not any(pat in n for pat in pats for n in names)]
     rows, bad = [], []
     for k in lc:
         err, erre = abs(ln[k] - lc[k]), abs(le[k] - lc[k])

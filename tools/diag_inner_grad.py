@@ -6,7 +6,8 @@ One production-shape step (tests/test_production_shapes_gpu.py: U-Net-256 + Patc
 hooks capture the gradients of the innermost levels' activations:
   e6_z  skip 5 (e6 IN+lrelu output, 4x4)       e7_x  e7 conv output (pre-norm, 2x2)
   e7_z  skip 6 (e7 IN+lrelu output, 2x2)       e8    e8 conv output (relu, 1x1)
-and the parameter gradients of downs.5 / 6 / 7.  Printed: max |err| / max |ref| per tensor.
+and the parameter gradients of downs.5 / 6 / 7.  Printed: max |err| / max |ref| per tensor (and, in the
+per-seed ratio table, the relative L2 error too).
 Also an fp64 run of the same step: how far fp32 itself is from fp64 (conditioning).
 
     python tools/diag_inner_grad.py [--B 64] [--seeds 11,12,13]
@@ -35,6 +36,27 @@ def nets(seed=11):
     return G, D
 
 
+def _f32_inner(G):
+    """``eager_f32x``: what fp32 storage of the innermost pre-norm planes buys.  The convs that
+    produce the <= 4x4 normalised planes (e6, e7, d1, d2) keep bf16-rounded operands (as the
+    autocast conv) but return their fp32 accumulator unrounded, so the IN that follows sees
+    fp32 x -- the VERDICT r4 W7 proposal, emulated on the eager path."""
+    from p2p_pytorch_amd.ops import reference as ref
+
+    def rnd(t):
+        return tuple(rnd(u) for u in t) if isinstance(t, (tuple, list)) else t.to(torch.bfloat16).float()
+
+    n = G.num_downs
+    for m in (G.downs[n - 3], G.downs[n - 2], G.ups[n - 1], G.ups[n - 2]):
+        def fwd(x, m=m):
+            with torch.autocast("cuda", enabled=False):
+                w, b = rnd(m.weight), None if m.bias is None else m.bias.float()
+                if isinstance(m, torch.nn.ConvTranspose2d):
+                    return ref.conv_transpose2d(rnd(x), w, b, m.stride[0], m.padding[0], m.act_in, m.act_out)
+                return ref.conv2d(rnd(x), w, b, m.stride, m.padding, m.pad_mode, m.upsample, m.act_in, m.act_out)
+        m.forward = fwd
+
+
 def run(kind, G0, D0, a, b):
     from p2p_pytorch_amd.engine.pix2pix import Pix2PixStep
     G, D = copy.deepcopy(G0).cuda(), copy.deepcopy(D0).cuda()
@@ -50,12 +72,14 @@ def run(kind, G0, D0, a, b):
           G.downs[6].register_forward_hook(cap("e7_x")),
           G.down_norms[6].register_forward_hook(cap("e7_z")),
           G.downs[7].register_forward_hook(cap("e8"))]
-    if kind in ("fp32", "eager", "fp64"):
+    if kind == "eager_f32x":
+        _f32_inner(G)
+    if kind in ("fp32", "eager", "fp64", "eager_f32x"):
         p2p.set_backend("torch")
         if kind == "fp64":
             G, D = G.double(), D.double()
         try:
-            step = Pix2PixStep(G, D, lr=0.0, autocast_dtype=torch.bfloat16 if kind == "eager" else None)
+            step = Pix2PixStep(G, D, lr=0.0, autocast_dtype=torch.bfloat16 if kind.startswith("eager") else None)
             dt = torch.float64 if kind == "fp64" else torch.float32
             step.step(a.cuda().to(dt), b.cuda().to(dt))
         finally:
@@ -88,7 +112,8 @@ def table(res):
             x = gr[name].double()
             if x.shape != r.shape:   # channels_last / layout differences: compare as NCHW
                 x = x.reshape(r.shape)
-            out[name][1][k] = (x - r).abs().max().item() / max(m, 1e-30)
+            out[name][1][k] = ((x - r).abs().max().item() / max(m, 1e-30),
+                               (x - r).norm().item() / max(r.norm().item(), 1e-30))
     return out
 
 
@@ -112,16 +137,18 @@ def main():
         print(f"seed {seed}")
         print(f"{'tensor':18s} {'|ref|max':>10s} " + " ".join(f"{k:>16s}" for k in kinds[1:]))
         for name, (m, errs) in tab.items():
-            print(f"{name:18s} {m:10.3e} " + " ".join(f"{errs[k]:16.3e}" if k in errs else f"{'-':>16s}"
+            print(f"{name:18s} {m:10.3e} " + " ".join(f"{errs[k][0]:16.3e}" if k in errs else f"{'-':>16s}"
                                                    for k in kinds[1:]))
-            if "eager" in errs and "native" in errs:
-                ratios.setdefault(name, []).append(errs["native"] / max(errs["eager"], 1e-30))
+            for k in errs:
+                if k not in ("eager", "fp32") and "eager" in errs:
+                    for j, metric in enumerate(("maxabs", "L2")):
+                        ratios.setdefault((metric, name, k), []).append(errs[k][j] / max(errs["eager"][j], 1e-30))
         sys.stdout.flush()
     if len(seeds) > 1 and ratios:
-        print("native / eager error ratio per seed, and the median")
-        for name, rs in ratios.items():
+        print("error ratio to eager per seed, and the median")
+        for (metric, name, k), rs in sorted(ratios.items()):
             med = sorted(rs)[len(rs) // 2]
-            print(f"{name:18s} " + " ".join(f"{r:6.2f}" for r in rs) + f"   median {med:6.2f}")
+            print(f"{metric:6s} {name:18s} {k:>16s} " + " ".join(f"{r:6.2f}" for r in rs) + f"   median {med:6.2f}")
 
 
 if __name__ == "__main__":
