@@ -82,6 +82,8 @@ int p2p_weight_prep_pairs(int count, const float* const* w, void* const* out0, v
                           int* const* site, hipStream_t st);
 int p2p_m32_enabled();
 int p2p_set_m32(int on);
+int p2p_oob_counts(unsigned int* out4, int reset);
+int p2p_oob_selftest(void* scratch, hipStream_t st);
 int p2p_conv_fwd_m32(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t st);
 int p2p_up2_dgrad_image(const float* w, int Cout, int Cin, int Xp, int Yp, void* out, hipStream_t st);
 int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, int reflect,
@@ -1000,6 +1002,20 @@ Tensor weight_prep(const Tensor& w, int64_t swap, int64_t Xp, int64_t Yp,
 // runtime A/B switch of the 32x32x16 conv tiles (returns the previous setting)
 int64_t set_m32(int64_t on) { return p2p_set_m32((int)on); }
 
+// P2P_BOUNDS_ASSERT build (csrc/bounds.h): [enabled, failed checks, largest site id, last bad
+// index, its limit] summed over every translation unit's device counters (reset when asked)
+// launches one deliberately out-of-range check (site 99) on the scratch tensor's stream
+void oob_selftest(Tensor scratch) {
+  TORCH_CHECK(scratch.is_cuda() && scratch.scalar_type() == at::kInt && scratch.numel() >= 1, "oob_selftest: int32 scratch");
+  check_rc(p2p_oob_selftest(scratch.data_ptr(), cur_stream(scratch)), "oob_selftest");
+}
+
+std::vector<int64_t> oob_counts(bool reset) {
+  unsigned int v[4] = {0, 0, 0, 0};
+  const int on = p2p_oob_counts(v, reset ? 1 : 0);
+  return {on, v[0], v[1], v[2], v[3]};
+}
+
 // input-gradient image of a nearest-x2 + reflect-1 3x3 conv: [Xp][4][4][Yp] bf16 (misc.hip)
 Tensor up2_dgrad_image(const Tensor& w, int64_t Xp, int64_t Yp) {
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.dim() == 4 &&
@@ -1851,7 +1867,9 @@ TORCH_LIBRARY(p2p, m) {
         "Tensor? qs_q2=None) -> bool");
   m.def("weight_prep(Tensor w, int swap, int Xp, int Yp, Tensor? scale) -> Tensor");
   m.def("up2_dgrad_image(Tensor w, int Xp, int Yp) -> Tensor");
-  m.def("set_m32(int on) -> int", set_m32);   // no tensor arguments: a catch-all kernel
+  m.def("oob_selftest(Tensor scratch) -> ()");
+  m.def("set_m32(int on) -> int", set_m32);
+  m.def("oob_counts(bool reset) -> int[]", oob_counts);   // no tensor arguments: a catch-all kernel
   m.def("union_weight(Tensor w, int co_off, int nv, int Nrows, int Cpad, Tensor? bias) -> Tensor[]");
   m.def("conv_d2s(Tensor x1, Tensor? x2, Tensor w, Tensor bias, int act_in, int act_out, int mode, "
         "Tensor(a!) out, Tensor pk_a, Tensor? pk_f, float scale, Tensor? wscale=None) -> Tensor");
@@ -1913,6 +1931,7 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("conv_wgrad", conv_wgrad);
   m.impl("weight_prep", weight_prep);
   m.impl("up2_dgrad_image", up2_dgrad_image);
+  m.impl("oob_selftest", oob_selftest);
   m.impl("union_weight", union_weight);
   m.impl("conv_d2s", conv_d2s);
   m.impl("weight_prep_multi", weight_prep_multi);

@@ -2,6 +2,7 @@
 // staged; conv_fwd_glds.hip: global_load_lds multi-stage): tile geometry of the two GEMM
 // modes, the LDS swizzle of the [rows][64] bf16 operand tiles, and the fused epilogue.
 #pragma once
+#include "bounds.h"
 #include "conv.h"
 #include "fp8_dev.h"
 
@@ -122,7 +123,8 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
   auto finish = [&](int row, long pix, u32x4 xv, u32x4 rv, u32x4 nv) __attribute__((always_inline)) {
     u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * LDC + (tid % CPR) * 8);
     if (pix < 0) {   // fold frame pixel (no nb partials with a fold: host)
-      *reinterpret_cast<u32x4*>(static_cast<bf16*>(a.fold_buf) + (-pix - 2) * a.Cout + co_t) = v;
+      if (P2P_OOB_OK(1, (-pix - 2) * a.Cout + co_t, 8, (long)a.N * a.OH * a.OW * a.Cout))
+        *reinterpret_cast<u32x4*>(static_cast<bf16*>(a.fold_buf) + (-pix - 2) * a.Cout + co_t) = v;
       return;
     }
     if (gate_t) {
@@ -161,7 +163,9 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
       for (int q = 0; q < 8; ++q) vb[q] = (bf16)((float)vb[q] + (float)rb[q]);
       v = __builtin_bit_cast(u32x4, vb);
     }
-    *reinterpret_cast<u32x4*>(y_t + pix * ld_t + cof_t) = v;
+    if (P2P_OOB_OK(2, pix * ld_t + cof_t, 8,
+                   (long)a.N * (a.fold_buf ? (long)a.fold_H * a.fold_W : (long)a.OH * a.OW) * ld_t))
+      *reinterpret_cast<u32x4*>(y_t + pix * ld_t + cof_t) = v;
     if (nb_on) {   // from the stored bf16 dz, as the unfused partial pass reads it
       const bf16x8 dz = __builtin_bit_cast(bf16x8, v);
       const bf16x8 xn = __builtin_bit_cast(bf16x8, nv);
@@ -394,7 +398,8 @@ __device__ __forceinline__ void conv_epilogue_tail(const ConvFwdArgs& a, const C
     const long pix = out_pix(m);
     u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * LDC + cc * 8);
     if (pix < 0) {   // fold frame pixel: raw, folded by fold_band (host: Csplit == Cout)
-      *reinterpret_cast<u32x4*>(static_cast<bf16*>(a.fold_buf) + (-pix - 2) * a.Cout + co) = v;
+      if (P2P_OOB_OK(1, (-pix - 2) * a.Cout + co, 8, (long)a.N * a.OH * a.OW * a.Cout))
+        *reinterpret_cast<u32x4*>(static_cast<bf16*>(a.fold_buf) + (-pix - 2) * a.Cout + co) = v;
       continue;
     }
     const bool first = co < a.Csplit;
@@ -430,7 +435,9 @@ __device__ __forceinline__ void conv_epilogue_tail(const ConvFwdArgs& a, const C
       v = __builtin_bit_cast(u32x4, vb);
     }
     bf16* y = static_cast<bf16*>(first ? a.y1 : a.y2);
-    *reinterpret_cast<u32x4*>(y + pix * ld + cof) = v;
+    if (P2P_OOB_OK(2, pix * ld + cof, 8,
+                   (long)a.N * (a.fold_buf ? (long)a.fold_H * a.fold_W : (long)a.OH * a.OW) * ld))
+      *reinterpret_cast<u32x4*>(y + pix * ld + cof) = v;
     if (qsh.q) {  // host: only with Csplit == Cout, no act_bwd
       const bf16x8 vb = __builtin_bit_cast(bf16x8, v);
       float r[8];

@@ -206,7 +206,8 @@ __device__ __forceinline__ void s2t_ext_all(const ConvFwdArgs& a, const uint2 (&
         for (int r = 0; r < 4; ++r) f[r] = bfw(w, r) + bfw(rv[i][slot], r);
         w = uint2{pk2(f[0], f[1]), pk2(f[2], f[3])};
       }
-      __builtin_amdgcn_raw_buffer_store_b64(s2t_u32x2{w.x, w.y}, ry_, voff + 32 * j, soff(i, ld), 0);
+      if (P2P_OOB_OK(30, P0 * ld + (voff + 32 * j + soff(i, ld)) / 2, 4, (long)a.N * a.OH * a.OW * ld))
+        __builtin_amdgcn_raw_buffer_store_b64(s2t_u32x2{w.x, w.y}, ry_, voff + 32 * j, soff(i, ld), 0);
       if (nb_on) {   // from the stored bf16 dz, as the unfused partial pass reads it
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -371,7 +372,8 @@ __device__ __forceinline__ void s2t_epilogue(const ConvFwdArgs& a, f32x4 (&acc)[
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const long p = pix(i);
-        *reinterpret_cast<uint2*>(y + p * ld + cof) = v[i];
+        if (P2P_OOB_OK(30, p * ld + cof, 4, (long)a.N * a.OH * a.OW * ld))
+          *reinterpret_cast<uint2*>(y + p * ld + cof) = v[i];
         if (qsh.q) {
           const float fm = fp8_max(qsh.fmt);
           float f[4];
@@ -449,7 +451,8 @@ __device__ __forceinline__ void s2t_epilogue(const ConvFwdArgs& a, f32x4 (&acc)[
             for (int r = 0; r < 4; ++r) f[r] = bfw(w, r) + bfw(rv[u], r);
             w = uint2{pk2(f[0], f[1]), pk2(f[2], f[3])};
           }
-          *reinterpret_cast<uint2*>(y + p * ld + cof) = w;
+          if (P2P_OOB_OK(30, p * ld + cof, 4, (long)a.N * a.OH * a.OW * ld))
+            *reinterpret_cast<uint2*>(y + p * ld + cof) = w;
           if (nb_on) {   // from the stored bf16 dz, as the unfused partial pass reads it
 #pragma unroll
             for (int r = 0; r < 4; ++r) {

@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "bounds.h"
 #include "common.h"
 #include "conv.h"
 
@@ -897,10 +898,12 @@ __global__ void __launch_bounds__(256) wgrad_reduce_t_kernel(const float* __rest
   const int Kq = T * C;
   const long total = (long)R * Kq;
   const int E = T * CB;
+  if (!P2P_OOB_OK(22, T, 0, 82)) return;   // the LDS tile holds up to 81 taps (9 x 9)
   for (int idx = threadIdx.x; idx < E; idx += 256) {
     const int tap = idx / CB, cc = idx - tap * CB;
     float s = 0.f;
-    if (c0 + cc < C) {
+    if (c0 + cc < C && P2P_OOB_OK(21, (long)r * Kq + tap * C + c0 + cc + (long)(splits - 1) * total, 1,
+                                  (long)splits * total)) {
       const float* src = ws + (long)r * Kq + tap * C + c0 + cc;
       float acc[G];
 #pragma unroll
@@ -936,7 +939,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce_t_kernel(const float* __rest
       o = ((long)ci * Cr + r) * T + (T / KW - 1 - kh) * KW + (KW - 1 - kw);
     }
     const float v = tile[t * LDT + cl];
-    dw[o] = accumulate ? dw[o] + v : v;
+    if (P2P_OOB_OK(20, o, 1, (long)Rr * Cr * T)) dw[o] = accumulate ? dw[o] + v : v;
   }
 }
 

@@ -6,6 +6,7 @@
 // Every vector path moves 16 B per lane (bf16x8) -- hipcc does not vectorise bf16.
 // Reductions are two-stage (fixed-order block partials -> one finishing block), so every
 // loss and bias gradient is bitwise reproducible run to run.
+#include "bounds.h"
 #include "common.h"
 
 namespace p2p {
@@ -185,7 +186,8 @@ __global__ void __launch_bounds__(256) pad_fold_kernel(const bf16* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += rf[j];
     }
-    *reinterpret_cast<u32x4*>(dx + pix * C + cg * 8) = pack8e(acc);
+    if (P2P_OOB_OK(10, pix * C + cg * 8, 8, (long)N * H * W * C))
+      *reinterpret_cast<u32x4*>(dx + pix * C + cg * 8) = pack8e(acc);
   }
 }
 
@@ -520,6 +522,7 @@ __global__ void __launch_bounds__(256) pad_fold_s1_kernel(const bf16* __restrict
         for (int j = 0; j < 8; ++j) acc[k][j] += rf[j];
       }
     }
+    if (!P2P_OOB_OK(11, o, 32, N * H * W * C)) continue;
 #pragma unroll
     for (int k = 0; k < 4; ++k) *reinterpret_cast<u32x4*>(dx + o + k * 8) = pack8e(acc[k]);
   }
@@ -578,12 +581,19 @@ __global__ void __launch_bounds__(256) fold_band_kernel(const bf16* __restrict__
     for (int i = 0; i < ny; ++i)
       for (int k2 = 0; k2 < nx; ++k2) {
         if (i == 0 && k2 == 0) continue;   // the interior pixel itself: already in dx
+        const long fo = (((long)n * Hp + qy[i]) * Wp + qx[k2]) * C + cg * 8;
+        if (!P2P_OOB_OK(13, fo, 8, (long)N * Hp * Wp * C) || (unsigned)qy[i] >= (unsigned)Hp ||
+            (unsigned)qx[k2] >= (unsigned)Wp) {
+          (void)P2P_OOB_OK(13, -1, 0, 0);
+          continue;
+        }
         float f[8];
-        unpack8e(*reinterpret_cast<const u32x4*>(fb + (((long)n * Hp + qy[i]) * Wp + qx[k2]) * C + cg * 8), f);
+        unpack8e(*reinterpret_cast<const u32x4*>(fb + fo), f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += f[j];
       }
     const long o = (((long)n * H + y) * W + x) * C + cg * 8;
+    if (!P2P_OOB_OK(12, o, 8, (long)N * H * W * C)) continue;
     if (act) {
       float xf[8];
       unpack8e(*reinterpret_cast<const u32x4*>(xb + o), xf);

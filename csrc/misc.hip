@@ -7,6 +7,7 @@
 // one finishing block, fixed order).
 //   reference: networks.py:173-236 (C), :452 (PReLU), :732 (AvgPool), train.py:123-126
 //   (TV), generate_dataset.py:29-34 (quantiser), torchvision VGG19 (max-pool).
+#include "bounds.h"
 #include "common.h"
 
 namespace p2p {
@@ -501,3 +502,38 @@ int p2p_up2_dgrad_image(const float* w, int Cout, int Cin, int Xp, int Yp, void*
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- bounds-check registry
+// (P2P_BOUNDS_ASSERT build: every translation unit that includes bounds.h registers the host
+// reader of its own device counters here; see csrc/bounds.h)
+namespace p2p {
+// positive control of the counters: one index past the end (site 99); a no-op in the normal build
+__global__ void oob_selftest_kernel(int* out) {
+  if (P2P_OOB_OK(99, 1, 1, 1)) out[0] = 1;
+}
+}  // namespace p2p
+extern "C" int p2p_oob_selftest(void* scratch, hipStream_t st) {
+  hipLaunchKernelGGL(p2p::oob_selftest_kernel, dim3(1), dim3(1), 0, st, static_cast<int*>(scratch));
+  return (int)hipGetLastError();
+}
+#ifdef P2P_BOUNDS_ASSERT
+namespace p2p {
+static OobReader g_oob_readers[64];
+static int g_oob_nreaders = 0;
+int oob_register(OobReader fn) {
+  if (g_oob_nreaders < 64) g_oob_readers[g_oob_nreaders++] = fn;
+  return g_oob_nreaders;
+}
+}  // namespace p2p
+extern "C" int p2p_oob_counts(unsigned int* out4, int reset) {
+  out4[0] = out4[1] = out4[2] = out4[3] = 0;
+  (void)hipDeviceSynchronize();
+  for (int i = 0; i < p2p::g_oob_nreaders; ++i) p2p::g_oob_readers[i](out4, reset != 0);
+  return 1;
+}
+#else
+extern "C" int p2p_oob_counts(unsigned int* out4, int) {
+  out4[0] = out4[1] = out4[2] = out4[3] = 0;
+  return 0;
+}
+#endif

@@ -21,3 +21,19 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _bounds_check(request):
+    """P2P_BOUNDS_CHECK=1 (with P2P_LIB = the P2P_BOUNDS_ASSERT build, csrc/bounds.h): after
+    every GPU test, no kernel may have taken an out-of-range store / load index."""
+    yield
+    if os.environ.get("P2P_BOUNDS_CHECK") != "1" or "gpu" not in request.node.keywords:
+        return
+    import torch
+    from p2p_pytorch_amd import _native
+    if not _native.load():
+        return
+    on, count, site, idx, limit = torch.ops.p2p.oob_counts(True)
+    assert on == 1, "P2P_BOUNDS_CHECK=1 needs the P2P_BOUNDS_ASSERT build (P2P_LIB)"
+    assert count == 0, f"{count} out-of-range indices (largest site id {site}, last index {idx}, limit {limit})"

@@ -1101,3 +1101,18 @@ def test_rowsum_and_scalar_helpers(R, C):
     c = torch.tensor([41], dtype=torch.int64, device=DEV)
     P.i64_add_(c, 1)
     assert c.item() == 42
+
+
+def test_bounds_counters_positive_control():
+    """P2P_BOUNDS_ASSERT build (csrc/bounds.h): a deliberately out-of-range check is counted,
+    reported with its site id and reset; the normal build reports the counters disabled."""
+    scratch = torch.zeros(1, device=DEV, dtype=torch.int32)
+    torch.ops.p2p.oob_counts(True)
+    torch.ops.p2p.oob_selftest(scratch)
+    on, count, site, idx, limit = torch.ops.p2p.oob_counts(True)
+    if on:
+        assert (count, site, idx, limit) == (1, 99, 1, 1)
+        assert int(scratch.item()) == 0            # the access was skipped
+        assert torch.ops.p2p.oob_counts(True)[1] == 0
+    else:
+        assert count == 0 and int(scratch.item()) == 1
