@@ -82,6 +82,7 @@ int p2p_weight_prep_pairs(int count, const float* const* w, void* const* out0, v
                           int* const* site, hipStream_t st);
 int p2p_m32_enabled();
 int p2p_set_m32(int on);
+long p2p_wgrad_reduce_extra(int splits, long slab);
 int p2p_oob_counts(unsigned int* out4, int reset);
 int p2p_oob_selftest(void* scratch, hipStream_t st);
 int p2p_conv_fwd_m32(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t st);
@@ -917,7 +918,7 @@ bool conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, con
     const int64_t slab = R * (int64_t)a.Kq;
     splits = std::max<int64_t>(1, std::min<int64_t>(splits, (64ll << 20) / std::max<int64_t>(slab, 1)));
     a.splits = (int)splits;
-    Tensor ws = at::empty({splits * slab}, p1.options().dtype(at::kFloat));
+    Tensor ws = at::empty({splits * slab + p2p_wgrad_reduce_extra((int)splits, slab)}, p1.options().dtype(at::kFloat));
     a.ws = ws.data_ptr<float>();
     check_rc(p2p_conv_wgrad(&a, st), "conv_wgrad(fp8)");
     check_rc(p2p_wgrad_reduce(a.ws, a.splits, a.R, a.KH, a.KW, a.C, (int)Rr, (int)Cr, dw.data_ptr<float>(),
@@ -952,7 +953,8 @@ bool conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, con
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int blocks = std::max(1, std::min(h.ntiles, cus));
-    Tensor ws = at::empty({(int64_t)blocks * R * a.Kq}, p1.options().dtype(at::kFloat));
+    Tensor ws = at::empty({(int64_t)blocks * R * a.Kq + p2p_wgrad_reduce_extra(blocks, R * a.Kq)},
+                          p1.options().dtype(at::kFloat));
     h.ws = ws.data_ptr<float>();
     const int rc = p2p_halo_wgrad(&h, (int)KH, blocks, st);
     if (rc != -2) {
@@ -974,7 +976,7 @@ bool conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, con
   const int64_t slab = R * (int64_t)a.Kq;
   splits = std::max<int64_t>(1, std::min<int64_t>(splits, (64ll << 20) / std::max<int64_t>(slab, 1)));
   a.splits = (int)splits;
-  Tensor ws = at::empty({splits * slab}, p1.options().dtype(at::kFloat));
+  Tensor ws = at::empty({splits * slab + p2p_wgrad_reduce_extra((int)splits, slab)}, p1.options().dtype(at::kFloat));
   a.ws = ws.data_ptr<float>();
   check_rc(p2p_conv_wgrad(&a, st), "conv_wgrad");
   check_rc(p2p_wgrad_reduce(a.ws, a.splits, a.R, a.KH, a.KW, a.C, flip ? (int)Cr : (int)Rr,

@@ -1106,10 +1106,50 @@ extern "C" int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+namespace p2p {
+// Pre-sum for large split counts: slab group g of the output = sum of the input slabs
+// [32 g, 32 g + 32) in increasing order, one thread per (element, group) -- the many-split /
+// few-element weight gradients (first-layer convs: one 64 x 128 tile, 512 splits) had
+// ~64 blocks walking every split serially in the single reduce pass (0.3-0.65 ms per call in
+// the B = 1024 step); this pass spreads them over the whole chip and leaves the reduce <= 16
+// slabs.  Fixed order: deterministic.
+__global__ void __launch_bounds__(256) wgrad_presum_kernel(const float* __restrict__ ws, int splits, long total,
+                                                           float* __restrict__ out) {
+  const long e = blockIdx.x * 256L + threadIdx.x;
+  const int g = blockIdx.y;
+  if (e >= total) return;
+  const int k0 = g * 32, k1 = min(splits, k0 + 32);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int k = k0;
+  for (; k + 4 <= k1; k += 4) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ws[(long)(k + u) * total + e];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] += v[u];
+  }
+  for (; k < k1; ++k) acc[0] += ws[(long)k * total + e];
+  out[(long)g * total + e] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+}
+}  // namespace p2p
+
+// workspace floats p2p_wgrad_reduce needs behind the slabs (its pre-sum groups)
+extern "C" long p2p_wgrad_reduce_extra(int splits, long slab) {
+  return splits > 32 ? (long)((splits + 31) / 32) * slab : 0;
+}
+
 extern "C" int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int KW, int C, int Rr,
                                 int Cr, float* dw, float scale, int accumulate, int flip,
                                 hipStream_t st) {
   const long total = (long)R * KH * KW * C;
+  if (splits > 32) {   // ws holds p2p_wgrad_reduce_extra() more floats behind the slabs
+    const int groups = (splits + 31) / 32;
+    float* pre = const_cast<float*>(ws) + (long)splits * total;
+    hipLaunchKernelGGL(p2p::wgrad_presum_kernel, dim3((unsigned)((total + 255) / 256), (unsigned)groups), dim3(256), 0,
+                       st, ws, splits, total, pre);
+    ws = pre;
+    splits = groups;
+  }
   int G = 1;
   while (G < 32 && splits > 8 * G) G *= 2;   // <= ~8 slab reads per thread
   if (KH * KW <= 81) {
