@@ -227,7 +227,9 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
 
   // ---- loader decode: A rows row_i = wid*8 + rsub + RPP*i (pixel of the block's first image
   // + y / x origin of its taps); the source-side swizzle (row >> 1) & 7 does not depend on i
-  int r_img[AROWS], r_y[AROWS], r_x[AROWS];
+  // per A row: the image offset and the tap origin (y, x) packed as two int16 (one register
+  // instead of two); y = -16384 marks a padded row
+  int r_img[AROWS], r_yx[AROWS];
   const int r_c = (slot8 ^ (((wid * 8 + rsub) >> 1) & 7)) * 8;
 #pragma unroll
   for (int i = 0; i < AROWS; ++i) {
@@ -239,14 +241,16 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
     const int qy = (int)fdiv((uint32_t)r, fd_wq);
     const int qx = r - qy * g.Wq;
     r_img[i] = (n - img0) * a.H * a.W;
+    int y0, x0;
     if (MODE == 0) {
-      r_y[i] = qy * a.stride - a.pad;
-      r_x[i] = qx * a.stride - a.pad;
+      y0 = qy * a.stride - a.pad;
+      x0 = qx * a.stride - a.pad;
     } else {
-      r_y[i] = qy + g.dy;
-      r_x[i] = qx + g.dx;
+      y0 = qy + g.dy;
+      x0 = qx + g.dx;
     }
-    if (m >= g.Mc) r_y[i] = -(1 << 28);
+    if (m >= g.Mc) y0 = -16384;
+    r_yx[i] = (int)(((uint32_t)y0 << 16) | ((uint32_t)x0 & 0xffffu));
   }
   uint32_t b_vo[BROWS];
 #pragma unroll
@@ -278,8 +282,9 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
         int iy, ix;
         bool inb;
         if (MODE == 0) {
-          int uy = r_y[i] + t_y, ux = r_x[i] + t_x;
-          if (a.reflect && r_y[i] > -(1 << 27)) {
+          const int ry0 = r_yx[i] >> 16, rx0 = (int)(int16_t)(r_yx[i] & 0xffff);
+          int uy = ry0 + t_y, ux = rx0 + t_x;
+          if (a.reflect && ry0 > -8192) {
             uy = reflect_idx(uy, Hu);
             ux = reflect_idx(ux, Wu);
           }
@@ -287,8 +292,8 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
           iy = uy >> ush;
           ix = ux >> ush;
         } else {
-          iy = r_y[i] - t_y;
-          ix = r_x[i] - t_x;
+          iy = (r_yx[i] >> 16) - t_y;
+          ix = (int)(int16_t)(r_yx[i] & 0xffff) - t_x;
           inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
         }
         a_vo[i] = inb ? (uint32_t)(((r_img[i] + iy * a.W + ix) * cs + cio + r_c) * 2) : OOB;

@@ -17,8 +17,11 @@ Calibration (from the probe's own counter pass; its kernels issue exactly
   * MFMA busy % = 100 x (busy cycles / busy_per_mfma_bf16 x 16) / (1024 SIMDs x kernel cycles)
     -- i.e. MFMA-pipe cycles (16 per bf16 16x16x32, 32 per fp8 16x16x128) over the SIMD-cycles
     the kernel had; the probe's own row must read its FLOP-derived utilisation.
-FLOPs per MFMA instruction: 16384 (bf16 16x16x32), 65536 (fp8 16x16x128, the conv kernels'
-F8 template argument != 0).
+FLOPs per MFMA instruction: 16384 (bf16 16x16x32), 32768 (bf16 32x32x16: the *_m32_kernel
+tiles, instruction counts calibrated on the probe's k_bf16_32), 65536 (fp8 16x16x128, the conv
+kernels' F8 template argument != 0).  MFMA busy % converts the busy counter to pipe-cycles
+with the 16x16x32 calibration; the probe's k_bf16_32 row checks that the same conversion
+holds for the 32-cycle 32x32x16 instruction (its util_true must read ~1).
 """
 from __future__ import annotations
 
@@ -63,13 +66,14 @@ def calibrate(probe_dir):
     vals, dur = load(probe_dir)
     cal = {}
     for k, c in vals.items():
-        tag = "bf16" if "k_bf16" in k else ("fp8" if "k_fp8" in k else None)
+        tag = ("bf16_32" if "k_bf16_32" in k else "bf16" if "k_bf16" in k else
+               ("fp8" if "k_fp8" in k else None))
         if tag is None:
             continue
         ns = mean(dur.get(k, []))
         inst, busy, grbm = mean(c.get("SQ_INSTS_MFMA")), mean(c.get("SQ_VALU_MFMA_BUSY_CYCLES")), \
             mean(c.get("GRBM_GUI_ACTIVE"))
-        flop = PROBE_WAVE_MFMAS * (16384 if tag == "bf16" else 65536)
+        flop = PROBE_WAVE_MFMAS * {"bf16": 16384, "bf16_32": 32768, "fp8": 65536}[tag]
         clock = grbm / XCDS / ns if grbm and ns else None              # GHz
         pipe = PROBE_WAVE_MFMAS * (16 if tag == "bf16" else 32)       # MFMA-pipe SIMD-cycles
         cal[tag] = {
@@ -87,6 +91,11 @@ def is_fp8(kernel):
         args = [x.strip() for x in m.group(1).split(",")]
         return len(args) > 8 and args[8] not in ("0",)
     return False
+
+
+def is_m32(kernel):
+    """The 32x32x16 bf16 MFMA kernels (round 5): conv_fwd_m32 / conv_wgrad_m32."""
+    return "_m32_kernel" in kernel
 
 
 def short(k):
@@ -118,8 +127,9 @@ def main(root, steps, probe):
         lds, conf = mean(c.get("SQ_INSTS_LDS", [])), mean(c.get("SQ_LDS_BANK_CONFLICT", []))
         fetch = mean(fe.get(k, {}).get("FETCH_SIZE", []))
         write = mean(wr.get(k, {}).get("WRITE_SIZE", []))
-        fpi = 65536 if is_fp8(k) else 16384
-        flop = (mf / inst_scale) * fpi if mf else 0.0
+        fpi = 65536 if is_fp8(k) else 32768 if is_m32(k) else 16384
+        scale_i = (cal.get("bf16_32", {}).get("inst_scale") or inst_scale) if is_m32(k) else inst_scale
+        flop = (mf / scale_i) * fpi if mf else 0.0
         # MFMA-pipe SIMD-cycles: the busy counter in units of one bf16 16x16x32 (16 cycles)
         pipe = busy / busy_bf16 * 16 if busy else None
         util = 100.0 * pipe / (SIMDS * grbm / XCDS) if pipe and grbm else None
