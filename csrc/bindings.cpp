@@ -35,7 +35,7 @@ int p2p_sn_power_iter(const float* W, int h, int wd, float* u, float* v, float* 
                       float* scale, hipStream_t st);
 int p2p_sn_wgrad_blocks(long n);
 int p2p_sn_wgrad(const float* G, const float* W, const float* u, const float* v, const float* scale, int h,
-                 int wd, float* part, float* out, hipStream_t st);
+                 int wd, float* part, float* out, int accumulate, hipStream_t st);
 long p2p_norm_ws_floats(int N, int HW, int C);
 int p2p_norm_fwd_partials(const void* x, int N, int HW, int C, int nchunks, const float* partials,
                           float eps, const float* gamma, const float* beta, const float* prelu_w,
@@ -87,6 +87,8 @@ int p2p_oob_counts(unsigned int* out4, int reset);
 int p2p_oob_selftest(void* scratch, hipStream_t st);
 int p2p_conv_fwd_m32(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t st);
 int p2p_up2_dgrad_image(const float* w, int Cout, int Cin, int Xp, int Yp, void* out, hipStream_t st);
+int p2p_col_weight(const void* w, int T, int C, int Cv, int Cvp, int Ncol, void* out, hipStream_t st);
+int p2p_vec_pad(const float* x, int n, float fill, int nout, float* out, hipStream_t st);
 int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, int reflect,
                  const void* xb, int act, const void* res, void* dx, hipStream_t st);
 int p2p_fold_band(const void* fb, int N, int H, int W, int C, int pad, int edge, const void* xb, int act, void* dx,
@@ -95,7 +97,7 @@ int p2p_pad_channels(const void* a, int Ca, const void* b, int Cb, long P, int C
                      hipStream_t st);
 int p2p_slice_channels(const void* in, int Ci, int c0, long P, int C, void* out, hipStream_t st);
 int p2p_colsum_blocks(long M, int C);
-int p2p_colsum(const void* x, long M, int C, float scale, int accumulate, float* ws, float* out,
+int p2p_colsum(const void* x, long M, int C, float scale, int accumulate, float* ws, float* out, int Cout,
                hipStream_t st);
 int p2p_loss_blocks(long n);
 int p2p_loss_fwd(const void* a, const void* b, int is_f32, long n, int kind, float t, float scale,
@@ -333,9 +335,10 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     const int64_t Cvp = Cv <= 2 ? Cv : (Cv <= 4 ? 4 : (Cv <= 8 ? 8 : 16));
     const int64_t Ncol = ((T * Cvp + 7) / 8) * 8;
     Tensor wv = at::empty({Ncol, C}, w.options());
-    (void)hipMemsetAsync(wv.data_ptr(), 0, wv.numel() * wv.element_size(), st);   // pad taps / rows
-    wv.narrow(0, 0, T * Cvp).view({T, Cvp, C}).narrow(1, 0, Cv).copy_(
-        w.reshape({-1}).narrow(0, 0, Cout * T * C).view({Cout, T, C}).narrow(0, 0, Cv).transpose(0, 1));
+    TORCH_CHECK(w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.numel() >= Cout * T * C,
+                "conv_fwd(col): bf16 weight image [Cout][T][C]");
+    check_rc(p2p_col_weight(w.data_ptr(), (int)T, (int)C, (int)Cv, (int)Cvp, (int)Ncol, wv.data_ptr(), st),
+             "conv_fwd(col weight)");
     Tensor col = empty_nhwc(N, Ncol, H, W, obf);
     p2p::ConvFwdArgs g = a;
     g.KH = g.KW = 1;
@@ -1001,6 +1004,16 @@ Tensor weight_prep(const Tensor& w, int64_t swap, int64_t Xp, int64_t Yp,
   return out;
 }
 
+// out[:x.numel()] = x, out[x.numel():] = fill (fp32 vectors; out may be shorter: a copy)
+void vec_pad_into(const Tensor& x, Tensor out, double fill) {
+  TORCH_CHECK(x.is_cuda() && out.is_cuda() && x.scalar_type() == at::kFloat && out.scalar_type() == at::kFloat &&
+                  x.is_contiguous() && out.is_contiguous(), "vec_pad_into: contiguous fp32 vectors");
+  if (out.numel() == 0) return;
+  check_rc(p2p_vec_pad(x.data_ptr<float>(), (int)x.numel(), (float)fill, (int)out.numel(), out.data_ptr<float>(),
+                       cur_stream(out)),
+           "vec_pad_into");
+}
+
 // runtime A/B switch of the 32x32x16 conv tiles (returns the previous setting)
 int64_t set_m32(int64_t on) { return p2p_set_m32((int)on); }
 
@@ -1568,7 +1581,9 @@ Tensor sn_scale(const Tensor& w, Tensor u, Tensor v) {
 }
 
 // dL/dW_bar of a spectral-norm conv from its conv weight gradient G (see csrc/sn.hip)
-Tensor sn_wgrad(const Tensor& G, const Tensor& w, const Tensor& u, const Tensor& v, const Tensor& scale) {
+// acc: add this gradient into acc (a later contribution of the same backward) and return it
+Tensor sn_wgrad(const Tensor& G, const Tensor& w, const Tensor& u, const Tensor& v, const Tensor& scale,
+                const optional<Tensor>& acc) {
   TORCH_CHECK(G.is_cuda() && G.scalar_type() == at::kFloat && G.is_contiguous(), "sn_wgrad: G fp32 contiguous");
   TORCH_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == G.numel(), "sn_wgrad: W like G");
   const int64_t h = u.numel(), wd = v.numel();
@@ -1576,10 +1591,12 @@ Tensor sn_wgrad(const Tensor& G, const Tensor& w, const Tensor& u, const Tensor&
                   u.is_contiguous() && v.is_contiguous(), "sn_wgrad: u / v");
   TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() == 1, "sn_wgrad: scale");
   Tensor part = at::empty({p2p_sn_wgrad_blocks(h * wd)}, G.options());
-  Tensor out = at::empty_like(G);
+  if (acc) TORCH_CHECK(acc->is_cuda() && acc->scalar_type() == at::kFloat && acc->is_contiguous() &&
+                       acc->numel() == G.numel(), "sn_wgrad: acc fp32 contiguous like G");
+  Tensor out = acc ? *acc : at::empty_like(G);
   check_rc(p2p_sn_wgrad(G.data_ptr<float>(), w.data_ptr<float>(), u.data_ptr<float>(), v.data_ptr<float>(),
                         scale.data_ptr<float>(), (int)h, (int)wd, part.data_ptr<float>(), out.data_ptr<float>(),
-                        cur_stream(G)),
+                        acc ? 1 : 0, cur_stream(G)),
            "sn_wgrad");
   return out;
 }
@@ -1662,18 +1679,10 @@ void colsum(const Tensor& x, Tensor out, double scale, bool accumulate) {
               "colsum: out");
   const int nb = p2p_colsum_blocks(M, (int)C);
   Tensor ws = at::empty({(int64_t)nb * C}, x.options().dtype(at::kFloat));
-  if (out.numel() == C) {
-    check_rc(p2p_colsum(x.data_ptr(), M, (int)C, (float)scale, accumulate ? 1 : 0, ws.data_ptr<float>(),
-                        out.data_ptr<float>(), cur_stream(x)),
-             "colsum");
-  } else {  // padded channels: reduce all, keep the leading out.numel()
-    Tensor full = at::empty({C}, x.options().dtype(at::kFloat));
-    check_rc(p2p_colsum(x.data_ptr(), M, (int)C, (float)scale, 0, ws.data_ptr<float>(),
-                        full.data_ptr<float>(), cur_stream(x)),
-             "colsum");
-    if (accumulate) out.add_(full.narrow(0, 0, out.numel()));
-    else out.copy_(full.narrow(0, 0, out.numel()));
-  }
+  // padded channels (out.numel() < C): the kernel writes the leading out.numel() only
+  check_rc(p2p_colsum(x.data_ptr(), M, (int)C, (float)scale, accumulate ? 1 : 0, ws.data_ptr<float>(),
+                      out.data_ptr<float>(), (int)out.numel(), cur_stream(x)),
+           "colsum");
 }
 
 // ------------------------------------------------------------------ losses
@@ -1858,7 +1867,7 @@ TORCH_LIBRARY(p2p, m) {
   m.def("fp8_quant(Tensor x, Tensor(a!) site, int fmt, int use_cur=0) -> Tensor");
   m.def("sn_power_iter(Tensor w, Tensor(a!) u, Tensor(b!) v) -> Tensor");
   m.def("sn_scale(Tensor w, Tensor(a!) u, Tensor(b!) v) -> Tensor");
-  m.def("sn_wgrad(Tensor G, Tensor w, Tensor u, Tensor v, Tensor scale) -> Tensor");
+  m.def("sn_wgrad(Tensor G, Tensor w, Tensor u, Tensor v, Tensor scale, Tensor(a!)? acc=None) -> Tensor");
   m.def("fp8_amax(Tensor x, Tensor(a!) site, int slot) -> ()");
   m.def("fp8_roll(Tensor(a!) sites) -> ()");
   m.def("fp8_amax_multi(Tensor[] x, Tensor(a!) sites, int[] idx) -> ()");
@@ -1870,6 +1879,7 @@ TORCH_LIBRARY(p2p, m) {
   m.def("weight_prep(Tensor w, int swap, int Xp, int Yp, Tensor? scale) -> Tensor");
   m.def("up2_dgrad_image(Tensor w, int Xp, int Yp) -> Tensor");
   m.def("oob_selftest(Tensor scratch) -> ()");
+  m.def("vec_pad_into(Tensor x, Tensor(a!) out, float fill) -> ()");
   m.def("set_m32(int on) -> int", set_m32);
   m.def("oob_counts(bool reset) -> int[]", oob_counts);   // no tensor arguments: a catch-all kernel
   m.def("union_weight(Tensor w, int co_off, int nv, int Nrows, int Cpad, Tensor? bias) -> Tensor[]");
@@ -1934,6 +1944,7 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("weight_prep", weight_prep);
   m.impl("up2_dgrad_image", up2_dgrad_image);
   m.impl("oob_selftest", oob_selftest);
+  m.impl("vec_pad_into", vec_pad_into);
   m.impl("union_weight", union_weight);
   m.impl("conv_d2s", conv_d2s);
   m.impl("weight_prep_multi", weight_prep_multi);

@@ -243,7 +243,7 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const bf16* __restr
 template <int G>
 __global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restrict__ ws, int nb, int C,
                                                            float scale, int accumulate,
-                                                           float* __restrict__ out) {
+                                                           float* __restrict__ out, int Cout) {
   constexpr int EPB = 256 / G;
   const int le = threadIdx.x % EPB, sg = threadIdx.x / EPB;
   const int c = blockIdx.x * EPB + le;
@@ -253,7 +253,7 @@ __global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restri
   __shared__ float red[256];
   red[threadIdx.x] = a;
   __syncthreads();
-  if (sg != 0 || c >= C) return;
+  if (sg != 0 || c >= Cout) return;   // Cout <= C: the leading channels of a padded gradient
   for (int q = 1; q < G; ++q) a += red[q * EPB + le];
   a *= scale;
   out[c] = accumulate ? out[c] + a : a;
@@ -751,7 +751,7 @@ int p2p_colsum_blocks(long M, int C) {
   return (int)b;
 }
 
-int p2p_colsum(const void* x, long M, int C, float scale, int accumulate, float* ws, float* out,
+int p2p_colsum(const void* x, long M, int C, float scale, int accumulate, float* ws, float* out, int Cout,
                hipStream_t st) {
   using namespace p2p;
   const int nb = p2p_colsum_blocks(M, C);
@@ -760,7 +760,7 @@ int p2p_colsum(const void* x, long M, int C, float scale, int accumulate, float*
                      C, rpb, ws);
   // nb <= 1024 partials per channel: 32 threads per channel, <= 32 reads each
   hipLaunchKernelGGL(colsum_final_kernel<32>, dim3((C + 7) / 8), dim3(256), 0, st, ws, nb, C, scale,
-                     accumulate, out);
+                     accumulate, out, Cout);
   return (int)hipGetLastError();
 }
 
@@ -834,13 +834,13 @@ int p2p_rowsum_f32(const float* ws, long R, int C, float* tmp, float* out, hipSt
   using namespace p2p;
   if (R <= 0 || R > 0x7fffffff) return -1;
   if (R <= 64) {
-    hipLaunchKernelGGL(colsum_final_kernel<32>, dim3((C + 7) / 8), dim3(256), 0, st, ws, (int)R, C, 1.f, 0, out);
+    hipLaunchKernelGGL(colsum_final_kernel<32>, dim3((C + 7) / 8), dim3(256), 0, st, ws, (int)R, C, 1.f, 0, out, C);
     return (int)hipGetLastError();
   }
   const int nb = p2p_rowsum_blocks(R);
   const long rpb = (R + nb - 1) / nb;
   hipLaunchKernelGGL(rowsum_partial_kernel, dim3(nb), dim3(256), 0, st, ws, R, C, rpb, tmp);
-  hipLaunchKernelGGL(colsum_final_kernel<32>, dim3((C + 7) / 8), dim3(256), 0, st, tmp, nb, C, 1.f, 0, out);
+  hipLaunchKernelGGL(colsum_final_kernel<32>, dim3((C + 7) / 8), dim3(256), 0, st, tmp, nb, C, 1.f, 0, out, C);
   return (int)hipGetLastError();
 }
 

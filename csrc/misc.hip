@@ -364,6 +364,27 @@ __device__ __forceinline__ float up2_axis(const float* v, int a, int stride) {
   return a == 0 ? v[2 * stride] : a == 1 ? v[stride] + v[2 * stride] : a == 2 ? v[0] + v[stride] : v[0];
 }
 
+// out[i] = i < n ? x[i] : fill for i < nout (fp32): a norm's per-channel vectors padded to the
+// 8-channel groups of the norm kernels (odd channel counts: family R's BN(3)) and copied back
+__global__ void __launch_bounds__(256) vec_pad_kernel(const float* __restrict__ x, int n, float fill, int nout,
+                                                      float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < nout) out[i] = i < n ? x[i] : fill;
+}
+
+// The tiny-Cout "col" GEMM's weight (bindings.cpp conv_fwd): out[t * Cvp + co][c] =
+// w[co][t][c] for co < Cv, zero for the padded tap slots and rows (out is [Ncol][C]); one
+// pass instead of a memset + a strided aten copy per call.
+__global__ void __launch_bounds__(256) col_weight_kernel(const bf16* __restrict__ w, int T, int C, int Cv, int Cvp,
+                                                         int Ncol, bf16* __restrict__ out) {
+  const long total = (long)Ncol * C;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int row = (int)(e / C), c = (int)(e - (long)row * C);
+    const int t = row / Cvp, co = row - t * Cvp;
+    out[e] = (t < T && co < Cv) ? w[((long)co * T + t) * C + c] : (bf16)0.f;
+  }
+}
+
 __global__ void __launch_bounds__(256) up2_dgrad_image_kernel(const float* __restrict__ w, int Cout, int Cin,
                                                               int Xp, int Yp, bf16* __restrict__ out) {
   const long total = (long)Xp * 16 * Yp;
@@ -490,6 +511,18 @@ int p2p_pixel_shuffle(const void* in, int N, int OH, int OW, int OC, int r, int 
   const long n = (long)N * OH * OW * OC;
   hipLaunchKernelGGL(p2p::pixel_shuffle_kernel, dim3(p2p::mgrid(n)), dim3(256), 0, st,
                      static_cast<const p2p::bf16*>(in), N, OH, OW, OC, r, dir, static_cast<p2p::bf16*>(out));
+  return (int)hipGetLastError();
+}
+
+int p2p_vec_pad(const float* x, int n, float fill, int nout, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(p2p::vec_pad_kernel, dim3((nout + 255) / 256), dim3(256), 0, st, x, n, fill, nout, out);
+  return (int)hipGetLastError();
+}
+
+int p2p_col_weight(const void* w, int T, int C, int Cv, int Cvp, int Ncol, void* out, hipStream_t st) {
+  const long n = (long)Ncol * C;
+  hipLaunchKernelGGL(p2p::col_weight_kernel, dim3(p2p::mgrid(n)), dim3(256), 0, st, static_cast<const p2p::bf16*>(w),
+                     T, C, Cv, Cvp, Ncol, static_cast<p2p::bf16*>(out));
   return (int)hipGetLastError();
 }
 

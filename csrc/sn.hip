@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(256) sn_dot_kernel(const float* __restrict__ G
 __global__ void __launch_bounds__(256) sn_grad_kernel(const float* __restrict__ G, const float* __restrict__ u,
                                                       const float* __restrict__ v, const float* __restrict__ scale,
                                                       const float* __restrict__ part, int np, int h, int wd,
-                                                      float* __restrict__ out) {
+                                                      float* __restrict__ out, int accumulate) {
   __shared__ float dsh;
   if (threadIdx.x == 0) {
     float d = 0.f;
@@ -124,7 +124,8 @@ __global__ void __launch_bounds__(256) sn_grad_kernel(const float* __restrict__ 
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
     const int r = (int)(i / wd);
     const int c = (int)(i - (long)r * wd);
-    out[i] = sc * G[i] - k * u[r] * v[c];
+    const float g = sc * G[i] - k * u[r] * v[c];
+    out[i] = accumulate ? out[i] + g : g;   // accumulate: a later contribution of one backward
   }
 }
 
@@ -160,12 +161,12 @@ int p2p_sn_wgrad_blocks(long n) {
 
 // part: p2p_sn_wgrad_blocks(h * wd) floats
 int p2p_sn_wgrad(const float* G, const float* W, const float* u, const float* v, const float* scale, int h,
-                 int wd, float* part, float* out, hipStream_t st) {
+                 int wd, float* part, float* out, int accumulate, hipStream_t st) {
   using namespace p2p;
   const long n = (long)h * wd;
   const int nb = p2p_sn_wgrad_blocks(n);
   hipLaunchKernelGGL(sn_dot_kernel, dim3(nb), dim3(256), 0, st, G, W, n, part);
-  hipLaunchKernelGGL(sn_grad_kernel, dim3(nb), dim3(256), 0, st, G, u, v, scale, part, nb, h, wd, out);
+  hipLaunchKernelGGL(sn_grad_kernel, dim3(nb), dim3(256), 0, st, G, u, v, scale, part, nb, h, wd, out, accumulate);
   return (int)hipGetLastError();
 }
 }

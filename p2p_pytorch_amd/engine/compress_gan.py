@@ -78,6 +78,14 @@ class CompressGANStep:
         self.opt_d = make_adam(net_d.parameters(), lr=lr, betas=(beta1, 0.999))
         # D's trainable parameters (SN's weight_u / weight_v are Parameters that never train)
         self._d_trainable = [p for p in net_d.parameters() if p.requires_grad]
+        # the D phase runs D's fake and real passes separately (train.py:308-316) and G's one
+        # PReLU slope serves five sites: their second and later gradients of a backward are
+        # summed in place by the kernels (ops/hip.py _pair_first), not by autograd adds
+        for p in self._d_trainable:
+            p._p2p_pair = True
+        pw = getattr(getattr(net_g, "relu", None), "weight", None)
+        if isinstance(pw, torch.Tensor):
+            pw._p2p_pair = True
         self.train_c = train_c
         self.opt_c = make_adam(net_c.parameters(), lr=lr, betas=(beta1, 0.999)) if train_c else None
         self.c_phase_backward = c_phase_backward

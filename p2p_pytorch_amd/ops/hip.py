@@ -29,6 +29,8 @@ import itertools
 import os
 import sys
 
+import weakref
+
 import torch
 
 from .. import _native
@@ -139,6 +141,57 @@ def _take_nbp(g):
 def _take_colsum(gy):
     ent = _colsum_stash.pop((gy.data_ptr(), tuple(gy.shape)), None)
     return None if ent is None else ent[1]
+
+
+# ------------------------------------------------------------ one gradient per parameter
+# A parameter read by several ops of one forward -- family R's discriminator runs its fake and
+# real passes separately in the D phase (/root/reference/train.py:308-316), so every D weight
+# and bias gets two contributions in one backward -- would have them summed by an aten add in
+# autograd's input buffer.  Instead the first contribution's tensor is remembered for the
+# current graph task and the later ones are accumulated into it by the producing kernel
+# (wgrad / sn_wgrad accumulate mode, colsum accumulate); they return None to autograd.  Within
+# one graph task AccumulateGrad runs only after every producer of the leaf, so the first
+# tensor is still unconsumed when the later contributions land in it.
+_GRAD_PAIRS: dict = {}
+_GRAD_PAIRS_TASK = [-1]
+
+
+def _pair_first(param, on=False):
+    """The tensor already handed to autograd for ``param`` in the running backward, if any.
+    Only the spectral-norm convs (``on``: family R's discriminator, run twice per D phase) and
+    parameters a model marks ``_p2p_pair`` are paired; everything else keeps autograd's plain
+    single-contribution path."""
+    if (param is None or not isinstance(param, torch.Tensor) or not param.is_leaf
+            or not (on or getattr(param, "_p2p_pair", False))):
+        return None
+    if os.environ.get("P2P_GRAD_PAIR", "1") == "0":
+        return None
+    tid = torch._C._current_graph_task_id()
+    if tid < 0 or tid != _GRAD_PAIRS_TASK[0]:
+        return None
+    ent = _GRAD_PAIRS.get(id(param))
+    return ent[1] if ent is not None and ent[0]() is param else None
+
+
+def _pair_set(param, t, on=False):
+    """``t`` is the first contribution of ``param``'s gradient in the running backward."""
+    if (param is None or t is None or not isinstance(param, torch.Tensor) or not param.is_leaf
+            or not (on or getattr(param, "_p2p_pair", False))):
+        return
+    if os.environ.get("P2P_GRAD_PAIR", "1") == "0":
+        return
+    tid = torch._C._current_graph_task_id()
+    if tid < 0:
+        return
+    if tid != _GRAD_PAIRS_TASK[0]:      # a new backward: the old entries pin finished tensors
+        _GRAD_PAIRS.clear()
+        _GRAD_PAIRS_TASK[0] = tid
+    # keep an ALIAS (a second TensorImpl over the same storage), not ``t`` itself: an extra
+    # reference to ``t`` makes AccumulateGrad clone it instead of stealing it -- an extra copy
+    # kernel, and for a weight gradient written on the side stream a compute-stream read
+    # racing that write (``_wgrad_side``)
+    alias = t.new_empty((0,)).set_(t.untyped_storage(), t.storage_offset(), t.size(), t.stride())
+    _GRAD_PAIRS[id(param)] = (weakref.ref(param), alias)
 
 
 # ------------------------------------------------------------ weight-gradient side stream
@@ -582,6 +635,7 @@ class ConvFn(torch.autograd.Function):
         ctx.geo = (C1, C2, Cp, packed, Cout, Coutp, H, W)
         ctx.has_x2 = x2 is not None
         ctx.has_bias = bias is not None
+        ctx.bias_p = bias if (bias is not None and bias.is_leaf) else None   # gradient pairing
         ctx.nb = (None if packed else _norm_lookup(q1), _norm_lookup(q2))
         if (_NB_FUSE and bias is not None and bias.requires_grad and Coutp == Cout
                 and (cfg.act_out in (None, "none") or cfg.out_gated)):
@@ -601,14 +655,14 @@ class ConvFn(torch.autograd.Function):
                 _, _, gw, gb = _conv_backward(ctx.cfg, ctx.geo, q1, q2, weight, y, gy, False, False,
                                               ctx.needs_input_grad[2],
                                               ctx.has_bias and ctx.needs_input_grad[3],
-                                              side_ok=True)
+                                              side_ok=True, bias=ctx.bias_p)
                 return gx1, None, gw, gb, None
             return gx1, None, None, None, None
         gx1, gx2, gw, gb = _conv_backward(ctx.cfg, ctx.geo, q1, q2, weight, y, gy, need_x1,
                                           ctx.has_x2 and ctx.needs_input_grad[1],
                                           ctx.needs_input_grad[2],
                                           ctx.has_bias and ctx.needs_input_grad[3], nb=ctx.nb,
-                                          side_ok=True)
+                                          side_ok=True, bias=ctx.bias_p)
         return gx1, gx2, gw, gb, None
 
 
@@ -646,6 +700,8 @@ class SNConvFn(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.geo = (C1, 0, Cp, packed, Cout, Coutp, H, W)
         ctx.has_bias = bias is not None
+        ctx.bias_p = bias if (bias is not None and bias.is_leaf) else None   # gradient pairing
+        ctx.w_p = w_bar if w_bar.is_leaf else None
         ctx.uv = uv
         keep_y = cfg.act_out not in (None, "none") and not cfg.out_gated
         ctx.save_for_backward(q1, w_bar, sc, y if keep_y else None)
@@ -657,12 +713,20 @@ class SNConvFn(torch.autograd.Function):
         need_w = ctx.needs_input_grad[1] or ctx.needs_input_grad[3]
         gx, _, G, gb = _conv_backward(ctx.cfg, ctx.geo, q1, None, w_bar, y, gy,
                                       ctx.needs_input_grad[0], False, need_w,
-                                      ctx.has_bias and ctx.needs_input_grad[2], alpha=sc)
+                                      ctx.has_bias and ctx.needs_input_grad[2], alpha=sc,
+                                      bias=ctx.bias_p, pair=True)
         if ctx.uv is not None:
             u, v = ctx.uv
             wb = w_bar.detach()
             wb = wb if (wb.dtype == torch.float32 and wb.is_contiguous()) else wb.float().contiguous()
-            gw = P().sn_wgrad(G, wb, u.detach(), v.detach(), sc) if ctx.needs_input_grad[1] else None
+            gw = None
+            if ctx.needs_input_grad[1]:
+                first = _pair_first(ctx.w_p, True)   # the D phase's second pass: into the first
+                if first is not None:
+                    P().sn_wgrad(G, wb, u.detach(), v.detach(), sc, first)
+                else:
+                    gw = P().sn_wgrad(G, wb, u.detach(), v.detach(), sc)
+                    _pair_set(ctx.w_p, gw, True)
             return gx, gw, gb, None, None, None
         gw = G * sc if ctx.needs_input_grad[1] else None
         gs = (G * w_bar.detach()).sum().reshape(1) if ctx.needs_input_grad[3] else None
@@ -744,7 +808,7 @@ def _wgrad_fp8(cfg, weight, q1, q2, gyp, act_in):
 
 
 def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, need_b, alpha=None,
-                   nb=None, side_ok=False):
+                   nb=None, side_ok=False, bias=None, pair=False):
     """Input / weight / bias gradients of one fused conv (ConvFn's backward, shared with the
     image head): dgrad with the input-activation gate, concat split and skip-gradient
     hand-off in its epilogue; wgrad; bias = column sums (or the norm's exact zero).
@@ -854,8 +918,13 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
         # so the kernel may also run on the side stream
         red = getattr(weight, "_p2p_direct", None) if alpha is None else None
         direct = red is not None and red.direct_ok(weight)
+        # a later contribution of this backward goes into the first one (see _pair_first);
+        # the SN conv (alpha) pairs its final gradient in SNConvFn instead
+        first = None if (direct or alpha is not None) else _pair_first(weight)
         if direct:
             gw, wscale, wacc = weight.grad, red.scale, 1
+        elif first is not None:
+            gw, wscale, wacc = first, 1.0, 1
         else:
             red_any = getattr(weight, "_p2p_direct", None)
             if (red_any is not None and id(weight) in red_any._direct_seen and _WgradSide.on is not None
@@ -894,11 +963,24 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
         if direct:
             red.direct_done(weight, side)
             gw = None
+        elif first is not None:
+            gw = None
+        elif alpha is None:
+            _pair_set(weight, gw)
     if need_b:
         gb = _take_colsum(gy) if (cfg.act_out in (None, "none") or cfg.out_gated) else None
-        if gb is None:
-            gb = torch.empty(Cout, device=gy.device, dtype=torch.float32)
-            P().colsum(gyp, gb, 1.0, False)
+        first_b = _pair_first(bias, pair)
+        if first_b is not None:
+            if gb is not None:
+                P().lincomb_(first_b, gb, 1.0, 1.0, 0.0)
+            else:
+                P().colsum(gyp, first_b, 1.0, True)
+            gb = None
+        else:
+            if gb is None:
+                gb = torch.empty(Cout, device=gy.device, dtype=torch.float32)
+                P().colsum(gyp, gb, 1.0, False)
+            _pair_set(bias, gb, pair)
     return gx1, gx2, gw, gb
 
 
@@ -1245,6 +1327,15 @@ class NormFn(torch.autograd.Function):
                 _f8.stash_shadow(dx, qd, dsite)
             elif fresh:
                 _f8.bootstrap_shadow(dx, (ctx.qkey, "dx"), _f8.E5M2)
+        if gpw is not None:
+            # a shared PReLU slope (family R: one slope, five sites): its later gradients of this
+            # backward are added into the first in place (HIP) instead of by autograd (aten)
+            first = _pair_first(prelu_w)
+            if first is not None:
+                P().lincomb_(first, gpw, 1.0, 1.0, 0.0)
+                gpw = None
+            else:
+                _pair_set(prelu_w, gpw)
         return (dx if need_x else None), dg, db, gpw, None, None, None, None, None, None, None, None, gres, None
 
 
@@ -1285,22 +1376,42 @@ def _norm_any_c(x, gamma, beta, prelu_w, run_mean, run_var, eps, momentum, act, 
         return NormFn.apply(x, gamma, beta, prelu_w, run_mean, run_var, eps, momentum, act, batch,
                             training, qkey)
     # odd channel counts (family-R tail BN(3)): pad to 8 with identity channels, slice back
+    # (the per-channel vectors padded / copied back by a HIP kernel, not aten cat / copy)
     cp = _pad8(C)
-    pad = cp - C
     g8 = b8 = rm8 = rv8 = None
     if gamma is not None:
-        g8 = torch.cat((gamma, gamma.new_ones(pad)))
-        b8 = torch.cat((beta, beta.new_zeros(pad)))
+        g8 = _VecPadFn.apply(gamma, cp, 1.0)
+        b8 = _VecPadFn.apply(beta, cp, 0.0)
     if run_mean is not None:
-        rm8 = torch.cat((run_mean, run_mean.new_zeros(pad)))
-        rv8 = torch.cat((run_var, run_var.new_ones(pad)))
+        rm8 = _vec_pad(run_mean, cp, 0.0)
+        rv8 = _vec_pad(run_var, cp, 1.0)
     y8 = NormFn.apply(_PadCFn.apply(x, cp), g8, b8, prelu_w, rm8, rv8, eps, momentum, act, batch,
                       training)
     if run_mean is not None and training:
         with torch.no_grad():
-            run_mean.copy_(rm8[:C])
-            run_var.copy_(rv8[:C])
+            P().vec_pad_into(rm8[:C], run_mean, 0.0)
+            P().vec_pad_into(rv8[:C], run_var, 0.0)
     return _SliceCFn.apply(y8, C)
+
+
+def _vec_pad(v, n, fill):
+    out = torch.empty(n, device=v.device, dtype=torch.float32)
+    P().vec_pad_into(v.detach().float().contiguous(), out, float(fill))
+    return out
+
+
+class _VecPadFn(torch.autograd.Function):
+    """A norm's affine vector padded with ``fill`` to ``n`` channels; its gradient is the
+    leading slice (a view: no kernel)."""
+
+    @staticmethod
+    def forward(ctx, v, n, fill):
+        ctx.c = v.shape[0]
+        return _vec_pad(v, n, fill)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g[:ctx.c], None, None
 
 
 def instance_norm(x, eps=1e-5, act=None, weight=None, bias=None, qkey=None):
