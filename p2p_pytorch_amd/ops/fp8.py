@@ -79,8 +79,8 @@ class _Pool:
                 # a new site inside a hipGraph capture would bake its (re)initialisation into
                 # every replay and its row pointer into the graph: only sites
                 # registered by the eager warmup steps may be used under capture
-                raise RuntimeError(f"fp8: new scale site {key!r} requested during graph capture; "
-                                   "run an eager warmup step first")
+                raise RuntimeError(f"fp8: new scale site {key!r} ({_describe(key)}) requested during "
+                                   "graph capture; run an eager warmup step first")
             if self.free:
                 i = self.free.pop()
                 self.sites[i].zero_()    # no amax window inherited from the previous owner
@@ -106,6 +106,13 @@ class _Pool:
 # object -> key: id(obj) maps to (weakref, key); a recycled id with a dead weakref gets a new key
 _obj_keys: dict = {}
 _key_counter = itertools.count(1)
+# key -> short description of its object (type / shape / leaf), for the capture error
+_key_desc: dict = {}
+
+
+def _describe(key):
+    k = key[0] if isinstance(key, tuple) and key and isinstance(key[0], tuple) else key
+    return _key_desc.get(k, "no object")
 
 
 def obj_key(obj):
@@ -115,8 +122,13 @@ def obj_key(obj):
         return ent[1]
     k = ("obj", next(_key_counter))
     oid = id(obj)
+    if isinstance(obj, torch.Tensor):
+        _key_desc[k] = f"tensor {tuple(obj.shape)} {obj.dtype} leaf={obj.is_leaf} grad_fn={type(obj.grad_fn).__name__}"
+    else:
+        _key_desc[k] = type(obj).__name__
 
     def _dead(_ref, oid=oid, k=k):
+        _key_desc.pop(k, None)
         cur = _obj_keys.get(oid)
         if cur is not None and cur[1] == k:
             del _obj_keys[oid]
@@ -238,15 +250,17 @@ def quant_weight(img: torch.Tensor, key) -> tuple[torch.Tensor, torch.Tensor]:
     return P.fp8_quant(img, site, E4M3, 0), site
 
 
-def prepare_weight_pairs(ws, xa, xb):
+def prepare_weight_pairs(ws, xa, xb, owners=None):
     """e4m3 GEMM images (both layouts) of fp32 masters ``ws`` with current scaling: one
     fill (zero the amax words), one multi-tensor amax launch, one image launch per 24
-    tensors.  Returns [(img0, img1, site)]."""
+    tensors.  Returns [(img0, img1, site)].  ``owners``: the parameters the sites are keyed
+    by (``ws`` may be per-call ``detach()`` views, new objects every step -- keyed by
+    themselves they would take a new site each step, which a hipGraph capture refuses)."""
     if not ws:
         return []
     P = _native.ops()
     wp = wpool(ws[0].device)
-    idx = [wp.site(obj_key(w)) for w in ws]
+    idx = [wp.site(obj_key(o)) for o in (owners if owners is not None else ws)]
     wp.sites[: wp.high, 0].zero_()
     P.fp8_amax_multi(list(ws), wp.sites, idx)
     imgs = P.weight_prep_pairs(list(ws), list(xa), list(xb), wp.sites, idx)

@@ -444,7 +444,8 @@ def prepare_weights(*modules):
         # bf16 images for the image-facing rest
         sel = [i for i in range(len(pw)) if _f8.pair_ok(pkeys[i].shape[0], pkeys[i].shape[1])]
         for j, (i0, i1, site) in zip(sel, _f8.prepare_weight_pairs(
-                [pw[i] for i in sel], [pa[i] for i in sel], [pb[i] for i in sel])):
+                [pw[i] for i in sel], [pa[i] for i in sel], [pb[i] for i in sel],
+                [pkeys[i] for i in sel])):
             w = pkeys[j]
             entries.append((w, (0, pa[j], pb[j], "fp8"), (i0, site)))
             entries.append((w, (1, pb[j], pa[j], "fp8"), (i1, site)))

@@ -224,6 +224,33 @@ def test_unet_step_fp8_close_to_bf16():
     assert all(math.isfinite(v) for d in res["fp8"] for v in d.values())
 
 
+def test_unet_step_fp8_captures():
+    """The fp8 step is capturable in one hipGraph: every scale site (weights included) is
+    registered by the eager warmup, so the capture asks for none (the weight-pair sites were
+    once keyed by per-call ``detach()`` views -- a new site every step -- and bench.py's fp8
+    line fell back to eager with a CaptureError)."""
+    from p2p_pytorch_amd.engine.graph import CapturedStep
+    from p2p_pytorch_amd.engine.pix2pix import Pix2PixStep
+    from p2p_pytorch_amd.models import define_D, define_G
+    dev = torch.device(DEV)
+    torch.manual_seed(0)
+    G = define_G(netG="unet_256", gpu_id=dev, verbose=False)
+    D = define_D(6, 64, norm="instance", netD="basic", gpu_id=dev, verbose=False)
+    step = Pix2PixStep(G, D)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    A = bf(torch.rand(2, 3, 256, 256, device=dev, generator=g) * 2 - 1)
+    B = bf(torch.rand(2, 3, 256, 256, device=dev, generator=g) * 2 - 1)
+    p0 = next(G.parameters())
+    w0 = p0.detach().clone()
+    cap = CapturedStep(step.step, A, B, warmup=2)
+    for _ in range(2):
+        out = cap()
+    torch.cuda.synchronize()
+    vals = {k: float(v) for k, v in out.items()}
+    assert all(math.isfinite(v) for v in vals.values()), vals
+    assert not torch.equal(w0, p0.detach())   # the replays stepped the optimizer
+
+
 def _expect_fp8(y, site, fmt):
     k = 127 - int(site[2].item())
     tdt, fmax = (torch.float8_e4m3fn, 448.0) if fmt == 0 else (torch.float8_e5m2, 57344.0)
