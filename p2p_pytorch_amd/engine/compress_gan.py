@@ -182,7 +182,9 @@ class CompressGANStep:
             loss_d = (loss_d_fake + loss_d_real) * 0.5
         # ---- G losses: D frozen (its G-loss gradients are discarded by the reference)
         set_requires_grad(self._d_trainable, False)
-        pred_fake_g = D(self._d_in(real_a, fake_b))
+        # fake_b feeds D, VGG and TV: one fan-out node sums their gradients with HIP adds
+        fake_d, fake_v, fake_t = ops.fan_out(fake_b, 3)
+        pred_fake_g = D(self._d_in(real_a, fake_d))
         # back on before any backward: autograd's AccumulateGrad skips a leaf that no longer
         # requires grad, which would silently drop the D-loss gradients
         set_requires_grad(self._d_trainable, True)
@@ -207,8 +209,8 @@ class CompressGANStep:
         fy_real = (self.criterionVGG.target_features(real_b)
                    if hasattr(self.criterionVGG, "target_features")
                    and os.environ.get("P2P_VGG_REUSE", "1") != "0" else None)
-        vgg_g = self._vgg(fake_b, real_b, fy_real)
-        tv = calc_tv_Loss(fake_b)
+        vgg_g = self._vgg(fake_v, real_b, fy_real)
+        tv = calc_tv_Loss(fake_t)
         if native:
             terms = [loss_g_gan] + ([loss_feat] if feat else []) + [vgg_g, tv]
             loss_g = ops.lincomb_n(terms, [1.0] + ([1.0] if feat else []) + [self.lambda_vgg,

@@ -163,7 +163,7 @@ class ExpandNetwork(nn.Module):
         y = self.in1_e(y, prelu=pw)
         y = self.in2_e(self.conv2(y), prelu=pw)
         y = self.in3_e(self.conv3(y), prelu=pw)
-        res = y
+        y, res = ops.fan_out(y, 2)   # the trunk and the long skip: one HIP-summed gradient
         for k in range(1, 10):
             res = getattr(self, f"res{k}")(res)
         y = ops.add_act(res, y, "lrelu")
@@ -366,7 +366,16 @@ class MultiscaleDiscriminator(nn.Module):
     def forward(self, x):
         result = []
         for i in range(self.num_D):
-            result.append(self._single(self.num_D - 1 - i, x))
+            xs = x
+            if i != self.num_D - 1:
+                # this scale's PatchGAN and the next pyramid level both read x: their
+                # gradients meet in one fan-out node (HIP adds) instead of autograd's add
+                if isinstance(x, (tuple, list)):
+                    pairs = [ops.fan_out(t, 2) for t in x]
+                    xs, x = tuple(p[0] for p in pairs), tuple(p[1] for p in pairs)
+                else:
+                    xs, x = ops.fan_out(x, 2)
+            result.append(self._single(self.num_D - 1 - i, xs))
             if i != self.num_D - 1:
                 x = self.downsample(x)
         return result

@@ -94,6 +94,15 @@ def add_act(a, b, name, defer_b=False):
     return ref.apply_act(a + b, name)
 
 
+def fan_out(x, n):
+    """``n`` handles of ``x`` for ``n`` consumers.  HIP path: their gradients are summed by HIP
+    adds in one backward node, not by autograd's input-buffer accumulation (an aten add per
+    extra consumer); elsewhere the same tensor ``n`` times."""
+    if x is not None and x.requires_grad and _native.use_native(x):
+        return _hip().fan_out(x, n)
+    return (x,) * n
+
+
 def dropout(x, p, training, salt=None):
     """``salt``: per-module constant mixed with the device seed (advanced once per step), so
     a captured graph draws the same masks as the eager step it replays."""

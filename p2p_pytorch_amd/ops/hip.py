@@ -1490,6 +1490,34 @@ def add_act(a, b, name, defer_b=False):
     return AddActFn.apply(a, b, name, defer_b)
 
 
+class FanOutFn(torch.autograd.Function):
+    """One activation read by ``n`` consumers (family R: the generated image feeds D's first
+    conv, its pooling pyramid, VGG and TV; the expander's residual trunk input feeds the trunk
+    and the long skip): ``n`` aliases go to autograd, and their gradients meet here, summed
+    by the bf16 add of the act kernel (mode 3, act none) -- instead of an aten add per extra
+    consumer in autograd's input buffer."""
+
+    @staticmethod
+    def forward(ctx, x, n):
+        return tuple(x.view_as(x) for _ in range(n))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        acc = None
+        for g in gs:
+            if g is None:
+                continue
+            g = to_nhwc_bf16(g)
+            acc = g if acc is None else P().act(acc, g, 0, 3)
+        return acc, None
+
+
+def fan_out(x, n):
+    if n <= 1:
+        return (x,)
+    return FanOutFn.apply(x, int(n))
+
+
 class LinCombFn(torch.autograd.Function):
     """wa * a + wb * b of fp32 loss scalars (the step's loss composition) on a HIP kernel."""
 
