@@ -68,13 +68,15 @@ int p2p_prelu_bwd(const void* x, const void* dy, long n, const float* w, void* d
 int p2p_tv_fwd(const void* x, int N, int H, int W, int C, float* ws, float* out, hipStream_t st);
 int p2p_tv_bwd(const void* x, int N, int H, int W, int C, const float* gout, void* dx, hipStream_t st);
 int p2p_quantize(const void* x, long n, int bits, void* y, hipStream_t st);
+int p2p_quantize_unshuffle(const void* x, int N, int H, int W, int C, int bits, int r, void* y, void* yu, int Cp,
+                           hipStream_t st);
 int p2p_metrics_ws(int C, int H, int W);
 int p2p_image_metrics(const void* a, const void* b, int dtype, const long* strides, int N, int C, int H, int W,
                       int shift, double data_range, double* ws, hipStream_t st);
 int p2p_avgpool3s2(const void* x, int N, int H, int W, int C, int OH, int OW, void* y, int bwd, hipStream_t st);
 int p2p_maxpool2(const void* x, const void* gy, int N, int H, int W, int C, void* out, hipStream_t st);
-int p2p_l2norm(const void* x, const void* gy, long P, int C, float eps, const void* res, void* out,
-               hipStream_t st);
+int p2p_l2norm(const void* x, const void* gy, long P, int C, float eps, const void* res, void* out, int r, int IH,
+               int IW, hipStream_t st);
 int p2p_pixel_shuffle(const void* in, int N, int OH, int OW, int OC, int r, int dir, void* out,
                       hipStream_t st);
 int p2p_weight_prep_pairs(int count, const float* const* w, void* const* out0, void* const* out1,
@@ -1402,6 +1404,21 @@ Tensor quantize(const Tensor& x, int64_t bits) {
   return y;
 }
 
+// quantise + pixel-unshuffle(r) in one pass: [y (x's shape), yu (N, cp, H/r, W/r)] with yu's
+// channels [C*r*r, cp) zero (a pad-8 conv input, no channel-pad pass)
+std::vector<Tensor> quantize_unshuffle(const Tensor& x, int64_t bits, int64_t r, int64_t cp) {
+  check_nhwc(x, "quantize_unshuffle");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(bits >= 1 && bits <= 16 && r >= 1 && H % r == 0 && W % r == 0 && cp >= C * r * r,
+              "quantize_unshuffle: bits / r / cp");
+  Tensor y = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor yu = empty_nhwc(N, cp, H / r, W / r, x);
+  check_rc(p2p_quantize_unshuffle(x.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)bits, (int)r, y.data_ptr(),
+                                  yu.data_ptr(), (int)cp, cur_stream(x)),
+           "quantize_unshuffle");
+  return {y, yu};
+}
+
 // bwd = 0: x (N,C,H,W) -> pooled; bwd = 1: x = gy (N,C,OH,OW) -> gx (N,C,H,W)
 Tensor avgpool3s2(const Tensor& x, int64_t bwd, int64_t H, int64_t W) {
   check_nhwc(x, "avgpool3s2");
@@ -1431,17 +1448,27 @@ Tensor maxpool2(const Tensor& x, const optional<Tensor>& gy) {
   return out;
 }
 
-Tensor l2norm(const Tensor& x, const optional<Tensor>& gy, double eps, const optional<Tensor>& res) {
+// shuffle > 1: x is the pre-PixelShuffle tensor (C*r*r, H, W); the forward's output / the
+// backward's gy are the shuffled (C, H*r, W*r) one, the backward's dx is x-shaped again
+Tensor l2norm(const Tensor& x, const optional<Tensor>& gy, double eps, const optional<Tensor>& res, int64_t shuffle) {
   check_nhwc(x, "l2norm");
-  if (gy) check_nhwc(*gy, "l2norm gy");
+  const int64_t r = shuffle;
+  TORCH_CHECK(r >= 1 && x.size(1) % (r * r) == 0, "l2norm: channels % shuffle^2");
+  const int64_t N = x.size(0), C = x.size(1) / (r * r), IH = x.size(2), IW = x.size(3);
+  if (gy) {
+    check_nhwc(*gy, "l2norm gy");
+    TORCH_CHECK(gy->size(0) == N && gy->size(1) == C && gy->size(2) == IH * r && gy->size(3) == IW * r,
+                "l2norm: gy must be the (shuffled) output's shape");
+  }
   if (res) {
     check_nhwc(*res, "l2norm res");
-    TORCH_CHECK(res->sizes() == x.sizes() && !gy, "l2norm: res must match x (forward only)");
+    TORCH_CHECK(!gy && res->size(0) == N && res->size(1) == C && res->size(2) == IH * r && res->size(3) == IW * r,
+                "l2norm: res must match the output (forward only)");
   }
-  Tensor out = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const int64_t C = x.size(1);
-  check_rc(p2p_l2norm(x.data_ptr(), gy ? gy->data_ptr() : nullptr, x.numel() / C, (int)C, (float)eps,
-                      res ? res->data_ptr() : nullptr, out.data_ptr(), cur_stream(x)),
+  Tensor out = gy ? at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast))
+                  : empty_nhwc(N, C, IH * r, IW * r, x);
+  check_rc(p2p_l2norm(x.data_ptr(), gy ? gy->data_ptr() : nullptr, N * IH * r * IW * r, (int)C, (float)eps,
+                      res ? res->data_ptr() : nullptr, out.data_ptr(), (int)r, (int)IH, (int)IW, cur_stream(x)),
            "l2norm");
   return out;
 }
@@ -1890,10 +1917,11 @@ TORCH_LIBRARY(p2p, m) {
   m.def("tv_fwd(Tensor x) -> Tensor");
   m.def("tv_bwd(Tensor x, Tensor gout) -> Tensor");
   m.def("quantize(Tensor x, int bits) -> Tensor");
+  m.def("quantize_unshuffle(Tensor x, int bits, int r, int cp) -> Tensor[]");
   m.def("image_metrics(Tensor a, Tensor b, bool shift, float data_range) -> Tensor");
   m.def("avgpool3s2(Tensor x, int bwd, int H, int W) -> Tensor");
   m.def("maxpool2(Tensor x, Tensor? gy) -> Tensor");
-  m.def("l2norm(Tensor x, Tensor? gy, float eps, Tensor? res=None) -> Tensor");
+  m.def("l2norm(Tensor x, Tensor? gy, float eps, Tensor? res=None, int shuffle=1) -> Tensor");
   m.def("pixel_shuffle(Tensor x, int r, int dir) -> Tensor");
   m.def("pad_fold(Tensor dxp, int H, int W, int pad, int up, int reflect, Tensor? xb, int act, "
         "Tensor? res=None) -> Tensor");
@@ -1962,6 +1990,7 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("tv_fwd", tv_fwd);
   m.impl("tv_bwd", tv_bwd);
   m.impl("quantize", quantize);
+  m.impl("quantize_unshuffle", quantize_unshuffle);
   m.impl("image_metrics", image_metrics);
   m.impl("avgpool3s2", avgpool3s2);
   m.impl("maxpool2", maxpool2);

@@ -110,6 +110,35 @@ __global__ void __launch_bounds__(256) quantize_kernel(const bf16* __restrict__ 
   }
 }
 
+// quantise + pixel-unshuffle(r) in one pass: besides y (x's layout) it writes the unshuffled,
+// channel-padded copy yu [N][H/r][W/r][Cp], channel c*r*r + i*r + j = y[h*r+i][w*r+j][c], the
+// pad channels zero -- the ExpandNetwork's head input (networks.py:457, 494-496), which then
+// needs neither an unshuffle nor a channel-pad pass.  One thread per yu pixel.
+__global__ void __launch_bounds__(256) quantize_unshuffle_kernel(const bf16* __restrict__ x, int N, int H, int W,
+                                                                 int C, int r, float m, bf16* __restrict__ y,
+                                                                 bf16* __restrict__ yu, int Cp) {
+  const int OH = H / r, OW = W / r;
+  const long np = (long)N * OH * OW;
+  for (long p = blockIdx.x * 256L + threadIdx.x; p < np; p += (long)gridDim.x * 256) {
+    const int ow = (int)(p % OW);
+    const long t = p / OW;
+    const int oh = (int)(t % OH);
+    const long n = t / OH;
+    bf16* o = yu + p * Cp;
+    for (int c = C * r * r; c < Cp; ++c) o[c] = (bf16)0.f;
+    for (int i = 0; i < r; ++i)
+      for (int j = 0; j < r; ++j) {
+        const long src = ((n * H + oh * r + i) * W + ow * r + j) * C;
+        for (int c = 0; c < C; ++c) {
+          const float v = fminf(fmaxf((float)x[src + c], 0.f), 1.f);
+          const bf16 q = (bf16)(rintf(v * m) / m);
+          y[src + c] = q;
+          o[c * r * r + i * r + j] = q;
+        }
+      }
+  }
+}
+
 // ------------------------------------------------------------------ AvgPool 3x3 s2 p1, count_include_pad=False
 __device__ __forceinline__ int pool_count(int o, int n) {  // valid taps of window 2o-1 .. 2o+1
   const int lo = max(2 * o - 1, 0), hi = min(2 * o + 1, n - 1);
@@ -290,38 +319,61 @@ __global__ void __launch_bounds__(256) maxpool_bwd_vec_kernel(const bf16* __rest
 
 // ------------------------------------------------------------------ L2 normalise over channels
 // y = x / max(||x||, eps);  dx = (dy - y * <dy, y>) / max(||x||, eps)  (norm > eps),
-// dx = dy / eps otherwise (F.normalize's clamp_min has zero gradient below eps)
+// dx = dy / eps otherwise (F.normalize's clamp_min has zero gradient below eps).
+// r > 1: x is the PRE-PixelShuffle tensor [N][IH][IW][C*r*r] and y / dy the shuffled one
+// [N][IH*r][IW*r][C] (CompressionNetwork: conv s2 -> PixelShuffle(2) -> l2-normalise + x,
+// networks.py:217-218, 233-236): output pixel (oh, ow) channel c reads x[oh/r][ow/r]
+// [c*r*r + (oh%r)*r + ow%r] -- the shuffle is this pass's addressing, no pass of its own, and
+// the backward writes dx in the pre-shuffle layout (the un-shuffle of the gradient, too).
+struct L2Map {
+  int r, IW, OW, OH, Cin;
+  __device__ __forceinline__ long base(long p) const {   // x index of channel 0 of output pixel p
+    if (r == 1) return p * Cin;
+    const int ow = (int)(p % OW);
+    const long t = p / OW;
+    const int oh = (int)(t % OH);
+    const long b = t / OH;
+    return ((b * (OH / r) + oh / r) * IW + ow / r) * Cin + (oh % r) * r + ow % r;
+  }
+};
+
 __global__ void __launch_bounds__(256) l2norm_fwd_kernel(const bf16* __restrict__ x, long P, int C, float eps,
-                                                         const bf16* __restrict__ res, bf16* __restrict__ y) {
+                                                         const bf16* __restrict__ res, bf16* __restrict__ y,
+                                                         L2Map mp) {
+  const int cs = mp.r * mp.r;   // channel stride of the output's channels inside x
   for (long p = blockIdx.x * 256L + threadIdx.x; p < P; p += (long)gridDim.x * 256) {
+    const long xb = mp.base(p);
     float s = 0.f;
     for (int c = 0; c < C; ++c) {
-      const float v = (float)x[p * C + c];
+      const float v = (float)x[xb + c * cs];
       s += v * v;
     }
     const float inv = 1.f / fmaxf(sqrtf(s), eps);
     // res: the CompressionNetwork's residual input added in the same pass (networks.py:236)
     for (int c = 0; c < C; ++c)
-      y[p * C + c] = (bf16)((float)x[p * C + c] * inv + (res ? (float)res[p * C + c] : 0.f));
+      y[p * C + c] = (bf16)((float)x[xb + c * cs] * inv + (res ? (float)res[p * C + c] : 0.f));
   }
 }
 
 __global__ void __launch_bounds__(256) l2norm_bwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ gy,
-                                                         long P, int C, float eps, bf16* __restrict__ gx) {
+                                                         long P, int C, float eps, bf16* __restrict__ gx,
+                                                         L2Map mp) {
+  const int cs = mp.r * mp.r;
   for (long p = blockIdx.x * 256L + threadIdx.x; p < P; p += (long)gridDim.x * 256) {
+    const long xb = mp.base(p);
     float s = 0.f;
     for (int c = 0; c < C; ++c) {
-      const float v = (float)x[p * C + c];
+      const float v = (float)x[xb + c * cs];
       s += v * v;
     }
     const float nrm = sqrtf(s);
     const float d = fmaxf(nrm, eps);
     float dot = 0.f;
     if (nrm > eps)
-      for (int c = 0; c < C; ++c) dot += (float)gy[p * C + c] * (float)x[p * C + c];
+      for (int c = 0; c < C; ++c) dot += (float)gy[p * C + c] * (float)x[xb + c * cs];
     const float k = nrm > eps ? dot / (d * d * d) : 0.f;
     for (int c = 0; c < C; ++c)
-      gx[p * C + c] = (bf16)((float)gy[p * C + c] / d - (float)x[p * C + c] * k);
+      gx[xb + c * cs] = (bf16)((float)gy[p * C + c] / d - (float)x[xb + c * cs] * k);
   }
 }
 
@@ -455,6 +507,16 @@ int p2p_quantize(const void* x, long n, int bits, void* y, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+int p2p_quantize_unshuffle(const void* x, int N, int H, int W, int C, int bits, int r, void* y, void* yu, int Cp,
+                           hipStream_t st) {
+  const float m = (float)((1 << bits) - 1);
+  const long np = (long)N * (H / r) * (W / r);
+  hipLaunchKernelGGL(p2p::quantize_unshuffle_kernel, dim3(p2p::mgrid(np)), dim3(256), 0, st,
+                     static_cast<const p2p::bf16*>(x), N, H, W, C, r, m, static_cast<p2p::bf16*>(y),
+                     static_cast<p2p::bf16*>(yu), Cp);
+  return (int)hipGetLastError();
+}
+
 int p2p_avgpool3s2(const void* x, int N, int H, int W, int C, int OH, int OW, void* y, int bwd, hipStream_t st) {
   if (!bwd) {
     const long n = (long)N * OH * OW * C;
@@ -493,16 +555,18 @@ int p2p_maxpool2(const void* x, const void* gy, int N, int H, int W, int C, void
   return (int)hipGetLastError();
 }
 
-int p2p_l2norm(const void* x, const void* gy, long P, int C, float eps, const void* res, void* out,
-               hipStream_t st) {
+// r > 1: x pre-PixelShuffle [N][IH][IW][C*r*r], P = N * IH*r * IW*r output pixels of C channels
+int p2p_l2norm(const void* x, const void* gy, long P, int C, float eps, const void* res, void* out, int r, int IH,
+               int IW, hipStream_t st) {
+  const p2p::L2Map mp{r, IW, IW * r, IH * r, C * r * r};
   if (!gy)
     hipLaunchKernelGGL(p2p::l2norm_fwd_kernel, dim3(p2p::mgrid(P)), dim3(256), 0, st,
                        static_cast<const p2p::bf16*>(x), P, C, eps, static_cast<const p2p::bf16*>(res),
-                       static_cast<p2p::bf16*>(out));
+                       static_cast<p2p::bf16*>(out), mp);
   else
     hipLaunchKernelGGL(p2p::l2norm_bwd_kernel, dim3(p2p::mgrid(P)), dim3(256), 0, st,
                        static_cast<const p2p::bf16*>(x), static_cast<const p2p::bf16*>(gy), P, C, eps,
-                       static_cast<p2p::bf16*>(out));
+                       static_cast<p2p::bf16*>(out), mp);
   return (int)hipGetLastError();
 }
 

@@ -122,7 +122,10 @@ class CompressGANStep:
         return torch.cat((a, b), 1)
 
     def _quant(self, x):
-        return _STEQuantize.apply(x, self.bits) if self.train_c else ops.quantize(x, self.bits)
+        if self.train_c:
+            return _STEQuantize.apply(x, self.bits)
+        # the same pass writes G's pixel-unshuffled head input (ExpandNetwork.forward)
+        return ops.quantize(x, self.bits, unshuffle=2)
 
     @staticmethod
     def _no_deferred(x):

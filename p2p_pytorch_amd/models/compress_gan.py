@@ -156,7 +156,8 @@ class ExpandNetwork(nn.Module):
             raise ValueError(f"ExpandNetwork needs H, W divisible by 4, got {tuple(x.shape[-2:])}"
                              " (quirk A16: the reference silently returns a wrong-size image)")
         # pixel-unshuffle(2) followed by nearest x2: the conv sees 12 channels at full res.
-        y = self.inversePixel(x)
+        # (as a conv input only: the quantiser may have written it unshuffled and padded)
+        y = ops.pixel_unshuffle(x, self.inversePixel.downscale_factor, conv_input=True)
         y = ops.conv2d(y, self.conv1.conv2d.weight, self.conv1.conv2d.bias, 1, 4, "reflect", 2,
                        stats=self.training and _FUSED_STATS)
         pw = self.relu.weight            # PReLU fused into the BN passes (fwd and bwd)
@@ -188,8 +189,10 @@ class CompressionNetwork(nn.Module):
     def forward(self, x):
         conv, bn, act = self.conv_block1
         h = bn(conv(self.conv_input(x)), prelu=act.weight)   # BN + PReLU: one pass
-        res = self.conv_block2(h)
-        return ops.l2_normalize_channels(res, residual=x)
+        # conv s2 -> PixelShuffle(2) -> l2-normalise + x: the shuffle is the normalising
+        # pass's addressing (both directions), not a pass of its own
+        conv2, shuf = self.conv_block2
+        return ops.l2_normalize_channels(conv2(h), residual=x, shuffle=shuf.upscale_factor)
 
 
 # ----------------------------------------------------------------- spectral norm

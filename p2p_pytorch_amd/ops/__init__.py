@@ -153,9 +153,11 @@ def tv(x):
     return ref.tv(x)
 
 
-def quantize(x, bits):
+def quantize(x, bits, unshuffle=0):
+    """``unshuffle`` r (HIP path): the same pass also writes the pixel-unshuffled, channel-
+    padded copy that ``pixel_unshuffle(y, r, conv_input=True)`` hands to the next conv."""
     if _native.use_native(x):
-        return _hip().quantize(x, bits)
+        return _hip().quantize(x, bits, unshuffle)
     return ref.quantize(x, bits)
 
 
@@ -165,10 +167,14 @@ def avg_pool3_s2(x):
     return ref.avg_pool3_s2(x)
 
 
-def l2_normalize_channels(x, eps=1e-12, residual=None):
-    """x / ||x||_2 over channels, plus ``residual`` (fused into the same pass when native)."""
+def l2_normalize_channels(x, eps=1e-12, residual=None, shuffle=1):
+    """x / ||x||_2 over channels, plus ``residual`` (fused into the same pass when native).
+    ``shuffle`` r > 1: of ``pixel_shuffle(x, r)`` -- on the native path the shuffle is the
+    normalising pass's own addressing (forward and backward), not a pass."""
     if _native.use_native(x):
-        return _hip().l2_normalize_channels(x, eps, residual)
+        return _hip().l2_normalize_channels(x, eps, residual, shuffle)
+    if shuffle > 1:
+        x = torch.nn.functional.pixel_shuffle(x, shuffle)
     y = ref.l2_normalize_channels(x, eps)
     return y if residual is None else y + residual
 
@@ -192,9 +198,12 @@ def pixel_shuffle(x, r):
     return torch.nn.functional.pixel_shuffle(x, r)
 
 
-def pixel_unshuffle(x, r):
+def pixel_unshuffle(x, r, conv_input=False):
+    """``conv_input`` (HIP path): the result only feeds a conv -- a copy the producer of ``x``
+    already wrote unshuffled and channel-padded (``quantize(..., unshuffle=r)``) is returned
+    as is (a packed pad-8 conv input), so no unshuffle / pad pass runs."""
     if _native.use_native(x):
-        return _hip().pixel_unshuffle(x, r)
+        return _hip().pixel_unshuffle(x, r, conv_input)
     return torch.nn.functional.pixel_unshuffle(x, r)
 
 

@@ -65,6 +65,7 @@ def begin_step():
     _norm_out.clear()
     _nbp_stash.clear()
     _DEFERRED.clear()   # a backward that raised part-way must not leak parked skip gradients
+    _unshuffled.clear()
     if _f8._pools:
         _f8.begin_step()
 
@@ -1780,9 +1781,26 @@ def tv(x):
     return TVFn.apply(x)
 
 
-def quantize(x, bits):
-    """Forward value only: round() has zero gradient (the reference's quantiser)."""
-    return P().quantize(_nhwc(x.detach()), int(bits))
+# y -> its unshuffled, channel-padded copy written by the same quantise pass (the expander's
+# head input); entries hold y, so a key never aliases a recycled allocation
+_unshuffled: dict = {}
+
+
+def quantize(x, bits, unshuffle=0):
+    """Forward value only: round() has zero gradient (the reference's quantiser).
+    ``unshuffle`` r: also write the pixel-unshuffled copy, channel-padded to 8 and tagged as a
+    packed conv input, for ``pixel_unshuffle(y, r, conv_input=True)``."""
+    x = _nhwc(x.detach())
+    r = int(unshuffle)
+    if r <= 1 or x.shape[2] % r or x.shape[3] % r:
+        return P().quantize(x, int(bits))
+    cu = x.shape[1] * r * r
+    y, yu = P().quantize_unshuffle(x, int(bits), r, _pad8(cu))
+    yu._p2p_packed = (cu, 0)
+    if len(_unshuffled) >= 16:
+        _unshuffled.pop(next(iter(_unshuffled)))
+    _unshuffled[(y.data_ptr(), tuple(y.shape), r)] = (y, yu)
+    return y
 
 
 class AvgPoolFn(torch.autograd.Function):
@@ -1819,24 +1837,26 @@ def max_pool2(x):
 
 
 class L2NormFn(torch.autograd.Function):
-    """y = x / ||x||_C (+ res): the residual add rides in the same pass."""
+    """y = x / ||x||_C (+ res): the residual add rides in the same pass.  ``shuffle`` r > 1:
+    x is the pre-PixelShuffle(r) tensor and y the normalised shuffled one -- the shuffle is
+    the kernel's addressing (and the un-shuffle of the gradient the backward's), no pass."""
 
     @staticmethod
-    def forward(ctx, x, eps, res):
+    def forward(ctx, x, eps, res, shuffle=1):
         x = _nhwc(x)
-        ctx.eps, ctx.has_res = eps, res is not None
+        ctx.eps, ctx.has_res, ctx.r = eps, res is not None, shuffle
         ctx.save_for_backward(x)
-        return P().l2norm(x, None, eps, _nhwc(res) if res is not None else None)
+        return P().l2norm(x, None, eps, _nhwc(res) if res is not None else None, shuffle)
 
     @staticmethod
     def backward(ctx, gy):
         (x,) = ctx.saved_tensors
         gy = _nhwc(gy)
-        return P().l2norm(x, gy, ctx.eps), None, (gy if ctx.has_res else None)
+        return P().l2norm(x, gy, ctx.eps, None, ctx.r), None, (gy if ctx.has_res else None), None
 
 
-def l2_normalize_channels(x, eps=1e-12, residual=None):
-    return L2NormFn.apply(x, float(eps), residual)
+def l2_normalize_channels(x, eps=1e-12, residual=None, shuffle=1):
+    return L2NormFn.apply(x, float(eps), residual, int(shuffle))
 
 
 class PixelShuffleFn(torch.autograd.Function):
@@ -1854,5 +1874,9 @@ def pixel_shuffle(x, r):
     return PixelShuffleFn.apply(x, int(r), 1)
 
 
-def pixel_unshuffle(x, r):
+def pixel_unshuffle(x, r, conv_input=False):
+    if conv_input and not x.requires_grad:
+        ent = _unshuffled.get((x.data_ptr(), tuple(x.shape), int(r)))
+        if ent is not None and ent[0] is x:
+            return ent[1]
     return PixelShuffleFn.apply(x, int(r), 0)

@@ -783,6 +783,30 @@ def test_quantize_3bit():
     assert rel_err(y, r) < 1e-2
 
 
+def test_quantize_unshuffle_feeds_the_head_conv():
+    """The quantiser's second output is pixel_unshuffle(quantize(x), 2), channel-padded with
+    zeros and tagged as a packed conv input; the expander's 9x9 head (nearest x2, reflect 4)
+    reading it equals the same conv over the plain unshuffle (no unshuffle / pad pass)."""
+    from p2p_pytorch_amd.ops import hip
+    hip.begin_step()
+    x = bf(torch.rand(2, 3, 64, 48, device=DEV))
+    y = ops.quantize(x, 3, unshuffle=2)
+    assert torch.equal(y.float(), ops.quantize(x, 3).float())
+    u = ops.pixel_unshuffle(y, 2, conv_input=True)
+    assert u.shape == (2, 16, 32, 24) and getattr(u, "_p2p_packed", None) == (12, 0)
+    ru = F.pixel_unshuffle(y.float(), 2)
+    assert torch.equal(u[:, :12].float(), ru) and not u[:, 12:].float().any()
+    w = _leaf(torch.randn(32, 12, 9, 9, device=DEV) * 0.05)
+    b = _leaf(torch.randn(32, device=DEV) * 0.1)
+    z = ops.conv2d(u, w, b, 1, 4, "reflect", 2)
+    plain = ops.pixel_unshuffle(y, 2)          # the unfused route (12 channels, pad pass)
+    zr = ops.conv2d(plain, w, b, 1, 4, "reflect", 2)
+    assert z.shape == zr.shape == (2, 32, 64, 48)
+    assert torch.equal(z.float(), zr.float())
+    hip.begin_step()
+    assert ops.pixel_unshuffle(y, 2, conv_input=True).shape == (2, 12, 32, 24)   # stash per step
+
+
 @pytest.mark.parametrize("C,H,W", [(3, 32, 32), (6, 33, 20), (8, 7, 9)])
 def test_avg_pool3_s2(C, H, W):
     x = rand_img(2, C, H, W, seed=14)
@@ -859,6 +883,25 @@ def test_l2_normalize_channels_residual():
     rx, rr = _leaf(x.float()), _leaf(r0.float())
     ry = ref.l2_normalize_channels(rx) + rr
     ry.backward(gy.float())
+    assert rel_err(y, ry) < 1e-2
+    assert rel_err(hx.grad, rx.grad) < 2e-2 and rel_err(hr.grad, rr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(2, 12, 16, 16), (3, 12, 9, 7), (2, 48, 8, 4)])
+def test_l2_normalize_pixel_shuffle_fused(shape):
+    """CompressionNetwork tail: PixelShuffle(2) -> l2-normalise + residual in ONE pass (the
+    shuffle is the kernel's addressing; its backward writes the un-shuffled gradient) against
+    the fp32 oracle F.pixel_shuffle -> normalize -> + res."""
+    n, c, h, w = shape
+    x, r0 = rand_img(*shape, seed=27), rand_img(n, c // 4, 2 * h, 2 * w, seed=28)
+    hx, hr = _leaf(x), _leaf(r0)
+    y = ops.l2_normalize_channels(hx, residual=hr, shuffle=2)
+    gy = rand_img(n, c // 4, 2 * h, 2 * w, seed=29)
+    y.backward(gy)
+    rx, rr = _leaf(x.float()), _leaf(r0.float())
+    ry = ref.l2_normalize_channels(F.pixel_shuffle(rx, 2)) + rr
+    ry.backward(gy.float())
+    assert y.shape == ry.shape
     assert rel_err(y, ry) < 1e-2
     assert rel_err(hx.grad, rx.grad) < 2e-2 and rel_err(hr.grad, rr.grad) < 1e-2
 
