@@ -542,13 +542,14 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                          act_bwd == 0 && !a.res1 && !a.q_out && !a.stats && !a.nb_ws && !a.alpha &&
                          (mode == 0 || (up == 1 && !reflect && pad <= KH - 1)) &&
                          std::getenv("P2P_NO_HALO") == nullptr;
-  // reflect fold: in the implicit-GEMM epilogue (interior pixels straight into y1, the frame
-  // folded by fold_band); the split-K / halo routes write the whole padded grid and pad_fold
-  // folds it afterwards (gate and skip gradient applied there)
+  // reflect fold: in the implicit-GEMM epilogue or the halo kernel's store loop (interior
+  // pixels straight into y1, the frame folded by fold_band); the split-K route writes the whole
+  // padded grid and pad_fold folds it afterwards (gate and skip gradient applied there)
   bool fold_late = false;
   if (fold) {
     const int64_t bw = fold_edge ? 1 : fold_p;   // band rows / columns per side (elementwise.hip fold_band)
-    fold_late = splits > 1 || halo_cond || fold_H < 2 * bw + 2 || fold_W < 2 * bw + 2;
+    // (the halo kernel folds in its store loop too: interior to y1, frame to fold_buf)
+    fold_late = splits > 1 || fold_H < 2 * bw + 2 || fold_W < 2 * bw + 2;
     if (fold_late) {
       a.y1 = fbuf.data_ptr();
       a.xb1 = nullptr;
@@ -620,6 +621,10 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     h.tiles_x = (int)((OW + 15) / 16);
     h.tiles_y = (int)((OH + 15) / 16);
     h.ntiles = (int)N * h.tiles_x * h.tiles_y;
+    h.fold_buf = static_cast<__bf16*>(a.fold_buf);
+    h.fold_H = a.fold_H;
+    h.fold_W = a.fold_W;
+    h.fold_p = a.fold_p;
     if (OH == H * up + 2 * h.pad - KH + 1 && OW == W * up + 2 * h.pad - KW + 1) {
       int dev = 0, cus = 256;
       (void)hipGetDevice(&dev);

@@ -183,9 +183,14 @@ struct HaloKArgs {
   const __bf16* w;     // [Cout][K*K][C] weight image
   const float* bias;   // [Cout] or null
   int Cout, act_out;
-  __bf16* y;           // NHWC [N][OH][OW][Cout]
+  __bf16* y;           // NHWC [N][OH][OW][Cout]  (with a fold: the real grid [N][fold_H][fold_W])
   const __bf16* zero;
   int tiles_x, tiles_y, ntiles;
+  // reflect-pad fold of an input gradient on the padded grid (as ConvFwdArgs.fold_buf): interior
+  // pixels go straight to y on the real grid, the p-wide frame raw to fold_buf [N][OH][OW]
+  // (elementwise.hip fold_band adds it onto the band afterwards); null = plain store
+  __bf16* fold_buf;
+  int fold_H, fold_W, fold_p;
 };
 
 // Halo-tile weight gradient of the same 9x9 stride-1 layers (csrc/halo_wgrad.hip): per-block

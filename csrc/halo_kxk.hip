@@ -20,6 +20,7 @@
 // pixels x one chunk index cover the 16 slots of a 256-B bank row, and lanes with odd kq read
 // their two 8-B halves in the opposite order (the matching B lanes do the same, so the k
 // order inside the MFMA stays consistent): conflict-free for every tap shift.
+#include "bounds.h"
 #include "conv.h"
 #include "common.h"
 
@@ -227,9 +228,20 @@ __global__ void __launch_bounds__(256) halo_kxk_kernel(HaloKArgs a) {
     for (int u = tid; u < 256 * upp; u += 256) {
       const int q = u / upp, k = u - q * upp;
       const int oy = oy0 + (q >> 4), ox = ox0 + (q & 15);
-      if (oy < a.OH && ox < a.OW)
-        *reinterpret_cast<u32x4*>(a.y + (((long)n * a.OH + oy) * a.OW + ox) * a.Cout + k * 8) =
-            *reinterpret_cast<const u32x4*>(Cs + q * LDCS + k * 8);
+      if (oy < a.OH && ox < a.OW) {
+        __bf16* dst = a.y + (((long)n * a.OH + oy) * a.OW + ox) * a.Cout + k * 8;
+        if (a.fold_buf) {   // interior -> the real grid; frame -> fold_buf (fold_band folds it)
+          const int iy = oy - a.fold_p, ix = ox - a.fold_p;
+          if ((unsigned)iy < (unsigned)a.fold_H && (unsigned)ix < (unsigned)a.fold_W) {
+            const long o = (((long)n * a.fold_H + iy) * a.fold_W + ix) * a.Cout + k * 8;
+            dst = P2P_OOB_OK(4, o, 8, (long)a.N * a.fold_H * a.fold_W * a.Cout) ? a.y + o : nullptr;
+          } else {
+            const long o = (((long)n * a.OH + oy) * a.OW + ox) * a.Cout + k * 8;
+            dst = P2P_OOB_OK(4, o, 8, (long)a.N * a.OH * a.OW * a.Cout) ? a.fold_buf + o : nullptr;
+          }
+        }
+        if (dst) *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(Cs + q * LDCS + k * 8);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();   // staging read before the stage is re-filled

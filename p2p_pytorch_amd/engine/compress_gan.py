@@ -250,7 +250,7 @@ class CompressGANStep:
         if self.train_c:
             self._zero(self.opt_c, self.reducer_c)
             with paused_g:      # the G grads of this backward are discarded (zeroed next step)
-                loss_c.backward()
+                loss_c.backward(self._seed_grad(loss_c))
             self._no_deferred(real_a)
             if self.reducer_c is not None:
                 self.reducer_c.finish()
@@ -262,7 +262,7 @@ class CompressGANStep:
                 # add per G parameter saved; the backward's own work is unchanged)
                 self.opt_g.zero_grad(set_to_none=True)
             with paused_g:      # reference: grads land on G (zeroed next step) -- no effect
-                loss_c.backward()
+                loss_c.backward(self._seed_grad(loss_c))
             self._no_deferred(real_a)
         return {"D": loss_d.detach(), "G_GAN": loss_g_gan.detach(),
                 "C": loss_c.detach(), "G_GAN_Feat": torch.as_tensor(loss_feat).detach(),

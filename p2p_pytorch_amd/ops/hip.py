@@ -1799,7 +1799,7 @@ def quantize(x, bits, unshuffle=0):
     yu._p2p_packed = (cu, 0)
     if len(_unshuffled) >= 16:
         _unshuffled.pop(next(iter(_unshuffled)))
-    _unshuffled[(y.data_ptr(), tuple(y.shape), r)] = (y, yu)
+    _unshuffled[(y.data_ptr(), tuple(y.shape), r)] = (y, yu, y._version)
     return y
 
 
@@ -1876,7 +1876,9 @@ def pixel_shuffle(x, r):
 
 def pixel_unshuffle(x, r, conv_input=False):
     if conv_input and not x.requires_grad:
+        # y itself or a view of it (``compressed.detach()``): the entry holds y, so a matching
+        # address is y's storage, and the shared version counter says it is unmodified
         ent = _unshuffled.get((x.data_ptr(), tuple(x.shape), int(r)))
-        if ent is not None and ent[0] is x:
+        if ent is not None and x._version == ent[2] and x.stride() == ent[0].stride():
             return ent[1]
     return PixelShuffleFn.apply(x, int(r), 0)

@@ -794,6 +794,7 @@ def test_quantize_unshuffle_feeds_the_head_conv():
     assert torch.equal(y.float(), ops.quantize(x, 3).float())
     u = ops.pixel_unshuffle(y, 2, conv_input=True)
     assert u.shape == (2, 16, 32, 24) and getattr(u, "_p2p_packed", None) == (12, 0)
+    assert ops.pixel_unshuffle(y.detach(), 2, conv_input=True) is u   # G(compressed.detach())
     ru = F.pixel_unshuffle(y.float(), 2)
     assert torch.equal(u[:, :12].float(), ru) and not u[:, 12:].float().any()
     w = _leaf(torch.randn(32, 12, 9, 9, device=DEV) * 0.05)
