@@ -55,8 +55,8 @@ int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const floa
                  float* dsum, void* q, int* qsite, int qfmt, int frozen, hipStream_t st);
 int p2p_norm_bwd_partials(const void* x, const void* dy, int N, int HW, int C, int nchunks,
                           const float* partials, const float* mean, const float* rstd,
-                          const float* gamma, const float* beta, int act, float* dgamma, float* dbeta,
-                          float* coef, void* dx, float* dsum, void* q, int* qsite, int qfmt,
+                          const float* gamma, const float* beta, int act, const float* prelu_w, float* dgamma,
+                          float* dbeta, float* coef, void* dx, float* dsum, void* q, int* qsite, int qfmt,
                           hipStream_t st);
 int p2p_act(const void* a, const void* b, long n, int act, int mode, void* out, hipStream_t st);
 int p2p_dropout(const void* x, long n, float p, const int64_t* seed, unsigned salt, void* y,
@@ -93,8 +93,11 @@ int p2p_col_weight(const void* w, int T, int C, int Cv, int Cvp, int Ncol, void*
 int p2p_vec_pad(const float* x, int n, float fill, int nout, float* out, hipStream_t st);
 int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, int reflect,
                  const void* xb, int act, const void* res, void* dx, hipStream_t st);
+int p2p_fold_band_nb_blocks();
 int p2p_fold_band(const void* fb, int N, int H, int W, int C, int pad, int edge, const void* xb, int act, void* dx,
-                  hipStream_t st);
+                  float* nb_ws, long nb_plane, int nb_chunk0, const void* nb_x, const float* nb_mean,
+                  const float* nb_rstd, const float* nb_gamma, const float* nb_beta, const float* nb_prelu,
+                  int nb_act, hipStream_t st);
 int p2p_pad_channels(const void* a, int Ca, const void* b, int Cb, long P, int Co, void* out,
                      hipStream_t st);
 int p2p_slice_channels(const void* in, int Ci, int c0, long P, int C, void* out, hipStream_t st);
@@ -110,6 +113,7 @@ int p2p_adam_max_tensors();
 int p2p_union_weight(const float* w, int CinT, int CoutT, int co_off, int nv, int Nrows, int Cpad,
                      const float* bias, void* out, float* bias_out, hipStream_t st);
 int p2p_sum_partials(const float* ws, int nb, float scale, float* out, hipStream_t st);
+int p2p_sum_long(const float* ws, long n, float scale, float* part, float* out, hipStream_t st);
 int p2p_rowsum_blocks(long R);
 long p2p_s2t_dbg_bytes();
 int p2p_s2t_dbg_read(void* dst, long bytes);
@@ -209,7 +213,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                              const optional<Tensor>& nb_rstd, const optional<Tensor>& nb_gamma,
                              const optional<Tensor>& nb_beta, int64_t nb_act, int64_t nb_half, bool nb_batch,
                              bool nb_colsum, bool nb_gate, int64_t fold_H, int64_t fold_W, int64_t fold_p,
-                             int64_t fold_edge) {
+                             int64_t fold_edge, const optional<Tensor>& nb_prelu) {
   check_act(x1, "conv_fwd x1", true);
   // fp8 operands: x e4m3 (activations) or e5m2 (gradients), weight image e4m3, each with
   // an fp8 scale site (csrc/fp8.hip); outputs stay bf16
@@ -245,7 +249,8 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   const bool fold = fold_p > 0;
   if (fold)
     TORCH_CHECK(((mode == 1 && pad == 0 && !fold_edge) || (mode == 0 && fold_edge && fold_p <= 2)) && up == 1 &&
-                    !reflect && !x2 && Csplit == Cout && !want_stats && !y_qsite && !nb_x && !nb_colsum &&
+                    !reflect && !x2 && Csplit == Cout && !want_stats && !y_qsite && (!nb_x || nb_batch) &&
+                    !nb_colsum &&
                     OH == fold_H + 2 * fold_p && OW == fold_W + 2 * fold_p,
                 "conv_fwd: fold geometry");
   const int64_t RH = fold ? fold_H : OH, RW = fold ? fold_W : OW;
@@ -485,8 +490,18 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   // the packed-image halo kernel (below) beats the generic tile with fused partials: keep it
   const bool pk8_halo = mode == 0 && !fp8 && C1 == 8 && C2 == 0 && KH == 4 && KW == 4 && stride == 2 && pad == 1 &&
                         (Cout == 64 || Cout == 128) && std::getenv("P2P_NO_HALO") == nullptr;
-  if ((nb_x || nb_colsum) && nb_half && !nb_gamma && (glds_ok || s2t_ok) && splits == 1 && fp8 != 1 && !want_stats &&
-      !pk8_halo) {
+  // affine / PReLU norms and folds: batch norm only, on the implicit-GEMM tiles (the s2t kernel
+  // has its own partial code, non-affine only; the halo kernels none -- keep their routes)
+  const bool nb_ext = nb_gamma || nb_prelu || fold;
+  const bool nb_halo = KH == 9 || (KH == 3 && C1 == 64 && Cout <= 32);
+  int64_t nb_band = 0;
+  if (fold) {
+    const int64_t bw = fold_edge ? 1 : fold_p;
+    nb_band = (fold_H >= 2 * bw + 2 && fold_W >= 2 * bw + 2 && 256 % (Cout / 8) == 0) ? p2p_fold_band_nb_blocks() : -1;
+  }
+  if ((nb_x || nb_colsum) && nb_half && (glds_ok || s2t_ok) && splits == 1 && fp8 != 1 && !want_stats &&
+      !pk8_halo && (!nb_ext || (nb_batch && !nb_colsum && !s2t_ok && !nb_halo && nb_band >= 0 && nb_half == 1 &&
+                                Csplit == Cout))) {
     const int64_t c0 = nb_half == 1 ? 0 : Csplit;
     const int64_t nC = nb_half == 1 ? Csplit : Cout - Csplit;
     bool ok = nC > 0 && nC % 8 == 0 && (nb_half == 1 || Csplit < Cout);
@@ -495,10 +510,13 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       ok = ok && OH % stride == 0 && OW % stride == 0;
       hwq = (OH / stride) * (OW / stride);
     }
-    ok = ok && hwq % bm == 0;
+    // batch-norm extension: flat tiles over all images (every class N * hwq pixels)
+    const bool flat = nb_ext;
+    const int64_t tiles_cls = (N * hwq + bm - 1) / bm;
+    ok = ok && (flat || hwq % bm == 0);
     if (ok && !nb_colsum) {
       check_act(*nb_x, "conv_fwd nb_x");
-      TORCH_CHECK(nb_x->size(0) == N && nb_x->size(1) == nC && nb_x->size(2) == OH && nb_x->size(3) == OW,
+      TORCH_CHECK(nb_x->size(0) == N && nb_x->size(1) == nC && nb_x->size(2) == RH && nb_x->size(3) == RW,
                   "conv_fwd: nb_x must match the gradient half");
       const int64_t groups = nb_batch ? 1 : N;
       TORCH_CHECK(nb_mean && nb_rstd && nb_mean->numel() == groups * nC && nb_rstd->numel() == groups * nC &&
@@ -507,20 +525,30 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     }
     if (ok) {
       if (nb_gamma) TORCH_CHECK(nb_beta && nb_gamma->numel() == nC && nb_beta->numel() == nC, "conv_fwd: nb affine");
-      const int64_t nch = classes * (hwq / bm);
-      nbp = at::empty({2, N, nch, nC}, x1.options().dtype(at::kFloat));
+      if (nb_prelu)
+        TORCH_CHECK(nb_prelu->numel() == 1 && nb_prelu->scalar_type() == at::kFloat && nb_prelu->is_cuda(),
+                    "conv_fwd: nb_prelu must be a 1-element fp32 GPU tensor");
+      const int64_t planes = nb_prelu ? 3 : 2;
+      const int64_t nch = flat ? classes * tiles_cls + std::max<int64_t>(nb_band, 0) : classes * (hwq / bm);
+      nbp = flat ? at::empty({planes, 1, nch, nC}, x1.options().dtype(at::kFloat))
+                 : at::empty({2, N, nch, nC}, x1.options().dtype(at::kFloat));
       a.nb_colsum = nb_colsum ? 1 : 0;
       a.nb_x = nb_colsum ? nullptr : nb_x->data_ptr();
       a.nb_mean = nb_colsum ? nullptr : nb_mean->data_ptr<float>();
       a.nb_rstd = nb_colsum ? nullptr : nb_rstd->data_ptr<float>();
       a.nb_gamma = nb_gamma ? nb_gamma->data_ptr<float>() : nullptr;
       a.nb_beta = nb_gamma ? nb_beta->data_ptr<float>() : nullptr;
+      a.nb_prelu = nb_prelu ? nb_prelu->data_ptr<float>() : nullptr;
       a.nb_act = (int)nb_act;
-      a.nb_gate = (nb_gate && !nb_colsum && nb_act == 0 && P2P_KNOB_ONCE("P2P_NB_GATE_LOAD") == nullptr) ? 1 : 0;
+      a.nb_gate = (nb_gate && !nb_colsum && nb_act == 0 && !nb_gamma && !nb_prelu &&
+                   P2P_KNOB_ONCE("P2P_NB_GATE_LOAD") == nullptr) ? 1 : 0;
       a.nb_batch = nb_batch ? 1 : 0;
       a.nb_c0 = (int)c0;
       a.nb_C = (int)nC;
       a.nb_nchunks = (int)nch;
+      a.nb_flat = flat ? 1 : 0;
+      a.nb_tiles_cls = (int)tiles_cls;
+      a.nb_planes = (int)planes;
       a.nb_ws = nbp.data_ptr<float>();
     }
   }
@@ -670,8 +698,10 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                "conv_fwd(pad_fold)");
     else
       check_rc(p2p_fold_band(fbuf.data_ptr(), (int)N, (int)fold_H, (int)fold_W, (int)Cout, (int)fold_p,
-                             (int)fold_edge, xg,
-                             (int)act_bwd, y1.data_ptr(), st),
+                             (int)fold_edge, xg, (int)act_bwd, y1.data_ptr(), a.nb_ws,
+                             a.nb_ws ? (long)a.nb_nchunks * a.nb_C : 0L,
+                             a.nb_ws ? a.nb_nchunks - p2p_fold_band_nb_blocks() : 0, a.nb_x, a.nb_mean, a.nb_rstd,
+                             a.nb_gamma, a.nb_beta, a.nb_prelu, a.nb_act, st),
                "conv_fwd(fold_band)");
   }
   std::vector<Tensor> out{y1};
@@ -1268,16 +1298,28 @@ Tensor norm_bwd(const Tensor& x, const Tensor& dy, const Tensor& mean, const Ten
   Tensor dx;
   if (need_dx) dx = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   if (partials) {
-    // [2][N][nch][C] sum(d) / sum(d * xhat) from the consumer conv's dgrad epilogue
-    TORCH_CHECK(!prelu_w && partials->dim() == 4 && partials->size(0) == 2 && partials->size(1) == N &&
-                    partials->size(3) == C && partials->scalar_type() == at::kFloat,
+    // [2][N][nch][C] sum(d) / sum(d * xhat) from the consumer conv's dgrad epilogue; batch
+    // norm may come flat ([P][1][nch][C], tiles over all images) and with a shared-slope PReLU
+    // as a third plane of sum(dz * z * [z <= 0]) -- the slope gradient is its total
+    const int64_t planes = partials->dim() == 4 ? partials->size(0) : 0;
+    TORCH_CHECK(partials->dim() == 4 && (planes == 2 || (planes == 3 && prelu_w && batch)) &&
+                    (partials->size(1) == N || (batch && partials->size(1) == 1)) && partials->size(3) == C &&
+                    partials->scalar_type() == at::kFloat && partials->is_contiguous() && (!prelu_w || planes == 3),
                 "norm_bwd: partials shape");
-    const int nch = (int)(batch ? N * partials->size(2) : partials->size(2));
+    const int nch = (int)(batch ? partials->size(1) * partials->size(2) : partials->size(2));
     Tensor coef = at::empty({3 * gN * C}, x.options().dtype(at::kFloat));
+    if (dprelu) {
+      const long plane = (long)nch * C;   // batch: gN = 1
+      Tensor part = at::empty({256}, x.options().dtype(at::kFloat));
+      check_rc(p2p_sum_long(partials->data_ptr<float>() + 2 * plane, plane, 1.f, part.data_ptr<float>(),
+                            dprelu->data_ptr<float>(), cur_stream(x)),
+               "norm_bwd(partials: dprelu)");
+    }
     check_rc(p2p_norm_bwd_partials(x.data_ptr(), dy.data_ptr(), gN, gHW, (int)C, nch, partials->data_ptr<float>(),
                                    mean.data_ptr<float>(), rstd.data_ptr<float>(),
                                    gamma ? gamma->data_ptr<float>() : nullptr,
                                    beta ? beta->data_ptr<float>() : nullptr, (int)act,
+                                   prelu_w ? prelu_w->data_ptr<float>() : nullptr,
                                    dgamma ? dgamma->data_ptr<float>() : nullptr,
                                    dbeta ? dbeta->data_ptr<float>() : nullptr, coef.data_ptr<float>(),
                                    need_dx ? dx.data_ptr() : nullptr,
@@ -1894,8 +1936,8 @@ TORCH_LIBRARY(p2p, m) {
         "Tensor? qs_x2=None, Tensor? qs_w=None, Tensor(a!)? y_qsite=None, int y_qfmt=0, Tensor? res=None, "
         "Tensor? alpha=None, Tensor? nb_x=None, Tensor? nb_mean=None, Tensor? nb_rstd=None, "
         "Tensor? nb_gamma=None, Tensor? nb_beta=None, int nb_act=0, int nb_half=0, bool nb_batch=False, "
-        "bool nb_colsum=False, bool nb_gate=False, int fold_H=0, int fold_W=0, int fold_p=0, int fold_edge=0) "
-        "-> Tensor[]");
+        "bool nb_colsum=False, bool nb_gate=False, int fold_H=0, int fold_W=0, int fold_p=0, int fold_edge=0, "
+        "Tensor? nb_prelu=None) -> Tensor[]");
   m.def("fp8_quant(Tensor x, Tensor(a!) site, int fmt, int use_cur=0) -> Tensor");
   m.def("sn_power_iter(Tensor w, Tensor(a!) u, Tensor(b!) v) -> Tensor");
   m.def("sn_scale(Tensor w, Tensor(a!) u, Tensor(b!) v) -> Tensor");

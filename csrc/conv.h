@@ -79,7 +79,7 @@ struct ConvFwdArgs {
   const void* nb_x;
   const float* nb_mean;   // [N][nb_C] (instance) or [nb_C] (batch, nb_batch = 1)
   const float* nb_rstd;
-  const float* nb_gamma;  // unused: the host fuses non-affine norms only
+  const float* nb_gamma;  // affine norms (batch norm only: the host checks): z = xhat * g + b
   const float* nb_beta;
   int nb_act, nb_batch, nb_c0, nb_C, nb_nchunks;
   float* nb_ws;
@@ -99,6 +99,12 @@ struct ConvFwdArgs {
   // (MODE 0, 4x4 stride 2 over dY onto the edge-padded grid).  Unsplit single-output GEMMs.
   void* fold_buf;
   int fold_H, fold_W, fold_p;
+  // batch-norm partials over a whole batch (nb_batch): nb_flat = 1 -> chunk = class *
+  // nb_tiles_cls + m0 / BM over ALL images (tiles may straddle images: a fold's padded grid),
+  // planes [nb_planes][nb_nchunks][nb_C]; nb_prelu (device slope, shared-slope PReLU): the
+  // gate slope, and a third plane of sum(dz * z * [z <= 0]) (the slope gradient's terms)
+  const float* nb_prelu;
+  int nb_flat, nb_tiles_cls, nb_planes;
 };
 
 // Weight gradient: C[R][Kq] = sum_m P[m][R] * im2col(Q)[m][Kq], written to per-split

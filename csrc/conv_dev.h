@@ -101,22 +101,27 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
   const int nb_co = co_t - a.nb_c0;
   const bool nb_on = a.nb_ws != nullptr && nb_co >= 0 && nb_co < a.nb_C;
   const bool nb_x_on = nb_on && !a.nb_colsum;   // colsum mode: d = dz, xhat = 0 (rs = c1 = 0)
-  const float nb_slope = (a.nb_act && !a.nb_colsum) ? neg_slope(a.nb_act) : 1.f;
+  const float nb_slope = a.nb_colsum ? 1.f : (a.nb_prelu ? *a.nb_prelu : (a.nb_act ? neg_slope(a.nb_act) : 1.f));
+  const bool nb_p3 = a.nb_prelu != nullptr;   // third plane: the PReLU slope-gradient terms
   // act' gate (a null half is gated by its producer's backward): from the xhat of the nb
   // partials when the gated input is the norm's output itself (nb_gate), else loaded
   const bool gate_nb = a.act_bwd && xb_t && nb_x_on && a.nb_gate;
   const bool gate_t = a.act_bwd && xb_t && !gate_nb;
   const float gate_slope = gate_nb ? neg_slope(a.act_bwd) : 0.f;
-  // xhat = x * rs + c1 (c1 = -mean * rstd)
-  float rs[8], c1[8], s1[8], s2[8];
+  // xhat = x * rs + c1 (c1 = -mean * rstd); the gate's z = xhat * g + b = x * zs + zc
+  float rs[8], c1[8], zs[8], zc[8], s1[8], s2[8], s3[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    rs[j] = c1[j] = s1[j] = s2[j] = 0.f;
+    rs[j] = c1[j] = s1[j] = s2[j] = s3[j] = 0.f;
     if (nb_on && !a.nb_colsum) {
       const long si = a.nb_batch ? nb_co + j : (long)(m0 / HWq) * a.nb_C + nb_co + j;
       rs[j] = a.nb_rstd[si];
       c1[j] = -a.nb_mean[si] * rs[j];
     }
+    const float ga = a.nb_gamma && nb_on ? a.nb_gamma[nb_co + j] : 1.f;
+    const float be = a.nb_gamma && nb_on ? a.nb_beta[nb_co + j] : 0.f;
+    zs[j] = rs[j] * ga;
+    zc[j] = c1[j] * ga + be;
   }
   const u32x4 z4 = {0u, 0u, 0u, 0u};
   auto ld16 = [](const bf16* p) __attribute__((always_inline)) { return *reinterpret_cast<const u32x4*>(p); };
@@ -171,10 +176,13 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
       const bf16x8 xn = __builtin_bit_cast(bf16x8, nv);
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const float xh = (float)xn[q] * rs[q] + c1[q];
-        const float d = (float)dz[q] * (xh > 0.f ? 1.f : nb_slope);
+        const float xv = (float)xn[q];
+        const float xh = xv * rs[q] + c1[q];
+        const float z = xv * zs[q] + zc[q];
+        const float d = (float)dz[q] * (z > 0.f ? 1.f : nb_slope);
         s1[q] += d;
         s2[q] += d * xh;
+        if (nb_p3) s3[q] += z <= 0.f ? (float)dz[q] * z : 0.f;
       }
     }
   };
@@ -225,6 +233,7 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
       for (int q = 0; q < 8; ++q) {
         s1[q] += __shfl_xor(s1[q], off);
         s2[q] += __shfl_xor(s2[q], off);
+        if (nb_p3) s3[q] += __shfl_xor(s3[q], off);
       }
     __syncthreads();   // every thread is done with the staged tile
     float* red = reinterpret_cast<float*>(smem);
@@ -232,8 +241,9 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
     if (lane < CPR) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        red[(wid * CPR + lane) * 16 + q] = s1[q];
-        red[(wid * CPR + lane) * 16 + 8 + q] = s2[q];
+        red[(wid * CPR + lane) * 24 + q] = s1[q];
+        red[(wid * CPR + lane) * 24 + 8 + q] = s2[q];
+        red[(wid * CPR + lane) * 24 + 16 + q] = s3[q];
       }
     }
     __syncthreads();
@@ -241,17 +251,28 @@ __device__ __forceinline__ void conv_epilogue_ext(const ConvFwdArgs& a, const Cl
       const int cc = tid >> 3, q = tid & 7;
       const int co = n0 + tid - a.nb_c0;
       if (co >= 0 && co < a.nb_C) {
-        float S1 = 0.f, S2 = 0.f;
+        float S1 = 0.f, S2 = 0.f, S3 = 0.f;
         for (int k = 0; k < NT / 64; ++k) {
-          S1 += red[(k * CPR + cc) * 16 + q];
-          S2 += red[(k * CPR + cc) * 16 + 8 + q];
+          S1 += red[(k * CPR + cc) * 24 + q];
+          S2 += red[(k * CPR + cc) * 24 + 8 + q];
+          S3 += red[(k * CPR + cc) * 24 + 16 + q];
         }
-        const int img = m0 / HWq;
         const int cls = g.ry * s + g.rx;
-        const int chunk = cls * (HWq / BM) + (m0 - img * HWq) / BM;
-        const long o = ((long)img * a.nb_nchunks + chunk) * a.nb_C + co;
-        a.nb_ws[o] = S1;
-        a.nb_ws[(long)a.N * a.nb_nchunks * a.nb_C + o] = S2;
+        long o, plane;
+        if (a.nb_flat) {   // batch norm, tiles over all images (a fold's padded grid)
+          o = ((long)cls * a.nb_tiles_cls + m0 / BM) * a.nb_C + co;
+          plane = (long)a.nb_nchunks * a.nb_C;
+        } else {
+          const int img = m0 / HWq;
+          const int chunk = cls * (HWq / BM) + (m0 - img * HWq) / BM;
+          o = ((long)img * a.nb_nchunks + chunk) * a.nb_C + co;
+          plane = (long)a.N * a.nb_nchunks * a.nb_C;
+        }
+        if (P2P_OOB_OK(3, o, 1, plane)) {
+          a.nb_ws[o] = S1;
+          a.nb_ws[plane + o] = S2;
+          if (nb_p3) a.nb_ws[2 * plane + o] = S3;
+        }
       }
     }
   }

@@ -332,6 +332,19 @@ __global__ void __launch_bounds__(256) loss_final_kernel(const float* __restrict
   if (threadIdx.x == 0) out[0] = (red[0] + red[1] + red[2] + red[3]) * scale;
 }
 
+// first stage of a long sum: block b adds its contiguous segment (fixed order) -> part[b]
+__global__ void __launch_bounds__(256) seg_sum_kernel(const float* __restrict__ ws, long n, long seg,
+                                                      float* __restrict__ part) {
+  const long lo = blockIdx.x * seg, hi = min(n, lo + seg);
+  float s = 0.f;
+  for (long i = lo + threadIdx.x; i < hi; i += 256) s += ws[i];
+  __shared__ float red[4];
+  s = warp_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 // ga = gout * scale * dloss/da (bf16 or fp32 like a); gb = -ga (l1 / mse pairs) if requested
 __global__ void __launch_bounds__(256) loss_grad_kernel(const void* __restrict__ a,
                                                         const void* __restrict__ b, int is_f32, long n,
@@ -535,9 +548,39 @@ __global__ void __launch_bounds__(256) pad_fold_s1_kernel(const bf16* __restrict
 // pixels only: 2p rows x W + (H - 2p) rows x 2p columns per image (host: H, W >= 2p + 2).
 // edge = 1 (replicate pad, the nearest-x2 + reflect-1 dgrad): the band is the outermost row /
 // column on each side, which collects all p frame rows / columns beyond it (host: p <= 4).
+// nb.ws (batch norm fused into the dgrad epilogue, conv_dev.h nb_flat): the epilogue's
+// partials counted each band pixel's PRE-fold value; this pass adds, per channel, the change of
+// the partial sums d = dz * act'(z), d * xhat (and PReLU's dz * z * [z <= 0]) from the old to
+// the new bf16 value of every pixel it rewrites -- block b's sums go to chunk nb.chunk0 + b in
+// a fixed order (host: a fixed grid of NB_BAND_BLOCKS blocks), so the norm sees the folded dz.
+struct NbBand {
+  float* ws;
+  long plane;
+  int chunk0;
+  const bf16* x;
+  const float *mean, *rstd, *gamma, *beta, *prelu;
+  int act;
+};
+
 __global__ void __launch_bounds__(256) fold_band_kernel(const bf16* __restrict__ fb, int N, int H, int W, int C,
                                                         int pad, int edge, const bf16* __restrict__ xb, int act,
-                                                        bf16* __restrict__ dx) {
+                                                        bf16* __restrict__ dx, NbBand nb) {
+  float s1[8], s2[8], s3[8], zs[8], zc[8], rs[8], c1[8];
+  const int cgt = threadIdx.x % (C >> 3);   // fixed per thread (host: 256 % (C / 8) == 0)
+  const float slope = nb.ws ? (nb.prelu ? *nb.prelu : (nb.act ? neg_slope(nb.act) : 1.f)) : 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s1[j] = s2[j] = s3[j] = 0.f;
+    rs[j] = c1[j] = zs[j] = zc[j] = 0.f;
+    if (nb.ws) {
+      const int c = cgt * 8 + j;
+      rs[j] = nb.rstd[c];
+      c1[j] = -nb.mean[c] * rs[j];
+      const float ga = nb.gamma ? nb.gamma[c] : 1.f, be = nb.gamma ? nb.beta[c] : 0.f;
+      zs[j] = rs[j] * ga;
+      zc[j] = c1[j] * ga + be;
+    }
+  }
   const int CP = C >> 3;
   const int Hp = H + 2 * pad, Wp = W + 2 * pad;
   const int bw = edge ? 1 : pad;   // band rows / columns per side
@@ -604,7 +647,49 @@ __global__ void __launch_bounds__(256) fold_band_kernel(const bf16* __restrict__
     unpack8e(*reinterpret_cast<const u32x4*>(dx + o), d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] += d[j];
-    *reinterpret_cast<u32x4*>(dx + o) = pack8e(acc);
+    const u32x4 nv = pack8e(acc);
+    *reinterpret_cast<u32x4*>(dx + o) = nv;
+    if (nb.ws) {   // partial-sum change from the old to the new stored value
+      float nf[8], xf[8];
+      unpack8e(nv, nf);
+      unpack8e(*reinterpret_cast<const u32x4*>(nb.x + o), xf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float dd = nf[j] - d[j];
+        const float xh = xf[j] * rs[j] + c1[j];
+        const float z = xf[j] * zs[j] + zc[j];
+        const float g = dd * (z > 0.f ? 1.f : slope);
+        s1[j] += g;
+        s2[j] += g * xh;
+        s3[j] += z <= 0.f ? dd * z : 0.f;
+      }
+    }
+  }
+  if (nb.ws) {
+    // fixed-order block reduction per channel: the 256 / CP threads sharing a channel group
+    __shared__ float red[3][256][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[0][threadIdx.x][j] = s1[j];
+      red[1][threadIdx.x][j] = s2[j];
+      red[2][threadIdx.x][j] = s3[j];
+    }
+    __syncthreads();
+    const int CP = C >> 3;
+    for (int c = threadIdx.x; c < C; c += 256) {
+      float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      for (int t = c >> 3; t < 256; t += CP) {
+        a1 += red[0][t][c & 7];
+        a2 += red[1][t][c & 7];
+        a3 += red[2][t][c & 7];
+      }
+      const long oo = (long)(nb.chunk0 + blockIdx.x) * C + c;
+      if (P2P_OOB_OK(14, oo, 1, nb.plane)) {
+        nb.ws[oo] = a1;
+        nb.ws[nb.plane + oo] = a2;
+        if (nb.prelu) nb.ws[2 * nb.plane + oo] = a3;
+      }
+    }
   }
 }
 }  // namespace p2p
@@ -724,14 +809,25 @@ int p2p_pad_fold(const void* dxp, int N, int H, int W, int C, int pad, int up, i
   return (int)hipGetLastError();
 }
 
+// blocks of a fold_band pass that also corrects fused batch-norm partials (one chunk each)
+int p2p_fold_band_nb_blocks() { return 256; }
+
+// nb_ws: batch-norm partial planes [2 or 3][nchunks][C] (plane = nchunks * C floats) whose
+// chunks [nb_chunk0, nb_chunk0 + p2p_fold_band_nb_blocks()) this pass writes (null = off)
 int p2p_fold_band(const void* fb, int N, int H, int W, int C, int pad, int edge, const void* xb, int act, void* dx,
-                  hipStream_t st) {
+                  float* nb_ws, long nb_plane, int nb_chunk0, const void* nb_x, const float* nb_mean,
+                  const float* nb_rstd, const float* nb_gamma, const float* nb_beta, const float* nb_prelu,
+                  int nb_act, hipStream_t st) {
   using namespace p2p;
   const int bw = edge ? 1 : pad;
   if (C % 8 || pad < 1 || (edge && pad > 4) || H < 2 * bw + 2 || W < 2 * bw + 2) return -2;
+  if (nb_ws && (256 % (C / 8) || !nb_x || !nb_mean || !nb_rstd)) return -2;
   const long total = (long)N * (2 * bw * W + (H - 2 * bw) * 2 * bw) * (C / 8);
-  hipLaunchKernelGGL(fold_band_kernel, dim3(egrid(total)), dim3(256), 0, st, static_cast<const bf16*>(fb), N, H, W,
-                     C, pad, edge, static_cast<const bf16*>(xb), act, static_cast<bf16*>(dx));
+  const NbBand nb{nb_ws, nb_plane, nb_chunk0, static_cast<const bf16*>(nb_x), nb_mean, nb_rstd, nb_gamma, nb_beta,
+                  nb_prelu, nb_act};
+  hipLaunchKernelGGL(fold_band_kernel, dim3(nb_ws ? p2p_fold_band_nb_blocks() : egrid(total)), dim3(256), 0, st,
+                     static_cast<const bf16*>(fb), N, H, W, C, pad, edge, static_cast<const bf16*>(xb), act,
+                     static_cast<bf16*>(dx), nb);
   return (int)hipGetLastError();
 }
 
@@ -795,6 +891,16 @@ int p2p_guard_flag(const float* const* v, int n, float* flag, float* counter, hi
   for (int i = 0; i < n; ++i) a.v[i] = v[i];
   a.n = n;
   hipLaunchKernelGGL(guard_flag_kernel, dim3(1), dim3(64), 0, st, a, flag, counter);
+  return (int)hipGetLastError();
+}
+
+// out[0] = scale * sum(ws[0..n)) for long n: 256 segment sums, then one block (both fixed
+// order); part: 256 floats of workspace
+int p2p_sum_long(const float* ws, long n, float scale, float* part, float* out, hipStream_t st) {
+  using namespace p2p;
+  const long seg = (n + 255) / 256;
+  hipLaunchKernelGGL(seg_sum_kernel, dim3(256), dim3(256), 0, st, ws, n, seg > 0 ? seg : 1, part);
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, part, 256, scale, out);
   return (int)hipGetLastError();
 }
 

@@ -728,13 +728,15 @@ int p2p_norm_bwd(const void* x, const void* dy, int N, int HW, int C, const floa
 // backward from per-chunk partials [2][N][nchunks][C] of sum(d) / sum(d * xhat) produced by the
 // consumer conv's dgrad epilogue (conv_dev.h nb_*): the partial pass over (x, dy) is gone;
 // finalize (+ the affine parameter gradients) and apply as in p2p_norm_bwd.  coef: [3][N][C].
+// prelu_w: the shared-slope PReLU of the forward (the apply pass gates with it; its slope
+// gradient comes from the partials' third plane, summed by the caller)
 int p2p_norm_bwd_partials(const void* x, const void* dy, int N, int HW, int C, int nchunks,
                           const float* partials, const float* mean, const float* rstd,
-                          const float* gamma, const float* beta, int act, float* dgamma, float* dbeta,
-                          float* coef, void* dx, float* dsum, void* q, int* qsite, int qfmt,
+                          const float* gamma, const float* beta, int act, const float* prelu_w, float* dgamma,
+                          float* dbeta, float* coef, void* dx, float* dsum, void* q, int* qsite, int qfmt,
                           hipStream_t st) {
   using namespace p2p;
-  if (nchunks <= 0 || HW % nchunks) return -1;
+  if (nchunks <= 0) return -1;   // (the backward's sums do not use the chunk size)
   NormGeom pg;
   pg.N = N;
   pg.HW = HW;
@@ -754,10 +756,10 @@ int p2p_norm_bwd_partials(const void* x, const void* dy, int N, int HW, int C, i
   if (dx) {
     P2P_FIN_LAUNCH(norm_bwd_finalize_kernel, pg, N, st, partials, pg, rstd, gamma, coef);
     NormGeom g = make_geom(N, HW, C);
-    with_act(act, [&](auto t) {
+    with_act(prelu_w ? ACT_PRELU_T : act, [&](auto t) {
       hipLaunchKernelGGL((norm_bwd_apply_kernel<decltype(t)::value>), dim3(g.nchunks, N), dim3(256), 0, st,
                          static_cast<const bf16*>(x), static_cast<const bf16*>(dy), g, mean, rstd, gamma, beta,
-                         nullptr, coef, static_cast<bf16*>(dx), Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
+                         prelu_w, coef, static_cast<bf16*>(dx), Fp8Shadow{static_cast<uint8_t*>(q), qsite, qfmt});
     });
     if (dsum) (void)hipMemsetAsync(dsum, 0, sizeof(float) * C, st);
   }

@@ -39,6 +39,10 @@ from . import fp8 as _f8
 ACT = {None: 0, "none": 0, "relu": 1, "lrelu": 2, "tanh": 3, "sigmoid": 4}
 # P2P_NB_FUSE=0: norm backward runs its own partial pass (A/B knob for the dgrad-epilogue fusion)
 _NB_FUSE = os.environ.get("P2P_NB_FUSE", "1") != "0"
+# P2P_NB_FOLD=1: batch-norm partials also from the reflect / nearest-x2 fold dgrads (epilogue +
+# fold_band).  Off by default: measured slower on family R (profiles/kernel_experiments_r5.md
+# section 12: the EXT epilogue costs the 256-row tiles more than the partial pass it replaces)
+_NB_FOLD = os.environ.get("P2P_NB_FOLD", "0") == "1"
 _NB_LOG = os.environ.get("P2P_NB_LOG", "0") == "1"
 # reflect-pad dgrads fold in the conv epilogue (P2P_FOLD_EPI=0: padded grid + pad_fold, A/B)
 _FOLD_EPI = os.environ.get("P2P_FOLD_EPI", "1") != "0"
@@ -399,12 +403,15 @@ def _nb_kwargs(nb):
     half, info = nb
     if info is _CS:
         return dict(nb_half=half, nb_colsum=True)
-    nx, nmean, nrstd, ng, nbeta, nact, nbatch = info
+    nx, nmean, nrstd, ng, nbeta, nact, nbatch, npw = info
     # the half's act' gate input is the norm's output registered for it (ctx.nb comes from
     # _norm_lookup of that very input): with no fused act and no affine it IS xhat, so the
-    # epilogue gates from the xhat it already forms instead of re-reading the output
+    # epilogue gates from the xhat it already forms instead of re-reading the output.
+    # Affine / shared-slope PReLU norms: batch norm only (the binding checks; family R's BNs,
+    # whose partials the reflect-dgrad epilogue + fold_band emit)
     return dict(nb_x=nx, nb_mean=nmean, nb_rstd=nrstd, nb_gamma=ng, nb_beta=nbeta, nb_act=nact,
-                nb_half=half, nb_batch=nbatch, nb_gate=(ng is None and not nact))
+                nb_half=half, nb_batch=nbatch, nb_gate=(ng is None and not nact and npw is None),
+                nb_prelu=npw)
 
 
 def prepare_weights(*modules):
@@ -842,6 +849,10 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
                 if res is not None and res.shape != (q1.shape[0], Cp, H, W):
                     _DEFERRED[q1.data_ptr()] = res   # not fusable: added below instead
                     res = None
+            # a batch norm's output (family R): its partials from this dgrad's epilogue (interior
+            # pixels) and fold_band (the band's folded values)
+            nbh = (_nb_half(cfg, None, nb, res is not None or q1.data_ptr() not in _DEFERRED)
+                   if (_NB_FOLD and not packed) else None)
             if (cfg.up == 2 and cfg.reflect and p == 1 and KH == 3 and KW == 3 and s == 1
                     and _UP_FOLD):
                 # nearest x2 then reflect pad 1 == edge-replicate pad 1 of the upsample: the
@@ -850,13 +861,13 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
                 # instead of 36 taps per input pixel (_up2_dgrad_image)
                 outs = _conv_call(gyp, None, _up2_dgrad_image(weight, Cp, Coutp), None, 0, 4, 4, 2, 3,
                                   0, 1, 0, H + 2, W + 2, Cp, 0, Cp, q1 if act_in else None, None, act_in,
-                                  C1, False, role="gy", res=res, fold=(H, W, 1, 1))[:1]
+                                  C1, False, role="gy", res=res, fold=(H, W, 1, 1), nb=nbh)
             elif cfg.up == 1 and cfg.reflect and p > 0 and _FOLD_EPI:
                 # reflect pad only: the fold happens in the dgrad's epilogue (interior pixels
                 # gated + skip gradient straight into dx) plus a frame-band pass
                 outs = _conv_call(gyp, None, None, None, 1, KH, KW, s, 0, 0, 1, 0, Hp, Wp, Cp,
                                   0, Cp, q1 if act_in else None, None, act_in, C1, False, weight,
-                                  1, Cp, Coutp, "gy", res=res, fold=(H, W, p))[:1]
+                                  1, Cp, Coutp, "gy", res=res, fold=(H, W, p), nb=nbh)
             else:
                 dxp = _conv_call(gyp, None, None, None, 1, KH, KW, s, 0, 0, 1, 0, Hp, Wp, Cp,
                                  0, Cp, None, None, 0, C1, False, weight, 1, Cp, Coutp, "gy")[0]
@@ -1252,9 +1263,9 @@ class NormFn(torch.autograd.Function):
             rstd = torch.rsqrt(run_var.float() + eps).view(1, -1)
             y = P().norm_apply(x, mean, rstd, g, b, pw, _act_code(act), True, res=res)
         ctx.cfg = (eps, act, batch, training)
-        if (training and pw is None and act in (None, "none", "relu", "lrelu") and _NB_FUSE
+        if (training and (pw is None or batch) and act in (None, "none", "relu", "lrelu") and _NB_FUSE
                 and res is None):
-            _register_norm_out(y, (x, mean, rstd, g, b, _act_code(act), bool(batch)))
+            _register_norm_out(y, (x, mean, rstd, g, b, _act_code(act), bool(batch), pw))
         # the gate of a post-residual activation needs y (not recomputable from x alone)
         keep_y = act not in (None, "none") and (act not in ("relu", "lrelu") or not training
                                                 or res is not None)
@@ -1310,13 +1321,14 @@ class NormFn(torch.autograd.Function):
             if not fresh:
                 qd = _f8.shadow_buffer(x, _f8.E5M2)
                 qargs = (dsite, qd, _f8.E5M2)
-        parts = _take_nbp(gy) if pw is None else None
+        parts = _take_nbp(gy)
         if _NB_LOG:   # which norm backwards still run the partial-sum pass (tools/diag)
             print(f"[nb] {'fused' if parts is not None else 'PARTIAL PASS'} x{tuple(x.shape)} "
                   f"act={act} batch={bool(batch)}", file=sys.stderr)
         if parts is not None:
             dx = P().norm_bwd(x, gy, mean, rstd, g, b, fused_act, dg, db, need_x, batch, dsum,
-                              *(qargs or (None, None, 0)), partials=parts)
+                              *(qargs or (None, None, 0)), prelu_w=pw,
+                              dprelu=gpw if pw is not None else None, partials=parts)
         elif qargs:
             dx = P().norm_bwd(x, gy, mean, rstd, g, b, fused_act, dg, db, need_x, batch, dsum,
                               *qargs, prelu_w=pw, dprelu=gpw if pw is not None else None)

@@ -22,7 +22,7 @@ class _Cfg:
 def test_norm_output_lookup_is_identity_based():
     hip.begin_step()
     z = torch.randn(2, 8, 4, 4)
-    info = ("x", "mean", "rstd", None, None, 2, False)
+    info = ("x", "mean", "rstd", None, None, 2, False, None)
     hip._register_norm_out(z, info)
     assert hip._norm_lookup(z) is info
     assert hip._norm_lookup(z.view(2, 8, 4, 4)) is None       # same storage, other object
@@ -65,5 +65,9 @@ def test_which_half_carries_the_partials():
 def test_nb_kwargs_modes():
     assert hip._nb_kwargs(None) == {}
     assert hip._nb_kwargs((1, hip._CS)) == {"nb_half": 1, "nb_colsum": True}
-    kw = hip._nb_kwargs((2, ("x", "m", "r", None, None, 1, True)))
+    kw = hip._nb_kwargs((2, ("x", "m", "r", None, None, 1, True, None)))
     assert kw["nb_half"] == 2 and kw["nb_act"] == 1 and kw["nb_batch"] is True and kw["nb_x"] == "x"
+    assert kw["nb_prelu"] is None and kw["nb_gate"] is False
+    # affine batch norm with a shared-slope PReLU (family R): slope handed over, no xhat gate
+    kw = hip._nb_kwargs((1, ("x", "m", "r", "g", "b", 0, True, "w")))
+    assert kw["nb_prelu"] == "w" and kw["nb_gamma"] == "g" and kw["nb_gate"] is False
