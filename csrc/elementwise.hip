@@ -562,17 +562,18 @@ struct NbBand {
   int act;
 };
 
+template <bool NB>   // NB: the partial-sum corrections (their LDS only in that instance)
 __global__ void __launch_bounds__(256) fold_band_kernel(const bf16* __restrict__ fb, int N, int H, int W, int C,
                                                         int pad, int edge, const bf16* __restrict__ xb, int act,
                                                         bf16* __restrict__ dx, NbBand nb) {
   float s1[8], s2[8], s3[8], zs[8], zc[8], rs[8], c1[8];
   const int cgt = threadIdx.x % (C >> 3);   // fixed per thread (host: 256 % (C / 8) == 0)
-  const float slope = nb.ws ? (nb.prelu ? *nb.prelu : (nb.act ? neg_slope(nb.act) : 1.f)) : 0.f;
+  const float slope = NB ? (nb.prelu ? *nb.prelu : (nb.act ? neg_slope(nb.act) : 1.f)) : 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     s1[j] = s2[j] = s3[j] = 0.f;
     rs[j] = c1[j] = zs[j] = zc[j] = 0.f;
-    if (nb.ws) {
+    if constexpr (NB) {
       const int c = cgt * 8 + j;
       rs[j] = nb.rstd[c];
       c1[j] = -nb.mean[c] * rs[j];
@@ -649,7 +650,7 @@ __global__ void __launch_bounds__(256) fold_band_kernel(const bf16* __restrict__
     for (int j = 0; j < 8; ++j) acc[j] += d[j];
     const u32x4 nv = pack8e(acc);
     *reinterpret_cast<u32x4*>(dx + o) = nv;
-    if (nb.ws) {   // partial-sum change from the old to the new stored value
+    if constexpr (NB) {   // partial-sum change from the old to the new stored value
       float nf[8], xf[8];
       unpack8e(nv, nf);
       unpack8e(*reinterpret_cast<const u32x4*>(nb.x + o), xf);
@@ -665,7 +666,7 @@ __global__ void __launch_bounds__(256) fold_band_kernel(const bf16* __restrict__
       }
     }
   }
-  if (nb.ws) {
+  if constexpr (NB) {
     // fixed-order block reduction per channel: the 256 / CP threads sharing a channel group
     __shared__ float red[3][256][8];
 #pragma unroll
@@ -825,9 +826,13 @@ int p2p_fold_band(const void* fb, int N, int H, int W, int C, int pad, int edge,
   const long total = (long)N * (2 * bw * W + (H - 2 * bw) * 2 * bw) * (C / 8);
   const NbBand nb{nb_ws, nb_plane, nb_chunk0, static_cast<const bf16*>(nb_x), nb_mean, nb_rstd, nb_gamma, nb_beta,
                   nb_prelu, nb_act};
-  hipLaunchKernelGGL(fold_band_kernel, dim3(nb_ws ? p2p_fold_band_nb_blocks() : egrid(total)), dim3(256), 0, st,
-                     static_cast<const bf16*>(fb), N, H, W, C, pad, edge, static_cast<const bf16*>(xb), act,
-                     static_cast<bf16*>(dx), nb);
+  if (nb_ws)
+    hipLaunchKernelGGL(fold_band_kernel<true>, dim3(p2p_fold_band_nb_blocks()), dim3(256), 0, st,
+                       static_cast<const bf16*>(fb), N, H, W, C, pad, edge, static_cast<const bf16*>(xb), act,
+                       static_cast<bf16*>(dx), nb);
+  else
+    hipLaunchKernelGGL(fold_band_kernel<false>, dim3(egrid(total)), dim3(256), 0, st, static_cast<const bf16*>(fb),
+                       N, H, W, C, pad, edge, static_cast<const bf16*>(xb), act, static_cast<bf16*>(dx), nb);
   return (int)hipGetLastError();
 }
 
