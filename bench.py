@@ -40,9 +40,9 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batch", type=int, default=None,
-                   help="images per GPU (default: 2048 for the pix2pix headline; 256 for --family ref -- 64 / "
-                        "128 / 256 measured 869 / 967 / 1015 img/s at 12.3 / 24.0 / 47.5 GiB, "
-                        "profiles/batch_sweep_famr_r4.jsonl; 256 for --mode infer, 128 for --impl torch), sized for the 288 GB HBM: pix2pix 1024 / 1536 / 2048 measured "
+                   help="images per GPU (default: 2048 for the pix2pix headline; 512 for --family ref -- 256 / "
+                        "512 measured 1035 / 1063 img/s captured at 52 / 104 GiB, "
+                        "profiles/ab_r5/famr_batch_256_vs_512_r5ar.txt; 256 for --mode infer, 128 for --impl torch), sized for the 288 GB HBM: pix2pix 1024 / 1536 / 2048 measured "
                         "7387 / 7400 / 7444 img/s at 50.8 / 75.3 / 99.8 GiB (profiles/batch_sweep_r4.jsonl; "
                         "fp8 9951 / 10139 at 1024 / 2048); the eager baseline's best batch was 128")
     p.add_argument("--size", type=int, default=256)
@@ -145,7 +145,7 @@ def main():
     if args.batch is None:
         # fp8 trains at 1024: at 2048 its hipGraph capture ran out of memory (the warmup's fp8
         # shadows + the capture pool; round 4), and an eager number is not the captured step
-        args.batch = (256 if args.family == "ref" else 128 if args.impl == "torch"
+        args.batch = (512 if args.family == "ref" else 128 if args.impl == "torch"
                       else 256 if args.mode == "infer" else 1024 if args.precision == "fp8" else 2048)
     B, S = args.batch, args.size
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
