@@ -143,10 +143,10 @@ def main():
                               autocast_dtype=autocast)
 
     if args.batch is None:
-        # fp8 trains at 1024: at 2048 its hipGraph capture ran out of memory (the warmup's fp8
-        # shadows + the capture pool; round 4), and an eager number is not the captured step
+        # (fp8 at 2048 captures since round 5: CapturedStep releases the hand-off registries
+        # and the allocator cache before capturing; 9908 vs 9679-9763 img/s at 1024, one box)
         args.batch = (512 if args.family == "ref" else 128 if args.impl == "torch"
-                      else 256 if args.mode == "infer" else 1024 if args.precision == "fp8" else 2048)
+                      else 256 if args.mode == "infer" else 2048)
     B, S = args.batch, args.size
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     real_A = (torch.rand(B, 3, S, S, device=dev, generator=gen) * 2 - 1).to(act_dtype)

@@ -142,7 +142,12 @@ class CapturedStep:
             snap.restore()
             torch.cuda.synchronize()
         drain_collectives()               # no eager RCCL Work left for the watchdog to poll
+        # the capture allocates from a private pool that cannot reuse the caching allocator's
+        # free blocks: hand the warmup's cached activations back first, so the captured step
+        # needs about one step's memory, not two (HBM-sized batches: 3072 bf16 / 2048 fp8)
         from ..ops import hip as _hip
+        _hip.release_handoffs()           # (their entries pin the warmup step's activations)
+        torch.cuda.empty_cache()
         salt = copy.copy(_hip._salt)      # python-side state the capture advances
         self.graph = torch.cuda.CUDAGraph()
         try:

@@ -64,14 +64,23 @@ def P():
 def begin_step():
     """Start a new step generation: weight images are re-cast on first use (graph-safe)."""
     _gen[0] += 1
+    release_handoffs()
+    if _f8._pools:
+        _f8.begin_step()
+
+
+def release_handoffs():
+    """Drop every cross-op registry entry (they hold activations of the last step: a norm's
+    input, parked gradients, fp8 copies) -- host-only, no kernel.  ``CapturedStep`` calls it
+    before ``empty_cache`` so the capture's private pool can take that memory."""
     _colsum_stash.clear()
     _stats_stash.clear()
     _norm_out.clear()
     _nbp_stash.clear()
     _DEFERRED.clear()   # a backward that raised part-way must not leak parked skip gradients
     _unshuffled.clear()
-    if _f8._pools:
-        _f8.begin_step()
+    _f8._qcache.clear()
+    _f8._shadows.clear()
 
 
 # Bias gradients handed from the norm backward to the producing conv: for a conv feeding a
