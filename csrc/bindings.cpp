@@ -1727,6 +1727,14 @@ void fp8_amax_multi(at::TensorList xs, Tensor sites, at::IntArrayRef idx) {
   }
 }
 
+// word `word` of the first n sites of a [.][4] int32 pool (or of one [4] site) := 0
+void fp8_word_zero(Tensor sites, int64_t n, int64_t word) {
+  TORCH_CHECK(sites.is_cuda() && sites.scalar_type() == at::kInt && sites.is_contiguous() && sites.numel() >= 4 * n &&
+                  word >= 0 && word < 4,
+              "fp8_word_zero: int32 [n][4] sites");
+  check_rc(p2p_fp8_word_zero(sites.data_ptr<int>(), (int)n, (int)word, cur_stream(sites)), "fp8_word_zero");
+}
+
 void fp8_roll(Tensor sites) {
   TORCH_CHECK(sites.is_cuda() && sites.scalar_type() == at::kInt && sites.is_contiguous() && sites.numel() % 4 == 0,
               "fp8_roll: int32 [n][4] pool");
@@ -1944,6 +1952,7 @@ TORCH_LIBRARY(p2p, m) {
   m.def("sn_wgrad(Tensor G, Tensor w, Tensor u, Tensor v, Tensor scale, Tensor(a!)? acc=None) -> Tensor");
   m.def("fp8_amax(Tensor x, Tensor(a!) site, int slot) -> ()");
   m.def("fp8_roll(Tensor(a!) sites) -> ()");
+  m.def("fp8_word_zero(Tensor(a!) sites, int n, int word) -> ()");
   m.def("fp8_amax_multi(Tensor[] x, Tensor(a!) sites, int[] idx) -> ()");
   m.def("fp8_dequant(Tensor q, Tensor site) -> Tensor");
   m.def("conv_wgrad(Tensor p1, Tensor? p2, int p_act, Tensor q1, Tensor? q2, int q_act, int KH, int KW, "
@@ -2013,6 +2022,7 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("sn_wgrad", sn_wgrad);
   m.impl("fp8_amax", fp8_amax);
   m.impl("fp8_roll", fp8_roll);
+  m.impl("fp8_word_zero", fp8_word_zero);
   m.impl("fp8_amax_multi", fp8_amax_multi);
   m.impl("fp8_dequant", fp8_dequant);
   m.impl("conv_wgrad", conv_wgrad);

@@ -230,6 +230,7 @@ int p2p_conv_wgrad(const p2p::ConvWgradArgs* a, hipStream_t stream);
 int p2p_fp8_quant(const void* x, long n, int* site, int use_cur, int fmt, void* q, hipStream_t st);
 int p2p_fp8_amax(const void* x, int is_f32, long n, int* site, int slot, hipStream_t st);
 int p2p_fp8_roll(int* sites, int nsites, hipStream_t st);
+int p2p_fp8_word_zero(int* sites, int nsites, int word, hipStream_t st);
 int p2p_fp8_amax_multi(int count, const float* const* x, const long* n, int* const* site, hipStream_t st);
 int p2p_fp8_dequant(const void* q, long n, const int* site, int fmt, void* y, hipStream_t st);
 int p2p_conv_wgrad_tile_rows(int R);

@@ -118,6 +118,13 @@ __global__ void fp8_roll_kernel(int* sites, int nsites) {
   s[1] = 0;
 }
 
+// word `word` of sites [0, nsites) := 0 (a current-scaling weight site's amax before its
+// per-step measurement; a HIP launch instead of an aten fill on a strided view)
+__global__ void fp8_word_zero_kernel(int* sites, int nsites, int word) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nsites) sites[4 * i + word] = 0;
+}
+
 // fp8 -> bf16 with the site's dequant exponent (tests / debugging)
 template <int FMT>
 __global__ void fp8_dequant_kernel(const uint8_t* __restrict__ q, long n, const int* site, bf16* __restrict__ y) {
@@ -185,6 +192,12 @@ int p2p_fp8_amax_multi(int count, const float* const* x, const long* n, int* con
   long g = (mx / 4 + 256 * 8 - 1) / (256 * 8);
   g = g < 1 ? 1 : (g > 256 ? 256 : g);
   hipLaunchKernelGGL(fp8_amax_multi_kernel, dim3((unsigned)g, count), dim3(256), 0, st, L);
+  return (int)hipGetLastError();
+}
+
+int p2p_fp8_word_zero(int* sites, int nsites, int word, hipStream_t st) {
+  if (nsites <= 0) return 0;
+  hipLaunchKernelGGL(p2p::fp8_word_zero_kernel, dim3((nsites + 255) / 256), dim3(256), 0, st, sites, nsites, word);
   return (int)hipGetLastError();
 }
 

@@ -245,7 +245,7 @@ def quant_weight(img: torch.Tensor, key) -> tuple[torch.Tensor, torch.Tensor]:
     i = pool.site(key)
     pool.fresh.discard(i)
     site = pool.sites[i]
-    site[0].zero_()
+    P.fp8_word_zero(site, 1, 0)
     P.fp8_amax(img, site, 0)
     return P.fp8_quant(img, site, E4M3, 0), site
 
@@ -261,7 +261,7 @@ def prepare_weight_pairs(ws, xa, xb, owners=None):
     P = _native.ops()
     wp = wpool(ws[0].device)
     idx = [wp.site(obj_key(o)) for o in (owners if owners is not None else ws)]
-    wp.sites[: wp.high, 0].zero_()
+    P.fp8_word_zero(wp.sites, wp.high, 0)
     P.fp8_amax_multi(list(ws), wp.sites, idx)
     imgs = P.weight_prep_pairs(list(ws), list(xa), list(xb), wp.sites, idx)
     return [(imgs[2 * j], imgs[2 * j + 1], wp.sites[i]) for j, i in enumerate(idx)]
