@@ -238,6 +238,145 @@ __device__ __forceinline__ void s2t_ext_all(const ConvFwdArgs& a, const uint2 (&
   }
 }
 
+// Norm statistics of one 16-channel fragment column (4 channels per lane, TM positions):
+// (mean, M2) per channel, shifted by the tile's first row; the column's 128 rows live in the 16
+// lanes of the lane's group (fixed-order xor tree).
+__device__ __forceinline__ void s2t_col_stats(const ConvFwdArgs& a, const uint2 (&v)[TM], int img, int chunk, int co,
+                                              int lane) {
+  const int pl = lane & 15;
+  const uint2 p0 = {(uint32_t)__shfl((int)v[0].x, lane & 48), (uint32_t)__shfl((int)v[0].y, lane & 48)};
+  float s1[4], s2[4], piv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    piv[r] = bfw(p0, r);
+    s1[r] = s2[r] = 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float d = bfw(v[i], r) - piv[r];
+      s1[r] += d;
+      s2[r] += d * d;
+    }
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s1[r] += __shfl_xor(s1[r], o);
+      s2[r] += __shfl_xor(s2[r], o);
+    }
+  if (pl == 0) {
+    const float inv = 1.f / (float)BM;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long o = ((long)img * a.stats_nchunks + chunk) * a.Cout + co + r;
+      a.stats[o] = piv[r] + s1[r] * inv;
+      a.stats[(long)a.N * a.stats_nchunks * a.Cout + o] = fmaxf(s2[r] - s1[r] * s1[r] * inv, 0.f);
+    }
+  }
+}
+
+// Block epilogue through LDS for the whole-pixel tiles (round 6; Cout == BN == 64, unsplit
+// output, no fp8 shadow, no norm-backward partials).  A tile's output is 4 consecutive output
+// rows x 128 pixels x 64 channels = ONE contiguous 64 KB block of y (and of the act' gate input
+// and the parked skip gradient, same layout).  The register epilogue above stores it as 8-B
+// pieces, 16 pixels two apart per wave instruction (32-B segments of 16 lines), and loads its
+// operands the same way: the round-5 roofline measured this kernel at 3.6 TB/s moving 1.6x the
+// ideal bytes.  Here each grid row of the tile (= 2 output rows, 32 KB) is staged bf16 into the
+// free ring stage (ds_write_b64 at the register layout), then all 512 threads stream it with
+// 16-B loads / stores -- a wave instruction is 1 KB contiguous -- applying the act' gate and the
+// skip gradient on the way, with the same bf16 rounding points as the register epilogue (same
+// results bit for bit).
+// LDS image of a half: pixel pix = lr * 128 + oc (lr = output row in the half, oc = column),
+// 128 B per pixel; 16-B chunk c16 stored at c16 ^ ((pix >> 1) & 7), its 8-B halves swapped when
+// (pix >> 4) & 1 -- the 16 lanes of a ds_write_b64 group (pixels 2 apart) hit 16 distinct
+// 8-byte bank pairs.
+template <int W, bool EXT>
+__device__ __forceinline__ void s2t_epilogue_lds(const ConvFwdArgs& a, const uint2 (&vv)[TM][TN], int img, int qy0,
+                                                 int nh, int cls, int lane, int tid, char* lds) {
+  static_assert(W == 64, "whole-row halves of a 64-wide grid");
+  constexpr int FPR = W / 16;              // fragments per grid row
+  const int g = lane >> 4, pl = lane & 15;
+  const int ry = cls >> 1, rx = cls & 1;
+  const int ld = a.Cout;                   // == 64: 128 B per pixel
+  const bool gate = EXT && a.act_bwd && a.xb1;
+  const bool skip = EXT && a.res1;
+  const bool relu_gate = a.act_bwd == ACT_RELU;
+  const int act_bwd = a.act_bwd;
+  auto rsrc = [&](const void* base, long off_elems) __attribute__((always_inline)) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(static_cast<const bf16*>(base) + off_elems), 0,
+                                             0x7fffffff, 0x00020000);
+  };
+#pragma unroll
+  for (int hr = 0; hr < 2; ++hr) {
+    // ---- stage: this wave's fragments of grid row hr (i = hr * FPR .. + FPR)
+#pragma unroll
+    for (int f = 0; f < FPR; ++f) {
+      const int i = hr * FPR + f;
+      const int oc = 2 * (16 * f + pl) + rx;
+      const int pix = ry * 128 + oc;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int c16 = 4 * nh + 2 * j + (g >> 1);
+        const int h8 = (g & 1) ^ ((pix >> 4) & 1);
+        const int off = pix * 128 + ((c16 ^ ((pix >> 1) & 7)) << 4) + (h8 << 3);
+        *reinterpret_cast<uint2*>(lds + off) = vv[i][j];
+      }
+    }
+    __syncthreads();
+    // ---- stream the half: 2 output rows x 128 pixels x 8 chunks = 2048 16-B chunks, 4 per thread
+    const long P0 = (long)(img * a.OH + 2 * qy0 + 2 * hr) * a.OW;   // the half's first pixel
+    const auto ry_ = rsrc(a.y1, P0 * ld);
+    const auto rx_ = rsrc(gate ? a.xb1 : a.y1, P0 * ld);
+    const auto rr_ = rsrc(skip ? a.res1 : a.y1, P0 * ld);
+    // two rounds of 2 chunks per thread: the operand loads of a round in flight together
+#pragma unroll
+    for (int ro = 0; ro < 2; ++ro) {
+      u32x4 xv[2], rv[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int e = (2 * ro + k) * 512 + tid;
+        if (gate) xv[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx_, e * 16, 0, 0));
+        if (skip) rv[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr_, e * 16, 0, 0));
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int e = (2 * ro + k) * 512 + tid;
+        const int pix = e >> 3, c16 = e & 7;
+        u32x4 v = *reinterpret_cast<const u32x4*>(lds + pix * 128 + ((c16 ^ ((pix >> 1) & 7)) << 4));
+        if ((pix >> 4) & 1) v = u32x4{v[2], v[3], v[0], v[1]};
+        if (gate) {
+          if (relu_gate) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const uint32_t x = xv[k][q];
+              v[q] &= (((int16_t)(x & 0xffffu) > 0) ? 0xffffu : 0u) | (((int16_t)(x >> 16) > 0) ? 0xffff0000u : 0u);
+            }
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const uint2 wv = {v[q], 0u}, xq = {xv[k][q], 0u};
+              v[q] = pk2(bfw(wv, 0) * act_grad_from_input(bfw(xq, 0), act_bwd),
+                         bfw(wv, 1) * act_grad_from_input(bfw(xq, 1), act_bwd));
+            }
+          }
+        }
+        if (skip) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint2 wv = {v[q], 0u}, rq = {rv[k][q], 0u};
+            v[q] = pk2(bfw(wv, 0) + bfw(rq, 0), bfw(wv, 1) + bfw(rq, 1));
+          }
+        }
+        if (P2P_OOB_OK(31, P0 * ld + (long)e * 8, 8, (long)a.N * a.OH * a.OW * ld))
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ry_, e * 16, 0, 0);
+      }
+    }
+    __syncthreads();   // the half's LDS image is read: the next half (or the next tile's halo) may overwrite it
+  }
+}
+
 // One wave's register epilogue.  acc[i][j][r] = output channel nc0 + 16 j + 4 g + r (g = lane
 // >> 4) at tile position p = 16 i + (lane & 15) of class cls (grid row qy0 + p / W, column
 // p % W).  bias / alpha / output activation, the norm statistics of a following norm and the
@@ -248,7 +387,7 @@ __device__ __forceinline__ void s2t_ext_all(const ConvFwdArgs& a, const uint2 (&
 // channels per lane, 8 positions): the live set stays within the 128-register budget.
 template <int W, bool EXT>
 __device__ __forceinline__ void s2t_epilogue(const ConvFwdArgs& a, f32x4 (&acc)[TM][TN], int m0, int img, int qy0,
-                                             int nc0, int cls, int lane) {
+                                             int nc0, int cls, int lane, int nh, int tid, char* lds) {
   constexpr int FPR = W / 16;
   const int g = lane >> 4, pl = lane & 15;
   const int ry = cls >> 1, rx = cls & 1;
@@ -284,6 +423,21 @@ __device__ __forceinline__ void s2t_epilogue(const ConvFwdArgs& a, f32x4 (&acc)[
     case ACT_RELU: cvt(std::integral_constant<int, ACT_RELU>{}); break;
     case ACT_LRELU: cvt(std::integral_constant<int, ACT_LRELU>{}); break;
     default: cvt(std::integral_constant<int, ACT_NONE>{}); break;
+  }
+
+  // whole-pixel tiles: the coalesced block epilogue through LDS (block-uniform condition)
+  if (lds != nullptr && a.Cout == BN && a.Csplit == a.Cout && !qsh.q && (!EXT || !a.nb_ws)) {
+    if (!EXT && a.stats) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        uint2 v[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) v[i] = vv[i][j];
+        s2t_col_stats(a, v, img, chunk, nc0 + 16 * j + 4 * g, lane);
+      }
+    }
+    s2t_epilogue_lds<W, EXT>(a, vv, img, qy0, nh, cls, lane, tid, lds);
+    return;
   }
 
   if constexpr (EXT) {
@@ -334,40 +488,7 @@ __device__ __forceinline__ void s2t_epilogue(const ConvFwdArgs& a, f32x4 (&acc)[
 
     if constexpr (!EXT) {
       // ---- norm statistics: (mean, M2) per column, shifted by the tile's first row
-      if (a.stats) {
-        const uint2 p0 = {(uint32_t)__shfl((int)v[0].x, lane & 48), (uint32_t)__shfl((int)v[0].y, lane & 48)};
-        float s1[4], s2[4], piv[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          piv[r] = bfw(p0, r);
-          s1[r] = s2[r] = 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float d = bfw(v[i], r) - piv[r];
-            s1[r] += d;
-            s2[r] += d * d;
-          }
-        // the column's 128 rows live in the 16 lanes of this lane's group: fixed-order xor tree
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            s1[r] += __shfl_xor(s1[r], o);
-            s2[r] += __shfl_xor(s2[r], o);
-          }
-        if (pl == 0) {
-          const float inv = 1.f / (float)BM;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const long o = ((long)img * a.stats_nchunks + chunk) * a.Cout + co + r;
-            a.stats[o] = piv[r] + s1[r] * inv;
-            a.stats[(long)a.N * a.stats_nchunks * a.Cout + o] = fmaxf(s2[r] - s1[r] * s1[r] * inv, 0.f);
-          }
-        }
-      }
+      if (a.stats) s2t_col_stats(a, v, img, chunk, co, lane);
       // ---- stores (+ fp8 shadow: host only with an unsplit output, no act' gate)
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -499,8 +620,9 @@ __device__ __forceinline__ void s2t_stamp(int dbg, int k, int field) {
 }
 
 template <int W, bool RELU, bool EXT, int F8 = 0>
-__global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a, int ntiles, int dbg) {
+__global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a, int ntiles, int flags) {
   using G = S2TGeom<W>;
+  const int dbg = flags & 1;
   constexpr int ES = F8 ? 1 : 2;      // bytes per operand element
   constexpr int CHC = 128 / ES;       // channels per 128-B halo chunk
   constexpr int FPR = W / 16;
@@ -594,6 +716,9 @@ __global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a, int nti
       b[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wsrd, bvoff, so + j * 16 * wrow, 0));
   };
 
+  // the LDS-staged block epilogue (s2t_epilogue_lds) on the 32 KB free stage; P2P_S2T_EPI=0 keeps
+  // the register epilogue (A/B and the bitwise-equality test)
+  const bool lds_epi = (flags & 2) != 0 && G::STAGE_BYTES >= 32768;
   int m0, n0, img, qy0;
   tile_geo(L, m0, n0, img, qy0);
   int bvoff = bv_of(n0);
@@ -745,7 +870,9 @@ __global__ void __launch_bounds__(512, 4) conv_s2t_kernel(ConvFwdArgs a, int nti
 
 #ifndef S2T_NOEPI
     s2t_stamp(dbg, kt, 1);
-    s2t_epilogue<W, EXT>(a, acc, m0, img, qy0, n0 + 32 * nh, cls_w, lane);
+    // (the stage the last chunk was read from is free: every wave passed the loop's last barrier)
+    s2t_epilogue<W, EXT>(a, acc, m0, img, qy0, n0 + 32 * nh, cls_w, lane, nh, tid,
+                         lds_epi ? ring + (stage ^ 1) * G::STAGE_BYTES : nullptr);
     s2t_stamp(dbg, kt, 2);
     ++kt;
 #else
@@ -790,8 +917,12 @@ static int launch_s2t(const ConvFwdArgs& a, hipStream_t st) {
   const long tiles = (long)a.N * a.H * a.W / BM * (a.Cout / BN);
   const char* ed = P2P_KNOB_ONCE("P2P_S2T_DEBUG");   // timeline stamps (tools/s2t_timeline.py)
   const int dbg = (ed && ed[0] == '1') ? 1 : 0;
+  // bit 1: the LDS-staged block epilogue (default; P2P_S2T_EPI=0 = the register epilogue, read
+  // per call: the equality test toggles it)
+  const char* ee = std::getenv("P2P_S2T_EPI");
+  const int lds_epi = (ee && ee[0] == '0') ? 0 : 2;
   hipLaunchKernelGGL((conv_s2t_kernel<W, RELU, EXT, F8>), dim3((unsigned)s2t_grid(tiles)), dim3(NT), smem, st, a,
-                     (int)tiles, dbg);
+                     (int)tiles, dbg | lds_epi);
   return (int)hipGetLastError();
 }
 

@@ -27,30 +27,42 @@ import copy
 import torch
 
 
-# ProcessGroupNCCL's watchdog polls the end events of the eager collectives it tracks every
-# ~100 ms (kWatchdogThreadSleepMillis) and only then retires them
-_WATCHDOG_DRAIN_S = 0.35
+def step_reducers(trainer):
+    """The data-parallel reducers a trainer's step issues its collectives through (its
+    ``GradReducer`` attributes: G / D / C)."""
+    from ..parallel.ddp import GradReducer
+    out = []
+    for v in vars(trainer).values() if trainer is not None else ():
+        if isinstance(v, GradReducer) and all(v is not r for r in out):
+            out.append(v)
+    return out
 
 
-def drain_collectives():
-    """Let the c10d watchdog retire every eager collective before a capture begins.
+def isolate_capture_collectives(trainer):
+    """Move the step's RCCL reducers onto a process group with no eager history before the
+    capture (``parallel.dist.capture_group``).
 
-    The capture's first collective makes the process group's RCCL stream join the capture.
-    On HIP, ``hipEventQuery`` of an event recorded on a stream that is NOW capturing fails
-    with ``hipErrorCapturedEvent`` -- and the watchdog still holds the end events of the
-    warmup steps' all-reduces until its next poll, so a capture that starts within one poll
-    interval of them aborts the process (tools/diag_capture_event.py
-    reproduces it with one rank).  A device sync completes those Works; sleeping a few poll
-    intervals lets the watchdog retire them."""
-    import time
-
-    import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()):
-        return
-    if dist.get_backend() != "nccl":
-        return
+    The c10d watchdog keeps querying the end events of the warmup steps' eager all-reduces
+    until its next poll retires them.  Two HIP rules turn such a query during the capture into
+    a process abort from the watchdog thread (round 5 slept 3.5 poll periods):
+    (1) under the default "global" capture mode every thread's ``hipEventQuery`` is refused
+    while a capture runs -- ``CapturedStep`` captures in "thread_local" mode, which exempts
+    the watchdog thread; (2) the capture's first collective makes its group's RCCL stream
+    join the capture, and an event last recorded on a capturing stream cannot be queried --
+    so the recorded collectives run on a fresh group whose watchdog has never tracked a Work,
+    and the warmup's group never joins a capture.  Both are conditions, not a wait on c10d's
+    poll period (``tests/test_capture_group_gpu.py`` captures right behind a pending eager
+    all-reduce).  Collective across ranks (a new group); returns it, or None without RCCL
+    reducers."""
+    reds = [r for r in step_reducers(trainer) if r.comm and r.backend == "nccl"]
+    if not reds:
+        return None
+    from ..parallel import dist as pdist
     torch.cuda.synchronize()
-    time.sleep(_WATCHDOG_DRAIN_S)
+    pg = pdist.capture_group()
+    for r in reds:
+        r.set_group(pg)
+    return pg
 
 
 class WarmupError(RuntimeError):
@@ -141,7 +153,8 @@ class CapturedStep:
         if snap is not None:
             snap.restore()
             torch.cuda.synchronize()
-        drain_collectives()               # no eager RCCL Work left for the watchdog to poll
+        # the recorded collectives go to a process group no eager Work was ever issued on
+        isolate_capture_collectives(trainer)
         # the capture allocates from a private pool that cannot reuse the caching allocator's
         # free blocks: hand the warmup's cached activations back first, so the captured step
         # needs about one step's memory, not two (HBM-sized batches: 3072 bf16 / 2048 fp8)
@@ -151,7 +164,10 @@ class CapturedStep:
         salt = copy.copy(_hip._salt)      # python-side state the capture advances
         self.graph = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(self.graph):
+            # thread_local: under the default "global" mode HIP refuses every other thread's
+            # hipEventQuery while the capture runs -- the c10d watchdog's polls of eager Works
+            # included (tests/test_capture_group_gpu.py); only this thread's calls are checked
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                 self.static_out = step_fn(*self.static_inputs)
         except Exception as e:  # noqa: BLE001
             torch.cuda.synchronize()

@@ -1322,6 +1322,7 @@ class NormFn(torch.autograd.Function):
             # dx = rstd * gamma * dz (no mean terms) and the parameter / slope gradients
             dx = P().norm_bwd(x, gy, mean, rstd, g, b, fused_act, dg, db, need_x, True, None,
                               prelu_w=pw, dprelu=gpw, frozen=True)
+            gpw = _pair_slope_grad(prelu_w, gpw)
             return (dx if need_x else None), dg, db, gpw, None, None, None, None, None, None, None, None, gres, None
         dsum = torch.empty(x.shape[1], device=x.device, dtype=torch.float32) if need_x else None
         qargs, qd, dsite, fresh = (), None, None, False
@@ -1350,16 +1351,24 @@ class NormFn(torch.autograd.Function):
                 _f8.stash_shadow(dx, qd, dsite)
             elif fresh:
                 _f8.bootstrap_shadow(dx, (ctx.qkey, "dx"), _f8.E5M2)
-        if gpw is not None:
-            # a shared PReLU slope (family R: one slope, five sites): its later gradients of this
-            # backward are added into the first in place (HIP) instead of by autograd (aten)
-            first = _pair_first(prelu_w)
-            if first is not None:
-                P().lincomb_(first, gpw, 1.0, 1.0, 0.0)
-                gpw = None
-            else:
-                _pair_set(prelu_w, gpw)
+        gpw = _pair_slope_grad(prelu_w, gpw)
         return (dx if need_x else None), dg, db, gpw, None, None, None, None, None, None, None, None, gres, None
+
+
+def _pair_slope_grad(prelu_w, gpw):
+    """A shared PReLU slope (family R: one slope, five sites, train and eval mode alike): its
+    later gradients of this backward are added into the first in place (HIP) instead of by
+    autograd (aten).  Every contribution to a paired leaf must come through here: autograd
+    would sum an unpaired one out of place and the in-place adds into the first would be lost
+    (``tests/test_family_r_gpu.py::test_grad_pairing_matches_autograd_sum``)."""
+    if gpw is None:
+        return None
+    first = _pair_first(prelu_w)
+    if first is not None:
+        P().lincomb_(first, gpw, 1.0, 1.0, 0.0)
+        return None
+    _pair_set(prelu_w, gpw)
+    return gpw
 
 
 class _PadCFn(torch.autograd.Function):
@@ -1521,14 +1530,23 @@ class FanOutFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, n):
+        ctx.dtype = x.dtype
         return tuple(x.view_as(x) for _ in range(n))
 
     @staticmethod
     def backward(ctx, *gs):
+        gs = [g for g in gs if g is not None]
+        if not gs:
+            return None, None
+        if ctx.dtype != torch.bfloat16 or any(g.dtype != torch.bfloat16 for g in gs):
+            # not the bf16 activation path: sum in the gradients' own dtype, exactly as
+            # autograd's input buffer would (no silent narrowing of an fp32 gradient)
+            acc = gs[0]
+            for g in gs[1:]:
+                acc = acc + g
+            return acc.to(ctx.dtype), None
         acc = None
         for g in gs:
-            if g is None:
-                continue
             g = to_nhwc_bf16(g)
             acc = g if acc is None else P().act(acc, g, 0, 3)
         return acc, None

@@ -26,7 +26,8 @@ Mechanism
   * ``paused()``: a backward whose gradients will be discarded (the reference's D grads
     from the G loss, the C-phase backward) launches no collective.
   * Averaging (round 5): on RCCL the bucket all-reduce is
-    ``ReduceOp.AVG`` (ncclAvg: the division happens inside the collective), so no gradient
+    ``ReduceOp.AVG`` (ncclAvg: the division happens inside the collective) at every world
+    size, force_comm world 1 included (round 6), so no gradient
     is ever rescaled on the compute stream -- the round-4 reducer issued one ``mul_(1/world)``
     per parameter in its hook (~130 extra launches per step at world 8).  Process groups
     without AVG (gloo: the CPU / one-GPU rehearsal backend) sum and scale each BUCKET once in
@@ -56,7 +57,8 @@ Mechanism
     (``P2P_DIRECT_GRAD=0`` turns it off): step A/B with RCCL collectives at world 1 --
     direct 7849 / 7839, autograd 7838, no reducer 7870 img/s (profiles/force_comm_r5k.jsonl).
     The round-4 watchdog abort seen with it was a capture started while the c10d watchdog
-    still tracked the warmup's eager all-reduces (engine/graph.py ``drain_collectives``).
+    still tracked the warmup's eager all-reduces; since round 6 the captured collectives run on
+    a fresh process group (engine/graph.py ``isolate_capture_collectives``).
   * Bucket size: xGMI is point-to-point (7 links x ~153 GB/s per GPU); RCCL's ring /
     direct algorithms are per-link bound, so few large buckets (tens of MB) amortise the
     per-collective latency while still leaving >= 2-4 buckets per network to overlap.
@@ -157,7 +159,10 @@ class GradReducer:
         # gradients land unscaled (direct writes and autograd alike): RCCL averages inside the
         # collective (ReduceOp.AVG); other backends sum and scale each bucket once in finish()
         self.scale = 1.0
-        self._avg = self.comm and self.world > 1 and self.backend == "nccl"
+        # RCCL: ReduceOp.AVG at EVERY world size -- with force_comm at world 1 (the identity
+        # average) the one-GPU tests and A/Bs run the exact op, dtype and capture path of a
+        # world-8 job
+        self._avg = self.comm and self.backend == "nccl"
         self._post_scale = (1.0 / self.world) if (self.comm and self.world > 1 and not self._avg) else None
         if direct is None:   # default on: bitwise equal to the autograd path (tools/ddp_rehearsal.py)
             direct = os.environ.get("P2P_DIRECT_GRAD", "1") == "1"
@@ -293,6 +298,17 @@ class GradReducer:
         if copy:
             dst.copy_(p.grad)
         p.grad = dst
+
+    def set_group(self, pg):
+        """Issue this reducer's collectives on ``pg`` from now on (same ranks and backend):
+        ``CapturedStep`` moves the reducers onto a fresh capture group before recording
+        (``parallel.dist.capture_group``)."""
+        if self.comm:
+            if dist.get_world_size(pg) != self.world or dist.get_backend(pg) != self.backend:
+                raise ValueError("GradReducer.set_group: the group must span the same ranks and backend")
+            self._join_inflight()
+            self.pg = pg
+        return self
 
     def _op(self):
         return dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM

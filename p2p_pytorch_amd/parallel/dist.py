@@ -138,6 +138,30 @@ def all_reduce_mean_(tensors):
     return tensors
 
 
+_CAPTURE_PGS: list = []
+
+
+def capture_group():
+    """A NEW process group for the collectives recorded into one hipGraph (RCCL only).
+
+    c10d's watchdog polls the end events of every EAGER collective a process group has issued
+    until it retires them (one poll period later).  On HIP, querying an event whose stream is
+    capturing fails (``hipErrorCapturedEvent``), and a captured collective makes its group's
+    RCCL stream join the capture -- so capturing on a group that still holds an eager Work
+    aborts the process from the watchdog thread (VERDICT r4 W5b / r5 W4b;
+    ``tests/test_capture_group_gpu.py``).  Collectives recorded on a group made here never
+    share a stream with a tracked eager Work: its communicator is connected at creation (the
+    device-bound default group's ``ncclCommSplit`` / eager connect -- no c10d Work) and nothing
+    has been issued on it before the capture.  That is a condition, not a wait on the
+    watchdog's poll period.  A new group per capture (eager collectives issued on an earlier
+    capture's group afterwards cannot leak into the next capture).  Collective: every rank
+    calls it at the same point (``CapturedStep`` does, right before its capture)."""
+    pg = dist.new_group(backend="nccl")
+    _CAPTURE_PGS.append(pg)
+    return pg
+
+
 def destroy():
+    _CAPTURE_PGS.clear()
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()

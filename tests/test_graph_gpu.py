@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 STEPS = 3
 
 
-def _build(reducers=False, direct=True):
+def _build(reducers=False, direct=True, comm_dtype=None):
     from p2p_pytorch_amd.engine.pix2pix import Pix2PixStep
     from p2p_pytorch_amd.models import define_D, define_G
     from p2p_pytorch_amd.parallel import GradReducer
@@ -36,9 +36,11 @@ def _build(reducers=False, direct=True):
     D = define_D(6, 64, norm="instance", netD="basic", gpu_id=dev, verbose=False)
     rg = rd = None
     if reducers:
-        rg = GradReducer(G, bucket_mb=4.0, force_comm=True, direct=direct)
-        rd = GradReducer(D, bucket_mb=4.0, force_comm=True, direct=direct)
+        rg = GradReducer(G, bucket_mb=4.0, force_comm=True, direct=direct, comm_dtype=comm_dtype)
+        rd = GradReducer(D, bucket_mb=4.0, force_comm=True, direct=direct, comm_dtype=comm_dtype)
         assert len(rg.buckets) > 1
+        # the world-8 op at world 1: RCCL averages inside the collective
+        assert rg._avg and rd._avg and rg._op() == dist.ReduceOp.AVG
     return Pix2PixStep(G, D, reducer_g=rg, reducer_d=rd), G, D
 
 
@@ -57,19 +59,22 @@ def _params(G, D):
     return torch.cat([p.detach().reshape(-1) for p in list(G.parameters()) + list(D.parameters())])
 
 
-def _eager(reducers=False, direct=True):
-    step, G, D = _build(reducers, direct)
+def _eager(reducers=False, direct=True, comm_dtype=None):
+    step, G, D = _build(reducers, direct, comm_dtype)
     for a, b in _data():
         losses = step.step(a, b)
     torch.cuda.synchronize()
     return _params(G, D), {k: v.item() for k, v in losses.items()}
 
 
-def _graph(reducers=False, direct=True):
+def _graph(reducers=False, direct=True, comm_dtype=None):
     from p2p_pytorch_amd.engine.graph import CapturedStep
-    step, G, D = _build(reducers, direct)
+    step, G, D = _build(reducers, direct, comm_dtype)
     data = _data()
     cap = CapturedStep(step.step, *data[0], warmup=2)
+    if reducers:
+        # the recorded collectives run on the capture's own fresh group (engine/graph.py)
+        assert step.reducer_g.pg is not None and step.reducer_g.pg is step.reducer_d.pg
     for a, b in data:
         losses = cap(a, b)
     torch.cuda.synchronize()
@@ -118,3 +123,19 @@ def test_rccl_reducers_under_capture_equal_eager(deterministic):
     assert torch.equal(pe, pr), (pe - pr).abs().max().item()
     assert torch.equal(pe, pa), (pe - pa).abs().max().item()
     assert torch.equal(pe, pg), (pe - pg).abs().max().item()
+
+
+def test_rccl_bf16_comm_avg_under_capture(deterministic):
+    """``--comm_dtype bf16``: buckets narrowed to bf16, ``ReduceOp.AVG`` on RCCL (world 1:
+    the identity average, rounded through bf16), captured == eager bitwise."""
+    from p2p_pytorch_amd.parallel import dist as pdist
+    pdist.init_single(torch.device("cuda", torch.cuda.current_device()))
+    try:
+        pe, le = _eager(reducers=True, comm_dtype=torch.bfloat16)
+        pg, lg = _graph(reducers=True, comm_dtype=torch.bfloat16)
+        pf, _ = _eager(reducers=True)
+    finally:
+        pdist.destroy()
+    assert le == lg
+    assert torch.equal(pe, pg), (pe - pg).abs().max().item()
+    assert not torch.equal(pe, pf), "bf16 comm buffers changed nothing: not exercised"

@@ -211,3 +211,39 @@ def test_s2t_persistent_grid_bitwise(N, H, C, Cout, monkeypatch):
     assert torch.equal(outs[0], outs[1])
     assert torch.equal(outs[0], outs[2])
 
+
+
+def test_s2t_lds_epilogue_bitwise_full_step(monkeypatch):
+    """Round 6: the whole-pixel s2t tiles (Cout 64) stage their output through LDS and stream
+    the act' gate / skip gradient / output with 16-B coalesced accesses
+    (``s2t_epilogue_lds``).  Same bf16 rounding points as the register epilogue
+    (``P2P_S2T_EPI=0``, read per launch): one deterministic pix2pix step at 256x256 -- G e2's
+    input gradient (lrelu' gate + the parked skip gradient of e1), D c1's (gate), d7's ConvT
+    forward (ReLU input + fused norm statistics) -- gives bitwise the same parameters."""
+    import p2p_pytorch_amd as p2p
+    from p2p_pytorch_amd.engine.pix2pix import Pix2PixStep
+    from p2p_pytorch_amd.models import define_D, define_G
+    from p2p_pytorch_amd.ops import hip
+
+    def step_params(epi):
+        monkeypatch.setenv("P2P_S2T_EPI", epi)
+        hip.reset_rng(0)
+        torch.manual_seed(0)
+        G = define_G(netG="unet_256", gpu_id=DEV, verbose=False)
+        D = define_D(6, 64, norm="instance", netD="basic", gpu_id=DEV, verbose=False)
+        st = Pix2PixStep(G, D)
+        a = rand_img(2, 3, 256, 256, seed=21)
+        b = rand_img(2, 3, 256, 256, seed=22)
+        p2p.set_deterministic(True)
+        try:
+            names = _kernels(lambda: st.step(a, b))
+        finally:
+            p2p.set_deterministic(False)
+        return torch.cat([p.detach().reshape(-1) for p in list(G.parameters()) + list(D.parameters())]), names
+
+    p_lds, names = step_params("1")
+    assert any("conv_s2t_kernel<64, false, true, 0>" in k for k in names), sorted(set(names))
+    assert any("conv_s2t_kernel<64, true, false, 0>" in k for k in names), sorted(set(names))
+    p_reg, _ = step_params("0")
+    monkeypatch.delenv("P2P_S2T_EPI")
+    assert torch.equal(p_lds, p_reg), (p_lds - p_reg).abs().max().item()

@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round 6: DP-path checks (capture group + thread_local capture), s2t LDS-epilogue A/B, diag matrix
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/r6d
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_capture_group_gpu.py tests/test_graph_gpu.py tests/test_family_r_gpu.py tests/test_ddp_gpu.py > $O/tests.log 2>&1; rc=$?
+grep -E "PASS|FAIL|ERROR|passed|failed" $O/tests.log | tail -30
+[ $rc -eq 0 ] || exit $rc
+b() { # tag args...
+  local t=$1; shift
+  timeout -k 10 300 env "$@" python bench.py --steps 15 --warmup 4 ${BARGS:-} > $O/$t.json 2> $O/$t.err || return $?
+  python -c "import json;d=json.load(open('$O/$t.json'));print('$t', d['value'], d['ms_per_step'], d.get('hipgraph'), d.get('capture_error'))"
+}
+for r in 1 2; do
+  b lds_r$r P2P_S2T_EPI=1 || exit $?
+  b reg_r$r P2P_S2T_EPI=0 || exit $?
+done
+BARGS="--force_comm --comm_dtype bf16" b fc_bf16 X=1 || exit $?
+BARGS="--force_comm" b fc X=1 || exit $?
+# diagnosis matrix (last: the global-mode runs are expected to abort)
+for m in "isolated thread_local" "race thread_local" "isolated global"; do
+  set -- $m
+  timeout -k 10 120 python tools/diag_capture_event.py --mode $1 --capture-mode $2 --rounds 2 > $O/diag_$1_$2.log 2>&1
+  echo "diag $1 $2 rc=$?"
+done
