@@ -666,7 +666,12 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
     TORCH_CHECK(rc != -2, "conv_fwd: the s2t kernel refused a geometry the host accepted");
   }
   // the 32x32x16 MFMA tiles (conv_fwd_m32.hip) take the 256-row bf16 FASTK layers first
-  if (rc == -2 && glds_ok && !fp8 && p2p_m32_enabled()) rc = p2p_conv_fwd_m32(&a, (int)mode, variant, st);
+  // (fp8: the 32x32x64 f8f6f4 tiles since round 6; P2P_M32_F8=0 -- read per call, the tests A/B
+  // it -- keeps fp8 on the 16x16x128 glds tiles)
+  const char* m32f8 = fp8 ? std::getenv("P2P_M32_F8") : nullptr;
+  const bool m32_f8_on = !(m32f8 && m32f8[0] == '0');
+  if (rc == -2 && glds_ok && (!fp8 || m32_f8_on) && p2p_m32_enabled())
+    rc = p2p_conv_fwd_m32(&a, (int)mode, variant, st);
   if (rc == -2 && glds_ok) rc = p2p_conv_fwd_glds(&a, (int)mode, variant, st);
   if (rc == -2 && a.stats) {  // glds refused after all: no fused statistics
     a.stats = nullptr;

@@ -57,6 +57,19 @@ __device__ __forceinline__ u32x4 ds_rd128(uint32_t addr) {
   return r;
 }
 
+typedef int m32_i32x8 __attribute__((ext_vector_type(8)));
+typedef int m32_i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ m32_i32x8 m32_cat8(u32x4 lo, u32x4 hi) {
+  return __builtin_shufflevector(__builtin_bit_cast(m32_i32x4, lo), __builtin_bit_cast(m32_i32x4, hi), 0, 1, 2, 3, 4,
+                                 5, 6, 7);
+}
+// ReLU on 16 packed fp8 bytes (e4m3: sign = bit 7 of each byte): zero the negative ones
+__device__ __forceinline__ u32x4 m32_relu_fp8x16(u32x4 v) {
+#pragma unroll
+  for (int w = 0; w < 4; ++w) v[w] &= ~(((v[w] >> 7) & 0x01010101u) * 0xffu);
+  return v;
+}
+
 // one k16 step's operands: TM A fragments (32 pixel rows x 16 k) and TN B fragments
 template <int TM, int TN>
 struct Frag {
@@ -172,9 +185,21 @@ struct M32Geom {
   static_assert(2 * NR <= 15, "two steps of reads within the lgkm counter");
 };
 
-template <int BN, int MODE, bool RELU, bool EXT>
+// F8 (round 6): fp8 operands -- 1: e4m3 activations (forward / ConvT
+// forward), 2: e5m2 gradients (input gradients, EXT epilogue) -- x e4m3 weights, on
+// v_mfma_scale_f32_32x32x64_f8f6f4 with the per-tensor E8M0 exponents as its scale operands.
+// The LDS image is byte-for-byte the bf16 one (a 128-B row = 128 fp8 k instead of 64 bf16 k),
+// so staging, swizzle and fragment reads are unchanged: one fp8 k64 step is the union of the
+// reads of two bf16 k16 steps (lane half h: chunks 4s + h and 4s + 2 + h), fed as the low /
+// high 16 bytes of the 32-byte operand.  A and B take the same lane map, so the products pair
+// whatever k order the instruction assigns inside the 32 bytes, and one per-tensor scale per
+// operand makes the per-32-k scale blocks uniform.  Half the K tiles of the bf16 GEMM for the
+// same MFMA cycles per tile: twice the FLOP per staged byte.
+template <int BN, int MODE, bool RELU, bool EXT, int F8 = 0>
 __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
   using G = M32Geom<BN>;
+  constexpr int ES = F8 ? 1 : 2;            // bytes per operand element
+  constexpr int BKE = F8 ? 2 * BK : BK;     // operand elements per 128-B K tile row
   constexpr int BM = G::BM, WN = G::WN, TM = G::TM, TN = G::TN, STAGES = G::STAGES, NT = G::NT;
   constexpr int RPP = G::RPP, AROWS = G::AROWS, BROWS = G::BROWS, LOADS = G::LOADS;
   constexpr int NR = G::NR;
@@ -196,7 +221,11 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
   const int mt = bid / ntiles, nt = bid % ntiles;
   const int m0 = mt * BM, n0 = nt * BN;
   if (m0 >= g.Mc) return;
-  const int kt1 = (g.Kc + BK - 1) / BK;   // no split-K: K tiles [0, kt1)
+  const int kt1 = (g.Kc + BKE - 1) / BKE;   // no split-K: K tiles [0, kt1)
+  // fp8: E8M0 dequant exponents of the two A sources and of the weights (fp8 scale sites)
+  const int ex1 = (F8 && a.qs_x1) ? a.qs_x1[2] : 127;
+  const int ex2 = (F8 && a.qs_x2) ? a.qs_x2[2] : 127;
+  const int ew = (F8 && a.qs_w) ? a.qs_w[2] : 127;
   M32_STAMP(0, __builtin_amdgcn_s_memtime());
   M32_STAMP(4, __builtin_amdgcn_s_memrealtime());
 
@@ -218,12 +247,12 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
   const long img_elems = (long)a.H * a.W;
   auto img_rsrc = [&](const void* base, int cs) __attribute__((always_inline)) {
     const long first = (long)img0 * img_elems * cs;
-    return make_rsrc(static_cast<const bf16*>(base) + first, ((long)a.N * img_elems * cs - first) * 2);
+    return make_rsrc(static_cast<const char*>(base) + first * ES, ((long)a.N * img_elems * cs - first) * ES);
   };
   const auto rx1 = img_rsrc(a.x1, C1);
   const auto rx2 = img_rsrc(C2 > 0 ? a.x2 : a.x1, C2 > 0 ? C2 : C1);
   const long wrow = (MODE == 0) ? (long)g.Kc : (long)a.KH * a.KW * C;
-  const auto rw = make_rsrc(a.w, a.Cout * wrow * 2);
+  const auto rw = make_rsrc(a.w, a.Cout * wrow * ES);
 
   // ---- loader decode: A rows row_i = wid*8 + rsub + RPP*i (pixel of the block's first image
   // + y / x origin of its taps); the source-side swizzle (row >> 1) & 7 does not depend on i
@@ -256,7 +285,7 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
 #pragma unroll
   for (int i = 0; i < BROWS; ++i) {
     const int co = n0 + wid * 8 + rsub + RPP * i;
-    b_vo[i] = co < a.Cout ? (uint32_t)((co * wrow + r_c) * 2) : OOB;
+    b_vo[i] = co < a.Cout ? (uint32_t)(co * wrow * ES + r_c * 2) : OOB;
   }
   const FastDiv fd_c = make_fastdiv((uint32_t)C), fd_ti = make_fastdiv((uint32_t)g.Ti);
   uint32_t a_vo[AROWS];
@@ -267,7 +296,7 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
   // offsets are formed once per channel segment, later tiles of the segment only move the
   // uniform soffset by 128 B)
   auto prep = [&](int kt) __attribute__((always_inline)) {
-    const int k0 = kt * BK;
+    const int k0 = kt * BKE;
     const int tap = (int)fdiv((uint32_t)k0, fd_c);
     const int ci0 = k0 - tap * C;
     const int t_y = (int)fdiv((uint32_t)tap, fd_ti);
@@ -296,17 +325,17 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
           ix = (int)(int16_t)(r_yx[i] & 0xffff) - t_x;
           inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
         }
-        a_vo[i] = inb ? (uint32_t)(((r_img[i] + iy * a.W + ix) * cs + cio + r_c) * 2) : OOB;
+        a_vo[i] = inb ? (uint32_t)(((r_img[i] + iy * a.W + ix) * cs + cio) * ES + r_c * 2) : OOB;
       }
       a_soff = 0;
     } else {
       a_soff += BK * 2;
     }
     if (MODE == 0) {
-      w_soff = k0 * 2;
+      w_soff = k0 * ES;
     } else {
       const int ky = g.ky0 + a.stride * t_y, kx = g.kx0 + a.stride * t_x;
-      w_soff = ((ky * a.KW + kx) * C + ci0) * 2;
+      w_soff = ((ky * a.KW + kx) * C + ci0) * ES;
     }
   };
   // load number q (A rows first, then B rows) of the prepared tile into LDS slot SLOT
@@ -319,8 +348,14 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
       bld16(rw, Bs + SLOT * (G::B_SLOT / 2) + (wid * 8 + RPP * i) * BK, b_vo[i], w_soff);
     }
   };
+  // fp8: the E8M0 exponent of the A source of the tile in each LDS slot (a 128-deep tile never
+  // straddles the concat halves: host-checked C1 % 128 == 0)
+  int sa_slot[STAGES];
+#pragma unroll
+  for (int s = 0; s < STAGES; ++s) sa_slot[s] = ex1;
   auto issue_all = [&](auto slot_c, int kt) __attribute__((always_inline)) {
     prep(kt);
+    if constexpr (F8 != 0) sa_slot[decltype(slot_c)::value] = a_first ? ex1 : ex2;
 #pragma unroll
     for (int q = 0; q < LOADS; ++q) fire(slot_c, q);
   };
@@ -386,6 +421,100 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
       }
     }
   };
+  // fp8: one k64 step = the fragments of two bf16 k16 steps (lo: chunks 4s + h, hi: 4s + 2 + h)
+  // held as fixed lo / hi pairs (one 8-register MFMA operand each), with glds Q0 .. Q0 + NQ - 1
+  // spread over its P MFMAs (up to two after an MFMA)
+  struct F8Frag {
+    u32x4 alo[TM], ahi[TM], blo[TN], bhi[TN];
+  };
+  auto read_f8 = [&](auto slot_c, auto s_c, F8Frag& f) __attribute__((always_inline)) {
+    constexpr int SLOT = decltype(slot_c)::value, S = decltype(s_c)::value;
+    const uint32_t a0 = fa[2 * S] + SLOT * G::A_SLOT, a1 = fa[2 * S + 1] + SLOT * G::A_SLOT;
+    const uint32_t b0 = fb[2 * S] + SLOT * G::B_SLOT, b1 = fb[2 * S + 1] + SLOT * G::B_SLOT;
+    f.alo[0] = ds_rd128<0>(a0);
+    f.ahi[0] = ds_rd128<0>(a1);
+    f.alo[1] = ds_rd128<4096>(a0);
+    f.ahi[1] = ds_rd128<4096>(a1);
+    if constexpr (TM > 2) {
+      f.alo[2] = ds_rd128<8192>(a0);
+      f.ahi[2] = ds_rd128<8192>(a1);
+      f.alo[3] = ds_rd128<12288>(a0);
+      f.ahi[3] = ds_rd128<12288>(a1);
+    }
+    f.blo[0] = ds_rd128<0>(b0);
+    f.bhi[0] = ds_rd128<0>(b1);
+    f.blo[1] = ds_rd128<4096>(b0);
+    f.bhi[1] = ds_rd128<4096>(b1);
+  };
+  auto wait_f8 = [&](auto n_c, F8Frag& f) __attribute__((always_inline)) {
+    constexpr int N = decltype(n_c)::value;
+    static_assert(N >= 0 && N <= 15, "lgkmcnt range");
+    if constexpr (TM == 4) {
+      asm volatile("s_waitcnt lgkmcnt(%12)"
+                   : "+v"(f.alo[0]), "+v"(f.alo[1]), "+v"(f.alo[2]), "+v"(f.alo[3]), "+v"(f.ahi[0]), "+v"(f.ahi[1]),
+                     "+v"(f.ahi[2]), "+v"(f.ahi[3]), "+v"(f.blo[0]), "+v"(f.blo[1]), "+v"(f.bhi[0]), "+v"(f.bhi[1])
+                   : "n"(N));
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(%8)"
+                   : "+v"(f.alo[0]), "+v"(f.alo[1]), "+v"(f.ahi[0]), "+v"(f.ahi[1]), "+v"(f.blo[0]), "+v"(f.blo[1]),
+                     "+v"(f.bhi[0]), "+v"(f.bhi[1])
+                   : "n"(N));
+    }
+  };
+  // k64 step of MFMAs on f, streaming the NEXT step's fragments into f behind them (RD: A
+  // fragment i is re-read once its MFMAs are issued, the B fragments after the last one): one
+  // register set of 8-register operands (a second set spilled the 256-wide tile)
+  auto mma_f8 = [&](F8Frag& f, auto nq_c, auto q0_c, auto slot_c, bool refill, int sa, auto rslot_c, auto rstep_c,
+                    bool rd) __attribute__((always_inline)) {
+    constexpr int NQ = decltype(nq_c)::value, Q0 = decltype(q0_c)::value, P = TM * TN;
+    constexpr int RSLOT = decltype(rslot_c)::value, RS = decltype(rstep_c)::value;
+    static_assert(NQ <= 2 * P, "at most two glds per MFMA");
+    if constexpr (RELU) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        f.alo[i] = m32_relu_fp8x16(f.alo[i]);
+        f.ahi[i] = m32_relu_fp8x16(f.ahi[i]);
+      }
+    }
+    const uint32_t a0 = fa[2 * RS] + RSLOT * G::A_SLOT, a1 = fa[2 * RS + 1] + RSLOT * G::A_SLOT;
+    const uint32_t b0 = fb[2 * RS] + RSLOT * G::B_SLOT, b1 = fb[2 * RS + 1] + RSLOT * G::B_SLOT;
+    m32_i32x8 bv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bv[j] = m32_cat8(f.blo[j], f.bhi[j]);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const m32_i32x8 av = m32_cat8(f.alo[i], f.ahi[i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        // weights (e4m3) as src A, pixels (e4m3 / e5m2) as src B: pixel-major accumulator
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bv[j], av, acc[i][j], 0, F8 - 1, 0, ew, 0, sa);
+        const int p = i * TN + j;
+        if (NQ > 0 && refill) {
+#pragma unroll
+          for (int q = (p * NQ) / P; q < ((p + 1) * NQ) / P; ++q) {
+            __builtin_amdgcn_sched_barrier(0);
+            fire(slot_c, Q0 + q);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+      if (rd) {
+        __builtin_amdgcn_sched_barrier(0);
+        // ds offsets: row block i is 32 rows = 4 KB further (same XOR key)
+        if (i == 0) { f.alo[0] = ds_rd128<0>(a0); f.ahi[0] = ds_rd128<0>(a1); }
+        if (i == 1) { f.alo[1] = ds_rd128<4096>(a0); f.ahi[1] = ds_rd128<4096>(a1); }
+        if (i == 2) { f.alo[2] = ds_rd128<8192>(a0); f.ahi[2] = ds_rd128<8192>(a1); }
+        if (i == 3) { f.alo[3] = ds_rd128<12288>(a0); f.ahi[3] = ds_rd128<12288>(a1); }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (rd) {
+      f.blo[0] = ds_rd128<0>(b0);
+      f.bhi[0] = ds_rd128<0>(b1);
+      f.blo[1] = ds_rd128<4096>(b0);
+      f.bhi[1] = ds_rd128<4096>(b1);
+    }
+  };
 
   F fr[3];
   // ---- prologue: tiles 0 .. STAGES-1 in flight, tile 0 landed, its steps 0 / 1 being read
@@ -405,8 +534,13 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
   }
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
-  read_step(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, fr[0]);
-  read_step(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, fr[1]);
+  F8Frag p8;
+  if constexpr (F8 != 0) {
+    read_f8(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, p8);
+  } else {
+    read_step(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, fr[0]);
+    read_step(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, fr[1]);
+  }
   M32_STAMP(1, __builtin_amdgcn_s_memtime());
 
   // ---- one 64-deep K tile; T = kt mod 6 (ring index R = T % 3, LDS slot T % STAGES)
@@ -454,20 +588,60 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
     mma_step(fr[R], std::integral_constant<int, QB>{}, std::integral_constant<int, QA>{}, SC{}, refill);
     __builtin_amdgcn_sched_barrier(0);
   };
-  for (int kt = 0;;) {
-    tile(std::integral_constant<int, 0>{}, kt);
-    if (++kt >= kt1) break;
-    tile(std::integral_constant<int, 1>{}, kt);
-    if (++kt >= kt1) break;
-    tile(std::integral_constant<int, 2>{}, kt);
-    if (++kt >= kt1) break;
-    tile(std::integral_constant<int, 3>{}, kt);
-    if (++kt >= kt1) break;
-    tile(std::integral_constant<int, 4>{}, kt);
-    if (++kt >= kt1) break;
-    tile(std::integral_constant<int, 5>{}, kt);
-    if (++kt >= kt1) break;
-  }
+  // ---- fp8: one 128-deep K tile = two k64 steps on ONE operand register set p8 (entry: p8
+  // holds step 0's reads, in flight); each step's MFMAs stream the next step's reads into p8.
+  // Same barrier / refill structure as the bf16 tile: the slot's last reads are retired before
+  // the barrier, the refill glds run behind the second step's MFMAs.
+  auto tile_f8 = [&](auto t_c, int kt) __attribute__((always_inline)) {
+    constexpr int T = decltype(t_c)::value;
+    constexpr int SLOT = T % STAGES, NSLOT = (T + 1) % STAGES;
+    using SC = std::integral_constant<int, SLOT>;
+    using NC = std::integral_constant<int, NSLOT>;
+    const bool refill = kt + STAGES < kt1;
+    const int sa = sa_slot[SLOT];
+    wait_f8(std::integral_constant<int, 0>{}, p8);
+    __builtin_amdgcn_sched_barrier(0);
+    mma_f8(p8, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, SC{}, false, sa, SC{},
+           std::integral_constant<int, 1>{}, true);
+    __builtin_amdgcn_sched_barrier(0);
+    // sync: all my reads of this slot retired, my share of tile kt + 1 landed
+    wait_f8(std::integral_constant<int, 0>{}, p8);
+    if constexpr (STAGES == 3) {
+      if (kt + 2 < kt1) m32_vmcnt<LOADS>();
+      else m32_vmcnt<0>();
+    } else {
+      m32_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (refill) {
+      prep(kt + STAGES);
+      sa_slot[SLOT] = a_first ? ex1 : ex2;
+    }
+    // (the last tile reads the next slot anyway: unconditional reads keep one dataflow for p8; the
+    // values are never used)
+    mma_f8(p8, std::integral_constant<int, LOADS>{}, std::integral_constant<int, 0>{}, SC{}, refill, sa, NC{},
+           std::integral_constant<int, 0>{}, true);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto run = [&](auto body) __attribute__((always_inline)) {
+    for (int kt = 0;;) {
+      body(std::integral_constant<int, 0>{}, kt);
+      if (++kt >= kt1) break;
+      body(std::integral_constant<int, 1>{}, kt);
+      if (++kt >= kt1) break;
+      body(std::integral_constant<int, 2>{}, kt);
+      if (++kt >= kt1) break;
+      body(std::integral_constant<int, 3>{}, kt);
+      if (++kt >= kt1) break;
+      body(std::integral_constant<int, 4>{}, kt);
+      if (++kt >= kt1) break;
+      body(std::integral_constant<int, 5>{}, kt);
+      if (++kt >= kt1) break;
+    }
+  };
+  if constexpr (F8 != 0) run(tile_f8);
+  else run(tile);
   __syncthreads();  // every wave done with the ring before the epilogue reuses the LDS
   M32_STAMP(2, __builtin_amdgcn_s_memtime());
 
@@ -484,11 +658,11 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
 #endif
 }
 
-template <int BN, int MODE, bool RELU, bool EXT>
+template <int BN, int MODE, bool RELU, bool EXT, int F8 = 0>
 static int launch_m32(const ConvFwdArgs& a, hipStream_t st) {
   using G = M32Geom<BN>;
   static std::atomic<uint64_t> attr_mask{0};
-  smem_attr_once(reinterpret_cast<const void*>(&conv_fwd_m32_kernel<BN, MODE, RELU, EXT>), G::SMEM, attr_mask);
+  smem_attr_once(reinterpret_cast<const void*>(&conv_fwd_m32_kernel<BN, MODE, RELU, EXT, F8>), G::SMEM, attr_mask);
   const int classes = MODE == 0 ? 1 : a.stride * a.stride;
   long mmax = 0;
   for (int c = 0; c < classes; ++c) {
@@ -504,8 +678,26 @@ static int launch_m32(const ConvFwdArgs& a, hipStream_t st) {
   const long mtiles = (mmax + G::BM - 1) / G::BM;
   const long ntiles = (a.Cout + BN - 1) / BN;
   dim3 grid((unsigned)(mtiles * ntiles * classes), 1, 1);
-  hipLaunchKernelGGL((conv_fwd_m32_kernel<BN, MODE, RELU, EXT>), grid, dim3(G::NT), G::SMEM, st, a);
+  hipLaunchKernelGGL((conv_fwd_m32_kernel<BN, MODE, RELU, EXT, F8>), grid, dim3(G::NT), G::SMEM, st, a);
   return (int)hipGetLastError();
+}
+
+// fp8 runs the 256 x 128 tile only (Cout 65..128): its 128-deep K tiles give it 175 FLOP per
+// staged byte (the bf16 256 x 256 tile: 128), and a 256-wide fp8 m32 tile spills (the
+// 8-register operands of 32x32x64 need ~24 registers per step more than two bf16 k16 steps)
+template <int MODE>
+static int dispatch_m32_f8(const ConvFwdArgs& a, hipStream_t st) {
+  if (a.fp8 == 1) {   // e4m3 activations: plain epilogue, optional input ReLU
+    if (a.nb_ws || a.act_bwd || a.res1) return -2;
+    return a.act_in == ACT_RELU ? launch_m32<128, MODE, true, false, 1>(a, st)
+                                : launch_m32<128, MODE, false, false, 1>(a, st);
+  }
+  if (a.fp8 == 2) {   // e5m2 gradients: no input activation; the EXT epilogue for gated dgrads
+    if (a.act_in != ACT_NONE) return -2;
+    if (a.nb_ws || ((a.act_bwd || a.res1) && !a.epi_serial)) return launch_m32<128, MODE, false, true, 2>(a, st);
+    return launch_m32<128, MODE, false, false, 2>(a, st);
+  }
+  return -2;
 }
 
 template <int BN, int MODE>
@@ -541,9 +733,19 @@ extern "C" int p2p_m32_stamps(void* host_out, int nblocks) {
 // variant 5 -> 256 x 256 tile (Cout > 128), 4 -> 256 x 128 (Cout > 64); -2 = not covered
 extern "C" int p2p_conv_fwd_m32(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t st) {
   using namespace p2p;
-  if (a->fp8 != 0 || a->splits > 1 || a->d2s) return -2;
-  if (a->C1 % 64 || a->C2 % 64 || a->C1 > 1024 || a->C2 > 1024) return -2;
+  if (a->splits > 1 || a->d2s) return -2;
+  // FASTK: every 128-B K tile inside one tap and one source (64 bf16 / 128 fp8 channels)
+  const int chc = a->fp8 ? 128 : 64;
+  if (a->C1 % chc || a->C2 % chc || a->C1 > 1024 || a->C2 > 1024) return -2;
+  if (a->fp8 && (!a->qs_x1 || !a->qs_w || (a->C2 && !a->qs_x2) || a->fp8 > 2)) return -2;
   if (a->act_in != ACT_NONE && a->act_in != ACT_RELU) return -2;
+  if (a->fp8) {
+    // Cout 65..128 only: there the 256 x 128 fp8 tile beats the 16x16x128 glds tile by 3-10 %
+    // per layer; for Cout > 128 the glds 256 x 256 fp8 tile (A staged once for 256 columns)
+    // is 10-20 % faster than two 128-wide m32 column tiles (profiles/kernel_experiments_r6.md)
+    if ((variant != 4 && variant != 5) || a->Cout <= 64 || a->Cout > 128) return -2;
+    return mode == 0 ? dispatch_m32_f8<0>(*a, st) : dispatch_m32_f8<1>(*a, st);
+  }
   // (the ReLU 256-wide variants spill a few loop-invariant epilogue values before the K loop; the loop itself is spill-free)
   if (variant == 5 && a->Cout > 128)
     return mode == 0 ? dispatch_m32_epi<256, 0>(*a, st) : dispatch_m32_epi<256, 1>(*a, st);

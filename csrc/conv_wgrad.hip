@@ -977,11 +977,12 @@ static int wgrad_glds_shape(const p2p::ConvWgradArgs* a) {
 
 extern "C" int p2p_m32_enabled();
 extern "C" int p2p_conv_wgrad_m32_ok(const p2p::ConvWgradArgs* a);
+extern "C" int p2p_conv_wgrad_m32_br(int R);
 extern "C" int p2p_conv_wgrad_m32(const p2p::ConvWgradArgs* a, hipStream_t st);
 
 extern "C" int p2p_conv_wgrad_tile(const p2p::ConvWgradArgs* a, int* tr, int* tq) {
-  if (p2p_m32_enabled() && p2p_conv_wgrad_m32_ok(a)) {   // conv_wgrad_m32.hip: 256 x 256
-    *tr = 256;
+  if (p2p_m32_enabled() && p2p_conv_wgrad_m32_ok(a)) {   // conv_wgrad_m32.hip: 256 / 128 x 256
+    *tr = p2p_conv_wgrad_m32_br(a->R);
     *tq = 256;
     return 6;
   }

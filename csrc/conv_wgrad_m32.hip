@@ -69,17 +69,22 @@ __device__ __forceinline__ u32x4 tr_frag32(uint32_t addr) {
   return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
 }
 
+template <int TM>
 struct WFrag {
-  u32x4 a[4];   // P^T fragments (R rows)
+  u32x4 a[TM];  // P^T fragments (R rows)
   u32x4 b[2];   // Q fragments (Kq columns)
 };
 
-template <int N>
-__device__ __forceinline__ void wfrag_wait(WFrag& f) {
+template <int N, int TM>
+__device__ __forceinline__ void wfrag_wait(WFrag<TM>& f) {
   static_assert(N >= 0 && N <= 15, "lgkmcnt range");
-  asm volatile("s_waitcnt lgkmcnt(%6)"
-               : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.a[2]), "+v"(f.a[3]), "+v"(f.b[0]), "+v"(f.b[1])
-               : "n"(N));
+  if constexpr (TM == 4) {
+    asm volatile("s_waitcnt lgkmcnt(%6)"
+                 : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.a[2]), "+v"(f.a[3]), "+v"(f.b[0]), "+v"(f.b[1])
+                 : "n"(N));
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.b[0]), "+v"(f.b[1]) : "n"(N));
+  }
 }
 
 // physical 16-B chunk of logical chunk c in row r of a [64][128] sub-tile
@@ -87,12 +92,17 @@ __device__ __forceinline__ int wm32_chunk(int r, int c) { return c ^ (4 * (r & 3
 
 }  // namespace
 
-// RM: bit 0 = ReLU on the P fragments, bit 1 = ReLU on the Q fragments
-template <int RM>
+// RM: bit 0 = ReLU on the P fragments, bit 1 = ReLU on the Q fragments.
+// BR: R edge of the tile -- 256 (8 waves of 128 x 64) or 128 (round 6, VERDICT r5 item 5: the
+// R = 128 weight gradients -- family R's residual 3x3s, the U-Net e2 / PatchGAN c2 -- ran on the
+// 16x16 glds tile at 19-31 % MFMA busy): 8 waves of 64 x 64, one P sub-tile per stage (the LDS
+// stage keeps the 64 KB layout, its second P sub-tile unused, so the slot toggle stays bit 16).
+template <int RM, int BR = 256>
 __global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
-  constexpr int TM = 4, TN = 2, WN = 4;
+  static_assert(BR == 256 || BR == 128, "tile R edge");
+  constexpr int TM = BR == 256 ? 4 : 2, TN = 2, WN = 4;
   constexpr int NR = 2 * (TM + TN);    // transposed reads per k16 step
-  constexpr int PL = 4, QL = 4, LOADS = PL + QL;
+  constexpr int PL = BR == 256 ? 4 : 2, QL = 4, LOADS = PL + QL;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -101,7 +111,7 @@ __global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
   const int qtiles = (a.Kq + WM32_TB - 1) / WM32_TB;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int rt = bid / qtiles, qt = bid % qtiles;
-  const int r0 = rt * WM32_TB, q0 = qt * WM32_TB;
+  const int r0 = rt * BR, q0 = qt * WM32_TB;
 
   const int stages = (a.M + WM32_SROWS - 1) / WM32_SROWS;
   const int sps = (stages + a.splits - 1) / a.splits;
@@ -120,11 +130,12 @@ __global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
   const int lch = wm32_chunk(rowi0, pch);        // logical chunk this lane fetches
   const long pm0 = (long)s0 * WM32_SROWS;         // first pixel of this split
   // P: [M][ld] per concat half; sub s covers columns r0 + 128 s + [0, 128)
-  __amdgpu_buffer_rsrc_t rp[2];
-  uint32_t p_vo[2];
-  int p_ld2[2];   // row stride in bytes
+  constexpr int PS = BR / 128;   // P sub-tiles per stage
+  __amdgpu_buffer_rsrc_t rp[PS];
+  uint32_t p_vo[PS];
+  int p_ld2[PS];   // row stride in bytes
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < PS; ++s) {
     const int cb = r0 + 128 * s;                  // sub-tile's first column (uniform)
     const bool first = cb < a.R1;
     const int ld = first ? a.R1 : a.R2;
@@ -175,14 +186,16 @@ __global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
   const int d_n = WM32_SROWS / OHW, d_rem = WM32_SROWS % OHW;
   const int d_h = d_rem / a.OW, d_w = d_rem % a.OW;
   uint32_t q_vo[2][2];       // [rr][s]: this stage's gather offsets
-  int p_soff[2] = {0, 0};    // stage displacement of the P rows (uniform)
+  int p_soff[PS];            // stage displacement of the P rows (uniform)
+#pragma unroll
+  for (int s = 0; s < PS; ++s) p_soff[s] = 0;
 
   // advance the pixel rows to stage st (called for consecutive stages from s0) and form the
   // gather offsets of its Q loads; the P rows only move their uniform soffset
   auto prep = [&](int st) __attribute__((always_inline)) {
     const int ds = st - s0;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) p_soff[s] = ds * WM32_SROWS * p_ld2[s];
+    for (int s = 0; s < PS; ++s) p_soff[s] = ds * WM32_SROWS * p_ld2[s];
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
       if (ds != 0) {
@@ -214,13 +227,17 @@ __global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
       }
     }
   };
-  // load q of the prepared stage into slot SLOT: q 0..3 = P (row sel q >> 1, sub q & 1),
-  // q 4..7 = Q; the wave's 1 KB lands at rows 4 (wid + 8 rr) of the sub-tile
+  // load q of the prepared stage into slot SLOT: q < PL = P (BR 256: row sel q >> 1, sub q & 1;
+  // BR 128: row sel q, sub 0), then Q (row sel (q - PL) >> 1, sub (q - PL) & 1); the wave's
+  // 1 KB lands at rows 4 (wid + 8 rr) of the sub-tile
   auto fire = [&](int slot, auto q_c) __attribute__((always_inline)) {
     constexpr int Q = decltype(q_c)::value;
-    constexpr int RR = (Q & 3) >> 1, S = Q & 1;
-    char* dst = smem + slot * WM32_STAGE + (Q < 4 ? 0 : 2 * WM32_SUB) + S * WM32_SUB + (4 * (wid + 8 * RR)) * 256;
-    if constexpr (Q < 4) {
+    constexpr bool ISP = Q < PL;
+    constexpr int QQ = ISP ? Q : Q - PL;
+    constexpr int RR = ISP ? (PS == 2 ? QQ >> 1 : QQ) : QQ >> 1;
+    constexpr int S = ISP ? (PS == 2 ? QQ & 1 : 0) : QQ & 1;
+    char* dst = smem + slot * WM32_STAGE + (ISP ? 0 : 2 * WM32_SUB) + S * WM32_SUB + (4 * (wid + 8 * RR)) * 256;
+    if constexpr (ISP) {
       wm32_bld(rp[S], dst, p_vo[S] + RR * 32 * p_ld2[S], __builtin_amdgcn_readfirstlane(p_soff[S]));
     } else {
       wm32_bld(rq[S], dst, q_vo[RR][S], 0);
@@ -236,9 +253,10 @@ __global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
     const int krow = 8 * (G >> 1) + qq;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int col = i * 32 + 16 * (G & 1) + 4 * p;   // within P sub-tile wm
+      // BR 256: within P sub-tile wm; BR 128: columns 64 wm + 32 i of the one P sub-tile
+      const int col = (BR == 256 ? 0 : 64 * wm) + i * 32 + 16 * (G & 1) + 4 * p;
       const int ch = wm32_chunk(krow, col >> 3);
-      fa[i] = wm32_lds(smem + wm * WM32_SUB + krow * 256 + ch * 16 + (col & 7) * 2);
+      fa[i] = wm32_lds(smem + (BR == 256 ? wm : 0) * WM32_SUB + krow * 256 + ch * 16 + (col & 7) * 2);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -251,7 +269,7 @@ __global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
   // the P fragment address above is relative to sub-tile wm: wave row wm reads P columns
   // r0 + 128 wm + [0, 128), i.e. exactly sub-tile wm (its 4 fragments are 32 columns apart)
   // fa / fb address the CURRENT slot: toggled (bit 16 = the 64 KB slot offset) per stage
-  auto read_step = [&](auto s_c, WFrag& f) __attribute__((always_inline)) {
+  auto read_step = [&](auto s_c, WFrag<TM>& f) __attribute__((always_inline)) {
     constexpr int S = decltype(s_c)::value;
     constexpr int OFF = S * 16 * 256;   // k16 step: 16 rows further
 #pragma unroll
@@ -275,9 +293,9 @@ __global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // one k16 step; with `refill` one load of the next-next stage after each of the first
-  // LOADS MFMAs (TM * TN = 8 = LOADS)
-  // fire with a loop-index q (0..7): dispatched to the compile-time loads
+  // one k16 step; with `refill` the LOADS loads of the next-next stage spread over its
+  // TM * TN MFMAs (BR 256: one after each of the 8; BR 128: 6 over 4)
+  // fire with a loop-index q (0 .. LOADS - 1): dispatched to the compile-time loads
   auto fire_at = [&](int slot, int q) __attribute__((always_inline)) {
     switch (q) {
       case 0: fire(slot, std::integral_constant<int, 0>{}); break;
@@ -286,11 +304,11 @@ __global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
       case 3: fire(slot, std::integral_constant<int, 3>{}); break;
       case 4: fire(slot, std::integral_constant<int, 4>{}); break;
       case 5: fire(slot, std::integral_constant<int, 5>{}); break;
-      case 6: fire(slot, std::integral_constant<int, 6>{}); break;
-      default: fire(slot, std::integral_constant<int, 7>{}); break;
+      case 6: if constexpr (LOADS > 6) fire(slot, std::integral_constant<int, 6>{}); break;
+      default: if constexpr (LOADS > 7) fire(slot, std::integral_constant<int, 7>{}); break;
     }
   };
-  auto mma_step = [&](WFrag& f, int slot, bool refill) __attribute__((always_inline)) {
+  auto mma_step = [&](WFrag<TM>& f, int slot, bool refill) __attribute__((always_inline)) {
     if constexpr (RM & 1) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) f.a[i] = relu8(f.a[i]);
@@ -306,15 +324,20 @@ __global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f.a[i]),
                                                              __builtin_bit_cast(bf16x8, f.b[j]), acc[i][j], 0, 0, 0);
         if (refill) {
-          __builtin_amdgcn_sched_barrier(0);
-          fire_at(slot, i * TN + j);
-          __builtin_amdgcn_sched_barrier(0);
+          constexpr int P = TM * TN;
+          const int pi = i * TN + j;
+#pragma unroll
+          for (int q = (pi * LOADS) / P; q < ((pi + 1) * LOADS) / P; ++q) {
+            __builtin_amdgcn_sched_barrier(0);
+            fire_at(slot, q);
+            __builtin_amdgcn_sched_barrier(0);
+          }
         }
       }
     }
   };
 
-  WFrag fr[2];
+  WFrag<TM> fr[2];
   if (s0 < s1) {
     // ---- prologue: stages s0, s0 + 1 in flight, s0 landed, its first step being read
     prep(s0);
@@ -380,7 +403,7 @@ __global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = q0 + wn * 64 + j * 32 + (lane & 31);
-      const int rowb = r0 + wm * 128 + i * 32 + 4 * h;
+      const int rowb = r0 + wm * (BR / 2) + i * 32 + 4 * h;
       if (col < a.Kq) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -391,22 +414,31 @@ __global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
     }
 }
 
-template <int RM>
+template <int RM, int BR>
 static int launch_wm32(const ConvWgradArgs& a, hipStream_t st) {
   static std::atomic<uint64_t> attr_mask{0};
-  smem_attr_once(reinterpret_cast<const void*>(&conv_wgrad_m32_kernel<RM>), WM32_SMEM, attr_mask);
-  dim3 grid(((a.R + WM32_TB - 1) / WM32_TB) * ((a.Kq + WM32_TB - 1) / WM32_TB), a.splits, 1);
-  hipLaunchKernelGGL((conv_wgrad_m32_kernel<RM>), grid, dim3(WM32_NT), WM32_SMEM, st, a);
+  smem_attr_once(reinterpret_cast<const void*>(&conv_wgrad_m32_kernel<RM, BR>), WM32_SMEM, attr_mask);
+  dim3 grid(((a.R + BR - 1) / BR) * ((a.Kq + WM32_TB - 1) / WM32_TB), a.splits, 1);
+  hipLaunchKernelGGL((conv_wgrad_m32_kernel<RM, BR>), grid, dim3(WM32_NT), WM32_SMEM, st, a);
   return (int)hipGetLastError();
+}
+
+// the tile's R edge: 256, or 128 for R = 128 (P2P_WM32_R128=0 -- read per call, the tests A/B
+// it -- keeps R = 128 on the 16x16 glds tile)
+extern "C" int p2p_conv_wgrad_m32_br(int R) {
+  if (R >= 256) return 256;
+  const char* v = std::getenv("P2P_WM32_R128");
+  return (R == 128 && !(v && v[0] == '0')) ? 128 : 0;
 }
 
 }  // namespace p2p
 
-// the 256x256 32x32x16 weight-gradient tile (Kq % 128 == 0, R % 128 == 0 with R >= 256 or
-// Kq >= 256; ReLU-only operand activations); -2 = not covered
+// the 256x256 / 128x256 32x32x16 weight-gradient tiles (Kq % 128 == 0, Kq >= 256, R % 128 ==
+// 0 with R >= 256 or R == 128; ReLU-only operand activations); -2 = not covered
+extern "C" int p2p_conv_wgrad_m32_br(int R);
 extern "C" int p2p_conv_wgrad_m32_ok(const p2p::ConvWgradArgs* a) {
   using namespace p2p;
-  if (a->f8 || a->Kq % 128 || a->R % 128 || a->R < 256 || a->Kq < 256) return 0;
+  if (a->f8 || a->Kq % 128 || a->R % 128 || p2p_conv_wgrad_m32_br(a->R) == 0 || a->Kq < 256) return 0;
   if ((a->p_act != ACT_NONE && a->p_act != ACT_RELU) || (a->q_act != ACT_NONE && a->q_act != ACT_RELU)) return 0;
   // buffer resources are per 128-column sub-tile: each must lie inside one concat half
   if ((a->R2 > 0 && a->R1 % 128) || (a->C2 > 0 && (a->C1 % 128 || a->C % 128))) return 0;
@@ -427,10 +459,18 @@ extern "C" int p2p_conv_wgrad_m32(const p2p::ConvWgradArgs* a, hipStream_t st) {
   using namespace p2p;
   if (!p2p_conv_wgrad_m32_ok(a)) return -2;
   const int rm = (a->p_act == ACT_RELU ? 1 : 0) | (a->q_act == ACT_RELU ? 2 : 0);
+  if (p2p_conv_wgrad_m32_br(a->R) == 128) {
+    switch (rm) {
+      case 1: return launch_wm32<1, 128>(*a, st);
+      case 2: return launch_wm32<2, 128>(*a, st);
+      case 3: return launch_wm32<3, 128>(*a, st);
+      default: return launch_wm32<0, 128>(*a, st);
+    }
+  }
   switch (rm) {
-    case 1: return launch_wm32<1>(*a, st);
-    case 2: return launch_wm32<2>(*a, st);
-    case 3: return launch_wm32<3>(*a, st);
-    default: return launch_wm32<0>(*a, st);
+    case 1: return launch_wm32<1, 256>(*a, st);
+    case 2: return launch_wm32<2, 256>(*a, st);
+    case 3: return launch_wm32<3, 256>(*a, st);
+    default: return launch_wm32<0, 256>(*a, st);
   }
 }

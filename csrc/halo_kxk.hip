@@ -47,6 +47,18 @@ __device__ __forceinline__ bf16x8 lds_frag(const bf16* base_unit, bool swap) {
   return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
+// the same from a 32-bit LDS byte address (an opaque register: see the slice loop)
+typedef __attribute__((address_space(3))) const bf16x4 lds_bf16x4;
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)p));
+}
+__device__ __forceinline__ bf16x8 lds_frag_at(uint32_t addr, bool swap) {
+  const lds_bf16x4* p = (const lds_bf16x4*)(uintptr_t)addr;
+  const bf16x4 a = p[swap ? 1 : 0];
+  const bf16x4 b = p[swap ? 0 : 1];
+  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
 }  // namespace
 
 template <int KS, int CIN>
@@ -180,13 +192,27 @@ __global__ void __launch_bounds__(256) halo_kxk_kernel(HaloKArgs a) {
     for (int s = 0; s < G::S; ++s) {
       const int to = CIN > 32 || s * G::TPS + tsub < G::KK ? toff : 0;   // padding tap: zero weights
       const int csub = csub0 + sub * 4;
+      // every fragment's address goes through its own opaque register: left visible, hipcc
+      // pairs reads 512 B apart into ds_read2st64_b64, whose 16-lane / 32-bank service breaks
+      // the 64-bank conflict-free layout above (6-7 conflict cycles per LDS instruction in the
+      // round-5 family-R roofline); as separate ds_read_b64 they are conflict-free
       bf16x8 bfr[NBLK];
 #pragma unroll
-      for (int nb = 0; nb < NBLK; ++nb) bfr[nb] = lds_frag(bp + nb * 16 * 4 * 8, hswap);
+      for (int nb = 0; nb < NBLK; ++nb) {
+        uint32_t bq = lds_u32(bp + nb * 16 * 4 * 8);
+#ifndef P2P_HALO_NOLAUNDER   // (diagnostic build: the round-5 paired reads, for the A/B)
+        asm volatile("" : "+v"(bq));
+#endif
+        bfr[nb] = lds_frag_at(bq, hswap);
+      }
       const bf16* a0 = A + G::aslot(rowbase + to, csub) * 8;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const bf16x8 af = lds_frag(a0 + i * ISTRIDE, hswap);
+        uint32_t aq = lds_u32(a0 + i * ISTRIDE);
+#ifndef P2P_HALO_NOLAUNDER
+        asm volatile("" : "+v"(aq));
+#endif
+        const bf16x8 af = lds_frag_at(aq, hswap);
 #pragma unroll
         for (int nb = 0; nb < NBLK; ++nb)
           acc[i][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[nb], acc[i][nb], 0, 0, 0);

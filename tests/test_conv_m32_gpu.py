@@ -65,6 +65,10 @@ CASES = [
     ("wgrad_convT_concat", "g5", "convT", 16, 256, 256, 32, 256, 4, 2, 1, "zeros", None, None),
     ("wgrad_reflect3x3_r256", "g5", "conv", 32, 256, 0, 48, 256, 3, 1, 1, "reflect", None, None),
     ("wgrad_conv_relu_r256", "g5", "conv", 64, 256, 0, 64, 256, 4, 2, 1, "zeros", "relu", None),
+    # the 128 x 256 weight-gradient tile (R = 128, round 6): family R's residual 3x3 and the
+    # U-Net e2 / PatchGAN c2 shape (64 -> 128, 4x4 s2)
+    ("wgrad_reflect3x3_r128", "g5", "conv", 32, 128, 0, 64, 128, 3, 1, 1, "reflect", None, None),
+    ("wgrad_conv_s2_r128_c64", "g4", "conv", 32, 64, 0, 128, 128, 4, 2, 1, "zeros", None, None),
 ]
 WGRAD_M32 = {c[0] for c in CASES if c[0].startswith("wgrad_")}
 
@@ -132,7 +136,7 @@ def test_m32_conv_matches_fp32_oracle(case):
     assert rel_err(gb, rb.grad) < 3e-2, (name, "db")
 
 
-AB_CASES = CASES[:3] + [c for c in CASES if c[0] in WGRAD_M32][:2]
+AB_CASES = CASES[:3] + [c for c in CASES if c[0] in WGRAD_M32][:2] + [c for c in CASES if c[0].endswith("_r128")][:1]
 
 
 @pytest.mark.parametrize("case", AB_CASES, ids=[c[0] for c in AB_CASES])

@@ -110,6 +110,15 @@ FP8_CASES = [
     ("s2t_convT_concat_relu", 4, 128, 128, 64, 64, 4, 2, 1, "relu", True),
     ("s2t_convT_c128_cout128", 4, 128, 0, 64, 128, 4, 2, 1, None, True),
     ("s2t_dgrad_c64_cout128", 4, 64, 0, 128, 128, 4, 2, 1, None, False),
+    # >= 256 output tiles and 128-channel multiples: the 32x32x64 f8f6f4 tiles (conv_fwd_m32.hip
+    # F8 = 1 forward / 2 input gradient, round 6) -- conv (MODE 0 fwd, MODE 1 dgrad), ConvT on a
+    # virtual concat with input ReLU (MODE 1 fwd, MODE 0 dgrad), and a Cout that is not a tile
+    # multiple
+    # (Cout 65..128: the fp8 m32 route; wider layers stay on the glds 256 x 256 fp8 tile)
+    ("m32_enc_c128", 64, 128, 0, 64, 128, 4, 2, 1, None, False),
+    ("m32_convT_concat_relu", 64, 128, 128, 32, 128, 4, 2, 1, "relu", True),
+    ("m32_enc_c256_cout96", 64, 256, 0, 64, 96, 4, 2, 1, None, False),
+    ("m32_convT_c128", 64, 128, 0, 32, 128, 4, 2, 1, None, True),
 ]
 
 
@@ -138,6 +147,14 @@ def test_fp8_conv_fwd_dgrad_match_dequantised_oracle(case):
         gy = rand_img(*y.shape, scale=1e-3, seed=3)     # gradient-sized values: e5m2 + scaling
         y.backward(gy)
         torch.cuda.synchronize()
+    if name.startswith("m32_"):
+        names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
+        # e4m3 forward and e5m2 input gradient on the 32x32x64 tiles where the route takes them:
+        # 128-channel multiples in, 65..128 channels out (the input gradient reads dY = Cout
+        # channels and writes Cin)
+        dgrad_m32 = Cout % 128 == 0 and 64 < Cin <= 128
+        for f in ((1, 2) if dgrad_m32 else (1,)):
+            assert any("conv_fwd_m32_kernel<128" in k and f", {f}>(" in k for k in names), (f, sorted(set(names)))
     if name.startswith("s2t_"):
         names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
         want = "conv_s2t_kernel<64, true, false, 1>" if act_in == "relu" else (
