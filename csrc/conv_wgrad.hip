@@ -26,6 +26,21 @@
 
 namespace p2p {
 
+// (split, tile) of a flattened tiles x splits grid.  xcd = 1 (default, P2P_WGRAD_XCD): blocks
+// dealt to the XCDs in contiguous (split, tile) ranges, so the column tiles of one pixel range
+// -- all streaming the same P rows and overlapping Q rows -- share an XCD's L2; xcd = 0: the
+// round-5 split-major order (remap inside a split only).  conv_wgrad_m32.hip does the same.
+__device__ __forceinline__ void wg_split_tile(int xcd, int tiles, int& split, int& bid) {
+  if (xcd) {
+    const int T = xcd_remap(blockIdx.x, gridDim.x);
+    split = T / tiles;
+    bid = T - split * tiles;
+  } else {
+    split = blockIdx.x / tiles;
+    bid = xcd_remap(blockIdx.x - split * tiles, tiles);
+  }
+}
+
 constexpr int WBQ = 128;   // tile cols (Kq)
 constexpr int WBM = 64;    // reduction rows per stage
 constexpr int WROW = 128;  // elements per LDS row
@@ -337,7 +352,7 @@ __device__ __forceinline__ void wg_wait_vmcnt() {
 // RM: bit 0 = ReLU on the P fragments, bit 1 = ReLU on the Q fragments (compile-time, so
 // the fragment reads stay branch-free and can be batched ahead of the MFMAs).
 template <int TBR, int TBQ, int WM, int WN, int STAGES, int RM>
-__global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgradArgs a) {
+__global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgradArgs a, int xcd) {
   constexpr int NT = WM * WN * 64;
   constexpr int TM = TBR / WM / 16, TN = TBQ / WN / 16;
   constexpr int PW = TBR >= 128 ? 128 : TBR;          // P sub-tile width (elements)
@@ -357,13 +372,14 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int qtiles = (a.Kq + TBQ - 1) / TBQ;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  int split, bid;
+  wg_split_tile(xcd, ((a.R + TBR - 1) / TBR) * qtiles, split, bid);
   const int rt = bid / qtiles, qt = bid % qtiles;
   const int r0 = rt * TBR, q0 = qt * TBQ;
 
   const int stages = (a.M + WBM - 1) / WBM;
   const int sps = (stages + a.splits - 1) / a.splits;
-  const int s0 = blockIdx.y * sps;
+  const int s0 = split * sps;
   const int s1 = min(stages, s0 + sps);
 
   const bf16* __restrict__ p1 = static_cast<const bf16*>(a.p1);
@@ -571,7 +587,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_glds_kernel(ConvWgrad
     stage = stage + 1 == STAGES ? 0 : stage + 1;
   }
 
-  float* slab = a.ws + (long)blockIdx.y * a.R * a.Kq;
+  float* slab = a.ws + (long)split * a.R * a.Kq;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -632,7 +648,7 @@ __device__ __forceinline__ i32x8w relu_f8x32(i32x8w v) {
 // RM: bit 0 = ReLU on the P fragments, bit 1 = on the Q fragments (fp8 sign bits);
 // PF / QF: the MFMA operand formats of P / Q (0 = e4m3, 1 = e5m2)
 template <int TBR, int TBQ, int WM, int WN, int STAGES, int RM, int PF, int QF>
-__global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_f8_kernel(ConvWgradArgs a) {
+__global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_f8_kernel(ConvWgradArgs a, int xcd) {
   constexpr int NT = WM * WN * 64;
   constexpr int TM = TBR / WM / 16, TN = TBQ / WN / 16;
   constexpr int SROWS = 128;                          // pixels per stage (one K step)
@@ -649,13 +665,14 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_f8_kernel(ConvWgradAr
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int qtiles = (a.Kq + TBQ - 1) / TBQ;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  int split, bid;
+  wg_split_tile(xcd, ((a.R + TBR - 1) / TBR) * qtiles, split, bid);
   const int rt = bid / qtiles, qt = bid % qtiles;
   const int r0 = rt * TBR, q0 = qt * TBQ;
 
   const int stages = (a.M + SROWS - 1) / SROWS;
   const int sps = (stages + a.splits - 1) / a.splits;
-  const int s0 = blockIdx.y * sps;
+  const int s0 = split * sps;
   const int s1 = min(stages, s0 + sps);
 
   const uint8_t* __restrict__ p1 = static_cast<const uint8_t*>(a.p1);
@@ -822,7 +839,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_wgrad_f8_kernel(ConvWgradAr
     stage = stage + 1 == STAGES ? 0 : stage + 1;
   }
 
-  float* slab = a.ws + (long)blockIdx.y * a.R * a.Kq;
+  float* slab = a.ws + (long)split * a.R * a.Kq;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -999,12 +1016,19 @@ extern "C" int p2p_conv_wgrad_tile(const p2p::ConvWgradArgs* a, int* tr, int* tq
 
 extern "C" int p2p_conv_wgrad_tile_rows(int R) { return R <= 16 ? 16 : (R <= 64 ? 64 : 128); }
 
+// P2P_WGRAD_XCD (read per call: A/B in one process): 0 = the round-5 block order
+static int wgrad_xcd() {
+  const char* v = std::getenv("P2P_WGRAD_XCD");
+  return (v && v[0] == '0') ? 0 : 1;
+}
+
 template <int TBR, int TBQ, int WM, int WN, int STG, int RM>
 static int wg_launch(const p2p::ConvWgradArgs& a, dim3 grid, int smem, hipStream_t st) {
   static std::atomic<uint64_t> attr_mask{0};
   p2p::smem_attr_once(reinterpret_cast<const void*>(&p2p::conv_wgrad_glds_kernel<TBR, TBQ, WM, WN, STG, RM>), smem, attr_mask);
-  hipLaunchKernelGGL((p2p::conv_wgrad_glds_kernel<TBR, TBQ, WM, WN, STG, RM>), grid, dim3(WM * WN * 64), smem,
-                     st, a);
+  const dim3 g1(grid.x * grid.y, 1, 1);   // flattened tiles x splits (wg_split_tile)
+  hipLaunchKernelGGL((p2p::conv_wgrad_glds_kernel<TBR, TBQ, WM, WN, STG, RM>), g1, dim3(WM * WN * 64), smem,
+                     st, a, wgrad_xcd());
   return (int)hipGetLastError();
 }
 
@@ -1023,9 +1047,9 @@ static int wg8_launch(const p2p::ConvWgradArgs& a, hipStream_t st) {
   constexpr int smem = STG * (TBR + TBQ) * 128;
   static std::atomic<uint64_t> attr_mask{0};
   p2p::smem_attr_once(reinterpret_cast<const void*>(&p2p::conv_wgrad_f8_kernel<TBR, TBQ, WM, WN, STG, RM, PF, QF>), smem, attr_mask);
-  dim3 grid(((a.R + TBR - 1) / TBR) * ((a.Kq + TBQ - 1) / TBQ), a.splits, 1);
+  dim3 grid(((a.R + TBR - 1) / TBR) * ((a.Kq + TBQ - 1) / TBQ) * a.splits, 1, 1);
   hipLaunchKernelGGL((p2p::conv_wgrad_f8_kernel<TBR, TBQ, WM, WN, STG, RM, PF, QF>), grid, dim3(WM * WN * 64), smem,
-                     st, a);
+                     st, a, wgrad_xcd());
   return (int)hipGetLastError();
 }
 

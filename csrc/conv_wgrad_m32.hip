@@ -97,8 +97,13 @@ __device__ __forceinline__ int wm32_chunk(int r, int c) { return c ^ (4 * (r & 3
 // R = 128 weight gradients -- family R's residual 3x3s, the U-Net e2 / PatchGAN c2 -- ran on the
 // 16x16 glds tile at 19-31 % MFMA busy): 8 waves of 64 x 64, one P sub-tile per stage (the LDS
 // stage keeps the 64 KB layout, its second P sub-tile unused, so the slot toggle stays bit 16).
+// Grid: one dimension of tiles x splits.  xcd = 1 (default): blocks dealt to the XCDs in
+// contiguous (split, tile) ranges (xcd_remap over the whole grid), so the column tiles of one
+// pixel range -- every one of them streams the same P rows and overlapping Q rows -- share an
+// XCD's L2; xcd = 0: the round-5 order (split-major, the remap inside a split only), where a
+// split's 8 column tiles of a deep layer sat on 8 different XCDs and each read P from HBM.
 template <int RM, int BR = 256>
-__global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
+__global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a, int xcd) {
   static_assert(BR == 256 || BR == 128, "tile R edge");
   constexpr int TM = BR == 256 ? 4 : 2, TN = 2, WN = 4;
   constexpr int NR = 2 * (TM + TN);    // transposed reads per k16 step
@@ -109,13 +114,22 @@ __global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int qtiles = (a.Kq + WM32_TB - 1) / WM32_TB;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles = ((a.R + BR - 1) / BR) * qtiles;
+  int split, bid;
+  if (xcd) {
+    const int T = xcd_remap(blockIdx.x, gridDim.x);
+    split = T / tiles;
+    bid = T - split * tiles;
+  } else {
+    split = blockIdx.x / tiles;
+    bid = xcd_remap(blockIdx.x - split * tiles, tiles);
+  }
   const int rt = bid / qtiles, qt = bid % qtiles;
   const int r0 = rt * BR, q0 = qt * WM32_TB;
 
   const int stages = (a.M + WM32_SROWS - 1) / WM32_SROWS;
   const int sps = (stages + a.splits - 1) / a.splits;
-  const int s0 = blockIdx.y * sps;
+  const int s0 = split * sps;
   const int s1 = min(stages, s0 + sps);
 
   // ---- loader: buffer_load ... lds (32-bit offsets from a per-split base, out-of-range
@@ -396,7 +410,7 @@ __global__ void __launch_bounds__(512) conv_wgrad_m32_kernel(ConvWgradArgs a) {
   }
 
   // ---- fp32 partial slab ws[split][R][Kq]: acc[i][j][reg] = D[row (reg&3) + 8 (reg>>2) + 4 h][col l&31]
-  float* slab = a.ws + (long)blockIdx.y * a.R * a.Kq;
+  float* slab = a.ws + (long)split * a.R * a.Kq;
   const int h = lane >> 5;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -418,8 +432,10 @@ template <int RM, int BR>
 static int launch_wm32(const ConvWgradArgs& a, hipStream_t st) {
   static std::atomic<uint64_t> attr_mask{0};
   smem_attr_once(reinterpret_cast<const void*>(&conv_wgrad_m32_kernel<RM, BR>), WM32_SMEM, attr_mask);
-  dim3 grid(((a.R + BR - 1) / BR) * ((a.Kq + WM32_TB - 1) / WM32_TB), a.splits, 1);
-  hipLaunchKernelGGL((conv_wgrad_m32_kernel<RM, BR>), grid, dim3(WM32_NT), WM32_SMEM, st, a);
+  dim3 grid(((a.R + BR - 1) / BR) * ((a.Kq + WM32_TB - 1) / WM32_TB) * a.splits, 1, 1);
+  const char* v = std::getenv("P2P_WGRAD_XCD");   // (read per call: A/B in one process)
+  const int xcd = (v && v[0] == '0') ? 0 : 1;
+  hipLaunchKernelGGL((conv_wgrad_m32_kernel<RM, BR>), grid, dim3(WM32_NT), WM32_SMEM, st, a, xcd);
   return (int)hipGetLastError();
 }
 
