@@ -312,12 +312,6 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   a.ws = nullptr;
   a.splits = 1;
   a.zero = zero_page(x1);
-  {
-    const char* cm = P2P_KNOB_ONCE("P2P_CLASS_MAJOR");
-    a.cls_major = (cm && cm[0] == '1') ? 1 : 0;
-    const char* es = P2P_KNOB_ONCE("P2P_EPI_SERIAL");
-    a.epi_serial = (es && es[0] == '1') ? 1 : 0;
-  }
   a.stats = nullptr;
   a.stats_nchunks = 0;
   a.fp8 = fp8;
@@ -457,12 +451,9 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   Tensor ws;
   if (splits > 1) {
     // per-split fp32 slabs (plain stores, no zero fill) summed in split order by
-    // conv_finalize: deterministic, and no atomics; P2P_SPLITK_ATOMIC=1 restores the
-    // fp32-atomic accumulation into one zero-filled buffer (A/B only)
-    const char* av = P2P_KNOB_ONCE("P2P_SPLITK_ATOMIC");
-    a.det = (av && av[0] == '1') ? 0 : 1;
-    ws = a.det ? at::empty({splits, N * OH * OW, Cout}, obf.options().dtype(at::kFloat))
-               : at::zeros({1, N * OH * OW, Cout}, obf.options().dtype(at::kFloat));
+    // conv_finalize: deterministic, and no atomics
+    a.det = 1;
+    ws = at::empty({splits, N * OH * OW, Cout}, obf.options().dtype(at::kFloat));
     a.ws = ws.data_ptr<float>();
     a.splits = splits;
   }
@@ -490,16 +481,14 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
   // the packed-image halo kernel (below) beats the generic tile with fused partials: keep it
   const bool pk8_halo = mode == 0 && !fp8 && C1 == 8 && C2 == 0 && KH == 4 && KW == 4 && stride == 2 && pad == 1 &&
                         (Cout == 64 || Cout == 128) && std::getenv("P2P_NO_HALO") == nullptr;
-  // affine / PReLU norms and folds: batch norm only, on the implicit-GEMM tiles (the s2t kernel
-  // has its own partial code, non-affine only; the halo kernels none -- keep their routes)
-  const bool nb_ext = nb_gamma || nb_prelu || fold;
+  // affine / PReLU norms: batch norm only, on the implicit-GEMM tiles (the s2t kernel has its
+  // own partial code, non-affine only; the halo kernels none -- keep their routes).  Never with a
+  // pad fold: the fold dgrads' partials (round 5, opt-in) measured slower than the norm's own
+  // pass and were removed in round 6 (profiles/kernel_experiments_r5.md section 12)
+  const bool nb_ext = nb_gamma || nb_prelu;
   const bool nb_halo = KH == 9 || (KH == 3 && C1 == 64 && Cout <= 32);
-  int64_t nb_band = 0;
-  if (fold) {
-    const int64_t bw = fold_edge ? 1 : fold_p;
-    nb_band = (fold_H >= 2 * bw + 2 && fold_W >= 2 * bw + 2 && 256 % (Cout / 8) == 0) ? p2p_fold_band_nb_blocks() : -1;
-  }
-  if ((nb_x || nb_colsum) && nb_half && (glds_ok || s2t_ok) && splits == 1 && fp8 != 1 && !want_stats &&
+  const int64_t nb_band = 0;
+  if ((nb_x || nb_colsum) && nb_half && (glds_ok || s2t_ok) && splits == 1 && fp8 != 1 && !want_stats && !fold &&
       !pk8_halo && (!nb_ext || (nb_batch && !nb_colsum && !s2t_ok && !nb_halo && nb_band >= 0 && nb_half == 1 &&
                                 Csplit == Cout))) {
     const int64_t c0 = nb_half == 1 ? 0 : Csplit;
@@ -540,8 +529,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
       a.nb_beta = nb_gamma ? nb_beta->data_ptr<float>() : nullptr;
       a.nb_prelu = nb_prelu ? nb_prelu->data_ptr<float>() : nullptr;
       a.nb_act = (int)nb_act;
-      a.nb_gate = (nb_gate && !nb_colsum && nb_act == 0 && !nb_gamma && !nb_prelu &&
-                   P2P_KNOB_ONCE("P2P_NB_GATE_LOAD") == nullptr) ? 1 : 0;
+      a.nb_gate = (nb_gate && !nb_colsum && nb_act == 0 && !nb_gamma && !nb_prelu) ? 1 : 0;
       a.nb_batch = nb_batch ? 1 : 0;
       a.nb_c0 = (int)c0;
       a.nb_C = (int)nC;
@@ -1014,8 +1002,11 @@ bool conv_wgrad(const Tensor& p1, const optional<Tensor>& p2, int64_t p_act, con
   p2p_conv_wgrad_tile(&a, &wbr, &wbq);
   const int64_t tiles = ((R + wbr - 1) / wbr) * ((a.Kq + wbq - 1) / wbq);
   const int64_t stages = ((int64_t)a.M + 63) / 64;
-  // >= 2 waves of 256 CUs; every split keeps >= 8 reduction stages (pipeline depth 3)
-  int64_t splits = std::max<int64_t>(1, 512 / std::max<int64_t>(tiles, 1));
+  // >= P2P_WGRAD_BLOCKS blocks (default 512: 2 waves of 256 CUs); every split keeps >= 8
+  // reduction stages (pipeline depth 3)
+  const char* wbv = std::getenv("P2P_WGRAD_BLOCKS");   // (per call: A/B of the split target)
+  const int64_t wblocks = wbv ? std::max<int64_t>(1, std::atoll(wbv)) : 512;
+  int64_t splits = std::max<int64_t>(1, wblocks / std::max<int64_t>(tiles, 1));
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, stages / 8));
   // bound the fp32 slab workspace to ~256 MB
   const int64_t slab = R * (int64_t)a.Kq;

@@ -70,7 +70,6 @@ struct ConvFwdArgs {
   float d2s_scale;
   const float* d2s_w;   // mode 2: device multiplier of the sign term (dL/dl1; null = 1)
   float* l1_part;
-  int cls_major;   // MODE 1 block order A/B knob (P2P_CLASS_MAJOR=1: all tiles of class 0 first)
   // Norm-backward partial sums fused into a dgrad epilogue (null nb_ws = off): the output
   // channels [nb_c0, nb_c0 + nb_C) are the gradient dz of a norm's output z = act(xhat*g + b)
   // (xhat = (x - mean) * rstd, x = nb_x [N][OH][OW][nb_C]); every BM-row tile (one image /
@@ -85,7 +84,6 @@ struct ConvFwdArgs {
   float* nb_ws;
   int nb_colsum;    // 1: plain column sums sum(dz) of the half (the bias gradient of the conv
                     // that produced it), no norm input read: nb_ws[0] only, nb_x / stats unused
-  int epi_serial;   // A/B knob (P2P_EPI_SERIAL=1): gate / skip-gradient dgrads on the plain epilogue, not EXT
   int nb_gate;      // the act' gate of the nb half reads the norm's output, which IS xhat (non-affine,
                     // no fused act): compute the gate from the xhat the partials already form,
                     // instead of loading that output again (one operand stream fewer)

@@ -92,9 +92,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_fwd_glds_kernel(ConvFwdArgs
   const int split = blockIdx.z;
   const int ntiles = (a.Cout + BN - 1) / BN;
   const int bid0 = xcd_remap(blockIdx.x, gridDim.x);
-  const int per_cls = gridDim.x / classes;
-  const int cls = MODE == 1 ? (a.cls_major ? bid0 / per_cls : bid0 % classes) : 0;
-  const int bid = MODE == 1 ? (a.cls_major ? bid0 % per_cls : bid0 / classes) : bid0;
+  const int cls = MODE == 1 ? bid0 % classes : 0;
+  const int bid = MODE == 1 ? bid0 / classes : bid0;
   const ClassGeom g = class_geom<MODE>(a, cls);
   const int mt = bid / ntiles, nt = bid % ntiles;
   const int m0 = mt * BM, n0 = nt * BN;
@@ -556,7 +555,7 @@ static int dispatch_glds(const ConvFwdArgs& a, int variant, hipStream_t st) {
   if constexpr (F8 != 1) {
     // dgrads (bf16 or e5m2 gradient operands) with an act' gate / parked skip gradient / fused
     // norm partials: the EXT epilogue
-    if (a.nb_ws || ((a.act_bwd || a.res1) && !a.epi_serial))
+    if (a.nb_ws || (a.act_bwd || a.res1))
       return fastk ? dispatch_glds2<MODE, true, false, F8, false, true>(a, variant, st)
                    : dispatch_glds2<MODE, false, false, F8, false, true>(a, variant, st);
   }

@@ -214,9 +214,8 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
   const int classes = MODE == 1 ? a.stride * a.stride : 1;
   const int ntiles = (a.Cout + BN - 1) / BN;
   const int bid0 = xcd_remap(blockIdx.x, gridDim.x);
-  const int per_cls = gridDim.x / classes;
-  const int cls = MODE == 1 ? (a.cls_major ? bid0 / per_cls : bid0 % classes) : 0;
-  const int bid = MODE == 1 ? (a.cls_major ? bid0 % per_cls : bid0 / classes) : bid0;
+  const int cls = MODE == 1 ? bid0 % classes : 0;
+  const int bid = MODE == 1 ? bid0 / classes : bid0;
   const ClassGeom g = class_geom<MODE>(a, cls);
   const int mt = bid / ntiles, nt = bid % ntiles;
   const int m0 = mt * BM, n0 = nt * BN;
@@ -694,7 +693,7 @@ static int dispatch_m32_f8(const ConvFwdArgs& a, hipStream_t st) {
   }
   if (a.fp8 == 2) {   // e5m2 gradients: no input activation; the EXT epilogue for gated dgrads
     if (a.act_in != ACT_NONE) return -2;
-    if (a.nb_ws || ((a.act_bwd || a.res1) && !a.epi_serial)) return launch_m32<128, MODE, false, true, 2>(a, st);
+    if (a.nb_ws || (a.act_bwd || a.res1)) return launch_m32<128, MODE, false, true, 2>(a, st);
     return launch_m32<128, MODE, false, false, 2>(a, st);
   }
   return -2;
@@ -703,7 +702,7 @@ static int dispatch_m32_f8(const ConvFwdArgs& a, hipStream_t st) {
 template <int BN, int MODE>
 static int dispatch_m32_epi(const ConvFwdArgs& a, hipStream_t st) {
   if (a.act_in == ACT_RELU) return launch_m32<BN, MODE, true, false>(a, st);
-  if (a.nb_ws || ((a.act_bwd || a.res1) && !a.epi_serial)) return launch_m32<BN, MODE, false, true>(a, st);
+  if (a.nb_ws || (a.act_bwd || a.res1)) return launch_m32<BN, MODE, false, true>(a, st);
   return launch_m32<BN, MODE, false, false>(a, st);
 }
 

@@ -980,10 +980,9 @@ static int wgrad_glds_shape(const p2p::ConvWgradArgs* a) {
     return 0;
   const char* v = std::getenv("P2P_CONV_VARIANT");
   if (v && v[0] == 'v') return 0;
-  // 4 = 256x256 (half the VALU + LDS fragment traffic per MFMA of 1 / 2); P2P_WGRAD_TILE=256
-  // selects it for the weight gradients alone (census A/B)
-  const char* wt = P2P_KNOB_ONCE("P2P_WGRAD_TILE");
-  const bool w256 = (v && v[0] == 'g' && v[1] == '5') || (wt && wt[0] == '2' && wt[1] == '5');
+  // 4 = 256x256 (half the VALU + LDS fragment traffic per MFMA of 1 / 2): forced by the tests'
+  // P2P_CONV_VARIANT=g5 (the 32x32x16 m32 tile takes these shapes by default)
+  const bool w256 = v && v[0] == 'g' && v[1] == '5';
   if (w256 && a->R % 256 == 0 && a->Kq % 256 == 0) return 4;
   if (a->R >= 256) return 1;
   // 5 = 128x128 on 4 waves, 2-stage (two blocks per CU): Kq = 128, e.g. the packed 8-channel
@@ -1163,6 +1162,89 @@ extern "C" long p2p_wgrad_reduce_extra(int splits, long slab) {
   return splits > 32 ? (long)((splits + 31) / 32) * slab : 0;
 }
 
+// The same reduce with 16-B slab reads (C % 4 == 0): a block owns one weight row r and 64
+// channels of every tap; thread item (tap, 4-channel group) walks the splits with G float4
+// partial sums -- per element exactly the scalar kernel's order (bitwise equal) at a quarter
+// of the load instructions (4-B loads run at 0.54-0.70x the 16-B rate, MI355X_MICROARCH.md)
+namespace p2p {
+template <int G>
+__global__ void __launch_bounds__(256) wgrad_reduce_t4_kernel(const float* __restrict__ ws, int splits, int R,
+                                                              int T, int C, int KW, int Rr, int Cr,
+                                                              float* __restrict__ dw, float scale, int accumulate,
+                                                              int flip) {
+  constexpr int CB = 64, LDT = CB + 1;
+  __shared__ float tile[81 * LDT];
+  const int r = blockIdx.y, c0 = blockIdx.x * CB;
+  const int Kq = T * C;
+  const long total = (long)R * Kq;
+  if (!P2P_OOB_OK(22, T, 0, 82)) return;
+  for (int idx = threadIdx.x; idx < T * (CB / 4); idx += 256) {
+    const int tap = idx / (CB / 4), q = idx - tap * (CB / 4);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c0 + 4 * q < C && P2P_OOB_OK(21, (long)r * Kq + tap * C + c0 + 4 * q + (long)(splits - 1) * total, 4,
+                                      (long)splits * total)) {
+      const float4* src = reinterpret_cast<const float4*>(ws + (long)r * Kq + tap * C + c0 + 4 * q);
+      const long st4 = total / 4;
+      float4 acc[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) acc[g] = make_float4(0.f, 0.f, 0.f, 0.f);
+      int k0 = 0;
+      for (; k0 + G <= splits; k0 += G) {
+        float4 v[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) v[g] = src[(long)(k0 + g) * st4];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          acc[g].x += v[g].x;
+          acc[g].y += v[g].y;
+          acc[g].z += v[g].z;
+          acc[g].w += v[g].w;
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (k0 + g < splits) {
+          const float4 v = src[(long)(k0 + g) * st4];
+          acc[g].x += v.x;
+          acc[g].y += v.y;
+          acc[g].z += v.z;
+          acc[g].w += v.w;
+        }
+      s = acc[0];
+#pragma unroll
+      for (int g = 1; g < G; ++g) {
+        s.x += acc[g].x;
+        s.y += acc[g].y;
+        s.z += acc[g].z;
+        s.w += acc[g].w;
+      }
+    }
+    float* tp = tile + tap * LDT + 4 * q;
+    tp[0] = s.x * scale;
+    tp[1] = s.y * scale;
+    tp[2] = s.z * scale;
+    tp[3] = s.w * scale;
+  }
+  __syncthreads();
+  const int E = T * CB;
+  for (int j = threadIdx.x; j < E; j += 256) {
+    const int cl = j / T, t = j - cl * T;
+    const int ci = c0 + cl;
+    long o;
+    if (!flip) {
+      if (r >= Rr || ci >= Cr) continue;
+      o = ((long)r * Cr + ci) * T + t;
+    } else {
+      if (ci >= Rr || r >= Cr) continue;
+      const int kh = t / KW, kw = t - kh * KW;
+      o = ((long)ci * Cr + r) * T + (T / KW - 1 - kh) * KW + (KW - 1 - kw);
+    }
+    const float v = tile[t * LDT + cl];
+    if (P2P_OOB_OK(20, o, 1, (long)Rr * Cr * T)) dw[o] = accumulate ? dw[o] + v : v;
+  }
+}
+}  // namespace p2p
+
 extern "C" int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int KW, int C, int Rr,
                                 int Cr, float* dw, float scale, int accumulate, int flip,
                                 hipStream_t st) {
@@ -1177,6 +1259,24 @@ extern "C" int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int 
   }
   int G = 1;
   while (G < 32 && splits > 8 * G) G *= 2;   // <= ~8 slab reads per thread
+  if (KH * KW <= 81 && C % 4 == 0) {
+    const dim3 grid4((unsigned)((C + 63) / 64), (unsigned)R);
+#define P2P_REDT4(g)                                                                                        \
+  case g:                                                                                                    \
+    hipLaunchKernelGGL(p2p::wgrad_reduce_t4_kernel<g>, grid4, dim3(256), 0, st, ws, splits, R, KH * KW, C, KW, \
+                       Rr, Cr, dw, scale, accumulate, flip);                                                 \
+    break;
+    switch (G) {
+      P2P_REDT4(1)
+      P2P_REDT4(2)
+      P2P_REDT4(4)
+      P2P_REDT4(8)
+      P2P_REDT4(16)
+      P2P_REDT4(32)
+    }
+#undef P2P_REDT4
+    return (int)hipGetLastError();
+  }
   if (KH * KW <= 81) {
     const dim3 grid((unsigned)((C + 31) / 32), (unsigned)R);
 #define P2P_REDT(g)                                                                                       \

@@ -39,10 +39,6 @@ from . import fp8 as _f8
 ACT = {None: 0, "none": 0, "relu": 1, "lrelu": 2, "tanh": 3, "sigmoid": 4}
 # P2P_NB_FUSE=0: norm backward runs its own partial pass (A/B knob for the dgrad-epilogue fusion)
 _NB_FUSE = os.environ.get("P2P_NB_FUSE", "1") != "0"
-# P2P_NB_FOLD=1: batch-norm partials also from the reflect / nearest-x2 fold dgrads (epilogue +
-# fold_band).  Off by default: measured slower on family R (profiles/kernel_experiments_r5.md
-# section 12: the EXT epilogue costs the 256-row tiles more than the partial pass it replaces)
-_NB_FOLD = os.environ.get("P2P_NB_FOLD", "0") == "1"
 _NB_LOG = os.environ.get("P2P_NB_LOG", "0") == "1"
 # reflect-pad dgrads fold in the conv epilogue (P2P_FOLD_EPI=0: padded grid + pad_fold, A/B)
 _FOLD_EPI = os.environ.get("P2P_FOLD_EPI", "1") != "0"
@@ -858,10 +854,11 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
                 if res is not None and res.shape != (q1.shape[0], Cp, H, W):
                     _DEFERRED[q1.data_ptr()] = res   # not fusable: added below instead
                     res = None
-            # a batch norm's output (family R): its partials from this dgrad's epilogue (interior
-            # pixels) and fold_band (the band's folded values)
-            nbh = (_nb_half(cfg, None, nb, res is not None or q1.data_ptr() not in _DEFERRED)
-                   if (_NB_FOLD and not packed) else None)
+            # (a batch norm's partials are NOT taken from a fold dgrad: built in round 5 and
+            # measured slower -- the EXT epilogue costs the 256-row tiles more than the partial
+            # pass it replaces, profiles/kernel_experiments_r5.md section 12 -- and removed in
+            # round 6; the norm runs its own partial pass)
+            nbh = None
             if (cfg.up == 2 and cfg.reflect and p == 1 and KH == 3 and KW == 3 and s == 1
                     and _UP_FOLD):
                 # nearest x2 then reflect pad 1 == edge-replicate pad 1 of the upsample: the

@@ -143,43 +143,6 @@ def test_nb_batch_norm_relu(monkeypatch, affine):
         assert rel_err(a, b) < 1e-2
 
 
-@pytest.mark.parametrize("consumer", ["reflect_s1", "reflect_s2", "up2_reflect"])
-@pytest.mark.parametrize("act", ["relu", "prelu"])
-def test_nb_batch_norm_fold(monkeypatch, consumer, act):
-    """Family R's BN -> ConvLayer (reflect pad 1; stride 1 or 2) / UpsampleConvLayer (nearest
-    x2 + reflect 1): the dgrad folds the pad (epilogue + fold_band) AND emits the affine batch
-    norm's partials -- the band's folded values corrected by fold_band -- incl. the shared
-    PReLU slope's gradient terms.  Fused vs the norm's own partial pass, same inputs."""
-    N, C, H = 32, 128, 64     # >= 256 output tiles: the dgrad runs without split-K (as at B=64)
-    x = bf(_rand(N, 64, H, H, seed=41))
-    w1 = _rand(C, 64, 3, 3, seed=42, scale=(1 / 576) ** 0.5)
-    w2 = _rand(C, C, 3, 3, seed=43, scale=(1 / 1152) ** 0.5)
-    gam = 1 + _rand(C, seed=44, scale=0.1)
-    bet = _rand(C, seed=45, scale=0.1)
-    pw0 = torch.full((1,), 0.25, device=DEV)
-    s, up = (2, 1) if consumer == "reflect_s2" else (1, 2 if consumer == "up2_reflect" else 1)
-    OH = H * up // s
-    gy = bf(_rand(N, C, OH, OH, seed=46))
-
-    def fn():
-        hx = x.clone().requires_grad_(True)
-        hg, hb = gam.clone().requires_grad_(True), bet.clone().requires_grad_(True)
-        hp = pw0.clone().requires_grad_(True) if act == "prelu" else None
-        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
-        h = ops.conv2d(hx, w1, None, 1, 1, stats=True)
-        z = ops.batch_norm(h, rm, rv, hg, hb, True, act=None if act == "prelu" else act, prelu_weight=hp)
-        ops.conv2d(z, w2, None, s, 1, "reflect", up).backward(gy)
-        return (hx.grad.float(), hg.grad.float(), hb.grad.float()) + ((hp.grad.float(),) if hp is not None else ())
-
-    monkeypatch.setattr(hip, "_NB_FOLD", True)   # opt-in path (off by default: measured slower)
-    cnt = _Count(monkeypatch)
-    fused = _run(monkeypatch, True, fn)
-    assert cnt.hits == 1, "the fused partials were not used"
-    plain = _run(monkeypatch, False, fn)
-    for a, b in zip(fused, plain):
-        assert rel_err(a, b) < 1e-2, (rel_err(a, b), a.flatten()[:4], b.flatten()[:4])
-
-
 def test_nb_unet256_generator_grads(monkeypatch):
     """Model level: U-Net-256 generator gradients with and without the fusion, each against
     the fp32 eager oracle (8 chained bf16 layers amplify any reordering of the sums, so the

@@ -32,7 +32,7 @@ def main():
                     help="comma list of P2P_CONV_VARIANT values also timed per conv_fwd call (e.g. g2,g3)")
     ap.add_argument("--wgrad_variants", default="",
                     help="comma list of NAME=VAL environment settings also timed per conv_wgrad call "
-                         "(e.g. P2P_WGRAD_TILE=256)")
+                         "(e.g. P2P_M32=0)")
     args = ap.parse_args()
 
     import p2p_pytorch_amd as p2p
