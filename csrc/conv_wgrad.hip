@@ -1259,6 +1259,7 @@ extern "C" int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int 
   }
   int G = 1;
   while (G < 32 && splits > 8 * G) G *= 2;   // <= ~8 slab reads per thread
+#ifndef P2P_REDUCE_SCALAR   // (build-time A/B: the scalar-load reduce below for every shape)
   if (KH * KW <= 81 && C % 4 == 0) {
     const dim3 grid4((unsigned)((C + 63) / 64), (unsigned)R);
 #define P2P_REDT4(g)                                                                                        \
@@ -1277,6 +1278,7 @@ extern "C" int p2p_wgrad_reduce(const float* ws, int splits, int R, int KH, int 
 #undef P2P_REDT4
     return (int)hipGetLastError();
   }
+#endif
   if (KH * KW <= 81) {
     const dim3 grid((unsigned)((C + 31) / 32), (unsigned)R);
 #define P2P_REDT(g)                                                                                       \

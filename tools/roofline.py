@@ -85,17 +85,36 @@ def calibrate(probe_dir):
     return cal
 
 
+def _targs(kernel, name):
+    m = re.search(name + r"<([^>]*)>", kernel)
+    return [x.strip() for x in m.group(1).split(",")] if m else None
+
+
 def is_fp8(kernel):
-    m = re.search(r"conv_fwd_glds_kernel<([^>]*)>", kernel)
-    if m:
-        args = [x.strip() for x in m.group(1).split(",")]
-        return len(args) > 8 and args[8] not in ("0",)
+    """fp8 (f8f6f4) MFMA kernels: the glds conv tile's FP8 argument, the fp8 weight-gradient
+    and s2t instances, and the round-6 32x32x64 m32 instances (5th template argument F8)."""
+    g = _targs(kernel, "conv_fwd_glds_kernel")
+    if g:
+        return len(g) > 8 and g[8] not in ("0",)
+    if "conv_wgrad_f8_kernel" in kernel:
+        return True
+    for name, pos in (("conv_fwd_m32_kernel", 4), ("conv_s2t_kernel", 3)):
+        g = _targs(kernel, name)
+        if g:
+            return len(g) > pos and g[pos] not in ("0",)
     return False
 
 
 def is_m32(kernel):
-    """The 32x32x16 bf16 MFMA kernels (round 5): conv_fwd_m32 / conv_wgrad_m32."""
+    """The 32x32 MFMA kernels: conv_fwd_m32 (32x32x16 bf16 / 32x32x64 f8f6f4), conv_wgrad_m32."""
     return "_m32_kernel" in kernel
+
+
+def flop_per_mfma(kernel):
+    """FLOP of one MFMA instruction of the kernel: 16x16x32 bf16 16384, 32x32x16 bf16 32768,
+    16x16x128 f8f6f4 65536, 32x32x64 f8f6f4 131072."""
+    return (131072 if is_m32(kernel) else 65536) if is_fp8(kernel) else \
+        (32768 if is_m32(kernel) else 16384)
 
 
 def short(k):
@@ -127,7 +146,7 @@ def main(root, steps, probe):
         lds, conf = mean(c.get("SQ_INSTS_LDS", [])), mean(c.get("SQ_LDS_BANK_CONFLICT", []))
         fetch = mean(fe.get(k, {}).get("FETCH_SIZE", []))
         write = mean(wr.get(k, {}).get("WRITE_SIZE", []))
-        fpi = 65536 if is_fp8(k) else 32768 if is_m32(k) else 16384
+        fpi = flop_per_mfma(k)
         scale_i = (cal.get("bf16_32", {}).get("inst_scale") or inst_scale) if is_m32(k) else inst_scale
         flop = (mf / scale_i) * fpi if mf else 0.0
         # MFMA-pipe SIMD-cycles: the busy counter in units of one bf16 16x16x32 (16 cycles)
