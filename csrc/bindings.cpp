@@ -88,6 +88,7 @@ long p2p_wgrad_reduce_extra(int splits, long slab);
 int p2p_oob_counts(unsigned int* out4, int reset);
 int p2p_oob_selftest(void* scratch, hipStream_t st);
 int p2p_conv_fwd_m32(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t st);
+int p2p_conv_m32_rows(const p2p::ConvFwdArgs* a, int mode, int variant);
 int p2p_up2_dgrad_image(const float* w, int Cout, int Cin, int Xp, int Yp, void* out, hipStream_t st);
 int p2p_col_weight(const void* w, int T, int C, int Cv, int Cvp, int Ncol, void* out, hipStream_t st);
 int p2p_vec_pad(const float* x, int n, float fill, int nout, float* out, hipStream_t st);
@@ -443,6 +444,10 @@ std::vector<Tensor> conv_fwd(const Tensor& x1, const optional<Tensor>& x2, const
                       (fp8 != 2 || act_in == 0) && (fp8 != 1 || (!act_bwd && !res)) &&
                       (!fp8 || (s2t_f8_mask() & (int)fp8)) && std::getenv("P2P_NO_S2T") == nullptr;
   if (s2t_ok) bm = 128;
+  // the 512 x 128 m32 tile: its fused-statistics / norm-partial chunks are 512 rows (one
+  // predicate with the kernel's own routing, conv_fwd_m32.hip p2p_conv_m32_rows)
+  if (!s2t_ok && glds_ok && splits == 1 && p2p_m32_enabled() && p2p_conv_m32_rows(&a, (int)mode, variant) == 512)
+    bm = 512;
   if (P2P_KNOB_ONCE("P2P_ROUTE_LOG"))   // routing trace (tools): one line per conv call
     fprintf(stderr, "[route] mode %d N %ld C %ld+%ld %ldx%ld -> %ld %ldx%ld k%d s%d p%d act_in %d act_bwd %d res %d "
             "fp8 %d splits %d s2t %d bm %d bn %d tiles %ld\n", (int)mode, (long)N, (long)C1, (long)C2, (long)H,

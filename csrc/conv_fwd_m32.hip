@@ -162,14 +162,18 @@ __device__ unsigned long long m32_stamps[65536 * 6];
   } while (0)
 #endif
 
-template <int BN>
+// BMT = 512 (round 6, BN = 128 only): 8 waves of 128 x 64 like the 256 x 256 tile -- the
+// 256 x 128 tile's 64 x 64 wave tiles read 128 KB of fragments per 64-deep K tile for 1024
+// MFMA cycles per SIMD (LDS-read bound at 128 B / clk / CU); 128 x 64 wave tiles read 192 KB
+// for 2048.  Two 80 KB stages fill the 160 KB LDS.
+template <int BN, int BMT = 256>
 struct M32Geom {
-  static constexpr int BM = 256;
+  static constexpr int BM = BMT;
   static constexpr int WM = BN == 256 ? 2 : 4;
   static constexpr int WN = 8 / WM;
   static constexpr int TM = BM / WM / 32;
   static constexpr int TN = BN / WN / 32;
-  static constexpr int STAGES = BN == 256 ? 2 : 3;
+  static constexpr int STAGES = (BN == 256 || BM == 512) ? 2 : 3;
   static constexpr int NT = 512;
   static constexpr int RPP = NT / 8;                // tile rows per glds pass (8 lanes per row)
   static constexpr int AROWS = BM / RPP;            // A glds per thread per tile
@@ -195,9 +199,10 @@ struct M32Geom {
 // whatever k order the instruction assigns inside the 32 bytes, and one per-tensor scale per
 // operand makes the per-32-k scale blocks uniform.  Half the K tiles of the bf16 GEMM for the
 // same MFMA cycles per tile: twice the FLOP per staged byte.
-template <int BN, int MODE, bool RELU, bool EXT, int F8 = 0>
+template <int BN, int MODE, bool RELU, bool EXT, int F8 = 0, int BMT = 256>
 __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
-  using G = M32Geom<BN>;
+  using G = M32Geom<BN, BMT>;
+  static_assert(BMT == 256 || (BMT == 512 && BN == 128 && F8 == 0), "512-row tile: bf16, 128 columns");
   constexpr int ES = F8 ? 1 : 2;            // bytes per operand element
   constexpr int BKE = F8 ? 2 * BK : BK;     // operand elements per 128-B K tile row
   constexpr int BM = G::BM, WN = G::WN, TM = G::TM, TN = G::TN, STAGES = G::STAGES, NT = G::NT;
@@ -257,29 +262,64 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
   // + y / x origin of its taps); the source-side swizzle (row >> 1) & 7 does not depend on i
   // per A row: the image offset and the tap origin (y, x) packed as two int16 (one register
   // instead of two); y = -16384 marks a padded row
-  int r_img[AROWS], r_yx[AROWS];
-  const int r_c = (slot8 ^ (((wid * 8 + rsub) >> 1) & 7)) * 8;
+  // 512-row tiles (host predicate p2p_conv_m32_rows: every parity class a multiple of 512
+  // pixels, so a tile lies in one image and has no padded rows): no per-row image offset.
+  // DERIVE: not even the per-row packed tap origins -- ONE register, the first row's in-image
+  // index, and rows i (that + RPP i) re-derived per channel segment: more VALU per segment, 7
+  // registers fewer.  The input-ReLU instances need it (their fragment masking spilled the
+  // per-row layout inside the K loop); -DP2P_M32_DERIVE_ROWS (build-time A/B) takes it for all.
+  constexpr bool ONE_IMG = BM == 512;
+#ifdef P2P_M32_DERIVE_ROWS
+  constexpr bool DERIVE = ONE_IMG;
+#else
+  constexpr bool DERIVE = ONE_IMG && RELU;
+#endif
+  int r_img[ONE_IMG ? 1 : AROWS], r_yx[DERIVE ? 1 : AROWS];
+  r_img[0] = 0;
+  if constexpr (DERIVE) {
+    r_yx[0] = m0 + wid * 8 + rsub - img0 * HWq;
+  } else {
 #pragma unroll
-  for (int i = 0; i < AROWS; ++i) {
-    const int row = wid * 8 + rsub + RPP * i;
-    const int m = m0 + row;
-    const int mm = m < g.Mc ? m : 0;
-    const int n = (int)fdiv((uint32_t)mm, fd_hwq);
-    const int r = mm - n * HWq;
-    const int qy = (int)fdiv((uint32_t)r, fd_wq);
-    const int qx = r - qy * g.Wq;
-    r_img[i] = (n - img0) * a.H * a.W;
-    int y0, x0;
-    if (MODE == 0) {
-      y0 = qy * a.stride - a.pad;
-      x0 = qx * a.stride - a.pad;
-    } else {
-      y0 = qy + g.dy;
-      x0 = qx + g.dx;
+    for (int i = 0; i < AROWS; ++i) {
+      const int row = wid * 8 + rsub + RPP * i;
+      const int m = m0 + row;
+      const int mm = m < g.Mc ? m : 0;
+      const int n = (int)fdiv((uint32_t)mm, fd_hwq);
+      const int r = mm - n * HWq;
+      const int qy = (int)fdiv((uint32_t)r, fd_wq);
+      const int qx = r - qy * g.Wq;
+      if constexpr (!ONE_IMG) r_img[i] = (n - img0) * a.H * a.W;
+      int y0, x0;
+      if (MODE == 0) {
+        y0 = qy * a.stride - a.pad;
+        x0 = qx * a.stride - a.pad;
+      } else {
+        y0 = qy + g.dy;
+        x0 = qx + g.dx;
+      }
+      if (m >= g.Mc) y0 = -16384;
+      r_yx[i] = (int)(((uint32_t)y0 << 16) | ((uint32_t)x0 & 0xffffu));
     }
-    if (m >= g.Mc) y0 = -16384;
-    r_yx[i] = (int)(((uint32_t)y0 << 16) | ((uint32_t)x0 & 0xffffu));
   }
+  // tap origin (y0, x0) and image offset of A row i
+  auto row_origin = [&](int i, int& y0, int& x0, int& rimg) __attribute__((always_inline)) {
+    if constexpr (DERIVE) {
+      // opaque per call: keeps the compiler from hoisting the 8 rows' loop-invariant origins
+      // out of the K loop (their registers are what this layout saves)
+      int r0 = r_yx[0];
+      asm volatile("" : "+v"(r0));
+      const int r = r0 + RPP * i;
+      const int qy = (int)fdiv((uint32_t)r, fd_wq);
+      const int qx = r - qy * g.Wq;
+      y0 = MODE == 0 ? qy * a.stride - a.pad : qy + g.dy;
+      x0 = MODE == 0 ? qx * a.stride - a.pad : qx + g.dx;
+    } else {
+      y0 = r_yx[i] >> 16;
+      x0 = (int)(int16_t)(r_yx[i] & 0xffff);
+    }
+    rimg = ONE_IMG ? 0 : r_img[i];
+  };
+  const int r_c = (slot8 ^ (((wid * 8 + rsub) >> 1) & 7)) * 8;
   uint32_t b_vo[BROWS];
 #pragma unroll
   for (int i = 0; i < BROWS; ++i) {
@@ -307,10 +347,10 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
       const int cio = s1 ? ci0 : ci0 - C1;
 #pragma unroll
       for (int i = 0; i < AROWS; ++i) {
-        int iy, ix;
+        int iy, ix, ry0, rx0, rimg;
         bool inb;
+        row_origin(i, ry0, rx0, rimg);
         if (MODE == 0) {
-          const int ry0 = r_yx[i] >> 16, rx0 = (int)(int16_t)(r_yx[i] & 0xffff);
           int uy = ry0 + t_y, ux = rx0 + t_x;
           if (a.reflect && ry0 > -8192) {
             uy = reflect_idx(uy, Hu);
@@ -320,11 +360,11 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
           iy = uy >> ush;
           ix = ux >> ush;
         } else {
-          iy = (r_yx[i] >> 16) - t_y;
-          ix = (int)(int16_t)(r_yx[i] & 0xffff) - t_x;
+          iy = ry0 - t_y;
+          ix = rx0 - t_x;
           inb = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
         }
-        a_vo[i] = inb ? (uint32_t)(((r_img[i] + iy * a.W + ix) * cs + cio) * ES + r_c * 2) : OOB;
+        a_vo[i] = inb ? (uint32_t)(((rimg + iy * a.W + ix) * cs + cio) * ES + r_c * 2) : OOB;
       }
       a_soff = 0;
     } else {
@@ -657,11 +697,12 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
 #endif
 }
 
-template <int BN, int MODE, bool RELU, bool EXT, int F8 = 0>
+template <int BN, int MODE, bool RELU, bool EXT, int F8 = 0, int BMT = 256>
 static int launch_m32(const ConvFwdArgs& a, hipStream_t st) {
-  using G = M32Geom<BN>;
+  using G = M32Geom<BN, BMT>;
   static std::atomic<uint64_t> attr_mask{0};
-  smem_attr_once(reinterpret_cast<const void*>(&conv_fwd_m32_kernel<BN, MODE, RELU, EXT, F8>), G::SMEM, attr_mask);
+  smem_attr_once(reinterpret_cast<const void*>(&conv_fwd_m32_kernel<BN, MODE, RELU, EXT, F8, BMT>), G::SMEM,
+                 attr_mask);
   const int classes = MODE == 0 ? 1 : a.stride * a.stride;
   long mmax = 0;
   for (int c = 0; c < classes; ++c) {
@@ -677,7 +718,7 @@ static int launch_m32(const ConvFwdArgs& a, hipStream_t st) {
   const long mtiles = (mmax + G::BM - 1) / G::BM;
   const long ntiles = (a.Cout + BN - 1) / BN;
   dim3 grid((unsigned)(mtiles * ntiles * classes), 1, 1);
-  hipLaunchKernelGGL((conv_fwd_m32_kernel<BN, MODE, RELU, EXT, F8>), grid, dim3(G::NT), G::SMEM, st, a);
+  hipLaunchKernelGGL((conv_fwd_m32_kernel<BN, MODE, RELU, EXT, F8, BMT>), grid, dim3(G::NT), G::SMEM, st, a);
   return (int)hipGetLastError();
 }
 
@@ -699,11 +740,11 @@ static int dispatch_m32_f8(const ConvFwdArgs& a, hipStream_t st) {
   return -2;
 }
 
-template <int BN, int MODE>
+template <int BN, int MODE, int BMT = 256>
 static int dispatch_m32_epi(const ConvFwdArgs& a, hipStream_t st) {
-  if (a.act_in == ACT_RELU) return launch_m32<BN, MODE, true, false>(a, st);
-  if (a.nb_ws || (a.act_bwd || a.res1)) return launch_m32<BN, MODE, false, true>(a, st);
-  return launch_m32<BN, MODE, false, false>(a, st);
+  if (a.act_in == ACT_RELU) return launch_m32<BN, MODE, true, false, 0, BMT>(a, st);
+  if (a.nb_ws || (a.act_bwd || a.res1)) return launch_m32<BN, MODE, false, true, 0, BMT>(a, st);
+  return launch_m32<BN, MODE, false, false, 0, BMT>(a, st);
 }
 
 }  // namespace p2p
@@ -729,26 +770,56 @@ extern "C" int p2p_m32_stamps(void* host_out, int nblocks) {
 }
 #endif
 
-// variant 5 -> 256 x 256 tile (Cout > 128), 4 -> 256 x 128 (Cout > 64); -2 = not covered
-extern "C" int p2p_conv_fwd_m32(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t st) {
+// Rows of the m32 tile that p2p_conv_fwd_m32 would run for these arguments: 0 = not covered
+// (-2 there), else 256 or 512.  The host sizes the fused-statistics / norm-partial chunks by
+// it (conv_epilogue_tail: one chunk per BM rows), so this is THE routing predicate.
+// 512 rows (bf16, variant 4: the 128-column tiles): every parity class a multiple of 512
+// pixels and >= 1024 blocks in the grid (four per CU), unless P2P_M32_BM (read per call: the
+// tests and A/Bs pin it) says 256 or 512.
+extern "C" int p2p_conv_m32_rows(const p2p::ConvFwdArgs* a, int mode, int variant) {
   using namespace p2p;
-  if (a->splits > 1 || a->d2s) return -2;
+  if (a->splits > 1 || a->d2s) return 0;
   // FASTK: every 128-B K tile inside one tap and one source (64 bf16 / 128 fp8 channels)
   const int chc = a->fp8 ? 128 : 64;
-  if (a->C1 % chc || a->C2 % chc || a->C1 > 1024 || a->C2 > 1024) return -2;
-  if (a->fp8 && (!a->qs_x1 || !a->qs_w || (a->C2 && !a->qs_x2) || a->fp8 > 2)) return -2;
-  if (a->act_in != ACT_NONE && a->act_in != ACT_RELU) return -2;
+  if (a->C1 % chc || a->C2 % chc || a->C1 > 1024 || a->C2 > 1024) return 0;
+  if (a->fp8 && (!a->qs_x1 || !a->qs_w || (a->C2 && !a->qs_x2) || a->fp8 > 2)) return 0;
+  if (a->act_in != ACT_NONE && a->act_in != ACT_RELU) return 0;
   if (a->fp8) {
     // Cout 65..128 only: there the 256 x 128 fp8 tile beats the 16x16x128 glds tile by 3-10 %
     // per layer; for Cout > 128 the glds 256 x 256 fp8 tile (A staged once for 256 columns)
     // is 10-20 % faster than two 128-wide m32 column tiles (profiles/kernel_experiments_r6.md)
-    if ((variant != 4 && variant != 5) || a->Cout <= 64 || a->Cout > 128) return -2;
-    return mode == 0 ? dispatch_m32_f8<0>(*a, st) : dispatch_m32_f8<1>(*a, st);
+    if ((variant != 4 && variant != 5) || a->Cout <= 64 || a->Cout > 128) return 0;
+    if (a->fp8 == 1 && (a->nb_ws || a->act_bwd || a->res1)) return 0;
+    if (a->fp8 == 2 && a->act_in != ACT_NONE) return 0;
+    return 256;
   }
+  if (variant == 5 && a->Cout > 128) return 256;
+  if (!(variant == 4 && a->Cout > 64)) return 0;
+  const char* env = std::getenv("P2P_M32_BM");
+  const int pin = env ? std::atoi(env) : 0;
+  if (pin == 256) return 256;
+  const int classes = mode == 0 ? 1 : a->stride * a->stride;
+  long hwq = (long)a->OH * a->OW;
+  if (mode == 1) {
+    if (a->OH % a->stride || a->OW % a->stride) return 256;
+    hwq = (long)(a->OH / a->stride) * (a->OW / a->stride);
+  }
+  if (hwq % 512) return 256;
+  const long blocks = (long)a->N * hwq / 512 * ((a->Cout + 127) / 128) * classes;
+  return (pin == 512 || blocks >= 1024) ? 512 : 256;
+}
+
+// variant 5 -> 256 x 256 tile (Cout > 128), 4 -> 256 x 128 or 512 x 128 (Cout > 64); -2 = not
+// covered
+extern "C" int p2p_conv_fwd_m32(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t st) {
+  using namespace p2p;
+  const int rows = p2p_conv_m32_rows(a, mode, variant);
+  if (rows == 0) return -2;
+  if (a->fp8) return mode == 0 ? dispatch_m32_f8<0>(*a, st) : dispatch_m32_f8<1>(*a, st);
   // (the ReLU 256-wide variants spill a few loop-invariant epilogue values before the K loop; the loop itself is spill-free)
-  if (variant == 5 && a->Cout > 128)
+  if (variant == 5)
     return mode == 0 ? dispatch_m32_epi<256, 0>(*a, st) : dispatch_m32_epi<256, 1>(*a, st);
-  if (variant == 4 && a->Cout > 64)
-    return mode == 0 ? dispatch_m32_epi<128, 0>(*a, st) : dispatch_m32_epi<128, 1>(*a, st);
-  return -2;
+  if (rows == 512)
+    return mode == 0 ? dispatch_m32_epi<128, 0, 512>(*a, st) : dispatch_m32_epi<128, 1, 512>(*a, st);
+  return mode == 0 ? dispatch_m32_epi<128, 0>(*a, st) : dispatch_m32_epi<128, 1>(*a, st);
 }

@@ -73,7 +73,7 @@ CASES = [
 WGRAD_M32 = {c[0] for c in CASES if c[0].startswith("wgrad_")}
 
 
-def _run(case, m32):
+def _run(case, m32, extra_env=None):
     name, var, kind, N, C1, C2, H, Cout, k, s, p, pad_mode, act_in, act_out = case
     x1 = rand_img(N, C1, H, H, seed=1)
     x2 = rand_img(N, C2, H, H, seed=2) if C2 else None
@@ -89,7 +89,7 @@ def _run(case, m32):
     prev = torch.ops.p2p.set_m32(1 if m32 else 0)
     # the tile under test, and none of the special-geometry kernels that would take some of
     # these layers first (stride-2 halo kernel, 3x3 / 9x9 halo kernels)
-    env = {"P2P_CONV_VARIANT": var, "P2P_NO_S2T": "1", "P2P_NO_HALO": "1"}
+    env = {"P2P_CONV_VARIANT": var, "P2P_NO_S2T": "1", "P2P_NO_HALO": "1", **(extra_env or {})}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -147,3 +147,85 @@ def test_m32_matches_16x16_tiles(case):
     for ta, tb in zip(out_a, out_b):
         if ta is not None:
             assert rel_err(ta, tb) < 1.5e-2
+
+
+# The 512 x 128 tile (round 6): bf16 layers with 65-128 output channels whose parity classes
+# are multiples of 512 pixels.  Pinned with P2P_M32_BM (read per call; the production route
+# takes it from 1024 blocks up).  Cases: conv on a virtual concat with Cout not a tile multiple,
+# a ReLU'd input whose input gradient carries the act' gate (EXT, MODE 1), and the ConvT with
+# input ReLU (MODE 1 RELU) -- e2 / PatchGAN c2 / d-layer shapes at 32x32 and 64x64.
+# (>= 256 tiles of 256 rows, as above: smaller grids take split-K)
+CASES_512 = [
+    ("conv_s2_concat_512x128", "g4", "conv", 16, 64, 64, 128, 96, 4, 2, 1, "zeros", None, "lrelu"),
+    ("conv_s2_relu_gate_512x128", "g4", "conv", 16, 128, 0, 128, 128, 4, 2, 1, "zeros", "relu", None),
+    ("convT_relu_512x128", "g4", "convT", 16, 256, 0, 64, 128, 4, 2, 1, "zeros", "relu", None),
+]
+
+
+@pytest.mark.parametrize("case", CASES_512, ids=[c[0] for c in CASES_512])
+def test_m32_512_rows_bitwise_vs_256(case):
+    """Per output element the 512-row tile runs the 256-row tile's MFMA chain (same K tiles,
+    same 32x32x16 blocks, same epilogue rounding): forward and input gradients bitwise equal,
+    and the 512-row instances must actually have run (forward and the MODE-1 gradient)."""
+    out_a, _, names = _run(case, True, {"P2P_M32_BM": "512"})
+    out_b, _, names_b = _run(case, True, {"P2P_M32_BM": "256"})
+    assert any(n.rstrip(")").split("(")[0].endswith(", 512>") for n in names), sorted(set(names))
+    assert not any(", 512>" in n for n in names_b), sorted(set(names_b))
+    if case[12] == "relu" and case[2] == "conv":   # gated input gradient: the EXT instance
+        assert any("conv_fwd_m32_kernel<128, 1, false, true, 0, 512>" in n for n in names), sorted(set(names))
+    for ta, tb in zip(out_a, out_b):
+        if ta is not None:
+            assert torch.equal(ta, tb), (case[0], (ta.float() - tb.float()).abs().max().item())
+
+
+def test_m32_512_rows_oracle():
+    """The first 512-row case against the fp32 oracle (bias, lrelu output, concat)."""
+    case = CASES_512[0]
+    name, var, kind, N, C1, C2, H, Cout, k, s, p, pad_mode, act_in, act_out = case
+    (y, gx1, gx2, gw, gb), (x1, x2, w, b, gy), names = _run(case, True, {"P2P_M32_BM": "512"})
+    assert any(", 512>" in n for n in names)
+    rx1, rx2, rw, rb = _leaf(x1.float()), _leaf(x2.float()), _leaf(w), _leaf(b)
+    ry = ref.conv2d((rx1, rx2), rw.to(torch.bfloat16).float(), rb, s, p, pad_mode, 1, act_in=act_in,
+                    act_out=act_out)
+    ry.backward(gy.float())
+    assert rel_err(y, ry) < 2e-2
+    assert rel_err(gx1, rx1.grad) < 3e-2 and rel_err(gx2, rx2.grad) < 3e-2
+
+
+def test_m32_512_rows_full_step_fused_norms(monkeypatch):
+    """Fused norm statistics and norm-backward partials are chunked per BM rows (host and
+    kernel share one predicate, p2p_conv_m32_rows): two pix2pix steps (batch-norm U-Net,
+    instance-norm PatchGAN) with the 512-row tiles pinned match the 256-row run's losses.
+    Batch 16: the Cout-128 layers (e2, c2, their input gradients) reach the 256 tiles below
+    which split-K takes them."""
+    import p2p_pytorch_amd as p2p
+    from p2p_pytorch_amd.engine.pix2pix import Pix2PixStep
+    from p2p_pytorch_amd.models import define_D, define_G
+    from p2p_pytorch_amd.ops import hip
+
+    def run(bm):
+        monkeypatch.setenv("P2P_M32_BM", bm)
+        hip.reset_rng(0)
+        torch.manual_seed(0)
+        G = define_G(netG="unet_256", gpu_id=DEV, verbose=False)
+        D = define_D(6, 64, norm="instance", netD="basic", gpu_id=DEV, verbose=False)
+        st = Pix2PixStep(G, D)
+        a = rand_img(16, 3, 256, 256, seed=31)
+        b = rand_img(16, 3, 256, 256, seed=32)
+        p2p.set_deterministic(True)
+        try:
+            with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+                losses = [st.step(a, b), st.step(a, b)]
+                torch.cuda.synchronize()
+        finally:
+            p2p.set_deterministic(False)
+        names = {e.name for e in prof.events() if "conv_fwd_m32_kernel" in e.name}
+        return [{k: float(v) for k, v in l.items()} for l in losses], names
+
+    l512, n512 = run("512")
+    l256, n256 = run("256")
+    assert any(", 512>" in n for n in n512), sorted(n512)
+    assert not any(", 512>" in n for n in n256)
+    for a, b in zip(l512, l256):
+        for k in a:
+            assert abs(a[k] - b[k]) <= 2e-3 * max(1.0, abs(b[k])), (k, a[k], b[k])
