@@ -774,8 +774,9 @@ extern "C" int p2p_m32_stamps(void* host_out, int nblocks) {
 // (-2 there), else 256 or 512.  The host sizes the fused-statistics / norm-partial chunks by
 // it (conv_epilogue_tail: one chunk per BM rows), so this is THE routing predicate.
 // 512 rows (bf16, variant 4: the 128-column tiles): every parity class a multiple of 512
-// pixels and >= 1024 blocks in the grid (four per CU), unless P2P_M32_BM (read per call: the
-// tests and A/Bs pin it) says 256 or 512.
+// pixels and >= 256 blocks in the grid (one per CU; family R's B = 64 residual 3x3s have 512
+// and gained 1 % on it), unless P2P_M32_BM (read per call: the tests and A/Bs pin it) says
+// 256 or 512.
 extern "C" int p2p_conv_m32_rows(const p2p::ConvFwdArgs* a, int mode, int variant) {
   using namespace p2p;
   if (a->splits > 1 || a->d2s) return 0;
@@ -806,7 +807,7 @@ extern "C" int p2p_conv_m32_rows(const p2p::ConvFwdArgs* a, int mode, int varian
   }
   if (hwq % 512) return 256;
   const long blocks = (long)a->N * hwq / 512 * ((a->Cout + 127) / 128) * classes;
-  return (pin == 512 || blocks >= 1024) ? 512 : 256;
+  return (pin == 512 || blocks >= 256) ? 512 : 256;
 }
 
 // variant 5 -> 256 x 256 tile (Cout > 128), 4 -> 256 x 128 or 512 x 128 (Cout > 64); -2 = not
