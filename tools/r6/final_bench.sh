@@ -9,6 +9,8 @@ run() {  # tag args...
   tail -1 $O/$t.out >> $O/bench_final.jsonl
   tail -1 $O/$t.out | python -c "import json,sys;d=json.loads(sys.stdin.read());print('$t', d['value'], d['ms_per_step'], d['config']['hipgraph'], d['config']['capture_error'], d.get('max_mem_gib'))"
 }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -5 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
 run bf16_a || exit 1
 run fp8_a --precision fp8 || exit 1
 run bf16_b || exit 1
@@ -20,4 +22,5 @@ run famr_b64 --family ref --batch 64 || exit 1
 run famr_b512 --family ref || exit 1
 run fc_bf16 --force_comm --comm_dtype bf16 || exit 1
 run s512_fp8 --size 512 --batch 512 --precision fp8 || exit 1
+run eager_b128 --impl torch --batch 128 --steps 10 --warmup 3 || echo "eager baseline failed (not fatal)"
 echo done
