@@ -89,6 +89,8 @@ int p2p_oob_counts(unsigned int* out4, int reset);
 int p2p_oob_selftest(void* scratch, hipStream_t st);
 int p2p_conv_fwd_m32(const p2p::ConvFwdArgs* a, int mode, int variant, hipStream_t st);
 int p2p_conv_m32_rows(const p2p::ConvFwdArgs* a, int mode, int variant);
+int p2p_dgrad_c1(const void* dy, int dyC, int N, int H, int W, const float* w, int KH, int KW, int pad, int OH,
+                 int OW, int Cp, const float* alpha, void* dx, hipStream_t st);
 int p2p_up2_dgrad_image(const float* w, int Cout, int Cin, int Xp, int Yp, void* out, hipStream_t st);
 int p2p_col_weight(const void* w, int T, int C, int Cv, int Cvp, int Ncol, void* out, hipStream_t st);
 int p2p_vec_pad(const float* x, int n, float fill, int nout, float* out, hipStream_t st);
@@ -1485,6 +1487,28 @@ Tensor avgpool3s2(const Tensor& x, int64_t bwd, int64_t H, int64_t W) {
   return y;
 }
 
+// input gradient of a stride-1 conv with one output channel (csrc/dgrad_c1.hip): gy is the
+// output gradient padded to C8 channels (channel 0 live), w the fp32 master weight
+// [1][Cp][KH][KW]; dX [N][Cp][OH][OW] NHWC, times the optional device scalar alpha (SN 1/sigma)
+Tensor dgrad_c1(const Tensor& gy, const Tensor& w, int64_t pad, int64_t OH, int64_t OW,
+                const optional<Tensor>& alpha) {
+  check_nhwc(gy, "dgrad_c1 gy");
+  const int64_t N = gy.size(0), C8 = gy.size(1), H = gy.size(2), W = gy.size(3);
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.dim() == 4 && w.size(0) == 1,
+              "dgrad_c1: fp32 master weight [1][Cin][KH][KW]");
+  const int64_t Cp = w.size(1), KH = w.size(2), KW = w.size(3);
+  TORCH_CHECK(OH + 2 * pad - KH + 1 == H && OW + 2 * pad - KW + 1 == W,
+              "dgrad_c1: (OH, OW) must be the stride-1 conv's input size");
+  if (alpha) TORCH_CHECK(alpha->is_cuda() && alpha->scalar_type() == at::kFloat && alpha->numel() == 1, "dgrad_c1: alpha");
+  Tensor dx = empty_nhwc(N, Cp, OH, OW, gy);
+  const int rc = p2p_dgrad_c1(gy.data_ptr(), (int)C8, (int)N, (int)H, (int)W, w.data_ptr<float>(), (int)KH, (int)KW,
+                              (int)pad, (int)OH, (int)OW, (int)Cp, alpha ? alpha->data_ptr<float>() : nullptr,
+                              dx.data_ptr(), cur_stream(gy));
+  TORCH_CHECK(rc != -2, "dgrad_c1: geometry not covered (16 taps, Cin / 8 a power of two <= 64)");
+  check_rc(rc, "dgrad_c1");
+  return dx;
+}
+
 Tensor maxpool2(const Tensor& x, const optional<Tensor>& gy) {
   check_nhwc(x, "maxpool2");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
@@ -1978,6 +2002,7 @@ TORCH_LIBRARY(p2p, m) {
   m.def("image_metrics(Tensor a, Tensor b, bool shift, float data_range) -> Tensor");
   m.def("avgpool3s2(Tensor x, int bwd, int H, int W) -> Tensor");
   m.def("maxpool2(Tensor x, Tensor? gy) -> Tensor");
+  m.def("dgrad_c1(Tensor gy, Tensor w, int pad, int OH, int OW, Tensor? alpha=None) -> Tensor");
   m.def("l2norm(Tensor x, Tensor? gy, float eps, Tensor? res=None, int shuffle=1) -> Tensor");
   m.def("pixel_shuffle(Tensor x, int r, int dir) -> Tensor");
   m.def("pad_fold(Tensor dxp, int H, int W, int pad, int up, int reflect, Tensor? xb, int act, "
@@ -2052,6 +2077,7 @@ TORCH_LIBRARY_IMPL(p2p, CUDA, m) {
   m.impl("image_metrics", image_metrics);
   m.impl("avgpool3s2", avgpool3s2);
   m.impl("maxpool2", maxpool2);
+  m.impl("dgrad_c1", dgrad_c1);
   m.impl("l2norm", l2norm);
   m.impl("pixel_shuffle", pixel_shuffle);
   m.impl("slice_channels", slice_channels);

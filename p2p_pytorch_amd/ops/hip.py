@@ -894,10 +894,23 @@ def _conv_backward(cfg, geo, q1, q2, weight, y, gy, need_x1, need_x2, need_w, ne
                     res = None
             take_ok = res is not None or q1.data_ptr() not in _DEFERRED
             nbh = _nb_half(cfg, q2, nb, take_ok) if not packed else None
-            outs = _conv_call(gyp, None, None, None, 1, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
-                              split, q1 if act_in else None,
-                              q2 if (act_in and q2 is not None) else None, act_in, C1 + C2,
-                              False, weight, 1, Cp, Coutp, "gy", res=res, alpha=alpha, nb=nbh)
+            # (an instance norm's partials are never fused on a grid that is not a multiple of
+            # the tile rows -- the PatchGAN logits' 31 x 31 input -- so dropping nbh there
+            # loses nothing: the norm runs its own partial pass either way)
+            nb_lost = nbh is not None and (nbh[1] is _CS or nbh[1][6] or (H * W) % 128 == 0)
+            if (Cout == 1 and s == 1 and KH * KW == 16 and q2 is None and not packed and not act_in
+                    and res is None and not nb_lost and Cp == C1 and Cp % 8 == 0 and Cp <= 512
+                    and (Cp // 8) & (Cp // 8 - 1) == 0 and weight.dtype == torch.float32
+                    and weight.is_contiguous()
+                    and os.environ.get("P2P_C1_DGRAD", "1") != "0"):
+                # the logits conv (1 output channel): a bandwidth kernel instead of a K = 16 x 8
+                # GEMM that is 7/8 zero padding (csrc/dgrad_c1.hip)
+                outs = [P().dgrad_c1(gyp, weight.detach(), p, H, W, alpha)]
+            else:
+                outs = _conv_call(gyp, None, None, None, 1, KH, KW, s, p, 0, 1, 0, H, W, Cp, 0,
+                                  split, q1 if act_in else None,
+                                  q2 if (act_in and q2 is not None) else None, act_in, C1 + C2,
+                                  False, weight, 1, Cp, Coutp, "gy", res=res, alpha=alpha, nb=nbh)
         nouts = 2 if q2 is not None else 1
         if nbh is not None and len(outs) > nouts:
             nbp = outs[nouts]
