@@ -110,6 +110,37 @@ __global__ void __launch_bounds__(256, TN >= 8 ? 1 : 2) halo_pk8_kernel(HaloPk8A
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     bf16* A = As + stage * SUNITS * 8;
+    // the epilogue's output pixels, and (GATE) the act' inputs of ALL its pieces, issued here:
+    // their HBM latency runs behind the K loop instead of once per 32-channel piece after a
+    // barrier (round 6: the 128-channel gated input gradient streamed at 3.1 TB/s)
+    int n, oy0, ox0;
+    origin(k, n, oy0, ox0);
+    long pix[4];
+    bool ok[4];
+    u32x4 xg[GATE ? NC / PC : 1][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {               // 256 pixels x 4 chunks of 8 channels
+      const int it = tid + q * 256, row = it >> 2;
+      const int oy = oy0 + (row >> 4), ox = ox0 + (row & 15);
+      ok[q] = oy < a.Ho && ox < a.Wo;
+      pix[q] = ((long)n * a.Ho + (ok[q] ? oy : 0)) * a.Wo + (ok[q] ? ox : 0);
+    }
+    if constexpr (GATE) {
+#pragma unroll
+      for (int piece = 0; piece < NC / PC; ++piece) {
+        const int co0 = piece * PC;
+        const bool first = co0 < a.Csplit;
+        const int ld = first ? a.Csplit : NC - a.Csplit;
+        const int cof0 = first ? co0 : co0 - a.Csplit;
+        const bf16* xb = first ? a.xb1 : a.xb2;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int it = tid + q * 256;
+          xg[piece][q] = xb ? *reinterpret_cast<const u32x4*>(xb + pix[q] * ld + cof0 + (it & 3) * 8)
+                            : u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};
+        }
+      }
+    }
     f32x4 acc[4][TN];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -135,9 +166,7 @@ __global__ void __launch_bounds__(256, TN >= 8 ? 1 : 2) halo_pk8_kernel(HaloPk8A
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();     // every wave done with this stage: it hosts the staging tile
     // ---- epilogue, 32 channels at a time: bias + act staged as bf16 in this stage's LDS,
-    // then 16-B stores (the ReLU-gate inputs of a piece are loaded before any is used)
-    int n, oy0, ox0;
-    origin(k, n, oy0, ox0);
+    // then 16-B stores (the ReLU-gate inputs were loaded before the K loop)
     bf16* Cs = A;
 #pragma unroll
     for (int piece = 0; piece < NC / PC; ++piece) {
@@ -160,21 +189,6 @@ __global__ void __launch_bounds__(256, TN >= 8 ? 1 : 2) halo_pk8_kernel(HaloPk8A
       const int ld = first ? a.Csplit : NC - a.Csplit;
       const int cof0 = first ? co0 : co0 - a.Csplit;
       bf16* yb = first ? a.y1 : a.y2;
-      const bf16* xb = first ? a.xb1 : a.xb2;
-      long pix[4];
-      bool ok[4];
-      u32x4 xv[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {               // 256 pixels x 4 chunks of 8 channels
-        const int it = tid + q * 256, row = it >> 2;
-        const int oy = oy0 + (row >> 4), ox = ox0 + (row & 15);
-        ok[q] = oy < a.Ho && ox < a.Wo;
-        pix[q] = ((long)n * a.Ho + (ok[q] ? oy : 0)) * a.Wo + (ok[q] ? ox : 0);
-        if constexpr (GATE) {
-          xv[q] = xb ? *reinterpret_cast<const u32x4*>(xb + pix[q] * ld + cof0 + (it & 3) * 8)
-                     : u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};
-        }
-      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int it = tid + q * 256, row = it >> 2, cc = it & 3;
@@ -183,7 +197,7 @@ __global__ void __launch_bounds__(256, TN >= 8 ? 1 : 2) halo_pk8_kernel(HaloPk8A
         if constexpr (GATE) {   // ReLU' of the layer's input (dgrad of a ReLU-input conv)
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
-            const uint32_t xw = xv[q][w];
+            const uint32_t xw = xg[GATE ? piece : 0][q][w];
             uint32_t keep = 0;
             if ((int16_t)(xw & 0xffffu) > 0) keep |= 0xffffu;
             if ((int16_t)(xw >> 16) > 0) keep |= 0xffff0000u;
