@@ -127,6 +127,13 @@ __global__ void __launch_bounds__(NTH) halo_union_kernel(HaloArgs a) {
   // mode 2: the L1 sign term's weight = scale x dL/dl1 (a device scalar written by autograd)
   const float l1w = a.scale * (a.mode == 2 && a.wscale ? *a.wscale : 1.f);
   const int px = lane & 15, kq = lane >> 4;
+  // the depth-to-space epilogue's packed-image operands of the current tile, loaded when its
+  // first chunk starts: their HBM latency runs behind the tile's MFMAs instead of after the
+  // epilogue's barrier (round 6; the kernel streamed at 3.9-4.4 TB/s)
+  constexpr int PQ = 1024 / NTH;   // output pixels per thread (256 q x 4 classes)
+  long P[PQ];
+  bool ok[PQ];
+  bf16x8 ab[PQ], af[PQ];
 
   issue(0, 0);
   for (int it = 0; it < total; ++it) {
@@ -141,6 +148,20 @@ __global__ void __launch_bounds__(NTH) halo_union_kernel(HaloArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     const int ch = it % NCH;
     const bf16* A = As + stage * (STAGE_UNITS * 8);
+    if (ch == 0) {
+      int n, qy0, qx0;
+      tile_origin(it / NCH, n, qy0, qx0);
+      const int Ho = 2 * a.H, Wo = 2 * a.W;
+#pragma unroll
+      for (int q = 0; q < PQ; ++q) {
+        const int item = tid + q * NTH, row = item >> 2, cls = item & 3;
+        const int qy = qy0 + (row >> 4), qx = qx0 + (row & 15);
+        ok[q] = qy < a.H && qx < a.W;
+        P[q] = ((long)n * Ho + 2 * (ok[q] ? qy : 0) + (cls >> 1)) * Wo + 2 * (ok[q] ? qx : 0) + (cls & 1);
+        ab[q] = *reinterpret_cast<const bf16x8*>(a.pk_a + P[q] * 8);
+        if (a.mode == 2) af[q] = *reinterpret_cast<const bf16x8*>(a.pk_f + P[q] * 8);
+      }
+    }
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int uy = tap / 3, ux = tap % 3;
@@ -178,22 +199,7 @@ __global__ void __launch_bounds__(NTH) halo_union_kernel(HaloArgs a) {
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      // depth-to-space stores: 4 output pixels per thread, their packed-image operands
-      // loaded before any is used (one HBM round trip per tile, not four)
-      const int Ho = 2 * a.H, Wo = 2 * a.W;
-      constexpr int PQ = 1024 / NTH;   // output pixels per thread (256 q x 4 classes)
-      long P[PQ];
-      bool ok[PQ];
-      bf16x8 ab[PQ], af[PQ];
-#pragma unroll
-      for (int q = 0; q < PQ; ++q) {
-        const int item = tid + q * NTH, row = item >> 2, cls = item & 3;
-        const int qy = qy0 + (row >> 4), qx = qx0 + (row & 15);
-        ok[q] = qy < a.H && qx < a.W;
-        P[q] = ((long)n * Ho + 2 * (ok[q] ? qy : 0) + (cls >> 1)) * Wo + 2 * (ok[q] ? qx : 0) + (cls & 1);
-        ab[q] = *reinterpret_cast<const bf16x8*>(a.pk_a + P[q] * 8);
-        if (a.mode == 2) af[q] = *reinterpret_cast<const bf16x8*>(a.pk_f + P[q] * 8);
-      }
+      // depth-to-space stores: 4 output pixels per thread (operands loaded at the tile start)
 #pragma unroll
       for (int q = 0; q < PQ; ++q) {
         const int item = tid + q * NTH, row = item >> 2, cls = item & 3;
