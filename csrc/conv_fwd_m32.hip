@@ -169,7 +169,7 @@ __device__ unsigned long long m32_stamps[65536 * 6];
 template <int BN, int BMT = 256>
 struct M32Geom {
   static constexpr int BM = BMT;
-  static constexpr int WM = BN == 256 ? 2 : 4;
+  static constexpr int WM = BN == 256 ? 2 : (BN == 64 ? 8 : 4);
   static constexpr int WN = 8 / WM;
   static constexpr int TM = BM / WM / 32;
   static constexpr int TN = BN / WN / 32;
@@ -202,7 +202,7 @@ struct M32Geom {
 template <int BN, int MODE, bool RELU, bool EXT, int F8 = 0, int BMT = 256>
 __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
   using G = M32Geom<BN, BMT>;
-  static_assert(BMT == 256 || (BMT == 512 && BN == 128 && F8 == 0), "512-row tile: bf16, 128 columns");
+  static_assert(BMT == 256 || (BMT == 512 && (BN == 128 || BN == 64) && F8 == 0), "512-row tile: bf16, 64 / 128 columns");
   constexpr int ES = F8 ? 1 : 2;            // bytes per operand element
   constexpr int BKE = F8 ? 2 * BK : BK;     // operand elements per 128-B K tile row
   constexpr int BM = G::BM, WN = G::WN, TM = G::TM, TN = G::TN, STAGES = G::STAGES, NT = G::NT;
@@ -439,7 +439,7 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
   // glds index is a compile-time constant once the loops are unrolled)
   auto mma_step = [&](F& f, auto nq_c, auto q0_c, auto slot_c, bool refill) __attribute__((always_inline)) {
     constexpr int NQ = decltype(nq_c)::value, Q0 = decltype(q0_c)::value, P = TM * TN;
-    static_assert(NQ <= P, "at most one glds per MFMA");
+    static_assert(NQ <= 2 * P, "at most two glds per MFMA");
     if constexpr (RELU) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) f.a[i] = relu8(f.a[i]);
@@ -452,10 +452,13 @@ __global__ void __launch_bounds__(512) conv_fwd_m32_kernel(ConvFwdArgs a) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f.b[j]),
                                                              __builtin_bit_cast(bf16x8, f.a[i]), acc[i][j], 0, 0, 0);
         const int p = i * TN + j;
-        if (NQ > 0 && ((p + 1) * NQ) / P > (p * NQ) / P && refill) {
-          __builtin_amdgcn_sched_barrier(0);
-          fire(slot_c, Q0 + (p * NQ) / P);
-          __builtin_amdgcn_sched_barrier(0);
+        if (NQ > 0 && refill) {
+#pragma unroll
+          for (int q = (p * NQ) / P; q < ((p + 1) * NQ) / P; ++q) {
+            __builtin_amdgcn_sched_barrier(0);
+            fire(slot_c, Q0 + q);
+            __builtin_amdgcn_sched_barrier(0);
+          }
         }
       }
     }
@@ -795,19 +798,24 @@ extern "C" int p2p_conv_m32_rows(const p2p::ConvFwdArgs* a, int mode, int varian
     return 256;
   }
   if (variant == 5 && a->Cout > 128) return 256;
-  if (!(variant == 4 && a->Cout > 64)) return 0;
+  // 33-64 output channels (variant 2, the glds 128 x 64 tile otherwise): only the 512 x 64
+  // tile (8 waves of 64 x 64), under the same geometry conditions as the 512 x 128 one
+  const bool c64 = variant == 2 && a->Cout > 32 && a->Cout <= 64 && a->KH * a->KW >= 4;
+  if (!(variant == 4 && a->Cout > 64) && !c64) return 0;
+  const int fallback = c64 ? 0 : 256;
   const char* env = std::getenv("P2P_M32_BM");
   const int pin = env ? std::atoi(env) : 0;
-  if (pin == 256) return 256;
+  if (pin == 256) return fallback;
+  if (c64 && std::getenv("P2P_M32_C64") && std::getenv("P2P_M32_C64")[0] == '0') return 0;
   const int classes = mode == 0 ? 1 : a->stride * a->stride;
   long hwq = (long)a->OH * a->OW;
   if (mode == 1) {
-    if (a->OH % a->stride || a->OW % a->stride) return 256;
+    if (a->OH % a->stride || a->OW % a->stride) return fallback;
     hwq = (long)(a->OH / a->stride) * (a->OW / a->stride);
   }
-  if (hwq % 512) return 256;
+  if (hwq % 512) return fallback;
   const long blocks = (long)a->N * hwq / 512 * ((a->Cout + 127) / 128) * classes;
-  return (pin == 512 || blocks >= 256) ? 512 : 256;
+  return (pin == 512 || blocks >= 256) ? 512 : fallback;
 }
 
 // variant 5 -> 256 x 256 tile (Cout > 128), 4 -> 256 x 128 or 512 x 128 (Cout > 64); -2 = not
@@ -820,6 +828,8 @@ extern "C" int p2p_conv_fwd_m32(const p2p::ConvFwdArgs* a, int mode, int variant
   // (the ReLU 256-wide variants spill a few loop-invariant epilogue values before the K loop; the loop itself is spill-free)
   if (variant == 5)
     return mode == 0 ? dispatch_m32_epi<256, 0>(*a, st) : dispatch_m32_epi<256, 1>(*a, st);
+  if (rows == 512 && a->Cout <= 64)
+    return mode == 0 ? dispatch_m32_epi<64, 0, 512>(*a, st) : dispatch_m32_epi<64, 1, 512>(*a, st);
   if (rows == 512)
     return mode == 0 ? dispatch_m32_epi<128, 0, 512>(*a, st) : dispatch_m32_epi<128, 1, 512>(*a, st);
   return mode == 0 ? dispatch_m32_epi<128, 0>(*a, st) : dispatch_m32_epi<128, 1>(*a, st);

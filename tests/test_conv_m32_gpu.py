@@ -229,3 +229,34 @@ def test_m32_512_rows_full_step_fused_norms(monkeypatch):
     for a, b in zip(l512, l256):
         for k in a:
             assert abs(a[k] - b[k]) <= 2e-3 * max(1.0, abs(b[k])), (k, a[k], b[k])
+
+
+# The 512 x 64 tile (round 6): 33-64 output channels (the glds 128 x 64 tile otherwise) --
+# family R's 64-channel 3x3 layers, VGG conv1_x / conv2_1's neighbours; forced onto the GEMM
+# route with variant g2 (no halo / s2t kernels), >= 256 tiles of 128 rows (no split-K)
+CASES_64 = [
+    ("conv3x3_c64_relu_out_512x64", "g2", "conv", 16, 64, 0, 64, 64, 3, 1, 1, "zeros", None, "relu"),
+    ("conv3x3_reflect_relu_in_cout48", "g2", "conv", 16, 128, 0, 64, 48, 3, 1, 1, "reflect", "relu", None),
+    ("convT_c64_512x64", "g2", "convT", 16, 128, 0, 32, 64, 4, 2, 1, "zeros", None, None),
+]
+
+
+@pytest.mark.parametrize("case", CASES_64, ids=[c[0] for c in CASES_64])
+def test_m32_512x64_matches_oracle_and_glds(case, monkeypatch):
+    name, var, kind, N, C1, C2, H, Cout, k, s, p, pad_mode, act_in, act_out = case
+    # (pinned: these grids have 128-256 blocks of 512 rows, below the route's one-per-CU bar)
+    (y, gx1, gx2, gw, gb), (x1, x2, w, b, gy), names = _run(case, True, {"P2P_M32_BM": "512"})
+    assert any("conv_fwd_m32_kernel<64, " in n and ", 512>" in n for n in names), sorted(set(names))
+    rx1, rw, rb = _leaf(x1.float()), _leaf(w), _leaf(b)
+    wq = rw.to(torch.bfloat16).float()
+    if kind == "conv":
+        ry = ref.conv2d(rx1, wq, rb, s, p, pad_mode, 1, act_in=act_in, act_out=act_out)
+    else:
+        ry = ref.conv_transpose2d(rx1, wq, rb, s, p, act_in, act_out)
+    ry.backward(gy.float())
+    assert rel_err(y, ry) < 2e-2, (name, "y", rel_err(y, ry))
+    assert rel_err(gx1, rx1.grad) < 3e-2, (name, "dx", rel_err(gx1, rx1.grad))
+    assert rel_err(gw, rw.grad) < 3e-2, (name, "dw")
+    out_b, _, names_b = _run(case, True, {"P2P_M32_BM": "512", "P2P_M32_C64": "0"})
+    assert not any("conv_fwd_m32_kernel<64, " in n for n in names_b)
+    assert rel_err(y, out_b[0]) < 1.5e-2 and rel_err(gx1, out_b[1]) < 1.5e-2
